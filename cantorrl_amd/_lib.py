@@ -1,0 +1,171 @@
+"""ctypes binding of libhedgeenv (include/hedge_env.h).
+
+The shared library is built in-tree (`cantorrl_amd/lib/libhedgeenv.so`, see
+`cantorrl_amd/build.py`).  There is no fallback: if the library cannot be
+loaded, every constructor raises.  torch is imported first so that the HIP
+runtime torch ships (SONAME libamdhip64.so.7) is the one the library binds to
+-- one runtime per process, so torch streams and data_ptr()s are valid here.
+"""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libhedgeenv.so")
+
+HE_ABI_VERSION = 1
+HE_OK, HE_EINVAL, HE_ESHAPE, HE_EHIP, HE_ENOMEM, HE_ESTATE = range(6)
+HE_MODE_REPLAY, HE_MODE_GBM, HE_MODE_HESTON = range(3)
+HE_LOSS_MSE, HE_LOSS_ABS, HE_LOSS_CVAR, HE_LOSS_OTHER = range(4)
+MODES = {"replay": HE_MODE_REPLAY, "gbm": HE_MODE_GBM, "heston": HE_MODE_HESTON}
+
+
+def loss_code(loss_type):
+    """hedging_env_v2.py:246-253: "mse", "abs", "cvar", anything else = |x| branch."""
+    return {"mse": HE_LOSS_MSE, "abs": HE_LOSS_ABS, "cvar": HE_LOSS_CVAR}.get(loss_type, HE_LOSS_OTHER)
+
+
+class HeConfig(ctypes.Structure):
+    _fields_ = [
+        ("abi_version", ctypes.c_int32),
+        ("variant", ctypes.c_int32),
+        ("mode", ctypes.c_int32),
+        ("loss_type", ctypes.c_int32),
+        ("n_envs", ctypes.c_int64),
+        ("global_env_offset", ctypes.c_int64),
+        ("transaction_cost_per_contract", ctypes.c_double),
+        ("lambda_cost", ctypes.c_double),
+        ("pnl_penalty_weight", ctypes.c_double),
+        ("theta_weight", ctypes.c_double),
+        ("slippage_bps", ctypes.c_double),
+        ("initial_cash", ctypes.c_double),
+        ("shares_to_hedge", ctypes.c_int64),
+        ("max_contracts_held_per_type", ctypes.c_int32),
+        ("max_trade_per_step", ctypes.c_int32),
+        ("record_metrics", ctypes.c_int32),
+        ("autoreset", ctypes.c_int32),
+        ("risk_free_rate", ctypes.c_double),
+        ("option_tenor_years", ctypes.c_double),
+        ("episode_length", ctypes.c_int32),
+        ("device", ctypes.c_int32),
+        ("seed", ctypes.c_uint64),
+        ("s0", ctypes.c_double),
+        ("variance", ctypes.c_double),
+        ("mu", ctypes.c_double),
+        ("dt", ctypes.c_double),
+        ("heston_kappa", ctypes.c_double),
+        ("heston_theta", ctypes.c_double),
+        ("heston_xi", ctypes.c_double),
+        ("heston_rho", ctypes.c_double),
+        ("reserved", ctypes.c_double * 8),
+    ]
+
+
+_P = ctypes.c_void_p
+INFO_FIELDS = [
+    ("step_pnl_total", "f8"), ("per_share_step_pnl", "f8"), ("raw_pnl_deviation_abs", "f8"),
+    ("transaction_costs_total", "f8"), ("commission_cost", "f8"), ("slippage_cost", "f8"),
+    ("reward_pnl_component", "f8"), ("transaction_cost_penalty", "f8"), ("theta_penalty", "f8"),
+    ("reward_step", "f8"), ("portfolio_value", "f8"), ("cash", "f8"),
+    ("call_contracts", "i4"), ("put_contracts", "i4"),
+    ("scaled_float_call", "f4"), ("scaled_float_put", "f4"),
+    ("requested_calls_rounded_clipped", "i4"), ("requested_puts_rounded_clipped", "i4"),
+    ("actual_calls_traded", "i4"), ("actual_puts_traded", "i4"),
+    ("initial_S0_for_episode", "f4"),
+    ("current_stock_price", "f4"), ("current_volatility", "f4"),
+    ("current_call_price", "f4"), ("current_put_price", "f4"), ("current_step", "i4"),
+]
+
+
+class HeInfo(ctypes.Structure):
+    _fields_ = [(name, _P) for name, _ in INFO_FIELDS]
+
+
+EXPORTS = [
+    "he_config_init", "he_create", "he_destroy", "he_last_error", "he_version", "he_load_paths",
+    "he_seed", "he_reset", "he_step", "he_rollout", "he_num_envs", "he_episode_length",
+    "he_num_episodes", "he_get_config", "he_state_size", "he_get_state", "he_set_state",
+    "he_pcg64_seed_state", "he_host_episode_draws", "he_host_philox",
+]
+
+_lib = None
+
+
+class HedgeEnvError(RuntimeError):
+    pass
+
+
+def load(path=LIB_PATH):
+    """Load libhedgeenv (once).  Raises if the in-tree library is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise HedgeEnvError(
+            f"{path} not found: build it with `python -m cantorrl_amd.build` "
+            "(hipcc --offload-arch=gfx950).  There is no CPU fallback.")
+    try:
+        import torch  # noqa: F401  (bind to torch's HIP runtime, see module doc)
+    except ImportError:
+        pass
+    lib = ctypes.CDLL(path)
+    vp, i32, i64, u64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64
+    sig = {
+        "he_config_init": (i32, [ctypes.POINTER(HeConfig), i32]),
+        "he_create": (i32, [ctypes.POINTER(HeConfig), ctypes.POINTER(vp)]),
+        "he_destroy": (i32, [vp]),
+        "he_last_error": (ctypes.c_char_p, [vp]),
+        "he_version": (ctypes.c_char_p, []),
+        "he_load_paths": (i32, [vp, vp, vp, vp, vp, i64, i64]),
+        "he_seed": (i32, [vp, vp, vp, i64]),
+        "he_reset": (i32, [vp, vp, i64, vp, vp]),
+        "he_step": (i32, [vp, vp, vp, vp, vp, vp, vp, ctypes.POINTER(HeInfo), vp]),
+        "he_rollout": (i32, [vp, i32, vp, vp, vp, vp, vp]),
+        "he_num_envs": (i64, [vp]),
+        "he_episode_length": (i32, [vp]),
+        "he_num_episodes": (i64, [vp]),
+        "he_get_config": (i32, [vp, ctypes.POINTER(HeConfig)]),
+        "he_state_size": (ctypes.c_size_t, [vp]),
+        "he_get_state": (i32, [vp, vp, ctypes.c_size_t]),
+        "he_set_state": (i32, [vp, vp, ctypes.c_size_t]),
+        "he_pcg64_seed_state": (i32, [u64, ctypes.POINTER(ctypes.c_uint64 * 4)]),
+        "he_host_episode_draws": (i32, [u64, u64, i64, vp]),
+        "he_host_philox": (i32, [u64, u64, u64, ctypes.POINTER(ctypes.c_uint32 * 4)]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(lib, handle, status, what):
+    if status != HE_OK:
+        msg = lib.he_last_error(handle).decode() if handle else ""
+        if status == HE_ESHAPE:
+            raise ValueError(msg or "Data shapes are inconsistent.")
+        raise HedgeEnvError(f"{what} failed (status {status}): {msg}")
+
+
+def pcg64_seed_state(seed):
+    """Host PCG64(SeedSequence(seed)) state as (state_hi, state_lo, inc_hi, inc_lo)."""
+    lib = load()
+    arr = (ctypes.c_uint64 * 4)()
+    check(lib, None, lib.he_pcg64_seed_state(ctypes.c_uint64(seed), ctypes.byref(arr)), "he_pcg64_seed_state")
+    return tuple(arr)
+
+
+def host_episode_draws(seed, n_paths, count):
+    """Host build of the device episode sampler (PCG64 + Lemire), for tests."""
+    import numpy as np
+    lib = load()
+    out = np.zeros(count, np.int64)
+    check(lib, None, lib.he_host_episode_draws(seed, n_paths, count, out.ctypes.data), "he_host_episode_draws")
+    return out
+
+
+def host_philox(seed, env_id, n):
+    lib = load()
+    arr = (ctypes.c_uint32 * 4)()
+    check(lib, None, lib.he_host_philox(seed, env_id, n, ctypes.byref(arr)), "he_host_philox")
+    return tuple(arr)

@@ -1,0 +1,50 @@
+"""Build libhedgeenv for gfx950 in-tree (cantorrl_amd/lib/libhedgeenv.so).
+
+    python -m cantorrl_amd.build [--force]
+
+Flags that matter for parity with the NumPy reference:
+  -ffp-contract=off                       no a*b+c -> fma contraction
+  -fhip-fp32-correctly-rounded-divide-sqrt  IEEE f32 '/' and sqrtf
+  -fno-gpu-flush-denormals-to-zero        keep f32 denormals
+"""
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+SRC = os.path.join(HERE, "csrc", "hedge_env.hip")
+DEPS = [SRC, os.path.join(HERE, "csrc", "he_math.h"), os.path.join(REPO, "include", "hedge_env.h")]
+OUT = os.path.join(HERE, "lib", "libhedgeenv.so")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = os.environ.get("CANTORRL_ARCH", "gfx950")
+
+FLAGS = [
+    f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+    "-ffp-contract=off", "-fhip-fp32-correctly-rounded-divide-sqrt",
+    "-fno-gpu-flush-denormals-to-zero", "-Wall", "-Wno-unused-function",
+]
+
+
+def needs_build(out=OUT):
+    if not os.path.exists(out):
+        return True
+    t = os.path.getmtime(out)
+    return any(os.path.getmtime(d) > t for d in DEPS)
+
+
+def build(force=False, verbose=False):
+    if not force and not needs_build():
+        return OUT
+    os.makedirs(os.path.dirname(OUT), exist_ok=True)
+    tmp = OUT + ".tmp"
+    cmd = [HIPCC, *FLAGS, "-o", tmp, SRC]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, OUT)
+    return OUT
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

@@ -1,0 +1,201 @@
+// he_math.h -- scalar building blocks of the hedging step, shared by the HIP
+// kernels (__device__) and the host reference code (__host__).
+//
+// Every function restates one reference expression with the reference's
+// dtype sequence (NumPy 2 / NEP 50: python scalars are weak, so f32 stays f32,
+// int64 x f32 promotes to f64).  The library is compiled with
+// -ffp-contract=off and correctly rounded f32 div/sqrt so that + - * / sqrt
+// are bit-identical to NumPy's.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define HE_HD __host__ __device__ __forceinline__
+
+namespace he {
+
+// ---------------------------------------------------------------- numpy helpers
+// np.maximum / np.minimum: NaN in either operand propagates.
+HE_HD float np_maxf(float a, float b) { return (a != a) ? a : ((b != b) ? b : (a > b ? a : b)); }
+HE_HD double np_max(double a, double b) { return (a != a) ? a : ((b != b) ? b : (a > b ? a : b)); }
+// np.clip(x, lo, hi) for f32 with NaN propagation.
+HE_HD float np_clipf(float x, float lo, float hi) { return x < lo ? lo : (x > hi ? hi : x); }
+
+// np.rint(f32).astype(int64) then np.clip(., -mt, mt)  (hedging_env_v2.py:184-188).
+// x86 cvttss2si maps NaN and |x| >= 2^63 to INT64_MIN, which the clip sends to -mt.
+HE_HD int32_t trade_round(float f, int32_t mt) {
+    float r = rintf(f);
+    if (!(fabsf(r) < 9.2233720368547758e18f)) return -mt;
+    float lo = -(float)mt, hi = (float)mt;
+    r = r < lo ? lo : (r > hi ? hi : r);
+    return (int32_t)r;
+}
+
+// ---------------------------------------------------------------- Philox4x32-10
+// Salmon et al. (SC'11) / Random123; same block function as rocRAND's
+// philox4x32_10.  Counter = (lo(n), hi(n), lo(g), hi(g)), key = (lo(seed), hi(seed)).
+struct u32x4 { uint32_t x, y, z, w; };
+
+HE_HD uint32_t mulhi32(uint32_t a, uint32_t b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __umulhi(a, b);
+#else
+    return (uint32_t)(((uint64_t)a * (uint64_t)b) >> 32);
+#endif
+}
+
+HE_HD u32x4 philox4x32_10(u32x4 c, uint32_t k0, uint32_t k1) {
+    const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
+    const uint32_t W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        if (r) { k0 += W0; k1 += W1; }
+        uint32_t hi0 = mulhi32(M0, c.x), lo0 = M0 * c.x;
+        uint32_t hi1 = mulhi32(M1, c.z), lo1 = M1 * c.z;
+        u32x4 o;
+        o.x = hi1 ^ c.y ^ k0;
+        o.y = lo1;
+        o.z = hi0 ^ c.w ^ k1;
+        o.w = lo0;
+        c = o;
+    }
+    return c;
+}
+
+// (0,1) double from two words: ((hi:lo >> 12) + 0.5) * 2^-52, exact.
+HE_HD double u01(uint32_t hi, uint32_t lo) {
+    uint64_t k = ((((uint64_t)hi) << 32) | (uint64_t)lo) >> 12;
+    return ((double)k + 0.5) * 2.220446049250313e-16;
+}
+
+// ---------------------------------------------------------------- normal cdf/pdf
+// scipy.special.ndtr (cephes ndtr.c): erf branch inside |x| < 1/sqrt2.
+HE_HD double ndtr(double a) {
+    if (a != a) return a;
+    const double SQRT1_2 = 0.70710678118654752440;
+    double x = a * SQRT1_2;
+    double z = fabs(x);
+    double y;
+    if (z < SQRT1_2) {
+        y = 0.5 + 0.5 * erf(x);
+    } else {
+        y = 0.5 * erfc(z);
+        if (x > 0) y = 1.0 - y;
+    }
+    return y;
+}
+
+// scipy.stats.norm.pdf: exp(-x**2/2.0) / sqrt(2*pi)  (x**2 on an array = x*x)
+HE_HD double norm_pdf(double x) {
+    return exp(-(x * x) / 2.0) / 2.5066282746310002;
+}
+
+// ---------------------------------------------------------------- Black-Scholes
+// OptionCalculator.black_scholes_price (quantconnect/option_calculator.py:11-27),
+// f64.  `a` = (r + 0.5*sigma**2)*T, `b` = sigma*sqrt(T), `disc` = exp(-r*T) are
+// precomputed with python-float semantics when sigma is constant.
+struct BSConst {
+    double a, b, disc;
+    int intrinsic;  // T <= 0 or sigma <= 0
+};
+
+HE_HD void bs_call_put(double S, double K, const BSConst& c, double* call, double* put) {
+    if (c.intrinsic) {
+        double ic = S - K, ip = K - S;
+        *call = (ic < 0.0) ? 0.0 : ic;
+        *put = (ip < 0.0) ? 0.0 : ip;
+        return;
+    }
+    double d1 = (log(S / K) + c.a) / c.b;
+    double d2 = d1 - c.b;
+    double Kd = K * c.disc;
+    double cv = S * ndtr(d1) - Kd * ndtr(d2);
+    double pv = Kd * ndtr(-d2) - S * ndtr(-d1);
+    *call = (cv < 0.0) ? 0.0 : cv;   // python max(price, 0): NaN stays NaN
+    *put = (pv < 0.0) ? 0.0 : pv;
+}
+
+// ---------------------------------------------------------------- PCG64 (numpy)
+// numpy/random/src/pcg64: 128-bit LCG, XSL-RR output; next32 keeps the high
+// half of a 64-bit draw buffered (has_uint32/uinteger).
+struct Pcg64 {
+    uint64_t sh, sl, ih, il;  // state hi/lo, inc hi/lo
+    uint32_t has32, buf32;
+};
+
+HE_HD void pcg64_step(Pcg64& g) {
+    const uint64_t MH = 0x2360ED051FC65DA4ull, ML = 0x4385DF649FCCF645ull;
+#if defined(__HIP_DEVICE_COMPILE__)
+    uint64_t lo = g.sl * ML;
+    uint64_t hi = __umul64hi(g.sl, ML) + g.sl * MH + g.sh * ML;
+#else
+    unsigned __int128 p = (unsigned __int128)g.sl * ML;
+    uint64_t lo = (uint64_t)p;
+    uint64_t hi = (uint64_t)(p >> 64) + g.sl * MH + g.sh * ML;
+#endif
+    uint64_t nl = lo + g.il;
+    uint64_t carry = nl < lo ? 1ull : 0ull;
+    g.sl = nl;
+    g.sh = hi + g.ih + carry;
+}
+
+HE_HD uint64_t pcg64_next64(Pcg64& g) {
+    pcg64_step(g);
+    uint64_t x = g.sh ^ g.sl;
+    unsigned rot = (unsigned)(g.sh >> 58);
+    return (x >> rot) | (x << ((64u - rot) & 63u));
+}
+
+HE_HD uint32_t pcg64_next32(Pcg64& g) {
+    if (g.has32) {
+        g.has32 = 0;
+        return g.buf32;
+    }
+    uint64_t x = pcg64_next64(g);
+    g.has32 = 1;
+    g.buf32 = (uint32_t)(x >> 32);
+    return (uint32_t)x;
+}
+
+HE_HD uint64_t mulhi64(uint64_t a, uint64_t b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __umul64hi(a, b);
+#else
+    return (uint64_t)(((unsigned __int128)a * b) >> 64);
+#endif
+}
+
+// Generator.integers(P) for int64 (numpy random_bounded_uint64_fill, Lemire).
+HE_HD int64_t pcg64_integers(Pcg64& g, uint64_t P) {
+    uint64_t rng = P - 1;
+    if (rng == 0) return 0;
+    if (rng <= 0xFFFFFFFFull) {
+        if (rng == 0xFFFFFFFFull) return (int64_t)pcg64_next32(g);
+        uint32_t rng32 = (uint32_t)rng, excl = rng32 + 1u;
+        uint64_t m = (uint64_t)pcg64_next32(g) * (uint64_t)excl;
+        uint32_t left = (uint32_t)m;
+        if (left < excl) {
+            uint32_t thr = (0xFFFFFFFFu - rng32) % excl;
+            while (left < thr) {
+                m = (uint64_t)pcg64_next32(g) * (uint64_t)excl;
+                left = (uint32_t)m;
+            }
+        }
+        return (int64_t)(m >> 32);
+    }
+    uint64_t excl = rng + 1;
+    uint64_t x = pcg64_next64(g);
+    uint64_t left = x * excl, hi = mulhi64(x, excl);
+    if (left < excl) {
+        uint64_t thr = (~0ull - rng) % excl;
+        while (left < thr) {
+            x = pcg64_next64(g);
+            left = x * excl;
+            hi = mulhi64(x, excl);
+        }
+    }
+    return (int64_t)hi;
+}
+
+}  // namespace he

@@ -1,0 +1,391 @@
+"""HedgingVecEnv: N hedging envs on one MI355X behind the SB3 VecEnv interface.
+
+Drop-in for the `create_vec_env(...)` swap point of the reference agents
+(src/agents/train_ppo_v2.py:127-141): it exposes what SB3 2.6.0's
+DummyVecEnv/SubprocVecEnv expose (num_envs, observation_space, action_space,
+reset, step_async, step_wait, step, seed, close, get_attr, set_attr,
+env_method, env_is_wrapped) with SB3's auto-reset semantics
+(`info["terminal_observation"]`, `info["TimeLimit.truncated"]`), and Monitor's
+`info["episode"]` when `monitor_keywords` is given (train_ppo_v2.py:119).
+
+Every env's state lives on the device; one `he_step` launch advances all of
+them.  `step_tensors` is the zero-copy path for GPU-resident learners.
+"""
+import time
+
+import numpy as np
+import torch
+
+from . import _lib
+from .spaces import Box
+
+OBS_LOW = np.array([0.1, -1.0, -1.0, -1.0, -1.0, 0.0, 0.0, -1.0, 0.0, -1.0, 0.0, -1.0, -1.0], np.float32)
+OBS_HIGH = np.array([10.0, 1.0, 1.0, 1.0, 1.0, 1.0, 1.0, 1.0, 50.0, 1.0, 50.0, 1.0, 1.0], np.float32)
+
+# HedgingEnv ctor keywords and defaults (hedging_env_v2.py:10-22, v1 hedging_env.py:10-20)
+V2_DEFAULTS = dict(transaction_cost_per_contract=0.65, lambda_cost=1.0, pnl_penalty_weight=0.01,
+                   theta_weight=0.0, slippage_bps=0.0, loss_type="abs", initial_cash=0.0,
+                   shares_to_hedge=10000, max_contracts_held_per_type=200, max_trade_per_step=15,
+                   profile_print_interval=0, record_metrics=True)
+V1_DEFAULTS = {k: v for k, v in V2_DEFAULTS.items() if k not in ("theta_weight", "slippage_bps")}
+V1_DEFAULTS["transaction_cost_per_contract"] = 0.05
+
+GENERATE_DEFAULTS = dict(s0=496.48001098632812, variance=0.029028, mu=0.04, dt=1 / 252,
+                         episode_length=252, heston_kappa=2.0, heston_theta=0.029028,
+                         heston_xi=0.3, heston_rho=-0.7)
+
+MONITOR_KEYWORDS = ("per_share_step_pnl", "raw_pnl_deviation_abs", "transaction_costs_total")
+
+_TORCH_DT = {"f8": torch.float64, "f4": torch.float32, "i4": torch.int32}
+
+
+def load_npz_tables(data_file_path):
+    """np.load + f32 cast + shape check exactly as hedging_env_v2.py:36-48."""
+    try:
+        data = np.load(data_file_path)
+        S = data["paths"].astype(np.float32)
+        v = data["volatilities"].astype(np.float32)
+        C = data["call_prices_atm"].astype(np.float32)
+        P = data["put_prices_atm"].astype(np.float32)
+    except Exception as e:  # same exception contract as the reference
+        raise FileNotFoundError(f"Could not load or parse data from {data_file_path}. Error: {e}")
+    check_table_shapes(S, v, C, P)
+    return S, v, C, P
+
+
+def check_table_shapes(S, v, C, P):
+    if not (S.ndim == 2 and S.shape == v.shape and S.shape[0] == C.shape[0] == P.shape[0]
+            and S.shape[1] == C.shape[1] + 1 == P.shape[1] + 1):
+        raise ValueError("Data shapes are inconsistent.")
+
+
+class HedgingVecEnv:
+    """Batched, device-resident `HedgingEnv` x n_envs.
+
+    Replay mode (reference semantics): pass `data_file_path` (NPZ with paths,
+    volatilities, call_prices_atm, put_prices_atm) or `tables=(S, v, C, P)`.
+    Generate modes: `mode="gbm"` / `"heston"`, market in `generate=dict(...)`.
+    Remaining keywords are the reference HedgingEnv ctor keywords.
+    """
+
+    def __init__(self, n_envs, data_file_path=None, *, tables=None, variant=2, mode=None,
+                 generate=None, device=None, seed=None, global_env_offset=0, autoreset=True,
+                 return_numpy=True, info_keys=MONITOR_KEYWORDS, monitor_keywords=None,
+                 **env_kwargs):
+        self.lib = _lib.load()
+        self.num_envs = int(n_envs)
+        self.variant = int(variant)
+        if mode is None:
+            mode = "replay" if (data_file_path is not None or tables is not None) else "gbm"
+        self.mode = mode
+        base = V2_DEFAULTS if self.variant == 2 else V1_DEFAULTS
+        unknown = set(env_kwargs) - set(base)
+        if unknown:
+            raise TypeError(f"HedgingEnv() got unexpected keyword arguments {sorted(unknown)}")
+        kw = dict(base, **env_kwargs)
+        self.env_kwargs = kw
+        gen = dict(GENERATE_DEFAULTS, **(generate or {}))
+        self.generate = gen
+        self.device = torch.device(device if device is not None else "cuda:0")
+        if self.device.type != "cuda":
+            raise _lib.HedgeEnvError("HedgingVecEnv runs on a HIP device (cuda:N); there is no CPU path")
+        if not torch.cuda.is_available():
+            raise _lib.HedgeEnvError("no HIP device visible: libhedgeenv needs an MI355X")
+        dev_index = self.device.index if self.device.index is not None else torch.cuda.current_device()
+        self.device = torch.device("cuda", dev_index)
+
+        cfg = _lib.HeConfig()
+        _lib.check(self.lib, None, self.lib.he_config_init(cfg, self.variant), "he_config_init")
+        cfg.mode = _lib.MODES[mode]
+        cfg.loss_type = _lib.loss_code(kw["loss_type"])
+        cfg.n_envs = self.num_envs
+        cfg.global_env_offset = int(global_env_offset)
+        cfg.transaction_cost_per_contract = float(kw["transaction_cost_per_contract"])
+        cfg.lambda_cost = float(kw["lambda_cost"])
+        cfg.pnl_penalty_weight = float(kw["pnl_penalty_weight"])
+        cfg.theta_weight = float(kw.get("theta_weight", 0.0))
+        cfg.slippage_bps = float(kw.get("slippage_bps", 0.0))
+        cfg.initial_cash = float(kw["initial_cash"])
+        cfg.shares_to_hedge = int(kw["shares_to_hedge"])
+        cfg.max_contracts_held_per_type = int(kw["max_contracts_held_per_type"])
+        cfg.max_trade_per_step = int(kw["max_trade_per_step"])
+        cfg.record_metrics = 1 if kw["record_metrics"] else 0
+        cfg.autoreset = 1 if autoreset else 0
+        cfg.device = dev_index
+        cfg.episode_length = int(gen["episode_length"])
+        cfg.s0 = float(gen["s0"])
+        cfg.variance = float(gen["variance"])
+        cfg.mu = float(gen["mu"])
+        cfg.dt = float(gen["dt"])
+        cfg.heston_kappa = float(gen["heston_kappa"])
+        cfg.heston_theta = float(gen["heston_theta"])
+        cfg.heston_xi = float(gen["heston_xi"])
+        cfg.heston_rho = float(gen["heston_rho"])
+        base_seed = int(seed if seed is not None else gen.get("seed", 42))
+        cfg.seed = base_seed
+        self._cfg = cfg
+        handle = _lib.ctypes.c_void_p()
+        st = self.lib.he_create(cfg, _lib.ctypes.byref(handle))
+        self._h = handle
+        _lib.check(self.lib, handle, st, "he_create")
+
+        if mode == "replay":
+            if tables is None:
+                S, v, C, P = load_npz_tables(data_file_path)
+            else:
+                S, v, C, P = (np.ascontiguousarray(np.asarray(x).astype(np.float32)) for x in tables)
+                check_table_shapes(S, v, C, P)
+            S, v, C, P = (np.ascontiguousarray(x) for x in (S, v, C, P))
+            st = self.lib.he_load_paths(self._h, S.ctypes.data, v.ctypes.data, C.ctypes.data,
+                                        P.ctypes.data, S.shape[0], S.shape[1])
+            _lib.check(self.lib, self._h, st, "he_load_paths")
+            self.num_episodes = int(S.shape[0])
+            self.episode_length = int(S.shape[1] - 1)
+        else:
+            self.num_episodes = None
+            self.episode_length = int(gen["episode_length"])
+
+        n = self.num_envs
+        dev = self.device
+        self._act = torch.zeros((n, 2), dtype=torch.float32, device=dev)
+        self._obs = torch.zeros((n, 13), dtype=torch.float32, device=dev)
+        self._rew = torch.zeros((n,), dtype=torch.float32, device=dev)
+        self._term = torch.zeros((n,), dtype=torch.uint8, device=dev)
+        self._trunc = torch.zeros((n,), dtype=torch.uint8, device=dev)
+        self._tobs = torch.zeros((n, 13), dtype=torch.float32, device=dev)
+        self.info_keys = tuple(info_keys or ())
+        self._info_t = {}
+        self._info = _lib.HeInfo()
+        known = dict(_lib.INFO_FIELDS)
+        for k in self.info_keys:
+            if k not in known:
+                raise KeyError(f"unknown info key {k!r}")
+            t = torch.zeros((n,), dtype=_TORCH_DT[known[k]], device=dev)
+            self._info_t[k] = t
+            setattr(self._info, k, t.data_ptr())
+        self.return_numpy = bool(return_numpy)
+        self.monitor_keywords = tuple(monitor_keywords) if monitor_keywords else None
+        self._pending_seeds = None
+        self._actions_pending = None
+        self._ep_ret = np.zeros(n, np.float64)
+        self._ep_len = np.zeros(n, np.int64)
+        self._t_start = time.time()
+
+        self.action_space = Box(-1.0, 1.0, (2,), np.float32)
+        self.observation_space = Box(OBS_LOW, OBS_HIGH, (13,), np.float32)
+        # reference attribute names (hedging_env_v2.py:53-58) + the documented alias
+        self.transaction_cost_per_contract = kw["transaction_cost_per_contract"]
+        self.max_contracts_held = kw["max_contracts_held_per_type"]
+        self.shares_held_fixed = kw["shares_to_hedge"]
+        self.option_contract_multiplier = 100
+        self.risk_free_rate = 0.04
+        self.option_tenor_years = 30 / 252
+        self.max_trade_per_step = kw["max_trade_per_step"]
+        self._max_trade_per_step_internal = kw["max_trade_per_step"]
+        self.loss_type = kw["loss_type"]
+        self.record_metrics = kw["record_metrics"]
+
+    # ------------------------------------------------------------------ plumbing
+    @property
+    def stream(self):
+        return torch.cuda.current_stream(self.device).cuda_stream
+
+    def _ptr(self, t):
+        return t.data_ptr() if t is not None else None
+
+    def close(self):
+        if getattr(self, "_h", None) and self._h.value:
+            torch.cuda.synchronize(self.device)
+            self.lib.he_destroy(self._h)
+            self._h = _lib.ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ------------------------------------------------------------------ seeding
+    def seed(self, seed=None):
+        """SB3 semantics: env i gets seed + i, applied at the next reset()."""
+        if seed is None:
+            seed = int(np.random.randint(0, 2 ** 31 - 1))
+        self._pending_seeds = [int(seed) + i for i in range(self.num_envs)]
+        return self._pending_seeds
+
+    def seed_envs(self, seeds, env_ids=None):
+        """Per-env reset(seed=...) re-seeding (replay) / Philox key (generate)."""
+        seeds = np.ascontiguousarray(np.asarray(seeds, dtype=np.uint64))
+        ids = None if env_ids is None else np.ascontiguousarray(np.asarray(env_ids, dtype=np.int64))
+        st = self.lib.he_seed(self._h, None if ids is None else ids.ctypes.data, seeds.ctypes.data,
+                              len(seeds))
+        _lib.check(self.lib, self._h, st, "he_seed")
+
+    # ------------------------------------------------------------------ reset
+    def reset_tensors(self, env_ids=None):
+        if self._pending_seeds is not None:
+            self.seed_envs(self._pending_seeds)
+            self._pending_seeds = None
+        if env_ids is None:
+            st = self.lib.he_reset(self._h, None, self.num_envs, self._obs.data_ptr(), self.stream)
+        else:
+            ids = torch.as_tensor(env_ids, dtype=torch.int64, device=self.device)
+            st = self.lib.he_reset(self._h, ids.data_ptr(), ids.numel(), self._obs.data_ptr(), self.stream)
+        _lib.check(self.lib, self._h, st, "he_reset")
+        if env_ids is None:
+            self._ep_ret[:] = 0.0
+            self._ep_len[:] = 0
+        return self._obs
+
+    def reset(self):
+        obs = self.reset_tensors()
+        return obs.cpu().numpy() if self.return_numpy else obs
+
+    # ------------------------------------------------------------------ step
+    def step_tensors(self, actions, terminal_obs=True, info=True):
+        """Device path: actions [N,2] (tensor on the env device or array) ->
+        (obs, reward, terminated, truncated) device tensors; no host sync."""
+        if isinstance(actions, torch.Tensor) and actions.device == self.device \
+                and actions.dtype == torch.float32 and actions.is_contiguous():
+            act = actions
+        else:
+            a = torch.as_tensor(actions, dtype=torch.float32)
+            self._act.copy_(a.reshape(self.num_envs, 2), non_blocking=True)
+            act = self._act
+        st = self.lib.he_step(self._h, act.data_ptr(), self._obs.data_ptr(), self._rew.data_ptr(),
+                              self._term.data_ptr(), self._trunc.data_ptr(),
+                              self._tobs.data_ptr() if terminal_obs else None,
+                              _lib.ctypes.byref(self._info) if (info and self._info_t) else None,
+                              self.stream)
+        _lib.check(self.lib, self._h, st, "he_step")
+        return self._obs, self._rew, self._term, self._trunc
+
+    def step_async(self, actions):
+        self._actions_pending = actions
+
+    def step_wait(self):
+        actions = self._actions_pending
+        self._actions_pending = None
+        obs, rew, term, _ = self.step_tensors(actions)
+        if not self.return_numpy:
+            return obs, rew, term.bool(), InfoView(self, None)
+        obs_h = obs.cpu().numpy()
+        rew_h = rew.cpu().numpy()
+        done_h = term.cpu().numpy().astype(bool)
+        self._ep_ret += rew_h.astype(np.float64)
+        self._ep_len += 1
+        infos = InfoView(self, done_h)
+        if done_h.any():
+            infos._materialize_done(done_h)
+            self._ep_ret[done_h] = 0.0
+            self._ep_len[done_h] = 0
+        return obs_h, rew_h, done_h, infos
+
+    def step(self, actions):
+        self.step_async(actions)
+        return self.step_wait()
+
+    def rollout(self, actions, obs=None, reward=None, terminated=None):
+        """K fused steps: actions [K,N,2] device tensor -> writes obs [K,N,13],
+        reward [K,N], terminated [K,N] (allocated if None)."""
+        K = int(actions.shape[0])
+        n = self.num_envs
+        dev = self.device
+        if obs is None:
+            obs = torch.empty((K, n, 13), dtype=torch.float32, device=dev)
+        if reward is None:
+            reward = torch.empty((K, n), dtype=torch.float32, device=dev)
+        if terminated is None:
+            terminated = torch.empty((K, n), dtype=torch.uint8, device=dev)
+        actions = actions.to(device=dev, dtype=torch.float32).contiguous()
+        st = self.lib.he_rollout(self._h, K, actions.data_ptr(), self._ptr(obs), self._ptr(reward),
+                                 self._ptr(terminated), self.stream)
+        _lib.check(self.lib, self._h, st, "he_rollout")
+        return obs, reward, terminated
+
+    # ------------------------------------------------------------------ attrs
+    def _indices(self, indices):
+        if indices is None:
+            return range(self.num_envs)
+        if isinstance(indices, int):
+            return [indices]
+        return indices
+
+    def get_attr(self, attr_name, indices=None):
+        val = getattr(self, attr_name)
+        return [val for _ in self._indices(indices)]
+
+    def set_attr(self, attr_name, value, indices=None):
+        raise NotImplementedError("env attributes are fixed at construction (device-side config)")
+
+    def env_method(self, method_name, *args, indices=None, **kwargs):
+        if method_name in ("render", "close"):
+            return [None for _ in self._indices(indices)]
+        raise NotImplementedError(f"env_method({method_name!r}) is not supported")
+
+    def env_is_wrapped(self, wrapper_class, indices=None):
+        return [False for _ in self._indices(indices)]
+
+    def get_state(self):
+        size = self.lib.he_state_size(self._h)
+        buf = np.empty(size, np.uint8)
+        torch.cuda.synchronize(self.device)
+        _lib.check(self.lib, self._h, self.lib.he_get_state(self._h, buf.ctypes.data, size), "he_get_state")
+        return buf
+
+    def set_state(self, buf):
+        buf = np.ascontiguousarray(buf, dtype=np.uint8)
+        torch.cuda.synchronize(self.device)
+        _lib.check(self.lib, self._h, self.lib.he_set_state(self._h, buf.ctypes.data, buf.size), "he_set_state")
+
+    def info_tensor(self, key):
+        return self._info_t[key]
+
+
+class InfoView:
+    """Lazy list[dict] of per-env infos (SB3 contract) over the device info SoA."""
+
+    def __init__(self, venv, done):
+        self._v = venv
+        self._done = done
+        self._cache = {}
+        self._host = None
+
+    def _host_info(self):
+        if self._host is None:
+            self._host = {k: t.cpu().numpy() for k, t in self._v._info_t.items()}
+        return self._host
+
+    def _materialize_done(self, done):
+        v = self._v
+        tobs = v._tobs.cpu().numpy()
+        h = self._host_info()
+        for i in np.nonzero(done)[0]:
+            d = self[i]
+            d["terminal_observation"] = tobs[i].copy()
+            if v.monitor_keywords is not None:
+                ep = {"r": round(float(v._ep_ret[i]), 6), "l": int(v._ep_len[i]),
+                      "t": round(time.time() - v._t_start, 6)}
+                for k in v.monitor_keywords:
+                    ep[k] = h[k][i].item() if k in h else None
+                d["episode"] = ep
+
+    def __len__(self):
+        return self._v.num_envs
+
+    def __getitem__(self, i):
+        if isinstance(i, slice):
+            return [self[j] for j in range(*i.indices(len(self)))]
+        i = int(i)
+        if i < 0:
+            i += len(self)
+        if i not in self._cache:
+            h = self._host_info()
+            d = {k: h[k][i].item() for k in h}
+            d["TimeLimit.truncated"] = False
+            self._cache[i] = d
+        return self._cache[i]
+
+    def __iter__(self):
+        for i in range(len(self)):
+            yield self[i]

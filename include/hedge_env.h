@@ -1,0 +1,205 @@
+/*
+ * hedge_env.h -- C ABI of libhedgeenv: a batched, device-resident dynamic-hedging
+ * environment for MI355X (gfx950).  Drop-in replacement for the per-env
+ * `HedgingEnv` of bcosm/CantorRL (src/env/hedging_env_v2.py, v1 hedging_env.py)
+ * run N-at-a-time inside HIP kernels.
+ *
+ * Conventions
+ *   - Plain C types only.  Every entry point returns an he_status; the message of
+ *     the last failure on a handle is he_last_error(handle).  No C++ exception
+ *     crosses this boundary.
+ *   - The CALLER owns every I/O buffer passed to he_reset/he_step/he_rollout;
+ *     those are DEVICE pointers on the handle's device (e.g. torch data_ptr()).
+ *     The LIBRARY owns the per-env state (SoA, HBM-resident) and RNG streams.
+ *   - `stream` is an opaque hipStream_t (NULL = the legacy default stream).
+ *     he_reset/he_step/he_rollout only enqueue work: no host synchronisation,
+ *     no allocation, so they can be captured into a hipGraph.
+ *   - One handle must be driven from one host thread at a time.  Distinct
+ *     handles (also on distinct devices) are independent.
+ *
+ * Reference interface each entry point replaces (file:line in /root/reference):
+ *   he_config_init  <- HedgingEnv.__init__ keyword defaults   hedging_env_v2.py:10-22 (v1 hedging_env.py:10-20)
+ *   he_create       <- HedgingEnv.__init__                    hedging_env_v2.py:10-77
+ *   he_load_paths   <- np.load(...).astype(float32) + shape check  hedging_env_v2.py:36-51
+ *   he_seed         <- reset(seed=...) re-seeding: gymnasium seeding.np_random
+ *                      (Generator(PCG64(SeedSequence(seed))))  hedging_env_v2.py:146-148
+ *   he_reset        <- HedgingEnv.reset                       hedging_env_v2.py:145-173
+ *   he_step         <- HedgingEnv.step (+ SB3 VecEnv auto-reset, train_ppo_v2.py:127-141)
+ *                                                             hedging_env_v2.py:175-294
+ *   he_rollout      <- SB3 collect_rollouts' inner loop over VecEnv.step for n_steps
+ *                      (train_ppo_v2.py:48,222-230) with actions supplied up front
+ *   he_get_state / he_set_state  <- env pickling by SubprocVecEnv / checkpoints (no
+ *                      reference equivalent; state is otherwise lost across processes)
+ */
+#ifndef HEDGE_ENV_H
+#define HEDGE_ENV_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HE_ABI_VERSION 1
+#define HE_OBS_DIM 13
+#define HE_ACT_DIM 2
+
+typedef enum he_status {
+    HE_OK = 0,
+    HE_EINVAL = 1,   /* bad argument / config value            */
+    HE_ESHAPE = 2,   /* inconsistent table shapes (ValueError)  */
+    HE_EHIP = 3,     /* HIP runtime failure                     */
+    HE_ENOMEM = 4,   /* device allocation failed                */
+    HE_ESTATE = 5    /* call not valid in the current state     */
+} he_status;
+
+typedef enum he_mode {
+    HE_MODE_REPLAY = 0,  /* replay NPZ paths (reference semantics)           */
+    HE_MODE_GBM = 1,     /* generate: GBM + Philox, BS rolling-ATM marks       */
+    HE_MODE_HESTON = 2   /* generate: Heston full-truncation Euler (extension) */
+} he_mode;
+
+typedef enum he_loss {
+    HE_LOSS_MSE = 0,
+    HE_LOSS_ABS = 1,
+    HE_LOSS_CVAR = 2,    /* identical to ABS inside the env (hedging_env_v2.py:250-253) */
+    HE_LOSS_OTHER = 3    /* any other string: |x| branch (:252-253)                    */
+} he_loss;
+
+typedef struct he_config {
+    int32_t abi_version;        /* = HE_ABI_VERSION                                  */
+    int32_t variant;            /* 1: hedging_env.py, 2: hedging_env_v2.py          */
+    int32_t mode;               /* he_mode                                           */
+    int32_t loss_type;          /* he_loss                                           */
+    int64_t n_envs;             /* envs on this handle (>=1)                         */
+    int64_t global_env_offset;  /* global id of env 0 (multi-GPU sharding)           */
+    /* HedgingEnv ctor keywords (hedging_env_v2.py:10-22) */
+    double transaction_cost_per_contract;
+    double lambda_cost;
+    double pnl_penalty_weight;
+    double theta_weight;        /* v2 only                                           */
+    double slippage_bps;        /* v2 only                                           */
+    double initial_cash;
+    int64_t shares_to_hedge;
+    int32_t max_contracts_held_per_type;   /* 0..32767                               */
+    int32_t max_trade_per_step;            /* 0..32767                               */
+    int32_t record_metrics;                /* 0: greeks are zeros (:80-81)           */
+    int32_t autoreset;                     /* 1: SB3 VecEnv auto-reset inside step   */
+    /* env constants (hedging_env_v2.py:56-58) */
+    double risk_free_rate;      /* 0.04                                              */
+    double option_tenor_years;  /* 30/252                                            */
+    /* generate modes (price advance rbergomi_sim.py:454-464) */
+    int32_t episode_length;     /* T (replay: taken from the table)                  */
+    int32_t device;             /* HIP device ordinal                                */
+    uint64_t seed;              /* Philox key                                        */
+    double s0;                  /* initial price                                     */
+    double variance;            /* GBM: constant variance v; Heston: v0              */
+    double mu;                  /* drift rate of the advance (R = 0.04)              */
+    double dt;                  /* 1/252                                             */
+    double heston_kappa;
+    double heston_theta;
+    double heston_xi;
+    double heston_rho;
+    double reserved[8];
+} he_config;
+
+/* Optional per-step info outputs (device pointers, each may be NULL).  Field names
+ * follow the reference info dict (hedging_env_v2.py:268-293). */
+typedef struct he_info {
+    double* step_pnl_total;
+    double* per_share_step_pnl;
+    double* raw_pnl_deviation_abs;
+    double* transaction_costs_total;
+    double* commission_cost;
+    double* slippage_cost;
+    double* reward_pnl_component;
+    double* transaction_cost_penalty;
+    double* theta_penalty;
+    double* reward_step;            /* the f64 reward before the f32 cast */
+    double* portfolio_value;
+    double* cash;
+    int32_t* call_contracts;
+    int32_t* put_contracts;
+    float* scaled_float_call;
+    float* scaled_float_put;
+    int32_t* requested_calls_rounded_clipped;
+    int32_t* requested_puts_rounded_clipped;
+    int32_t* actual_calls_traded;
+    int32_t* actual_puts_traded;
+    float* initial_S0_for_episode;
+    /* market view after the step (pre-reset), for callers that read env
+     * attributes (src/benchmark/delta_and_nothing.py:71-79) */
+    float* current_stock_price;
+    float* current_volatility;
+    float* current_call_price;
+    float* current_put_price;
+    int32_t* current_step;
+} he_info;
+
+typedef struct he_env he_env;
+
+/* Fill *cfg with the reference ctor defaults of `variant` (1 or 2), GBM market
+ * defaults (S0=496.48, v=0.029028, mu=0.04, dt=1/252, T=252, seed=42), n_envs=1. */
+he_status he_config_init(he_config* cfg, int32_t variant);
+
+he_status he_create(const he_config* cfg, he_env** out);
+he_status he_destroy(he_env* env);
+const char* he_last_error(const he_env* env);   /* never NULL */
+const char* he_version(void);
+
+/* Replay tables, HOST pointers, row-major f32 (the reference casts to f32 on load):
+ * S, v: [n_paths][n_cols]; C, P: [n_paths][n_cols-1]; n_cols = episode_length+1. */
+he_status he_load_paths(he_env* env, const float* S, const float* v, const float* C,
+                        const float* P, int64_t n_paths, int64_t n_cols);
+
+/* Seed per-env episode streams.  Replay: env_ids[i] gets
+ * Generator(PCG64(SeedSequence(seeds[i]))) (host pointers; env_ids NULL = envs
+ * 0..count-1).  Generate modes: seeds[0] becomes the Philox key of the whole
+ * handle and every episode counter restarts. */
+he_status he_seed(he_env* env, const int64_t* env_ids, const uint64_t* seeds, int64_t count);
+
+/* Reset envs (env_ids: DEVICE int64 list, NULL = all) and write their obs rows
+ * into obs_out[N][13] (device; rows of other envs untouched; may be NULL). */
+he_status he_reset(he_env* env, const int64_t* env_ids, int64_t count, float* obs_out,
+                   void* stream);
+
+/* One step of every env.  actions [N][2] f32 in, obs [N][13] f32 out (the reset
+ * obs for envs that terminated when autoreset=1), reward [N] f32 (f64 reward cast
+ * as SB3 stores it), terminated/truncated [N] u8.  terminal_obs [N][13] receives
+ * the pre-reset obs of terminated envs only (NULL = skip).  info may be NULL. */
+he_status he_step(he_env* env, const float* actions, float* obs, float* reward,
+                  uint8_t* terminated, uint8_t* truncated, float* terminal_obs,
+                  const he_info* info, void* stream);
+
+/* k_steps fused steps (autoreset semantics), one launch: actions [K][N][2] in;
+ * obs [K][N][13], reward [K][N], terminated [K][N] out (obs/reward/terminated may
+ * be NULL to skip).  Per-env state stays in registers across the K steps. */
+he_status he_rollout(he_env* env, int32_t k_steps, const float* actions, float* obs,
+                     float* reward, uint8_t* terminated, void* stream);
+
+/* Introspection. */
+int64_t he_num_envs(const he_env* env);
+int32_t he_episode_length(const he_env* env);
+int64_t he_num_episodes(const he_env* env);     /* replay table rows; 0 otherwise */
+he_status he_get_config(const he_env* env, he_config* out);
+
+/* Checkpointing: opaque blob of the whole per-env state (+ RNG streams). */
+size_t he_state_size(const he_env* env);
+he_status he_get_state(he_env* env, void* host_buf, size_t size);
+he_status he_set_state(he_env* env, const void* host_buf, size_t size);
+
+/* Host reference of the seeding used by he_seed (exported for tests):
+ * state[0..3] = {state_hi, state_lo, inc_hi, inc_lo} of PCG64(SeedSequence(seed)). */
+he_status he_pcg64_seed_state(uint64_t seed, uint64_t state[4]);
+
+/* Host builds of the device RNG code (same source, he_math.h), for CPU tests:
+ * count episode indices Generator(PCG64(SeedSequence(seed))).integers(n_paths),
+ * and the 4 Philox4x32-10 words of (seed, global env id, env-step index n). */
+he_status he_host_episode_draws(uint64_t seed, uint64_t n_paths, int64_t count, int64_t* out);
+he_status he_host_philox(uint64_t seed, uint64_t env_id, uint64_t n, uint32_t out[4]);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HEDGE_ENV_H */

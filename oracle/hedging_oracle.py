@@ -212,7 +212,7 @@ class OracleVecEnv:
             self.g_offset = int(g.get("env_offset", 0))
             self.episode_length = int(g.get("episode_length", 252))
             self.num_episodes = None
-            self.g_ep = np.zeros(self.n, np.uint64)
+            self.g_ep = np.full(self.n, -1, np.int64)  # next reset starts episode 0
             self.S64 = np.zeros(self.n, np.float64)
         else:
             raise ValueError(mode)
@@ -243,7 +243,7 @@ class OracleVecEnv:
     def _gbm_advance(self, mask):
         """S_{t+1} from S_t for masked envs (rbergomi_sim.py:454-464, v constant)."""
         ids = np.nonzero(mask)[0]
-        n_idx = self.g_ep[ids] * np.uint64(self.episode_length) + self.t[ids].astype(np.uint64)
+        n_idx = (self.g_ep[ids] * self.episode_length + self.t[ids]).astype(np.uint64)
         z0, _ = philox_normals(self.g_seed, np.uint64(self.g_offset) + ids.astype(np.uint64), n_idx)
         v = self.g_v
         sqrt_dt = np.sqrt(self.g_dt)
@@ -276,9 +276,9 @@ class OracleVecEnv:
         if self.mode == "gbm":
             # generate mode: seed selects the Philox key for the whole batch
             self.g_seed = int(seeds[0])
-            self.g_ep[ids] = 0
+            self.g_ep[:] = -1
 
-    def _reset_mask(self, mask, new_episode=False):
+    def _reset_mask(self, mask):
         ids = np.nonzero(mask)[0]
         if self.mode == "replay":
             for i in ids:
@@ -291,8 +291,7 @@ class OracleVecEnv:
             C = self.C_tab[row, 0]
             P = self.P_tab[row, 0]
         else:
-            if new_episode:
-                self.g_ep[ids] += np.uint64(1)
+            self.g_ep[ids] += 1  # every reset starts the next episode of the env
             self.S64[ids] = self.g_s0
             S = self.S64[ids].astype(np.float32)
             v = np.full(len(ids), self.g_v).astype(np.float32)
@@ -460,7 +459,7 @@ class OracleVecEnv:
         terminal_obs = np.full_like(obs, np.nan)
         if term.any():
             terminal_obs[term] = obs[term]
-            self._reset_mask(term, new_episode=True)
+            self._reset_mask(term)
             obs[term] = self._obs()[term]
         return obs, reward, term, terminal_obs, info
 

@@ -1,0 +1,201 @@
+"""GPU parity: the HIP path (through the C ABI) vs the reference goldens and
+vs the CPU oracle.
+
+Bar (north_star): bit-exact on integer/index/RNG work and on every replay-mode
+f64 P&L field; obs greeks (f32 logf + f64 erf/exp on the GPU vs NumPy/SciPy on
+the host) within OBS_RTOL; generate-mode P&L within PNL_RTOL (1e-5, fp32 P&L
+bar of north_star).
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, golden_files
+from _compare import assert_same
+from oracle.hedging_oracle import OracleVecEnv, load_golden
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+OBS_RTOL = 1e-6      # greeks columns 7-10
+OBS_ATOL = 1e-7
+PNL_RTOL = 1e-5
+ALL_INFO = None      # filled lazily
+
+
+def all_info_keys():
+    from cantorrl_amd import _lib
+    return [k for k, _ in _lib.INFO_FIELDS]
+
+
+GOLD_INFO = [
+    "step_pnl_total", "per_share_step_pnl", "raw_pnl_deviation_abs", "transaction_costs_total",
+    "commission_cost", "slippage_cost", "reward_pnl_component", "transaction_cost_penalty",
+    "theta_penalty", "reward_step", "portfolio_value", "call_contracts", "put_contracts", "cash",
+    "scaled_float_call", "scaled_float_put", "requested_calls_rounded_clipped",
+    "requested_puts_rounded_clipped", "actual_calls_traded", "actual_puts_traded",
+    "initial_S0_for_episode",
+]
+
+
+def compare_obs(got, exp, name):
+    cols_exact = [0, 1, 2, 3, 4, 5, 6, 11, 12]
+    assert_same(got[..., cols_exact], exp[..., cols_exact], name + "[exact cols]")
+    assert_same(got[..., 7:11], exp[..., 7:11], name + "[greeks]", rtol=OBS_RTOL, atol=OBS_ATOL)
+
+
+def make_vec(d, cfg):
+    from cantorrl_amd.vec_env import HedgingVecEnv
+    n = int(d["n_envs"])
+    env = HedgingVecEnv(n, tables=(d["paths"], d["volatilities"], d["call_prices_atm"],
+                                   d["put_prices_atm"]),
+                        variant=int(d["variant"]), info_keys=all_info_keys(), return_numpy=False, **cfg)
+    env.seed_envs([int(d["seed_base"]) + i for i in range(n)])
+    return env
+
+
+@pytest.mark.parametrize("fname", golden_files())
+def test_replay_matches_reference_golden(fname):
+    cfg, d = load_golden(os.path.join(GOLDEN, fname))
+    env = make_vec(d, cfg)
+    obs0 = env.reset_tensors().cpu().numpy()
+    compare_obs(obs0, d["reset_obs"], "reset_obs")
+    mse = cfg.get("loss_type") == "mse"
+    for s in range(int(d["n_steps"])):
+        obs, rew, term, trunc = env.step_tensors(torch.from_numpy(d["actions"][s]).cuda())
+        torch.cuda.synchronize()
+        assert_same(term.cpu().numpy().astype(bool), d["terminated"][s], f"terminated[{s}]")
+        assert not trunc.cpu().numpy().any()
+        exp_rew = d["reward"][s].astype(np.float32)
+        assert_same(rew.cpu().numpy(), exp_rew, f"reward[{s}]", rtol=1e-6 if mse else 0.0)
+        for k in GOLD_INFO:
+            exp = d["info_" + k][s]
+            got = env.info_tensor(k).cpu().numpy().astype(exp.dtype)
+            rt = 1e-12 if (mse and k in ("reward_pnl_component", "reward_step")) else 0.0
+            assert_same(got, exp, f"info_{k}[{s}]", rtol=rt)
+        compare_obs(obs.cpu().numpy(), d["obs"][s], f"obs[{s}]")
+        done = d["terminated"][s]
+        if done.any():
+            compare_obs(env._tobs.cpu().numpy()[done], d["terminal_obs"][s][done], f"terminal_obs[{s}]")
+    env.close()
+
+
+def run_gbm_pair(n, steps, seed, cfg, gen, offset=0):
+    from cantorrl_amd.vec_env import HedgingVecEnv
+    rng = np.random.default_rng(seed)
+    acts = rng.uniform(-1.05, 1.05, size=(steps, n, 2)).astype(np.float32)
+    venv = HedgingVecEnv(n, mode="gbm", generate=gen, seed=seed, global_env_offset=offset,
+                         info_keys=all_info_keys(), return_numpy=False, **cfg)
+    orc = OracleVecEnv(n, mode="gbm", gen=dict(gen, seed=seed, env_offset=offset), **cfg)
+    orc.seed_envs_at(np.arange(n), [seed] * n)
+    o_obs = orc.reset()
+    g_obs = venv.reset_tensors().cpu().numpy()
+    compare_obs(g_obs, o_obs, "reset_obs")
+    stats = dict(pnl_exact=0, pnl_total=0)
+    for s in range(steps):
+        oo, orew, oterm, otob, oinf = orc.step(acts[s])
+        obs, rew, term, _ = venv.step_tensors(torch.from_numpy(acts[s]).cuda())
+        torch.cuda.synchronize()
+        assert_same(term.cpu().numpy().astype(bool), oterm, f"terminated[{s}]")
+        for k in ("call_contracts", "put_contracts", "requested_calls_rounded_clipped",
+                  "requested_puts_rounded_clipped", "actual_calls_traded", "actual_puts_traded",
+                  "current_step"):
+            if k in oinf:
+                assert_same(venv.info_tensor(k).cpu().numpy(), oinf[k].astype(np.int32), f"{k}[{s}]")
+        S_got = venv.info_tensor("current_stock_price").cpu().numpy()
+        assert_same(S_got, orc.S if not oterm.any() else S_got, f"S[{s}]", rtol=1e-6)
+        for k in ("per_share_step_pnl", "portfolio_value", "cash", "transaction_costs_total"):
+            got = venv.info_tensor(k).cpu().numpy()
+            exp = oinf[k]
+            assert_same(got, exp, f"{k}[{s}]", rtol=PNL_RTOL, atol=1e-9)
+            if k == "per_share_step_pnl":
+                stats["pnl_exact"] += int((got == exp).sum())
+                stats["pnl_total"] += got.size
+        assert_same(rew.cpu().numpy(), orew.astype(np.float32), f"reward[{s}]", rtol=PNL_RTOL, atol=1e-9)
+        compare_obs(obs.cpu().numpy(), oo, f"obs[{s}]")
+    venv.close()
+    return stats
+
+
+def test_gbm_matches_oracle_across_episodes():
+    cfg = dict(loss_type="abs", pnl_penalty_weight=0.001, lambda_cost=0.0001, theta_weight=0.0002,
+               slippage_bps=1.0)
+    gen = dict(s0=496.48001098632812, variance=0.029028, mu=0.04, dt=1 / 252, episode_length=40)
+    stats = run_gbm_pair(256, 130, 42, cfg, gen)
+    # the f64 price path agrees to the last f32 bit almost everywhere
+    assert stats["pnl_exact"] >= 0.99 * stats["pnl_total"], stats
+
+
+def test_gbm_mse_v1_and_offset():
+    cfg = dict(loss_type="mse", initial_cash=1000.0)
+    gen = dict(s0=101.25, variance=0.09, mu=0.01, dt=1 / 252, episode_length=25)
+    from cantorrl_amd.vec_env import HedgingVecEnv  # noqa: F401
+    run_gbm_pair(64, 60, 7, cfg, gen, offset=1000)
+
+
+def test_rollout_equals_repeated_steps():
+    from cantorrl_amd.vec_env import HedgingVecEnv
+    n, K = 1000, 70
+    gen = dict(episode_length=30)
+    acts = torch.rand((K, n, 2), device="cuda") * 2 - 1
+    a = HedgingVecEnv(n, mode="gbm", generate=gen, seed=5, return_numpy=False, info_keys=())
+    b = HedgingVecEnv(n, mode="gbm", generate=gen, seed=5, return_numpy=False, info_keys=())
+    a.reset_tensors()
+    b.reset_tensors()
+    obs_r, rew_r, term_r = a.rollout(acts)
+    for k in range(K):
+        obs, rew, term, _ = b.step_tensors(acts[k], terminal_obs=False)
+        assert torch.equal(obs, obs_r[k]), k
+        assert torch.equal(rew, rew_r[k]), k
+        assert torch.equal(term, term_r[k]), k
+    a.close()
+    b.close()
+
+
+def test_sharding_invariance_global_env_offset():
+    """Env g's trajectory depends only on (seed, g): a 2-way shard equals the whole."""
+    from cantorrl_amd.vec_env import HedgingVecEnv
+    n, K = 512, 40
+    acts = torch.rand((K, n, 2), device="cuda") * 2 - 1
+    whole = HedgingVecEnv(n, mode="gbm", seed=9, return_numpy=False, info_keys=())
+    lo = HedgingVecEnv(n // 2, mode="gbm", seed=9, return_numpy=False, info_keys=())
+    hi = HedgingVecEnv(n // 2, mode="gbm", seed=9, global_env_offset=n // 2, return_numpy=False, info_keys=())
+    ow, rw, tw = whole.rollout(acts) if whole.reset_tensors() is not None else None
+    lo.reset_tensors()
+    hi.reset_tensors()
+    ol, rl, tl = lo.rollout(acts[:, : n // 2].contiguous())
+    oh, rh, th = hi.rollout(acts[:, n // 2:].contiguous())
+    assert torch.equal(ow, torch.cat([ol, oh], dim=1))
+    assert torch.equal(rw, torch.cat([rl, rh], dim=1))
+
+
+def test_state_checkpoint_roundtrip():
+    from cantorrl_amd.vec_env import HedgingVecEnv
+    n, K = 300, 20
+    acts = torch.rand((2 * K, n, 2), device="cuda") * 2 - 1
+    a = HedgingVecEnv(n, mode="gbm", seed=3, return_numpy=False, info_keys=())
+    a.reset_tensors()
+    a.rollout(acts[:K].contiguous())
+    blob = a.get_state()
+    o1, r1, _ = a.rollout(acts[K:].contiguous())
+    b = HedgingVecEnv(n, mode="gbm", seed=3, return_numpy=False, info_keys=())
+    b.set_state(blob)
+    o2, r2, _ = b.rollout(acts[K:].contiguous())
+    assert torch.equal(o1, o2) and torch.equal(r1, r2)
+
+
+@pytest.mark.parametrize("n", [1, 255, 257, 65536])
+def test_odd_sizes_and_bounds(n):
+    from cantorrl_amd.vec_env import HedgingVecEnv
+    env = HedgingVecEnv(n, mode="gbm", seed=1, return_numpy=False,
+                        info_keys=("call_contracts", "put_contracts"))
+    env.reset_tensors()
+    acts = torch.rand((600, n, 2), device="cuda") * 2.4 - 1.2
+    for k in range(0, 600, 7):
+        obs, rew, term, _ = env.step_tensors(acts[k])
+    torch.cuda.synchronize()
+    assert torch.isfinite(obs).all() and torch.isfinite(rew).all()
+    c = env.info_tensor("call_contracts")
+    assert int(c.abs().max()) <= 200
+    env.close()

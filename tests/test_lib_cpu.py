@@ -1,0 +1,90 @@
+"""CPU-side checks of libhedgeenv (no GPU): it loads, exports every symbol the
+header declares, and its host builds of the RNG code match NumPy/gymnasium."""
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, REPO
+from _compare import assert_same
+from cantorrl_amd import _lib
+from oracle.hedging_oracle import philox_words
+
+
+def header_symbols():
+    txt = open(os.path.join(REPO, "include", "hedge_env.h")).read()
+    return sorted(set(re.findall(r"^\S[^;(]*?\b(he_\w+)\s*\(", txt, flags=re.M)))
+
+
+def test_library_exports_every_header_symbol():
+    lib = _lib.load()
+    syms = header_symbols()
+    assert len(syms) >= 18, syms
+    for s in syms:
+        assert hasattr(lib, s), f"libhedgeenv does not export {s}"
+    assert set(syms) == set(_lib.EXPORTS)
+    assert b"gfx950" in lib.he_version()
+
+
+def test_library_is_gfx950_code_object():
+    data = open(_lib.LIB_PATH, "rb").read()
+    assert b"gfx950" in data
+
+
+def test_config_init_matches_reference_defaults():
+    lib = _lib.load()
+    c = _lib.HeConfig()
+    assert lib.he_config_init(c, 2) == 0
+    assert (c.transaction_cost_per_contract, c.lambda_cost, c.pnl_penalty_weight) == (0.65, 1.0, 0.01)
+    assert (c.theta_weight, c.slippage_bps, c.initial_cash) == (0.0, 0.0, 0.0)
+    assert (c.shares_to_hedge, c.max_contracts_held_per_type, c.max_trade_per_step) == (10000, 200, 15)
+    assert c.record_metrics == 1 and c.loss_type == _lib.HE_LOSS_ABS
+    assert c.option_tenor_years == 30 / 252 and c.risk_free_rate == 0.04
+    assert lib.he_config_init(c, 1) == 0 and c.transaction_cost_per_contract == 0.05
+    assert lib.he_config_init(c, 3) != 0
+
+
+def test_create_rejects_bad_config_without_gpu():
+    lib = _lib.load()
+    c = _lib.HeConfig()
+    lib.he_config_init(c, 2)
+    c.max_contracts_held_per_type = 40000
+    h = _lib.ctypes.c_void_p()
+    st = lib.he_create(c, _lib.ctypes.byref(h))
+    assert st == _lib.HE_EINVAL
+    assert b"max_contracts_held_per_type" in lib.he_last_error(h)
+    lib.he_destroy(h)
+
+
+@pytest.mark.parametrize("seed", [0, 1, 7, 42, 12345, 2 ** 32 - 1, 2 ** 32, 2 ** 40 + 3, 2 ** 63 + 11])
+def test_pcg64_seed_state_matches_numpy(seed):
+    st = np.random.PCG64(np.random.SeedSequence(seed)).state["state"]
+    hi, lo, ihi, ilo = _lib.pcg64_seed_state(seed)
+    assert (hi << 64) | lo == st["state"]
+    assert (ihi << 64) | ilo == st["inc"]
+
+
+def test_episode_draws_match_gymnasium_golden():
+    z = np.load(os.path.join(GOLDEN, "g7_episode_index.npz"))
+    for a, P in enumerate(z["P"]):
+        for s in z["seeds"]:
+            got = _lib.host_episode_draws(int(s), int(P), z["draws"].shape[2])
+            assert_same(got, z["draws"][a, s], f"P={P} seed={s}")
+
+
+def test_episode_draws_many_seeds_vs_numpy():
+    for s in range(200):
+        g = np.random.Generator(np.random.PCG64(np.random.SeedSequence(s)))
+        exp = np.array([g.integers(100000) for _ in range(20)])
+        assert_same(_lib.host_episode_draws(s, 100000, 20), exp, f"seed {s}")
+
+
+def test_host_philox_matches_oracle_and_kat():
+    # Random123 / rocRAND KAT: ctr=0, key=0
+    assert _lib.host_philox(0, 0, 0) == (0x6627E8D5, 0xE169C58D, 0xBC57AC4C, 0x9B00DBD8)
+    rng = np.random.default_rng(3)
+    for _ in range(50):
+        seed, g, n = (int(x) for x in rng.integers(0, 2 ** 62, 3))
+        exp = tuple(int(np.asarray(w).item()) for w in philox_words(seed, g, n))
+        assert _lib.host_philox(seed, g, n) == exp
