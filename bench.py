@@ -1,0 +1,262 @@
+#!/usr/bin/env python3
+"""Headline benchmark: env-steps/s of the batched hedging env on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--envs E] [--mode graph|eager|rollout]
+
+Workload = BASELINE.json configs[1]: 65,536 parallel envs per GPU, GBM price
+advance (Philox4x32-10 normals), Black-Scholes rolling-ATM marks, v2 env with
+the train_ppo_v2.py reward settings (abs loss, w=1e-3, lambda=1e-4,
+theta=2e-4, 1 bp slippage).  One "step" = one env-step of every env: actions
+[N,2] in (pre-generated, HBM-resident), obs [N,13] / reward [N] / done flags
+out, auto-reset inside the kernel.
+
+Modes: `graph` (default) replays he_step launches captured into a hipGraph,
+one kernel per step; `eager` calls he_step from Python every step; `rollout`
+fuses 64 steps per launch (he_rollout).  For N>1 the script runs under
+torch.distributed.run, one rank per GPU (weak scaling: E envs per rank, env
+ids offset by rank), and all-gathers per-env rewards over RCCL every 256 steps
+(the rollout-buffer boundary of train_ppo_v2.py:48).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+# algorithmic HBM bytes per env-step of step_kernel<GBM> (DESIGN.md "Roofline"):
+#   reads : action 8 + state (S 8, C 4, P 4, cash 8, t 4, pos 4, ep 4) 36        = 44
+#   writes: state (S 8, C 4, P 4, cash 8, t 4, pos 4) 32 + obs 52 + reward 4
+#           + terminated 1 + truncated 1                                          = 90
+STEP_BYTES_PER_ENV = 134
+# he_rollout per env-step: action 8 + obs 52 + reward 4 + terminated 1 (+ state / K)
+ROLLOUT_BYTES_PER_ENV = 65
+ROLLOUT_STATE_BYTES = 36 + 32
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+TRAIN_KW = dict(loss_type="abs", pnl_penalty_weight=0.001, lambda_cost=0.0001, theta_weight=0.0002,
+                slippage_bps=1.0)  # train_ppo_v2.py:74-80
+GEN = dict(s0=496.48001098632812, variance=0.029028, mu=0.04, dt=1 / 252, episode_length=252)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2520)
+    ap.add_argument("--warmup", type=int, default=256)
+    ap.add_argument("--envs", type=int, default=65536, help="envs per GPU")
+    ap.add_argument("--mode", choices=["graph", "eager", "rollout"], default="graph")
+    ap.add_argument("--graph-chunk", type=int, default=64)
+    ap.add_argument("--rollout-k", type=int, default=64)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--seed", type=int, default=42)
+    return ap.parse_args()
+
+
+def cpu_baseline(seconds):
+    """The oracle (NumPy restatement of the reference env) on host cores, N=256."""
+    from oracle.hedging_oracle import OracleVecEnv
+    n = 256
+    env = OracleVecEnv(n, mode="gbm", gen=dict(GEN, seed=42), **TRAIN_KW)
+    env.seed_envs_at(np.arange(n), [42] * n)
+    env.reset()
+    rng = np.random.default_rng(0)
+    acts = rng.uniform(-1, 1, size=(64, n, 2)).astype(np.float32)
+    for k in range(8):
+        env.step(acts[k])
+    steps = 0
+    t0 = time.perf_counter()
+    while True:
+        env.step(acts[steps % 64])
+        steps += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return dict(value=n * steps / el, unit="env-steps/s", cores=1, kind="port",
+                sample=f"oracle/hedging_oracle.py OracleVecEnv GBM, 256 envs x {steps} steps "
+                       f"({el:.1f} s, 1 thread, NumPy)")
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+
+    from cantorrl_amd.vec_env import HedgingVecEnv
+    n = args.envs
+    env = HedgingVecEnv(n, mode="gbm", generate=GEN, seed=args.seed, global_env_offset=rank * n,
+                        device=dev, return_numpy=False, info_keys=(), **TRAIN_KW)
+    env.reset_tensors()
+    ring = 256
+    g = torch.Generator(device=dev)
+    g.manual_seed(1234 + rank)
+    acts = torch.rand((ring, n, 2), device=dev, generator=g) * 2 - 1
+    stream = torch.cuda.Stream(device=dev)
+    gathered = torch.empty((world, n), dtype=torch.float32, device=dev) if world > 1 else None
+
+    lib = env.lib
+    h = env._h
+    obs, rew, term, trunc, tobs = env._obs, env._rew, env._term, env._trunc, env._tobs
+
+    def launch(k, s):
+        st = lib.he_step(h, acts[k % ring].data_ptr(), obs.data_ptr(), rew.data_ptr(), term.data_ptr(),
+                         trunc.data_ptr(), tobs.data_ptr(), None, s)
+        if st:
+            raise RuntimeError(lib.he_last_error(h).decode())
+
+    K = args.steps
+    W = args.warmup
+    graphs = []
+    if args.mode == "graph":
+        C = args.graph_chunk
+        # capture `ring // C` graphs of C steps each, covering the whole action ring
+        with torch.cuda.stream(stream):
+            for gi in range(ring // C):
+                gr = torch.cuda.CUDAGraph()
+                torch.cuda.synchronize()
+                with torch.cuda.graph(gr, stream=stream):
+                    cs = torch.cuda.current_stream().cuda_stream
+                    for j in range(C):
+                        launch(gi * C + j, cs)
+                graphs.append(gr)
+        env.reset_tensors()
+
+    roll_obs = roll_rew = roll_term = None
+    if args.mode == "rollout":
+        RK = args.rollout_k
+        roll_obs = torch.empty((RK, n, 13), dtype=torch.float32, device=dev)
+        roll_rew = torch.empty((RK, n), dtype=torch.float32, device=dev)
+        roll_term = torch.empty((RK, n), dtype=torch.uint8, device=dev)
+
+    def run(steps, s):
+        """Enqueue `steps` env-steps on stream s."""
+        done = 0
+        cs = s.cuda_stream
+        while done < steps:
+            if args.mode == "graph":
+                C = args.graph_chunk
+                gi = (done // C) % len(graphs)
+                if steps - done >= C:
+                    graphs[gi].replay()
+                    done += C
+                else:
+                    launch(done, cs)
+                    done += 1
+            elif args.mode == "eager":
+                launch(done, cs)
+                done += 1
+            else:
+                RK = min(args.rollout_k, steps - done)
+                a0 = (done % ring)
+                a = acts[a0:a0 + RK] if a0 + RK <= ring else acts[:RK]
+                st = lib.he_rollout(h, RK, a.data_ptr(), roll_obs.data_ptr(), roll_rew.data_ptr(),
+                                    roll_term.data_ptr(), cs)
+                if st:
+                    raise RuntimeError(lib.he_last_error(h).decode())
+                done += RK
+            if dist is not None and done % 256 == 0:
+                dist.all_gather_into_tensor(gathered, rew)
+
+    with torch.cuda.stream(stream):
+        run(W, stream)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    with torch.cuda.stream(stream):
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev1 = torch.cuda.Event(enable_timing=True)
+        ev0.record(stream)
+        run(K, stream)
+        ev1.record(stream)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    t = torch.tensor([wall], dtype=torch.float64, device=dev)
+    if dist is not None:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    wall = float(t.item())
+    dev_ms = ev0.elapsed_time(ev1)
+
+    # live per-launch kernel duration: HIP events bracketing single launches on `stream`
+    nprobe = 200
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(nprobe)]
+    torch.cuda.synchronize()
+    with torch.cuda.stream(stream):
+        for k in range(nprobe):
+            evs[k][0].record(stream)
+            if args.mode == "rollout":
+                RK = args.rollout_k
+                lib.he_rollout(h, RK, acts[:RK].data_ptr(), roll_obs.data_ptr(), roll_rew.data_ptr(),
+                               roll_term.data_ptr(), stream.cuda_stream)
+            else:
+                launch(k, stream.cuda_stream)
+            evs[k][1].record(stream)
+    torch.cuda.synchronize()
+    durs = np.array([a.elapsed_time(b) for a, b in evs[20:]])  # ms
+    kern_ms = float(np.median(durs))
+
+    total_envs = n * world
+    value = total_envs * K / wall
+    if args.mode == "rollout":
+        RK = args.rollout_k
+        bytes_launch = n * RK * (ROLLOUT_BYTES_PER_ENV + ROLLOUT_STATE_BYTES / RK)
+        kname = "step_kernel<GBM> (K=%d fused)" % RK
+    else:
+        bytes_launch = n * STEP_BYTES_PER_ENV
+        kname = "step_kernel<GBM> (K=1)"
+    achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
+    roof = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
+                frac=round(achieved / HBM_PEAK_GBS, 4), traffic=None, kernel=kname,
+                kernel_us=round(kern_ms * 1e3, 3), bytes_per_launch=int(bytes_launch))
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args.cpu_seconds)
+    if rank == 0:
+        line = {
+            "metric": "env-steps/sec (batched episodes)",
+            "value": round(value, 1),
+            "unit": "env-steps/s",
+            "n_gpus": world,
+            "steps": K,
+            "warmup": W,
+            "ms_per_step": round(wall * 1e3 / K, 6),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64+f32",
+            "data": "synthetic (GBM paths from Philox4x32-10, U(-1,1) actions pre-generated on device)",
+            "config": {"workload": "configs[1]: 65,536 parallel envs/GPU, European call (BS rolling-ATM marks), "
+                                   "GBM fp32 env view, v2 env, train_ppo_v2 reward", "envs_per_gpu": n,
+                       "episode_length": GEN["episode_length"], "mode": args.mode,
+                       "parallelism": f"env-shard x{world}"},
+            "device_ms_per_step": round(dev_ms / K, 6),
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    env.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
