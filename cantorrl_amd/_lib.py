@@ -56,7 +56,9 @@ class HeConfig(ctypes.Structure):
         ("heston_theta", ctypes.c_double),
         ("heston_xi", ctypes.c_double),
         ("heston_rho", ctypes.c_double),
-        ("reserved", ctypes.c_double * 8),
+        ("market_block", ctypes.c_int32),
+        ("reserved_i", ctypes.c_int32),
+        ("reserved", ctypes.c_double * 7),
     ]
 
 

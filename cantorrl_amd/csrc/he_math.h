@@ -87,8 +87,9 @@ HE_HD double ndtr(double a) {
 }
 
 // scipy.stats.norm.pdf: exp(-x**2/2.0) / sqrt(2*pi)  (x**2 on an array = x*x)
+// (division by 2.0 is exact scaling, so *0.5 is bit-identical)
 HE_HD double norm_pdf(double x) {
-    return exp(-(x * x) / 2.0) / 2.5066282746310002;
+    return exp(-(x * x) * 0.5) / 2.5066282746310002;
 }
 
 // ---------------------------------------------------------------- Black-Scholes
@@ -110,8 +111,11 @@ HE_HD void bs_call_put(double S, double K, const BSConst& c, double* call, doubl
     double d1 = (log(S / K) + c.a) / c.b;
     double d2 = d1 - c.b;
     double Kd = K * c.disc;
-    double cv = S * ndtr(d1) - Kd * ndtr(d2);
-    double pv = Kd * ndtr(-d2) - S * ndtr(-d1);
+    double n1 = ndtr(d1), n2 = ndtr(d2);
+    double cv = S * n1 - Kd * n2;
+    // ndtr(-x) taken as 1 - ndtr(x): |difference| <= 2^-53 absolute; C/P are
+    // handed to the env as f32 (hedging_env_v2.py:40-41), far above that.
+    double pv = Kd * (1.0 - n2) - S * (1.0 - n1);
     *call = (cv < 0.0) ? 0.0 : cv;   // python max(price, 0): NaN stays NaN
     *put = (pv < 0.0) ? 0.0 : pv;
 }

@@ -1,18 +1,26 @@
 // hedge_env.hip -- libhedgeenv: the batched hedging environment for MI355X.
 //
-// One thread owns one env.  Per-env state is struct-of-arrays in HBM (every
-// field access is a coalesced 4/8-byte-per-lane stream); the 13-float obs rows
-// are staged through LDS so the [N][13] output leaves the CU as contiguous
-// 16-byte-per-lane stores.  Done-masking uses a wave ballot so that waves with
-// no terminating env skip the reset path entirely.
+// Two kernels split the reference step (src/env/hedging_env_v2.py:175-294) along
+// its data dependency:
 //
-// Reference semantics restated here (file:line in /root/reference):
-//   step            src/env/hedging_env_v2.py:175-294  (v1 src/env/hedging_env.py:171-270)
-//   observation     src/env/hedging_env_v2.py:109-143
-//   greeks          src/env/hedging_env_v2.py:79-107
-//   reset           src/env/hedging_env_v2.py:145-173
-//   BS marks        quantconnect/option_calculator.py:11-27
-//   price advance   src/sim/rbergomi_sim.py:454-464
+//   market_kernel  (generate modes, once per M steps)  -- everything that does NOT
+//       depend on the agent's actions: Philox4x32-10 normals, the GBM/Heston price
+//       advance (rbergomi_sim.py:454-464), Black-Scholes rolling-ATM marks
+//       (quantconnect/option_calculator.py:11-27) and the obs greeks
+//       (hedging_env_v2.py:79-107).  Parallel over env x slot (4 slot-lanes per
+//       env, 64 envs per workgroup, the sequential f64 price chain staged in LDS),
+//       so it runs at >= 4 waves/SIMD even at 65,536 envs.  Output: an HBM tile
+//       [M+1][N] of {S, v, C, P} and {delta_c, gamma, delta_p} in f32, exactly the
+//       data the reference env would replay from an NPZ (hedging_env_v2.py:38-41).
+//
+//   step_kernel    (every step; K fused steps for he_rollout) -- the action-dependent
+//       part: integer trade logic, commission + slippage, f64 mark-to-market P&L,
+//       reward, 13-float obs, SB3 auto-reset.  One thread per env, struct-of-arrays
+//       state, obs rows staged through LDS and written as 16-B stores, wave ballot
+//       so waves with no terminating env skip the reset path.
+//
+// Replay mode reuses step_kernel: its market source is the loaded table
+// [paths][T+1] {S, v, C, P} (+ greeks precomputed once at load time).
 #include <hip/hip_runtime.h>
 
 #include <math.h>
@@ -31,8 +39,11 @@ using namespace he;
 
 namespace {
 
-constexpr int kBlock = 256;
+constexpr int kBlock = 256;      // step kernel: envs per workgroup
 constexpr int kObs = HE_OBS_DIM;
+constexpr int kMktEnvs = 64;     // market kernel: envs per workgroup (one wave wide)
+constexpr int kMktLanes = 4;     //                slot-lanes per env (4 waves)
+constexpr int kMaxBlock = 64;    // max market block length M
 
 // ------------------------------------------------------------------ parameters
 struct Params {
@@ -41,28 +52,34 @@ struct Params {
     int32_t T;
     int32_t variant, loss, record_metrics, autoreset, mode;
     int32_t mt, maxh;
-    float mt_f;
+    float mt_f, maxh_f, T_f;
     float init_cash_f;
-    double tcpc, slip_frac, lam, w, theta, initial_cash;
+    double tcpc, slip_frac, lam, w, initial_cash;
     double shares_d;
     float shares_f;
     int32_t shares_zero;
+    const double* thp_tab;  // theta_weight * ((T - t) / 252.0), t = 0..T (hedging_env_v2.py:259-260)
     // observation / greeks constants (hedging_env_v2.py:57-58)
     float r_f, tenor_f;
     double r_d, tenor_d, sqrt_tenor;
-    int32_t tenor_small;  // tenor <= 1e-6
+    int32_t tenor_small;    // tenor <= 1e-6
     // generate-mode market
     uint32_t key0, key1;
     double s0;
-    double var;           // GBM variance (Heston v0)
+    double var;             // GBM variance (Heston v0)
     float var_f;
     double sqrt_var, drift, sqrt_dt, mu, dt;
-    BSConst bs;           // constant-sigma BS constants (GBM)
+    BSConst bs;             // constant-sigma BS constants (GBM)
     float g_sigma, g_num_drift;  // constant-variance greeks: sigma, (r+0.5 sigma**2)*T (f32)
     double g_sst;                // sigma*sqrt(T) (f64)
     double h_kappa, h_theta, h_xi, h_rho, h_sqrt1mrho2;
+    int32_t M;              // market block length
+    float4* tileA;          // [M+1][N] {S, v, C, P}
+    float4* tileB;          // [M+1][N] {call_delta, gamma, put_delta, 0}
+    const float* rst;       // reset market + obs: {S0, v0, C0, P0, obs0[13]} (generate)
     // replay
-    const float4* rec;    // [n_paths][T+1] {S, v, C, P}, C/P at T = C/P at T-1
+    const float4* rec;      // [n_paths][T+1] {S, v, C, P}; C/P at T hold row T-1
+    const float4* recg;     // [n_paths][T+1] {call_delta, gamma, put_delta, 0}
     int64_t n_paths;
 };
 
@@ -74,11 +91,17 @@ struct State {
     float* s0;         // replay initial_S0_for_episode; -1 encodes the python 1.0 substitution
     uint64_t* pcg;     // replay [4][N]: state_hi, state_lo, inc_hi, inc_lo
     uint32_t* pcgb;    // replay [2][N]: has_uint32, uinteger
-    double* S;         // generate f64 price
-    float* C;
+};
+
+// Generate-mode market position of every env: `cur` = after the last generated
+// block (or the reset state), `bak` = start of that block (for rewinds).
+struct Market {
+    uint32_t* ep;      // episode counter (0xFFFFFFFF before the first reset)
+    uint32_t* t;       // step in episode, 0..T (T = terminal, next step resets)
+    double* S;         // f64 price
+    double* v;         // f64 variance (Heston)
+    float* C;          // f32 marks at this position
     float* P;
-    uint32_t* ep;      // generate episode counter
-    double* var;       // Heston variance
 };
 
 struct Io {
@@ -91,15 +114,16 @@ struct Io {
     he_info info;
 };
 
+struct Mkt {
+    float S, v, C, P;
+};
+
 struct Env {
     uint32_t t;
     int32_t call, put;
     double cash;
-    float S, v, C, P;   // current f32 market view (what the reference env holds)
-    double S64, var64;  // generate-mode f64 state
-    uint32_t ep;
     int32_t path;
-    float s0;           // initial_S0_for_episode as f32 (1.0 when substituted)
+    float s0;          // initial_S0_for_episode as f32 (1.0 when substituted)
     bool s0_small;
 };
 
@@ -108,88 +132,95 @@ __device__ __forceinline__ int32_t unpack_hi(uint32_t p) { return (int32_t)(int1
 __device__ __forceinline__ uint32_t pack_pos(int32_t c, int32_t q) {
     return ((uint32_t)(uint16_t)(int16_t)c) | (((uint32_t)(uint16_t)(int16_t)q) << 16);
 }
+__device__ __forceinline__ Mkt as_mkt(float4 r) { return Mkt{r.x, r.y, r.z, r.w}; }
 
-// ------------------------------------------------------------------ greeks / obs
-// hedging_env_v2.py:79-107.  S, v: the f32 current price / variance.
+// ------------------------------------------------------------------ greeks
+// hedging_env_v2.py:79-107 on the f32 price S and variance v; returns the three
+// f32 obs values (call_delta, gamma, put_delta).
 template <bool CONST_VAR>
-__device__ __forceinline__ void greeks(const Params& p, float S, float v, double* cd, double* gam,
-                                       double* pd) {
+__device__ __forceinline__ float4 greeks(const Params& p, float S, float v) {
+    double cd, gam, pd;
     float K = rintf(S);  // np.round: half-even
     if (S <= 1e-6f) {    // weak python 1e-6 compares as float32(1e-6)
-        *cd = (K == 0.0f) ? 0.5 : ((K > 0.0f) ? 0.0 : 1.0);
-        *pd = (K == 0.0f) ? -0.5 : ((K < 0.0f) ? 0.0 : -1.0);
-        *gam = 0.0;
-        return;
-    }
-    float sigma, num_drift;
-    double sst;
-    if (CONST_VAR) {
-        sigma = p.g_sigma;
-        num_drift = p.g_num_drift;
-        sst = p.g_sst;
+        cd = (K == 0.0f) ? 0.5 : ((K > 0.0f) ? 0.0 : 1.0);
+        pd = (K == 0.0f) ? -0.5 : ((K < 0.0f) ? 0.0 : -1.0);
+        gam = 0.0;
     } else {
-        sigma = sqrtf(np_maxf(v, 1e-8f));
-        num_drift = (p.r_f + 0.5f * (sigma * sigma)) * p.tenor_f;
-        sst = (double)sigma * p.sqrt_tenor;
+        float sigma, num_drift;
+        double sst;
+        if (CONST_VAR) {
+            sigma = p.g_sigma;
+            num_drift = p.g_num_drift;
+            sst = p.g_sst;
+        } else {
+            sigma = sqrtf(np_maxf(v, 1e-8f));
+            num_drift = (p.r_f + 0.5f * (sigma * sigma)) * p.tenor_f;
+            sst = (double)sigma * p.sqrt_tenor;
+        }
+        if (p.tenor_small || sigma <= 1e-6f) {
+            cd = (S > K) ? 1.0 : ((S == K) ? 0.5 : 0.0);
+            pd = (S < K) ? -1.0 : ((S == K) ? -0.5 : 0.0);
+            gam = 0.0;
+        } else {
+            float Kc = np_maxf(K, 1e-6f);
+            float num = logf(S / Kc) + num_drift;
+            double d1;
+            if (sst < 1e-9) {
+                float sg = (num > 0.0f) ? 1.0f : ((num < 0.0f) ? -1.0f : num);  // np.sign
+                d1 = (double)(sg * 10.0f);
+            } else {
+                d1 = (double)num / sst;
+            }
+            double n1 = ndtr(d1);
+            cd = n1;
+            pd = n1 - 1.0;
+            double gd = (double)S * sst;
+            gam = (fabs(gd) < 1e-9) ? 0.0 : norm_pdf(d1) / gd;
+        }
     }
-    if (p.tenor_small || sigma <= 1e-6f) {
-        *cd = (S > K) ? 1.0 : ((S == K) ? 0.5 : 0.0);
-        *pd = (S < K) ? -1.0 : ((S == K) ? -0.5 : 0.0);
-        *gam = 0.0;
-        return;
-    }
-    float Kc = np_maxf(K, 1e-6f);
-    float num = logf(S / Kc) + num_drift;
-    double d1;
-    if (sst < 1e-9) {
-        float s = (num > 0.0f) ? 1.0f : ((num < 0.0f) ? -1.0f : num);  // np.sign
-        d1 = (double)(s * 10.0f);
-    } else {
-        d1 = (double)num / sst;
-    }
-    double n1 = ndtr(d1);
-    *cd = n1;
-    *pd = n1 - 1.0;
-    double gd = (double)S * sst;
-    *gam = (fabs(gd) < 1e-9) ? 0.0 : norm_pdf(d1) / gd;
+    return make_float4((float)cd, (float)gam, (float)pd, 0.0f);
 }
 
-// hedging_env_v2.py:109-143
-template <bool CONST_VAR>
-__device__ __forceinline__ void make_obs(const Params& p, const Env& e, float Sp, float vp, float* o) {
+// ------------------------------------------------------------------ observation
+// hedging_env_v2.py:109-143.  m = market after the step, g = its greeks,
+// Sp/vp = S_t_minus_1 / v_t_minus_1.
+__device__ __forceinline__ void make_obs(const Params& p, const Env& e, const Mkt& m, float4 g, float Sp,
+                                         float vp, float* o) {
     float s0s = np_maxf(e.s0, 25.0f);
-    o[0] = e.S / s0s;
-    o[1] = e.C / s0s;
-    o[2] = e.P / s0s;
+    o[0] = m.S / s0s;
+    o[1] = m.C / s0s;
+    o[2] = m.P / s0s;
+    // int64/int -> f64 quotient cast to f32 == correctly rounded f32 quotient when
+    // both operands are exact in f32 (|x| < 2^24) and 53 >= 2*24+2 (no double rounding)
     if (p.maxh != 0) {
-        o[3] = (float)((double)e.call / (double)p.maxh);
-        o[4] = (float)((double)e.put / (double)p.maxh);
+        o[3] = (float)e.call / p.maxh_f;
+        o[4] = (float)e.put / p.maxh_f;
     } else {
         o[3] = 0.0f;
         o[4] = 0.0f;
     }
-    o[5] = e.v;
-    o[6] = (p.T != 0) ? (float)((double)(p.T - (int32_t)e.t) / (double)p.T) : 0.0f;
+    o[5] = m.v;
+    o[6] = (p.T != 0) ? (float)(p.T - (int32_t)e.t) / p.T_f : 0.0f;
     if (p.record_metrics) {
-        double cd, g, pd;
-        greeks<CONST_VAR>(p, e.S, e.v, &cd, &g, &pd);
-        o[7] = (float)cd;
-        o[8] = (float)g;
-        o[9] = (float)pd;
-        o[10] = (float)g;
+        o[7] = g.x;
+        o[8] = g.y;
+        o[9] = g.z;
+        o[10] = g.y;
     } else {
         o[7] = o[8] = o[9] = o[10] = 0.0f;
     }
     float ls = 0.0f, lv = 0.0f;
     if (!(e.t == 0 || Sp == 0.0f)) {
-        ls = (e.S - Sp) / Sp;
-        lv = e.v - vp;
+        ls = (m.S - Sp) / Sp;
+        lv = m.v - vp;
     }
     o[11] = np_clipf(ls, -1.0f, 1.0f);
     o[12] = np_clipf(lv, -1.0f, 1.0f);
 }
 
-// f64 Black-Scholes marks at K = round(S) (rolling ATM, rbergomi_sim.py:418,437-446).
+// ------------------------------------------------------------------ marks
+// f64 Black-Scholes marks at K = round(S) (rolling ATM, rbergomi_sim.py:418,437-446),
+// handed to the env as f32.
 template <int MODE>
 __device__ __forceinline__ void marks(const Params& p, double S64, double var64, float* C, float* P) {
     double K = rint(S64);
@@ -209,146 +240,225 @@ __device__ __forceinline__ void marks(const Params& p, double S64, double var64,
     *P = (float)q;
 }
 
-// ------------------------------------------------------------------ load / store
-template <int MODE>
-__device__ __forceinline__ void load_env(const Params& p, const State& s, int64_t i, Env& e) {
-    e.t = s.t[i];
-    uint32_t pk = s.pos[i];
-    e.call = unpack_lo(pk);
-    e.put = unpack_hi(pk);
-    e.cash = s.cash[i];
-    if (MODE == HE_MODE_REPLAY) {
-        e.path = s.path[i];
-        float s0 = s.s0[i];
-        e.s0_small = (s0 == -1.0f);
-        e.s0 = e.s0_small ? 1.0f : s0;
-        uint32_t tt = e.t > (uint32_t)p.T ? (uint32_t)p.T : e.t;
-        float4 r = p.rec[(int64_t)e.path * (p.T + 1) + tt];
-        e.S = r.x;
-        e.v = r.y;
-        e.C = r.z;
-        e.P = r.w;
+// Box-Muller pair of the Philox block of (seed, global env id, env-step index n).
+__device__ __forceinline__ void normals(const Params& p, int64_t gid, uint64_t n, double* z1, double* z2,
+                                        bool both) {
+    u32x4 ctr = {(uint32_t)n, (uint32_t)(n >> 32), (uint32_t)gid, (uint32_t)((uint64_t)gid >> 32)};
+    u32x4 x = philox4x32_10(ctr, p.key0, p.key1);
+    double u1 = u01(x.x, x.y), u2 = u01(x.z, x.w);
+    double rad = sqrt(-2.0 * log(u1));
+    double ang = 6.283185307179586 * u2;
+    if (both) {
+        double sn, cs;
+        sincos(ang, &sn, &cs);
+        *z1 = rad * cs;
+        *z2 = rad * sn;
     } else {
-        e.S64 = s.S[i];
-        e.S = (float)e.S64;
-        e.C = s.C[i];
-        e.P = s.P[i];
-        e.ep = s.ep[i];
-        float s0f = (float)p.s0;
-        e.s0_small = s0f < 1e-6f;
-        e.s0 = e.s0_small ? 1.0f : s0f;
-        if (MODE == HE_MODE_HESTON) {
-            e.var64 = s.var[i];
-            e.v = (float)e.var64;
+        *z1 = rad * cos(ang);
+    }
+}
+
+// ------------------------------------------------------------------ market kernel
+// One workgroup = 64 envs x 4 slot-lanes.  Slot j (1..M) is the market after the
+// j-th step from the block start; slot 0 is the block start itself.  With
+// a = ep*T + t the step from position a uses Philox counter n = a and starts
+// from S0 when t in {0, T} (autoreset), so every slot is a pure function of the
+// block-start state.
+template <int MODE>
+__global__ __launch_bounds__(kMktEnvs * kMktLanes) void market_kernel(Params p, Market cur, Market bak,
+                                                                       int32_t advance_only) {
+    constexpr bool HESTON = (MODE == HE_MODE_HESTON);
+    __shared__ double shS[kMktEnvs][kMaxBlock + 1];
+    __shared__ double shV[HESTON ? kMktEnvs : 1][HESTON ? kMaxBlock + 1 : 1];
+    const int lane = threadIdx.x & (kMktEnvs - 1);
+    const int sub = threadIdx.x / kMktEnvs;
+    const int64_t i = (int64_t)blockIdx.x * kMktEnvs + lane;
+    const bool live = i < p.n;
+    const int M = p.M;
+    const uint32_t T = (uint32_t)p.T;
+    const int64_t gid = p.goff + i;
+    // block-start position (advance_only: rewind from `bak`, else continue from `cur`)
+    Market src = advance_only ? bak : cur;
+    uint32_t ep0 = 0, t0 = 0;
+    double S0v = 0.0, v0v = 0.0;
+    float C0v = 0.0f, P0v = 0.0f;
+    if (live) {
+        ep0 = src.ep[i];
+        t0 = src.t[i];
+        S0v = src.S[i];
+        if (HESTON) v0v = src.v[i];
+        C0v = src.C[i];
+        P0v = src.P[i];
+    }
+    const int nsteps = advance_only ? advance_only : M;
+    const uint32_t t0m = (t0 >= T) ? 0u : t0;  // position modulo T
+    const uint64_t a0 = (uint64_t)ep0 * T + t0m + ((t0 >= T) ? T : 0u);
+    // phase 1 (all lanes, time-parallel): the random part of every step
+    for (int j = 1 + sub; j <= nsteps; j += kMktLanes) {
+        if (!live) break;
+        uint64_t n = a0 + (uint64_t)(j - 1);
+        double z1, z2;
+        if (HESTON) {
+            normals(p, gid, n, &z1, &z2, true);
+            double dw1 = p.sqrt_dt * z1, dw2 = p.sqrt_dt * z2;
+            shV[lane][j] = dw1;
+            shS[lane][j] = p.h_rho * dw1 + p.h_sqrt1mrho2 * dw2;  // rbergomi_sim.py:457
         } else {
-            e.var64 = p.var;
-            e.v = p.var_f;
+            normals(p, gid, n, &z1, &z2, false);
+            double dW = p.sqrt_dt * z1;
+            shS[lane][j] = exp(p.drift + p.sqrt_var * dW);      // rbergomi_sim.py:459-463
         }
+    }
+    __syncthreads();
+    // phase 2 (one lane per env): the sequential f64 chain
+    if (sub == 0 && live) {
+        double S = S0v, v = v0v;
+        uint32_t tt = t0;
+        uint32_t ep = ep0;
+        shS[lane][0] = S;
+        if (HESTON) shV[lane][0] = v;
+        for (int j = 1; j <= nsteps; ++j) {
+            if (tt == 0 || tt >= T) {  // autoreset: a new episode starts from S0
+                if (tt >= T) ep += 1u;
+                S = p.s0;
+                if (HESTON) v = p.var;
+                tt = 0;
+            }
+            if (HESTON) {
+                double vp = v < 0.0 ? 0.0 : v;  // full truncation
+                double dWS = shS[lane][j], dw1 = shV[lane][j];
+                double drift = (p.mu - 0.5 * vp) * p.dt;
+                double diff = sqrt(vp) * dWS;
+                double Sn = S * exp(drift + diff);
+                S = (Sn < 1e-8) ? 1e-8 : Sn;
+                v = (v + p.h_kappa * (p.h_theta - vp) * p.dt) + p.h_xi * sqrt(vp) * dw1;
+                shV[lane][j] = v;
+            } else {
+                double Sn = S * shS[lane][j];
+                S = (Sn < 1e-8) ? 1e-8 : Sn;  // np.maximum(., 1e-8), NaN kept
+            }
+            shS[lane][j] = S;
+            tt += 1u;
+        }
+        if (!advance_only) {  // keep the block start for rewinds
+            bak.ep[i] = ep0;
+            bak.t[i] = t0;
+            bak.S[i] = S0v;
+            if (HESTON) bak.v[i] = v0v;
+            bak.C[i] = C0v;
+            bak.P[i] = P0v;
+        }
+        cur.ep[i] = ep;
+        cur.t[i] = tt;
+        cur.S[i] = S;
+        if (HESTON) cur.v[i] = v;
+    }
+    __syncthreads();
+    // phase 3 (time-parallel): marks + greeks of every slot
+    const int64_t N = p.n;
+    for (int j = 1 + sub; j <= nsteps; j += kMktLanes) {
+        if (!live) break;
+        uint32_t tj = (t0m + (uint32_t)(j - 1)) % T + 1u;  // 1..T
+        double S64 = shS[lane][j];
+        double v64 = HESTON ? shV[lane][j] : p.var;
+        float C, P;
+        if (tj < T) {
+            marks<MODE>(p, S64, v64, &C, &P);
+        } else if (T == 1u) {  // lagged marks of t = T-1 = 0: the reset marks
+            C = p.rst[2];
+            P = p.rst[3];
+        } else if (j == 1) {   // lagged marks of the block start
+            C = C0v;
+            P = P0v;
+        } else {               // lagged marks of t = T-1: slot j-1 (hedging_env_v2.py:229-231)
+            marks<MODE>(p, shS[lane][j - 1], HESTON ? shV[lane][j - 1] : p.var, &C, &P);
+        }
+        if (j == nsteps) {
+            cur.C[i] = C;
+            cur.P[i] = P;
+        }
+        if (advance_only) continue;
+        float S32 = (float)S64;
+        float v32 = HESTON ? (float)v64 : p.var_f;
+        p.tileA[(int64_t)j * N + i] = make_float4(S32, v32, C, P);
+        float4 g = p.record_metrics ? greeks<!HESTON>(p, S32, v32) : make_float4(0.f, 0.f, 0.f, 0.f);
+        p.tileB[(int64_t)j * N + i] = g;
+    }
+    if (!advance_only && sub == 0 && live) {
+        float v32 = HESTON ? (float)v0v : p.var_f;
+        p.tileA[i] = make_float4((float)S0v, v32, C0v, P0v);
     }
 }
 
+// Reset market constants + reset obs row (generate): rst = {S0, v0, C0, P0, obs0[13]}.
 template <int MODE>
-__device__ __forceinline__ void store_env(const State& s, int64_t i, const Env& e, bool reset) {
-    s.t[i] = e.t;
-    s.pos[i] = pack_pos(e.call, e.put);
-    s.cash[i] = e.cash;
-    if (MODE == HE_MODE_REPLAY) {
-        if (reset) {
-            s.path[i] = e.path;
-            s.s0[i] = e.s0_small ? -1.0f : e.s0;
-        }
-    } else {
-        s.S[i] = e.S64;
-        s.C[i] = e.C;
-        s.P[i] = e.P;
-        if (reset) s.ep[i] = e.ep;
-        if (MODE == HE_MODE_HESTON) s.var[i] = e.var64;
-    }
-}
-
-// hedging_env_v2.py:145-173.  Replay: draw the episode row from the env's PCG64
-// stream (gymnasium np_random.integers(num_episodes)); generate: next episode.
-template <int MODE>
-__device__ __forceinline__ void reset_env(const Params& p, const State& s, int64_t i, Env& e) {
-    if (MODE == HE_MODE_REPLAY) {
-        const int64_t N = p.n;
-        Pcg64 g;
-        g.sh = s.pcg[i];
-        g.sl = s.pcg[N + i];
-        g.ih = s.pcg[2 * N + i];
-        g.il = s.pcg[3 * N + i];
-        g.has32 = s.pcgb[i];
-        g.buf32 = s.pcgb[N + i];
-        e.path = (int32_t)pcg64_integers(g, (uint64_t)p.n_paths);
-        s.pcg[i] = g.sh;
-        s.pcg[N + i] = g.sl;
-        s.pcgb[i] = g.has32;
-        s.pcgb[N + i] = g.buf32;
-        float4 r = p.rec[(int64_t)e.path * (p.T + 1)];
-        e.S = r.x;
-        e.v = r.y;
-        e.C = r.z;
-        e.P = r.w;
-        e.s0_small = e.S < 1e-6f;
-        e.s0 = e.s0_small ? 1.0f : e.S;
-    } else {
-        e.ep = e.ep + 1u;  // 0xFFFFFFFF after seeding -> episode 0
-        e.S64 = p.s0;
-        e.S = (float)e.S64;
-        if (MODE == HE_MODE_HESTON) {
-            e.var64 = p.var;
-            e.v = (float)e.var64;
-        }
-        marks<MODE>(p, e.S64, e.var64, &e.C, &e.P);
-    }
+__global__ void init_reset_kernel(Params p, float* rst) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    float C, P;
+    marks<MODE>(p, p.s0, p.var, &C, &P);
+    Mkt m{(float)p.s0, p.var_f, C, P};
+    Env e;
     e.t = 0;
-    e.call = 0;
-    e.put = 0;
+    e.call = e.put = 0;
     e.cash = p.initial_cash;
+    e.s0_small = m.S < 1e-6f;
+    e.s0 = e.s0_small ? 1.0f : m.S;
+    float4 g = p.record_metrics ? greeks<MODE == HE_MODE_GBM>(p, m.S, m.v) : make_float4(0.f, 0.f, 0.f, 0.f);
+    rst[0] = m.S;
+    rst[1] = m.v;
+    rst[2] = C;
+    rst[3] = P;
+    make_obs(p, e, m, g, m.S, m.v, rst + 4);
 }
 
-// ------------------------------------------------------------------ one step
+// Replay: obs greeks of every table entry, once at load time.
+__global__ __launch_bounds__(kBlock) void table_greeks_kernel(Params p, float4* recg, int64_t count) {
+    int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (k >= count) return;
+    float4 r = p.rec[k];
+    recg[k] = p.record_metrics ? greeks<false>(p, r.x, r.y) : make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
+// ------------------------------------------------------------------ step
 struct StepOut {
     double reward;
     bool term;
-    float Sp, vp;  // S_t_minus_1, v_t_minus_1 after the step
-    // info
     double pnl, ps, tc, commission, slippage, rpc, tcp, thp, pv;
     float fc, fp;
     int32_t rqc, rqp, dc, dp;
 };
 
-// hedging_env_v2.py:175-262 (v1: hedging_env.py:171-245)
-template <int MODE>
-__device__ __forceinline__ void step_env(const Params& p, Env& e, float a0, float a1, int64_t gid,
-                                         StepOut& o) {
+// hedging_env_v2.py:175-262 (v1: hedging_env.py:171-245).  pre/post: market before
+// and after the advance (post C/P already lagged on the terminal step).
+__device__ __forceinline__ void step_env(const Params& p, Env& e, const Mkt& pre, const Mkt& post, float a0,
+                                         float a1, StepOut& o) {
     // portfolio_value_t_minus_1 is a pure function of the pre-step state
     double pv_prev;
     if (e.t == 0) {
-        float pv0 = (p.shares_f * e.S + 0.0f) + p.init_cash_f;  // f32 (:167-168)
+        float pv0 = (p.shares_f * pre.S + 0.0f) + p.init_cash_f;  // f32 (:167-168)
         pv_prev = (double)pv0;
     } else {
-        double optv = ((double)e.call * (double)e.C) * 100.0 + ((double)e.put * (double)e.P) * 100.0;
-        pv_prev = ((double)(p.shares_f * e.S) + optv) + e.cash;
+        double optv = ((double)e.call * (double)pre.C) * 100.0 + ((double)e.put * (double)pre.P) * 100.0;
+        pv_prev = ((double)(p.shares_f * pre.S) + optv) + e.cash;
     }
     // (i)-(ii) integer trade logic (:181-200)
     float fc = a0 * p.mt_f;
     float fp = a1 * p.mt_f;
     int32_t rqc = trade_round(fc, p.mt);
     int32_t rqp = trade_round(fp, p.mt);
-    int32_t nc = e.call + rqc, np_ = e.put + rqp;
+    int32_t nc = e.call + rqc, nq = e.put + rqp;
     nc = nc < -p.maxh ? -p.maxh : (nc > p.maxh ? p.maxh : nc);
-    np_ = np_ < -p.maxh ? -p.maxh : (np_ > p.maxh ? p.maxh : np_);
-    int32_t dc = nc - e.call, dp = np_ - e.put;
+    nq = nq < -p.maxh ? -p.maxh : (nq > p.maxh ? p.maxh : nq);
+    int32_t dc = nc - e.call, dp = nq - e.put;
     e.call = nc;
-    e.put = np_;
-    // (iii) commission + slippage on pre-advance marks (:203-213)
+    e.put = nq;
+    // (iii) commission + slippage on the pre-advance marks (:203-213)
     int32_t adc = dc < 0 ? -dc : dc, adp = dp < 0 ? -dp : dp;
     double commission = (double)(adc + adp) * p.tcpc;
     double slippage = 0.0, tc;
     if (p.variant == 2) {
-        double sc = (((double)adc * (double)e.C) * 100.0) * p.slip_frac;
-        double sp = (((double)adp * (double)e.P) * 100.0) * p.slip_frac;
+        double sc = (((double)adc * (double)pre.C) * 100.0) * p.slip_frac;
+        double sp = (((double)adp * (double)pre.P) * 100.0) * p.slip_frac;
         slippage = sc + sp;
         tc = commission + slippage;
     } else {
@@ -356,61 +466,20 @@ __device__ __forceinline__ void step_env(const Params& p, Env& e, float a0, floa
     }
     e.cash = e.cash - tc;
     // (iv)-(v) advance (:216-231)
-    o.Sp = e.S;
-    o.vp = e.v;
-    uint32_t t_old = e.t;
     e.t = e.t + 1;
     bool term = (int32_t)e.t >= p.T;
-    if (MODE == HE_MODE_REPLAY) {
-        uint32_t tt = e.t > (uint32_t)p.T ? (uint32_t)p.T : e.t;
-        float4 r = p.rec[(int64_t)e.path * (p.T + 1) + tt];  // C/P at T hold row T-1
-        e.S = r.x;
-        e.v = r.y;
-        e.C = r.z;
-        e.P = r.w;
-    } else {
-        uint64_t n = (uint64_t)e.ep * (uint64_t)p.T + (uint64_t)t_old;
-        u32x4 ctr = {(uint32_t)n, (uint32_t)(n >> 32), (uint32_t)gid, (uint32_t)((uint64_t)gid >> 32)};
-        u32x4 x = philox4x32_10(ctr, p.key0, p.key1);
-        double u1 = u01(x.x, x.y), u2 = u01(x.z, x.w);
-        double rad = sqrt(-2.0 * log(u1));
-        double ang = 6.283185307179586 * u2;
-        double Snew;
-        if (MODE == HE_MODE_HESTON) {
-            double sn, cs;
-            sincos(ang, &sn, &cs);
-            double z1 = rad * cs, z2 = rad * sn;
-            double vp = e.var64 < 0.0 ? 0.0 : e.var64;  // full truncation
-            double dw1 = p.sqrt_dt * z1, dw2 = p.sqrt_dt * z2;
-            double dW = p.h_rho * dw1 + p.h_sqrt1mrho2 * dw2;  // rbergomi_sim.py:457
-            double drift = (p.mu - 0.5 * vp) * p.dt;
-            double diff = sqrt(vp) * dW;
-            Snew = e.S64 * exp(drift + diff);
-            e.var64 = e.var64 + p.h_kappa * (p.h_theta - vp) * p.dt + p.h_xi * sqrt(vp) * dw1;
-        } else {
-            double z0 = rad * cos(ang);
-            double dW = p.sqrt_dt * z0;
-            double diff = p.sqrt_var * dW;
-            Snew = e.S64 * exp(p.drift + diff);
-        }
-        e.S64 = (Snew < 1e-8) ? 1e-8 : Snew;  // np.maximum(., 1e-8), NaN kept
-        e.S = (float)e.S64;
-        if (MODE == HE_MODE_HESTON) e.v = (float)e.var64;
-        if (!term) marks<MODE>(p, e.S64, e.var64, &e.C, &e.P);
-    }
     // (vi) mark-to-market (:233-238)
-    double optv = ((double)e.call * (double)e.C) * 100.0 + ((double)e.put * (double)e.P) * 100.0;
-    double pv = ((double)(p.shares_f * e.S) + optv) + e.cash;
+    double optv = ((double)e.call * (double)post.C) * 100.0 + ((double)e.put * (double)post.P) * 100.0;
+    double pv = ((double)(p.shares_f * post.S) + optv) + e.cash;
     double pnl = pv - pv_prev;
     double ps = p.shares_zero ? pnl : pnl / p.shares_d;
     // (vii) reward (:243-262)
+    float f = np_maxf(e.s0, 25.0f);
     double term_v;
     if (p.loss == HE_LOSS_MSE) {
-        float f = np_maxf(e.s0, 25.0f);
         double den = e.s0_small ? (625.0 + 1e-9) : (double)(f * f + 1e-9f);
         term_v = (ps * ps) / den;
     } else {
-        float f = np_maxf(e.s0, 25.0f);
         double den = e.s0_small ? (25.0 + 1e-9) : (double)(f + 1e-9f);
         term_v = fabs(ps) / den;
     }
@@ -418,7 +487,7 @@ __device__ __forceinline__ void step_env(const Params& p, Env& e, float a0, floa
     double tcp = p.lam * tc;
     double thp = 0.0, reward;
     if (p.variant == 2) {
-        thp = p.theta * ((double)(p.T - (int32_t)e.t) / 252.0);
+        thp = p.thp_tab[e.t > (uint32_t)p.T ? p.T : e.t];
         reward = (rpc - tcp) - thp;
     } else {
         reward = rpc - tcp;
@@ -442,8 +511,8 @@ __device__ __forceinline__ void step_env(const Params& p, Env& e, float a0, floa
     o.dp = dp;
 }
 
-__device__ __forceinline__ void write_info(const he_info& inf, int64_t i, const StepOut& o,
-                                           const Env& e, int variant) {
+__device__ __forceinline__ void write_info(const he_info& inf, int64_t i, const StepOut& o, const Env& e,
+                                           const Mkt& m, int variant) {
     const double nan = __builtin_nan("");
     if (inf.step_pnl_total) inf.step_pnl_total[i] = o.pnl;
     if (inf.per_share_step_pnl) inf.per_share_step_pnl[i] = o.ps;
@@ -466,10 +535,10 @@ __device__ __forceinline__ void write_info(const he_info& inf, int64_t i, const 
     if (inf.actual_calls_traded) inf.actual_calls_traded[i] = o.dc;
     if (inf.actual_puts_traded) inf.actual_puts_traded[i] = o.dp;
     if (inf.initial_S0_for_episode) inf.initial_S0_for_episode[i] = e.s0;
-    if (inf.current_stock_price) inf.current_stock_price[i] = e.S;
-    if (inf.current_volatility) inf.current_volatility[i] = e.v;
-    if (inf.current_call_price) inf.current_call_price[i] = e.C;
-    if (inf.current_put_price) inf.current_put_price[i] = e.P;
+    if (inf.current_stock_price) inf.current_stock_price[i] = m.S;
+    if (inf.current_volatility) inf.current_volatility[i] = m.v;
+    if (inf.current_call_price) inf.current_call_price[i] = m.C;
+    if (inf.current_put_price) inf.current_put_price[i] = m.P;
     if (inf.current_step) inf.current_step[i] = (int32_t)e.t;
 }
 
@@ -484,73 +553,173 @@ __device__ __forceinline__ void flush_obs_tile(const float* tile, float* out, in
     for (int k = (nv << 2) + threadIdx.x; k < nf; k += kBlock) dst[k] = tile[k];
 }
 
-// ------------------------------------------------------------------ kernels
-// K fused steps; K == 1 is the Gym step.  INFO: write he_info fields.
+// replay reset (hedging_env_v2.py:145-173): draw the episode row from the env's
+// PCG64 stream, exactly gymnasium's np_random.integers(num_episodes).
+__device__ __forceinline__ void replay_reset(const Params& p, const State& s, int64_t i, Env& e) {
+    const int64_t N = p.n;
+    Pcg64 g;
+    g.sh = s.pcg[i];
+    g.sl = s.pcg[N + i];
+    g.ih = s.pcg[2 * N + i];
+    g.il = s.pcg[3 * N + i];
+    g.has32 = s.pcgb[i];
+    g.buf32 = s.pcgb[N + i];
+    e.path = (int32_t)pcg64_integers(g, (uint64_t)p.n_paths);
+    s.pcg[i] = g.sh;
+    s.pcg[N + i] = g.sl;
+    s.pcgb[i] = g.has32;
+    s.pcgb[N + i] = g.buf32;
+    float S0 = p.rec[(int64_t)e.path * (p.T + 1)].x;
+    e.s0_small = S0 < 1e-6f;
+    e.s0 = e.s0_small ? 1.0f : S0;
+}
+
+__device__ __forceinline__ void env_reset_common(const Params& p, Env& e) {
+    e.t = 0;
+    e.call = 0;
+    e.put = 0;
+    e.cash = p.initial_cash;
+}
+
+// K fused steps from market slot `slot0` (generate) / the env's own path row (replay).
 template <int MODE, bool INFO>
-__global__ __launch_bounds__(kBlock) void step_kernel(Params p, State s, Io io, int k_steps) {
+__global__ __launch_bounds__(kBlock) void step_kernel(Params p, State s, Io io, int k_steps, int slot0) {
+    constexpr bool REPLAY = (MODE == HE_MODE_REPLAY);
     __shared__ __attribute__((aligned(16))) float tile[kBlock * kObs];
     const int64_t row0 = (int64_t)blockIdx.x * kBlock;
     const int64_t i = row0 + threadIdx.x;
     const bool live = i < p.n;
     const int rows = (int)((p.n - row0) < kBlock ? (p.n - row0) : kBlock);
-    constexpr bool CONST_VAR = (MODE == HE_MODE_GBM);
+    const int64_t N = p.n;
     Env e;
-    if (live) load_env<MODE>(p, s, i, e);
+    Mkt pre;
+    if (live) {
+        e.t = s.t[i];
+        uint32_t pk = s.pos[i];
+        e.call = unpack_lo(pk);
+        e.put = unpack_hi(pk);
+        e.cash = s.cash[i];
+        if (REPLAY) {
+            e.path = s.path[i];
+            float s0 = s.s0[i];
+            e.s0_small = (s0 == -1.0f);
+            e.s0 = e.s0_small ? 1.0f : s0;
+            uint32_t tt = e.t > (uint32_t)p.T ? (uint32_t)p.T : e.t;
+            pre = as_mkt(p.rec[(int64_t)e.path * (p.T + 1) + tt]);
+        } else {
+            float s0f = p.rst[0];
+            e.s0_small = s0f < 1e-6f;
+            e.s0 = e.s0_small ? 1.0f : s0f;
+            pre = (e.t == 0) ? Mkt{p.rst[0], p.rst[1], p.rst[2], p.rst[3]}
+                             : as_mkt(p.tileA[(int64_t)slot0 * N + i]);
+        }
+    }
     bool reset_any = false;
     for (int k = 0; k < k_steps; ++k) {
-        const int64_t koff = (int64_t)k * p.n;
-        float o[kObs];
+        const int64_t koff = (int64_t)k * N;
+        float* orow = tile + threadIdx.x * kObs;
         bool term = false;
         if (live) {
+            Mkt post;
+            float4 g;
+            if (REPLAY) {
+                uint32_t tn = e.t + 1 > (uint32_t)p.T ? (uint32_t)p.T : e.t + 1;
+                int64_t r = (int64_t)e.path * (p.T + 1) + tn;
+                post = as_mkt(p.rec[r]);
+                g = p.recg[r];
+            } else {
+                int64_t r = (int64_t)(slot0 + k + 1) * N + i;
+                post = as_mkt(p.tileA[r]);
+                g = p.tileB[r];
+            }
             float2 a = reinterpret_cast<const float2*>(io.act)[koff + i];
             StepOut so;
-            step_env<MODE>(p, e, a.x, a.y, p.goff + i, so);
+            step_env(p, e, pre, post, a.x, a.y, so);
             term = so.term;
-            if (INFO) write_info(io.info, i, so, e, p.variant);
-            make_obs<CONST_VAR>(p, e, so.Sp, so.vp, o);
+            if (INFO) write_info(io.info, i, so, e, post, p.variant);
+            float o[kObs];
+            make_obs(p, e, post, g, pre.S, pre.v, o);
+#pragma unroll
+            for (int c = 0; c < kObs; ++c) orow[c] = o[c];
             if (io.rew) io.rew[koff + i] = (float)so.reward;
             if (io.term) io.term[koff + i] = term ? 1 : 0;
+            pre = post;
         }
         // wave-level done mask: waves without a terminating env skip the reset path
         if (p.autoreset && __ballot(term) != 0ull) {
             if (term) {
                 if (io.tobs) {
 #pragma unroll
-                    for (int c = 0; c < kObs; ++c) io.tobs[i * kObs + c] = o[c];
+                    for (int c = 0; c < kObs; ++c) io.tobs[i * kObs + c] = orow[c];
                 }
-                reset_env<MODE>(p, s, i, e);
-                make_obs<CONST_VAR>(p, e, e.S, e.v, o);
+                env_reset_common(p, e);
+                if (REPLAY) {
+                    replay_reset(p, s, i, e);
+                    int64_t r = (int64_t)e.path * (p.T + 1);
+                    pre = as_mkt(p.rec[r]);
+                    float o[kObs];
+                    make_obs(p, e, pre, p.recg[r], pre.S, pre.v, o);
+#pragma unroll
+                    for (int c = 0; c < kObs; ++c) orow[c] = o[c];
+                } else {
+                    pre = Mkt{p.rst[0], p.rst[1], p.rst[2], p.rst[3]};
+#pragma unroll
+                    for (int c = 0; c < kObs; ++c) orow[c] = p.rst[4 + c];
+                }
                 reset_any = true;
             }
         }
         if (io.obs) {
-#pragma unroll
-            for (int c = 0; c < kObs; ++c) tile[threadIdx.x * kObs + c] = o[c];
             __syncthreads();
             flush_obs_tile(tile, io.obs + koff * kObs, row0, rows);
             __syncthreads();
         }
     }
     if (live) {
-        store_env<MODE>(s, i, e, reset_any);
+        s.t[i] = e.t;
+        s.pos[i] = pack_pos(e.call, e.put);
+        s.cash[i] = e.cash;
+        if (REPLAY && reset_any) {
+            s.path[i] = e.path;
+            s.s0[i] = e.s0_small ? -1.0f : e.s0;
+        }
         if (io.trunc) io.trunc[i] = 0;
     }
 }
 
+// Explicit reset of envs `ids` (NULL: all).  Generate: the market position of a
+// reset env moves to the start of its next episode.
 template <int MODE>
-__global__ __launch_bounds__(kBlock) void reset_kernel(Params p, State s, const int64_t* ids,
+__global__ __launch_bounds__(kBlock) void reset_kernel(Params p, State s, Market cur, const int64_t* ids,
                                                        int64_t count, float* obs) {
     const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (j >= count) return;
     const int64_t i = ids ? ids[j] : j;
     if (i < 0 || i >= p.n) return;
     Env e;
-    load_env<MODE>(p, s, i, e);
-    reset_env<MODE>(p, s, i, e);
-    store_env<MODE>(s, i, e, true);
+    env_reset_common(p, e);
+    float o[kObs];
+    if (MODE == HE_MODE_REPLAY) {
+        replay_reset(p, s, i, e);
+        int64_t r = (int64_t)e.path * (p.T + 1);
+        Mkt m = as_mkt(p.rec[r]);
+        make_obs(p, e, m, p.recg[r], m.S, m.v, o);
+        s.path[i] = e.path;
+        s.s0[i] = e.s0_small ? -1.0f : e.s0;
+    } else {
+        cur.ep[i] = cur.ep[i] + 1u;  // 0xFFFFFFFF after seeding -> episode 0
+        cur.t[i] = 0;
+        cur.S[i] = p.s0;
+        if (MODE == HE_MODE_HESTON) cur.v[i] = p.var;
+        cur.C[i] = p.rst[2];
+        cur.P[i] = p.rst[3];
+#pragma unroll
+        for (int c = 0; c < kObs; ++c) o[c] = p.rst[4 + c];
+    }
+    s.t[i] = 0;
+    s.pos[i] = 0;
+    s.cash[i] = e.cash;
     if (obs) {
-        float o[kObs];
-        make_obs<MODE == HE_MODE_GBM>(p, e, e.S, e.v, o);
 #pragma unroll
         for (int c = 0; c < kObs; ++c) obs[i * kObs + c] = o[c];
     }
@@ -637,12 +806,18 @@ struct he_env {
     he_config cfg;
     Params p;
     State s;
+    Market cur, bak;
     std::string err;
     void* state_mem = nullptr;
     size_t state_bytes = 0;
     float4* rec = nullptr;
+    float4* recg = nullptr;
+    float4* tile = nullptr;   // tileA | tileB
+    double* thp = nullptr;    // theta table [T+1]
+    float* rst = nullptr;     // reset market + obs (generate)
     int64_t n_paths = 0;
-    bool seeded = false;
+    int32_t block_pos = 0;    // generate: next slot to consume; M = tile exhausted/invalid
+    bool ready = false;       // a reset happened since create/seed
     std::vector<std::pair<size_t, void*>> fields;  // (bytes, device ptr) for get/set_state
 };
 
@@ -663,6 +838,8 @@ static he_status fail(he_env* env, he_status st, const char* fmt, ...) {
             return fail((env), HE_EHIP, "%s failed: %s", #call, hipGetErrorString(_e));        \
     } while (0)
 
+static bool is_generate(const he_env* env) { return env->cfg.mode != HE_MODE_REPLAY; }
+
 static void fill_params(he_env* env) {
     const he_config& c = env->cfg;
     Params& p = env->p;
@@ -677,16 +854,17 @@ static void fill_params(he_env* env) {
     p.mt = c.max_trade_per_step;
     p.maxh = c.max_contracts_held_per_type;
     p.mt_f = (float)c.max_trade_per_step;
+    p.maxh_f = (float)c.max_contracts_held_per_type;
     p.init_cash_f = (float)c.initial_cash;
     p.tcpc = c.transaction_cost_per_contract;
     p.slip_frac = c.slippage_bps / 10000.0;
     p.lam = c.lambda_cost;
     p.w = c.pnl_penalty_weight;
-    p.theta = c.theta_weight;
     p.initial_cash = c.initial_cash;
     p.shares_d = (double)c.shares_to_hedge;
     p.shares_f = (float)c.shares_to_hedge;
     p.shares_zero = c.shares_to_hedge == 0;
+    p.thp_tab = env->thp;
     p.r_f = (float)c.risk_free_rate;
     p.tenor_f = (float)c.option_tenor_years;
     p.r_d = c.risk_free_rate;
@@ -724,43 +902,137 @@ static void fill_params(he_env* env) {
     double omr = 1.0 - c.heston_rho * c.heston_rho;
     p.h_sqrt1mrho2 = sqrt(omr < 0.0 ? 0.0 : omr);
     p.T = c.episode_length;
+    p.T_f = (float)c.episode_length;
+    p.M = c.market_block;
+    if (env->tile) {
+        p.tileA = env->tile;
+        p.tileB = env->tile + (size_t)(c.market_block + 1) * (size_t)c.n_envs;
+    }
+    p.rst = env->rst;
     p.rec = env->rec;
+    p.recg = env->recg;
     p.n_paths = env->n_paths;
+}
+
+template <int MODE>
+static void launch_init_reset(he_env* env) {
+    hipLaunchKernelGGL(init_reset_kernel<MODE>, dim3(1), dim3(64), 0, 0, env->p, env->rst);
+}
+
+// theta table + (generate) reset constants; re-run whenever T or the config changes.
+static he_status upload_tables(he_env* env) {
+    const int32_t T = env->cfg.episode_length;
+    std::vector<double> h((size_t)T + 1);
+    for (int32_t t = 0; t <= T; ++t) h[(size_t)t] = env->cfg.theta_weight * ((double)(T - t) / 252.0);
+    if (env->thp) (void)hipFree(env->thp);
+    env->thp = nullptr;
+    HE_HIP(env, hipMalloc(&env->thp, h.size() * sizeof(double)));
+    HE_HIP(env, hipMemcpy(env->thp, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice));
+    fill_params(env);
+    if (is_generate(env)) {
+        if (env->cfg.mode == HE_MODE_GBM) launch_init_reset<HE_MODE_GBM>(env);
+        else launch_init_reset<HE_MODE_HESTON>(env);
+        HE_HIP(env, hipGetLastError());
+        HE_HIP(env, hipDeviceSynchronize());
+    }
+    return HE_OK;
+}
+
+template <int MODE>
+static void launch_market(he_env* env, int32_t advance_only, hipStream_t st) {
+    int64_t blocks = (env->cfg.n_envs + kMktEnvs - 1) / kMktEnvs;
+    hipLaunchKernelGGL(market_kernel<MODE>, dim3((unsigned)blocks), dim3(kMktEnvs * kMktLanes), 0, st, env->p,
+                       env->cur, env->bak, advance_only);
+}
+
+static he_status market(he_env* env, int32_t advance_only, hipStream_t st) {
+    if (env->cfg.mode == HE_MODE_GBM) launch_market<HE_MODE_GBM>(env, advance_only, st);
+    else launch_market<HE_MODE_HESTON>(env, advance_only, st);
+    HE_HIP(env, hipGetLastError());
+    return HE_OK;
+}
+
+// Bring `cur` to the position the envs are actually at (mid-block rewind) and
+// invalidate the tile.  Needed before partial resets and checkpoints.
+static he_status materialize_market(he_env* env, hipStream_t st) {
+    const int32_t M = env->cfg.market_block;
+    if (env->block_pos < M) {
+        if (env->block_pos > 0) {
+            he_status s = market(env, env->block_pos, st);
+            if (s != HE_OK) return s;
+        } else {
+            // no step consumed yet: the current position is the block start
+            const int64_t N = env->cfg.n_envs;
+            HE_HIP(env, hipMemcpyAsync(env->cur.ep, env->bak.ep, N * 4, hipMemcpyDeviceToDevice, st));
+            HE_HIP(env, hipMemcpyAsync(env->cur.t, env->bak.t, N * 4, hipMemcpyDeviceToDevice, st));
+            HE_HIP(env, hipMemcpyAsync(env->cur.S, env->bak.S, N * 8, hipMemcpyDeviceToDevice, st));
+            HE_HIP(env, hipMemcpyAsync(env->cur.C, env->bak.C, N * 4, hipMemcpyDeviceToDevice, st));
+            HE_HIP(env, hipMemcpyAsync(env->cur.P, env->bak.P, N * 4, hipMemcpyDeviceToDevice, st));
+            if (env->cur.v)
+                HE_HIP(env, hipMemcpyAsync(env->cur.v, env->bak.v, N * 8, hipMemcpyDeviceToDevice, st));
+        }
+    }
+    env->block_pos = M;
+    return HE_OK;
 }
 
 template <int MODE>
 static void launch_reset(he_env* env, const int64_t* ids, int64_t count, float* obs, hipStream_t st) {
     int64_t blocks = (count + kBlock - 1) / kBlock;
     hipLaunchKernelGGL(reset_kernel<MODE>, dim3((unsigned)blocks), dim3(kBlock), 0, st, env->p, env->s,
-                       ids, count, obs);
+                       env->cur, ids, count, obs);
 }
 
 template <int MODE>
-static void launch_step(he_env* env, const Io& io, bool info, int k, hipStream_t st) {
+static void launch_step(he_env* env, const Io& io, bool info, int k, int slot0, hipStream_t st) {
     int64_t blocks = (env->cfg.n_envs + kBlock - 1) / kBlock;
     if (info)
         hipLaunchKernelGGL((step_kernel<MODE, true>), dim3((unsigned)blocks), dim3(kBlock), 0, st, env->p,
-                           env->s, io, k);
+                           env->s, io, k, slot0);
     else
         hipLaunchKernelGGL((step_kernel<MODE, false>), dim3((unsigned)blocks), dim3(kBlock), 0, st, env->p,
-                           env->s, io, k);
+                           env->s, io, k, slot0);
 }
 
-static he_status launch_any(he_env* env, const Io& io, bool info, int k, void* stream) {
+static he_status launch_steps(he_env* env, Io io, bool info, int k_total, void* stream) {
     const he_config& c = env->cfg;
     if (c.mode == HE_MODE_REPLAY && !env->rec) return fail(env, HE_ESTATE, "no paths loaded (he_load_paths)");
+    if (!env->ready) return fail(env, HE_ESTATE, "he_reset must be called before stepping");
     DeviceGuard dg(c.device);
     hipStream_t st = (hipStream_t)stream;
-    if (c.mode == HE_MODE_REPLAY) launch_step<HE_MODE_REPLAY>(env, io, info, k, st);
-    else if (c.mode == HE_MODE_GBM) launch_step<HE_MODE_GBM>(env, io, info, k, st);
-    else launch_step<HE_MODE_HESTON>(env, io, info, k, st);
-    HE_HIP(env, hipGetLastError());
+    if (c.mode == HE_MODE_REPLAY) {
+        launch_step<HE_MODE_REPLAY>(env, io, info, k_total, 0, st);
+        HE_HIP(env, hipGetLastError());
+        return HE_OK;
+    }
+    const int32_t M = c.market_block;
+    const int64_t N = c.n_envs;
+    int done = 0;
+    while (done < k_total) {
+        if (env->block_pos >= M) {
+            he_status s = market(env, 0, st);
+            if (s != HE_OK) return s;
+            env->block_pos = 0;
+        }
+        int k = k_total - done;
+        if (k > M - env->block_pos) k = M - env->block_pos;
+        Io sub = io;
+        sub.act = io.act + (int64_t)done * N * 2;
+        if (io.obs) sub.obs = io.obs + (int64_t)done * N * kObs;
+        if (io.rew) sub.rew = io.rew + (int64_t)done * N;
+        if (io.term) sub.term = io.term + (int64_t)done * N;
+        if (c.mode == HE_MODE_GBM) launch_step<HE_MODE_GBM>(env, sub, info, k, env->block_pos, st);
+        else launch_step<HE_MODE_HESTON>(env, sub, info, k, env->block_pos, st);
+        HE_HIP(env, hipGetLastError());
+        env->block_pos += k;
+        done += k;
+    }
     return HE_OK;
 }
 
 extern "C" {
 
-const char* he_version(void) { return "libhedgeenv 0.1 (gfx950)"; }
+const char* he_version(void) { return "libhedgeenv 0.2 (gfx950)"; }
 
 const char* he_last_error(const he_env* env) {
     if (!env) return "null handle";
@@ -801,6 +1073,7 @@ he_status he_config_init(he_config* cfg, int32_t variant) {
     cfg->heston_theta = 0.029028;
     cfg->heston_xi = 0.3;
     cfg->heston_rho = -0.7;  // RHO_DEFAULT, rbergomi_sim.py:26
+    cfg->market_block = 64;
     return HE_OK;
 }
 
@@ -810,71 +1083,76 @@ he_status he_create(const he_config* cfg, he_env** out) {
     he_env* env = new (std::nothrow) he_env();
     if (!env) return HE_ENOMEM;
     env->cfg = *cfg;
-    const he_config& c = env->cfg;
-    he_status st = HE_OK;
-    if (c.abi_version != HE_ABI_VERSION) st = fail(env, HE_EINVAL, "abi_version %d != %d", c.abi_version, HE_ABI_VERSION);
-    else if (c.variant != 1 && c.variant != 2) st = fail(env, HE_EINVAL, "variant must be 1 or 2");
-    else if (c.mode < 0 || c.mode > 2) st = fail(env, HE_EINVAL, "bad mode %d", c.mode);
-    else if (c.loss_type < 0 || c.loss_type > 3) st = fail(env, HE_EINVAL, "bad loss_type %d", c.loss_type);
-    else if (c.n_envs < 1 || c.n_envs > (int64_t)1 << 31) st = fail(env, HE_EINVAL, "n_envs out of range");
-    else if (c.global_env_offset < 0) st = fail(env, HE_EINVAL, "global_env_offset < 0");
-    else if (c.max_contracts_held_per_type < 0 || c.max_contracts_held_per_type > 32767)
-        st = fail(env, HE_EINVAL, "max_contracts_held_per_type must be in [0, 32767]");
-    else if (c.max_trade_per_step < 0 || c.max_trade_per_step > 32767)
-        st = fail(env, HE_EINVAL, "max_trade_per_step must be in [0, 32767]");
-    else if (c.mode != HE_MODE_REPLAY && (c.episode_length < 1 || c.episode_length > (1 << 30)))
-        st = fail(env, HE_EINVAL, "episode_length must be >= 1");
-    if (st != HE_OK) {
-        *out = env;  // keep the handle so the caller can read the message
-        return st;
-    }
+    he_config& c = env->cfg;
+    *out = env;  // returned even on failure so the caller can read the message
+    if (c.abi_version != HE_ABI_VERSION)
+        return fail(env, HE_EINVAL, "abi_version %d != %d", c.abi_version, HE_ABI_VERSION);
+    if (c.variant != 1 && c.variant != 2) return fail(env, HE_EINVAL, "variant must be 1 or 2");
+    if (c.mode < 0 || c.mode > 2) return fail(env, HE_EINVAL, "bad mode %d", c.mode);
+    if (c.loss_type < 0 || c.loss_type > 3) return fail(env, HE_EINVAL, "bad loss_type %d", c.loss_type);
+    if (c.n_envs < 1 || c.n_envs > (int64_t)1 << 31) return fail(env, HE_EINVAL, "n_envs out of range");
+    if (c.global_env_offset < 0) return fail(env, HE_EINVAL, "global_env_offset < 0");
+    if (c.max_contracts_held_per_type < 0 || c.max_contracts_held_per_type > 32767)
+        return fail(env, HE_EINVAL, "max_contracts_held_per_type must be in [0, 32767]");
+    if (c.max_trade_per_step < 0 || c.max_trade_per_step > 32767)
+        return fail(env, HE_EINVAL, "max_trade_per_step must be in [0, 32767]");
+    if (c.mode != HE_MODE_REPLAY && (c.episode_length < 1 || c.episode_length > (1 << 30)))
+        return fail(env, HE_EINVAL, "episode_length must be >= 1");
+    if (c.market_block == 0) c.market_block = 64;
+    if (c.market_block < 1 || c.market_block > kMaxBlock)
+        return fail(env, HE_EINVAL, "market_block must be in [1, %d]", kMaxBlock);
     DeviceGuard dg(c.device);
-    if (!dg.ok) {
-        *out = env;
-        return fail(env, HE_EHIP, "hipSetDevice(%d) failed", c.device);
-    }
+    if (!dg.ok) return fail(env, HE_EHIP, "hipSetDevice(%d) failed", c.device);
     const int64_t N = c.n_envs;
-    // carve one allocation: 256-B aligned SoA fields
-    struct F { size_t bytes; void** dst; };
+    // one allocation, 256-B aligned SoA fields
+    struct F {
+        size_t bytes;
+        void** dst;
+        bool state;  // part of the checkpoint blob
+    };
     std::vector<F> fs;
-    fs.push_back({(size_t)N * 4, (void**)&env->s.t});
-    fs.push_back({(size_t)N * 4, (void**)&env->s.pos});
-    fs.push_back({(size_t)N * 8, (void**)&env->s.cash});
+    fs.push_back({(size_t)N * 4, (void**)&env->s.t, true});
+    fs.push_back({(size_t)N * 4, (void**)&env->s.pos, true});
+    fs.push_back({(size_t)N * 8, (void**)&env->s.cash, true});
     if (c.mode == HE_MODE_REPLAY) {
-        fs.push_back({(size_t)N * 4, (void**)&env->s.path});
-        fs.push_back({(size_t)N * 4, (void**)&env->s.s0});
-        fs.push_back({(size_t)N * 32, (void**)&env->s.pcg});
-        fs.push_back({(size_t)N * 8, (void**)&env->s.pcgb});
+        fs.push_back({(size_t)N * 4, (void**)&env->s.path, true});
+        fs.push_back({(size_t)N * 4, (void**)&env->s.s0, true});
+        fs.push_back({(size_t)N * 32, (void**)&env->s.pcg, true});
+        fs.push_back({(size_t)N * 8, (void**)&env->s.pcgb, true});
     } else {
-        fs.push_back({(size_t)N * 8, (void**)&env->s.S});
-        fs.push_back({(size_t)N * 4, (void**)&env->s.C});
-        fs.push_back({(size_t)N * 4, (void**)&env->s.P});
-        fs.push_back({(size_t)N * 4, (void**)&env->s.ep});
-        if (c.mode == HE_MODE_HESTON) fs.push_back({(size_t)N * 8, (void**)&env->s.var});
+        Market* ms[2] = {&env->cur, &env->bak};
+        for (int k = 0; k < 2; ++k) {
+            fs.push_back({(size_t)N * 4, (void**)&ms[k]->ep, k == 0});
+            fs.push_back({(size_t)N * 4, (void**)&ms[k]->t, k == 0});
+            fs.push_back({(size_t)N * 8, (void**)&ms[k]->S, k == 0});
+            fs.push_back({(size_t)N * 4, (void**)&ms[k]->C, k == 0});
+            fs.push_back({(size_t)N * 4, (void**)&ms[k]->P, k == 0});
+            if (c.mode == HE_MODE_HESTON) fs.push_back({(size_t)N * 8, (void**)&ms[k]->v, k == 0});
+        }
     }
     size_t total = 0;
     for (auto& f : fs) total += (f.bytes + 255) & ~(size_t)255;
     void* mem = nullptr;
     hipError_t e = hipMalloc(&mem, total);
-    if (e != hipSuccess) {
-        *out = env;
-        return fail(env, HE_ENOMEM, "hipMalloc(%zu) failed: %s", total, hipGetErrorString(e));
-    }
+    if (e != hipSuccess) return fail(env, HE_ENOMEM, "hipMalloc(%zu) failed: %s", total, hipGetErrorString(e));
     env->state_mem = mem;
     env->state_bytes = total;
     size_t off = 0;
     for (auto& f : fs) {
         *f.dst = (char*)mem + off;
-        env->fields.push_back({f.bytes, *f.dst});
+        if (f.state) env->fields.push_back({f.bytes, *f.dst});
         off += (f.bytes + 255) & ~(size_t)255;
     }
-    e = hipMemset(mem, 0, total);
-    if (e != hipSuccess) {
-        *out = env;
-        return fail(env, HE_EHIP, "hipMemset failed: %s", hipGetErrorString(e));
+    HE_HIP(env, hipMemset(mem, 0, total));
+    if (is_generate(env)) {
+        size_t tb = (size_t)2 * (size_t)(c.market_block + 1) * (size_t)N * sizeof(float4);
+        e = hipMalloc(&env->tile, tb);
+        if (e != hipSuccess) return fail(env, HE_ENOMEM, "hipMalloc(tile %zu) failed: %s", tb, hipGetErrorString(e));
+        HE_HIP(env, hipMalloc(&env->rst, 32 * sizeof(float)));
+        env->block_pos = c.market_block;
     }
-    fill_params(env);
-    *out = env;
+    he_status st = upload_tables(env);
+    if (st != HE_OK) return st;
     // default streams: env i seeded with (seed + global id) until he_seed is called
     if (c.mode == HE_MODE_REPLAY) {
         std::vector<uint64_t> seeds(N);
@@ -891,6 +1169,10 @@ he_status he_destroy(he_env* env) {
         DeviceGuard dg(env->cfg.device);
         if (env->state_mem) (void)hipFree(env->state_mem);
         if (env->rec) (void)hipFree(env->rec);
+        if (env->recg) (void)hipFree(env->recg);
+        if (env->tile) (void)hipFree(env->tile);
+        if (env->thp) (void)hipFree(env->thp);
+        if (env->rst) (void)hipFree(env->rst);
     }
     delete env;
     return HE_OK;
@@ -922,19 +1204,36 @@ he_status he_load_paths(he_env* env, const float* S, const float* v, const float
             rec[(size_t)(q * n_cols + t)] = r;
         }
     }
+    const size_t bytes = rec.size() * sizeof(float4);
     float4* d = nullptr;
-    hipError_t e = hipMalloc(&d, rec.size() * sizeof(float4));
+    float4* dg2 = nullptr;
+    hipError_t e = hipMalloc(&d, bytes);
     if (e != hipSuccess) return fail(env, HE_ENOMEM, "hipMalloc(paths) failed: %s", hipGetErrorString(e));
-    e = hipMemcpy(d, rec.data(), rec.size() * sizeof(float4), hipMemcpyHostToDevice);
+    e = hipMalloc(&dg2, bytes);
     if (e != hipSuccess) {
         (void)hipFree(d);
+        return fail(env, HE_ENOMEM, "hipMalloc(path greeks) failed: %s", hipGetErrorString(e));
+    }
+    e = hipMemcpy(d, rec.data(), bytes, hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        (void)hipFree(d);
+        (void)hipFree(dg2);
         return fail(env, HE_EHIP, "hipMemcpy(paths) failed: %s", hipGetErrorString(e));
     }
     if (env->rec) (void)hipFree(env->rec);
+    if (env->recg) (void)hipFree(env->recg);
     env->rec = d;
+    env->recg = dg2;
     env->n_paths = n_paths;
     env->cfg.episode_length = (int32_t)T;
-    fill_params(env);
+    env->ready = false;
+    he_status st = upload_tables(env);
+    if (st != HE_OK) return st;
+    const int64_t count = (int64_t)rec.size();
+    hipLaunchKernelGGL(table_greeks_kernel, dim3((unsigned)((count + kBlock - 1) / kBlock)), dim3(kBlock), 0, 0,
+                       env->p, env->recg, count);
+    HE_HIP(env, hipGetLastError());
+    HE_HIP(env, hipDeviceSynchronize());
     return HE_OK;
 }
 
@@ -975,6 +1274,7 @@ he_status he_seed(he_env* env, const int64_t* env_ids, const uint64_t* seeds, in
     if (!seeds || count < 1) return fail(env, HE_EINVAL, "he_seed needs >= 1 seed");
     DeviceGuard dg(env->cfg.device);
     const int64_t N = env->cfg.n_envs;
+    HE_HIP(env, hipDeviceSynchronize());
     if (env->cfg.mode == HE_MODE_REPLAY) {
         // read-modify-write the PCG64 arrays on the host (setup path, not per step)
         std::vector<uint64_t> pcg((size_t)(4 * N));
@@ -995,10 +1295,11 @@ he_status he_seed(he_env* env, const int64_t* env_ids, const uint64_t* seeds, in
     } else {
         env->cfg.seed = seeds[0];
         fill_params(env);
-        // episode counters restart: 0xFFFFFFFF so that the next reset starts episode 0
-        HE_HIP(env, hipMemset(env->s.ep, 0xFF, (size_t)N * 4));
+        // episode counters restart: the next reset starts episode 0 of every env
+        HE_HIP(env, hipMemset(env->cur.ep, 0xFF, (size_t)N * 4));
+        env->block_pos = env->cfg.market_block;
+        env->ready = false;
     }
-    env->seeded = true;
     return HE_OK;
 }
 
@@ -1008,13 +1309,23 @@ he_status he_reset(he_env* env, const int64_t* env_ids, int64_t count, float* ob
     if (c.mode == HE_MODE_REPLAY && !env->rec) return fail(env, HE_ESTATE, "no paths loaded (he_load_paths)");
     if (!env_ids) count = c.n_envs;
     if (count < 0) return fail(env, HE_EINVAL, "count < 0");
+    if (env_ids && !env->ready) return fail(env, HE_ESTATE, "the first reset must reset every env");
     if (count == 0) return HE_OK;
     DeviceGuard dg(c.device);
     hipStream_t st = (hipStream_t)stream;
-    if (c.mode == HE_MODE_REPLAY) launch_reset<HE_MODE_REPLAY>(env, env_ids, count, obs_out, st);
-    else if (c.mode == HE_MODE_GBM) launch_reset<HE_MODE_GBM>(env, env_ids, count, obs_out, st);
-    else launch_reset<HE_MODE_HESTON>(env, env_ids, count, obs_out, st);
+    if (c.mode == HE_MODE_REPLAY) {
+        launch_reset<HE_MODE_REPLAY>(env, env_ids, count, obs_out, st);
+    } else {
+        if (env_ids) {
+            he_status s = materialize_market(env, st);
+            if (s != HE_OK) return s;
+        }
+        env->block_pos = c.market_block;  // tile regenerated on the next step
+        if (c.mode == HE_MODE_GBM) launch_reset<HE_MODE_GBM>(env, env_ids, count, obs_out, st);
+        else launch_reset<HE_MODE_HESTON>(env, env_ids, count, obs_out, st);
+    }
     HE_HIP(env, hipGetLastError());
+    env->ready = true;
     return HE_OK;
 }
 
@@ -1036,7 +1347,7 @@ he_status he_step(he_env* env, const float* actions, float* obs, float* reward, 
         const void* const* f = reinterpret_cast<const void* const*>(info);
         for (size_t k = 0; k < sizeof(he_info) / sizeof(void*); ++k) want_info |= f[k] != nullptr;
     }
-    return launch_any(env, io, want_info, 1, stream);
+    return launch_steps(env, io, want_info, 1, stream);
 }
 
 he_status he_rollout(he_env* env, int32_t k_steps, const float* actions, float* obs, float* reward,
@@ -1051,7 +1362,7 @@ he_status he_rollout(he_env* env, int32_t k_steps, const float* actions, float* 
     io.obs = obs;
     io.rew = reward;
     io.term = terminated;
-    return launch_any(env, io, false, k_steps, stream);
+    return launch_steps(env, io, false, k_steps, stream);
 }
 
 int64_t he_num_envs(const he_env* env) { return env ? env->cfg.n_envs : -1; }
@@ -1066,7 +1377,7 @@ he_status he_get_config(const he_env* env, he_config* out) {
 
 size_t he_state_size(const he_env* env) {
     if (!env) return 0;
-    size_t n = 0;
+    size_t n = 8;  // header: ready flag
     for (auto& f : env->fields) n += f.first;
     return n;
 }
@@ -1076,7 +1387,15 @@ he_status he_get_state(he_env* env, void* host_buf, size_t size) {
     if (size != he_state_size(env)) return fail(env, HE_EINVAL, "state buffer size %zu != %zu", size, he_state_size(env));
     DeviceGuard dg(env->cfg.device);
     HE_HIP(env, hipDeviceSynchronize());
+    if (is_generate(env)) {
+        he_status s = materialize_market(env, 0);
+        if (s != HE_OK) return s;
+        HE_HIP(env, hipDeviceSynchronize());
+    }
     char* dst = (char*)host_buf;
+    uint64_t hdr = env->ready ? 1u : 0u;
+    memcpy(dst, &hdr, 8);
+    dst += 8;
     for (auto& f : env->fields) {
         HE_HIP(env, hipMemcpy(dst, f.second, f.first, hipMemcpyDeviceToHost));
         dst += f.first;
@@ -1090,10 +1409,15 @@ he_status he_set_state(he_env* env, const void* host_buf, size_t size) {
     DeviceGuard dg(env->cfg.device);
     HE_HIP(env, hipDeviceSynchronize());
     const char* src = (const char*)host_buf;
+    uint64_t hdr;
+    memcpy(&hdr, src, 8);
+    src += 8;
     for (auto& f : env->fields) {
         HE_HIP(env, hipMemcpy(f.second, src, f.first, hipMemcpyHostToDevice));
         src += f.first;
     }
+    env->ready = hdr != 0;
+    env->block_pos = env->cfg.market_block;
     return HE_OK;
 }
 

@@ -101,7 +101,10 @@ typedef struct he_config {
     double heston_theta;
     double heston_xi;
     double heston_rho;
-    double reserved[8];
+    int32_t market_block;       /* generate modes: steps of market data generated per
+                                   market_kernel launch (1..64, default 64)          */
+    int32_t reserved_i;
+    double reserved[7];
 } he_config;
 
 /* Optional per-step info outputs (device pointers, each may be NULL).  Field names
