@@ -30,13 +30,15 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 # algorithmic HBM bytes per env-step of step_kernel<GBM> (DESIGN.md "Roofline"):
-#   reads : action 8 + state (S 8, C 4, P 4, cash 8, t 4, pos 4, ep 4) 36        = 44
-#   writes: state (S 8, C 4, P 4, cash 8, t 4, pos 4) 32 + obs 52 + reward 4
-#           + terminated 1 + truncated 1                                          = 90
-STEP_BYTES_PER_ENV = 134
-# he_rollout per env-step: action 8 + obs 52 + reward 4 + terminated 1 (+ state / K)
-ROLLOUT_BYTES_PER_ENV = 65
-ROLLOUT_STATE_BYTES = 36 + 32
+#   reads : state (t 4, pos 4, cash 8) 16 + action 8 + market tile slots
+#           (pre {S,v,C,P} 16, post {S,v,C,P} 16, post greeks 16) 48            = 72
+#   writes: state 16 + obs 52 + reward 4 + terminated 1 + truncated 1             = 74
+STEP_BYTES_PER_ENV = 146
+# market_kernel per env-step: tile {S,v,C,P} + greeks written (32) + per-block state
+MARKET_BYTES_PER_ENV = 32
+# he_rollout per env-step: action 8 + obs 52 + reward 4 + terminated 1 + tile read 32
+ROLLOUT_BYTES_PER_ENV = 97
+ROLLOUT_STATE_BYTES = 16 + 16 + 16
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 TRAIN_KW = dict(loss_type="abs", pnl_penalty_weight=0.001, lambda_cost=0.0001, theta_weight=0.0002,
@@ -135,6 +137,7 @@ def main():
                         launch(gi * C + j, cs)
                 graphs.append(gr)
         env.reset_tensors()
+        torch.cuda.synchronize()
 
     roll_obs = roll_rew = roll_term = None
     if args.mode == "rollout":
@@ -197,8 +200,10 @@ def main():
     dev_ms = ev0.elapsed_time(ev1)
 
     # live per-launch kernel duration: HIP events bracketing single launches on `stream`
-    nprobe = 200
+    # (the he_step of every 64th step also launches market_kernel for the next 64 steps)
+    nprobe = 256
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(nprobe)]
+    env.reset_tensors()
     torch.cuda.synchronize()
     with torch.cuda.stream(stream):
         for k in range(nprobe):
@@ -211,15 +216,23 @@ def main():
                 launch(k, stream.cuda_stream)
             evs[k][1].record(stream)
     torch.cuda.synchronize()
-    durs = np.array([a.elapsed_time(b) for a, b in evs[20:]])  # ms
-    kern_ms = float(np.median(durs))
+    durs = np.array([a.elapsed_time(b) for a, b in evs])  # ms
+    M = 64
+    if args.mode == "rollout":
+        kern_ms = float(np.median(durs[4:]))
+        mkt_ms = None
+    else:
+        with_mkt = durs[0::M][1:]
+        plain = np.delete(durs, np.arange(0, nprobe, M))[8:]
+        kern_ms = float(np.median(plain))
+        mkt_ms = float(np.median(with_mkt)) - kern_ms
 
     total_envs = n * world
     value = total_envs * K / wall
     if args.mode == "rollout":
         RK = args.rollout_k
         bytes_launch = n * RK * (ROLLOUT_BYTES_PER_ENV + ROLLOUT_STATE_BYTES / RK)
-        kname = "step_kernel<GBM> (K=%d fused)" % RK
+        kname = "step_kernel<GBM> (K=%d fused) + market_kernel" % RK
     else:
         bytes_launch = n * STEP_BYTES_PER_ENV
         kname = "step_kernel<GBM> (K=1)"
@@ -227,6 +240,9 @@ def main():
     roof = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
                 frac=round(achieved / HBM_PEAK_GBS, 4), traffic=None, kernel=kname,
                 kernel_us=round(kern_ms * 1e3, 3), bytes_per_launch=int(bytes_launch))
+    if mkt_ms is not None:
+        roof["market_kernel_us_per_64_steps"] = round(mkt_ms * 1e3, 3)
+        roof["market_kernel_us_per_step"] = round(mkt_ms * 1e3 / M, 3)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args.cpu_seconds)
