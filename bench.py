@@ -58,6 +58,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--seed", type=int, default=42)
+    ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC traffic pass")
+    ap.add_argument("--probe", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args()
 
 
@@ -85,9 +87,65 @@ def cpu_baseline(seconds):
                        f"({el:.1f} s, 1 thread, NumPy)")
 
 
+def probe(args):
+    """Short run for counter collection: 2 market blocks of eager he_step."""
+    torch.cuda.set_device(0)
+    from cantorrl_amd.vec_env import HedgingVecEnv
+    n = args.envs
+    env = HedgingVecEnv(n, mode="gbm", generate=GEN, seed=args.seed, return_numpy=False, info_keys=(),
+                        **TRAIN_KW)
+    env.reset_tensors()
+    acts = torch.rand((64, n, 2), device="cuda:0") * 2 - 1
+    for k in range(128):
+        env.step_tensors(acts[k % 64])
+    torch.cuda.synchronize()
+    env.close()
+
+
+def pmc_traffic(args):
+    """HBM bytes per step_kernel launch from rocprofv3 PMC counters, one counter per
+    pass (MI355X_MICROARCH.md "HBM": FETCH_SIZE reads 1/2 of a wide coalesced read on
+    gfx950, so bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024).  Runs BEFORE this process
+    touches the GPU; the profiled program is a child (`rocprofv3 ... -- python3`)."""
+    import csv
+    import glob
+    import shutil
+    import subprocess
+    import tempfile
+    if shutil.which("rocprofv3") is None:
+        return None, "rocprofv3 not found"
+    vals = {}
+    for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+        with tempfile.TemporaryDirectory(dir="/tmp") as td:
+            cmd = ["rocprofv3", "--pmc", ctr, "--output-format", "csv", "-d", td, "-o", "pmc", "--",
+                   sys.executable, os.path.abspath(__file__), "--probe", "--envs", str(args.envs)]
+            try:
+                subprocess.run(cmd, check=True, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
+                               timeout=240, cwd="/tmp", env=dict(os.environ, TMPDIR="/tmp"))
+            except Exception as e:  # noqa: BLE001
+                return None, f"rocprofv3 --pmc {ctr} failed: {e}"
+            rows = []
+            for f in glob.glob(os.path.join(td, "**", "*counter_collection.csv"), recursive=True):
+                with open(f) as fh:
+                    for r in csv.DictReader(fh):
+                        if "step_kernel" in r.get("Kernel_Name", "") and r.get("Counter_Name") == ctr:
+                            rows.append(float(r["Counter_Value"]))
+            if not rows:
+                return None, f"no {ctr} rows for step_kernel"
+            vals[ctr] = float(np.mean(rows[8:] if len(rows) > 16 else rows))
+    traffic = (2.0 * vals["FETCH_SIZE"] + vals["WRITE_SIZE"]) * 1024.0
+    return traffic, vals
+
+
 def main():
     args = parse()
+    if args.probe:
+        probe(args)
+        return
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    pmc = (None, "skipped")
+    if world == 1 and not args.no_pmc and args.mode != "rollout":
+        pmc = pmc_traffic(args)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
@@ -201,31 +259,36 @@ def main():
 
     # live per-launch kernel duration: HIP events bracketing single launches on `stream`
     # (the he_step of every 64th step also launches market_kernel for the next 64 steps)
+    # `kev` brackets exactly the step_kernel dispatch (he_time_next_step ->
+    # hipExtLaunchKernelGGL), `oev` the whole call (+ market_kernel every 64 steps)
     nprobe = 256
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(nprobe)]
+    mk = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
+    kev = [(mk(), mk()) for _ in range(nprobe)]
+    oev = [(mk(), mk()) for _ in range(nprobe)]
     env.reset_tensors()
     torch.cuda.synchronize()
     with torch.cuda.stream(stream):
         for k in range(nprobe):
-            evs[k][0].record(stream)
+            oev[k][0].record(stream)
+            lib.he_time_next_step(h, kev[k][0].cuda_event, kev[k][1].cuda_event)
             if args.mode == "rollout":
                 RK = args.rollout_k
                 lib.he_rollout(h, RK, acts[:RK].data_ptr(), roll_obs.data_ptr(), roll_rew.data_ptr(),
                                roll_term.data_ptr(), stream.cuda_stream)
             else:
                 launch(k, stream.cuda_stream)
-            evs[k][1].record(stream)
+            oev[k][1].record(stream)
     torch.cuda.synchronize()
-    durs = np.array([a.elapsed_time(b) for a, b in evs])  # ms
+    kd = np.array([a.elapsed_time(b) for a, b in kev])  # ms
+    od = np.array([a.elapsed_time(b) for a, b in oev])
     M = 64
     if args.mode == "rollout":
-        kern_ms = float(np.median(durs[4:]))
-        mkt_ms = None
+        kern_ms = float(np.mean(kd[4:]))
+        mkt_ms = float(np.mean(od[4:] - kd[4:]))
     else:
-        with_mkt = durs[0::M][1:]
-        plain = np.delete(durs, np.arange(0, nprobe, M))[8:]
-        kern_ms = float(np.median(plain))
-        mkt_ms = float(np.median(with_mkt)) - kern_ms
+        idx = np.arange(8, nprobe)
+        kern_ms = float(np.mean(kd[idx]))
+        mkt_ms = float(np.median(od[0::M][1:] - kd[0::M][1:]))
 
     total_envs = n * world
     value = total_envs * K / wall
@@ -243,6 +306,11 @@ def main():
     if mkt_ms is not None:
         roof["market_kernel_us_per_64_steps"] = round(mkt_ms * 1e3, 3)
         roof["market_kernel_us_per_step"] = round(mkt_ms * 1e3 / M, 3)
+    if pmc[0] is not None:
+        roof["traffic"] = int(pmc[0])
+        roof["traffic_counters_kb"] = {k: round(v, 1) for k, v in pmc[1].items()}
+    else:
+        roof["traffic_note"] = pmc[1]
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args.cpu_seconds)

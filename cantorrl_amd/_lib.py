@@ -86,7 +86,7 @@ EXPORTS = [
     "he_config_init", "he_create", "he_destroy", "he_last_error", "he_version", "he_load_paths",
     "he_seed", "he_reset", "he_step", "he_rollout", "he_num_envs", "he_episode_length",
     "he_num_episodes", "he_get_config", "he_state_size", "he_get_state", "he_set_state",
-    "he_pcg64_seed_state", "he_host_episode_draws", "he_host_philox",
+    "he_pcg64_seed_state", "he_host_episode_draws", "he_host_philox", "he_time_next_step",
 ]
 
 _lib = None
@@ -132,6 +132,7 @@ def load(path=LIB_PATH):
         "he_pcg64_seed_state": (i32, [u64, ctypes.POINTER(ctypes.c_uint64 * 4)]),
         "he_host_episode_draws": (i32, [u64, u64, i64, vp]),
         "he_host_philox": (i32, [u64, u64, u64, ctypes.POINTER(ctypes.c_uint32 * 4)]),
+        "he_time_next_step": (i32, [vp, vp, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

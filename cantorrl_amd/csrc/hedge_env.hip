@@ -22,6 +22,7 @@
 // Replay mode reuses step_kernel: its market source is the loaded table
 // [paths][T+1] {S, v, C, P} (+ greeks precomputed once at load time).
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <math.h>
 #include <stdarg.h>
@@ -818,6 +819,8 @@ struct he_env {
     int64_t n_paths = 0;
     int32_t block_pos = 0;    // generate: next slot to consume; M = tile exhausted/invalid
     bool ready = false;       // a reset happened since create/seed
+    void* ev_start = nullptr; // he_time_next_step events (hipEvent_t)
+    void* ev_stop = nullptr;
     std::vector<std::pair<size_t, void*>> fields;  // (bytes, device ptr) for get/set_state
 };
 
@@ -986,6 +989,17 @@ static void launch_reset(he_env* env, const int64_t* ids, int64_t count, float* 
 template <int MODE>
 static void launch_step(he_env* env, const Io& io, bool info, int k, int slot0, hipStream_t st) {
     int64_t blocks = (env->cfg.n_envs + kBlock - 1) / kBlock;
+    if (env->ev_start) {  // one-shot: bracket exactly this dispatch (hipExtLaunchKernelGGL)
+        hipEvent_t a = (hipEvent_t)env->ev_start, b = (hipEvent_t)env->ev_stop;
+        env->ev_start = env->ev_stop = nullptr;
+        if (info)
+            hipExtLaunchKernelGGL((step_kernel<MODE, true>), dim3((unsigned)blocks), dim3(kBlock), 0, st, a, b,
+                                  0, env->p, env->s, io, k, slot0);
+        else
+            hipExtLaunchKernelGGL((step_kernel<MODE, false>), dim3((unsigned)blocks), dim3(kBlock), 0, st, a, b,
+                                  0, env->p, env->s, io, k, slot0);
+        return;
+    }
     if (info)
         hipLaunchKernelGGL((step_kernel<MODE, true>), dim3((unsigned)blocks), dim3(kBlock), 0, st, env->p,
                            env->s, io, k, slot0);
@@ -1363,6 +1377,15 @@ he_status he_rollout(he_env* env, int32_t k_steps, const float* actions, float* 
     io.rew = reward;
     io.term = terminated;
     return launch_steps(env, io, false, k_steps, stream);
+}
+
+he_status he_time_next_step(he_env* env, void* start_event, void* stop_event) {
+    if (!env) return HE_EINVAL;
+    if ((start_event == nullptr) != (stop_event == nullptr))
+        return fail(env, HE_EINVAL, "pass both events or neither");
+    env->ev_start = start_event;
+    env->ev_stop = stop_event;
+    return HE_OK;
 }
 
 int64_t he_num_envs(const he_env* env) { return env ? env->cfg.n_envs : -1; }

@@ -181,6 +181,12 @@ he_status he_step(he_env* env, const float* actions, float* obs, float* reward,
 he_status he_rollout(he_env* env, int32_t k_steps, const float* actions, float* obs,
                      float* reward, uint8_t* terminated, void* stream);
 
+/* Measurement: the next step_kernel dispatch (he_step / he_rollout) records
+ * start_event / stop_event (opaque hipEvent_t) around exactly that dispatch
+ * (hipExtLaunchKernelGGL), so hipEventElapsedTime gives the kernel's own duration
+ * without the launch gaps.  One-shot; NULL, NULL cancels. */
+he_status he_time_next_step(he_env* env, void* start_event, void* stop_event);
+
 /* Introspection. */
 int64_t he_num_envs(const he_env* env);
 int32_t he_episode_length(const he_env* env);
