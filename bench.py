@@ -183,19 +183,26 @@ def main():
     W = args.warmup
     graphs = []
     if args.mode == "graph":
-        C = args.graph_chunk
-        # capture `ring // C` graphs of C steps each, covering the whole action ring
+        C = args.graph_chunk  # == market block: every graph = one block of steps
+        K = -(-K // C) * C
+        W = -(-W // C) * C
         with torch.cuda.stream(stream):
+            # one eager block first, so each captured graph is the steady state
+            # [fork: market_kernel(b+1) on the side stream || C x step_kernel(b)] + join
+            for j in range(C):
+                launch(j, stream.cuda_stream)
+            env.sync_market()
+            torch.cuda.synchronize()
             for gi in range(ring // C):
                 gr = torch.cuda.CUDAGraph()
-                torch.cuda.synchronize()
                 with torch.cuda.graph(gr, stream=stream):
                     cs = torch.cuda.current_stream().cuda_stream
                     for j in range(C):
                         launch(gi * C + j, cs)
+                    env.sync_market()
                 graphs.append(gr)
-        env.reset_tensors()
         torch.cuda.synchronize()
+        # device state = after the eager block; graphs replay in capture order from here
 
     roll_obs = roll_rew = roll_term = None
     if args.mode == "rollout":
@@ -204,20 +211,18 @@ def main():
         roll_rew = torch.empty((RK, n), dtype=torch.float32, device=dev)
         roll_term = torch.empty((RK, n), dtype=torch.uint8, device=dev)
 
+    replays = [0]
+
     def run(steps, s):
         """Enqueue `steps` env-steps on stream s."""
         done = 0
         cs = s.cuda_stream
         while done < steps:
             if args.mode == "graph":
-                C = args.graph_chunk
-                gi = (done // C) % len(graphs)
-                if steps - done >= C:
-                    graphs[gi].replay()
-                    done += C
-                else:
-                    launch(done, cs)
-                    done += 1
+                # K, W are multiples of the chunk; graphs replay in capture order
+                graphs[replays[0] % len(graphs)].replay()
+                replays[0] += 1
+                done += args.graph_chunk
             elif args.mode == "eager":
                 launch(done, cs)
                 done += 1
@@ -262,33 +267,73 @@ def main():
     # `kev` brackets exactly the step_kernel dispatch (he_time_next_step ->
     # hipExtLaunchKernelGGL), `oev` the whole call (+ market_kernel every 64 steps)
     nprobe = 256
-    mk = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so.7")  # the HIP runtime torch (and libhedgeenv) use
+
+    def mk():
+        e = ctypes.c_void_p()
+        if hip.hipEventCreate(ctypes.byref(e)) != 0:
+            raise RuntimeError("hipEventCreate failed")
+        return e
+
+    def elapsed(a, b):
+        ms = ctypes.c_float()
+        if hip.hipEventElapsedTime(ctypes.byref(ms), a, b) != 0:
+            raise RuntimeError("hipEventElapsedTime failed")
+        return ms.value
+
     kev = [(mk(), mk()) for _ in range(nprobe)]
     oev = [(mk(), mk()) for _ in range(nprobe)]
     env.reset_tensors()
     torch.cuda.synchronize()
+    sh = ctypes.c_void_p(stream.cuda_stream)
     with torch.cuda.stream(stream):
         for k in range(nprobe):
-            oev[k][0].record(stream)
-            lib.he_time_next_step(h, kev[k][0].cuda_event, kev[k][1].cuda_event)
+            hip.hipEventRecord(oev[k][0], sh)
+            lib.he_time_next_step(h, kev[k][0], kev[k][1])
             if args.mode == "rollout":
                 RK = args.rollout_k
                 lib.he_rollout(h, RK, acts[:RK].data_ptr(), roll_obs.data_ptr(), roll_rew.data_ptr(),
                                roll_term.data_ptr(), stream.cuda_stream)
             else:
                 launch(k, stream.cuda_stream)
-            oev[k][1].record(stream)
+            hip.hipEventRecord(oev[k][1], sh)
     torch.cuda.synchronize()
-    kd = np.array([a.elapsed_time(b) for a, b in kev])  # ms
-    od = np.array([a.elapsed_time(b) for a, b in oev])
+    kd = np.array([elapsed(a, b) for a, b in kev])  # ms
+    od = np.array([elapsed(a, b) for a, b in oev])
+    for a, b in kev + oev:
+        hip.hipEventDestroy(a)
+        hip.hipEventDestroy(b)
     M = 64
     if args.mode == "rollout":
         kern_ms = float(np.mean(kd[4:]))
-        mkt_ms = float(np.mean(od[4:] - kd[4:]))
+        mkt_ms = None  # prefetched on the side stream (see graph-mode probe)
     else:
         idx = np.arange(8, nprobe)
         kern_ms = float(np.mean(kd[idx]))
-        mkt_ms = float(np.median(od[0::M][1:] - kd[0::M][1:]))
+        # market_kernel is prefetched on the library's side stream here; time it on a
+        # handle without prefetch, where it runs inside the he_step of a block boundary
+        env2 = HedgingVecEnv(n, mode="gbm", generate=GEN, seed=args.seed, device=dev, return_numpy=False,
+                             info_keys=(), market_prefetch=False, **TRAIN_KW)
+        env2.reset_tensors()
+        m = []
+        with torch.cuda.stream(stream):
+            for k in range(4 * M):
+                a, b = mk(), mk()
+                hip.hipEventRecord(a, sh)
+                st2 = lib.he_step(env2._h, acts[k % ring].data_ptr(), env2._obs.data_ptr(), env2._rew.data_ptr(),
+                                  env2._term.data_ptr(), env2._trunc.data_ptr(), None, None, stream.cuda_stream)
+                hip.hipEventRecord(b, sh)
+                if st2:
+                    raise RuntimeError(lib.he_last_error(env2._h).decode())
+                m.append((a, b))
+        torch.cuda.synchronize()
+        d2 = np.array([elapsed(a, b) for a, b in m])
+        for a, b in m:
+            hip.hipEventDestroy(a)
+            hip.hipEventDestroy(b)
+        mkt_ms = float(np.median(d2[M::M])) - float(np.median(np.delete(d2, np.arange(0, 4 * M, M))))
+        env2.close()
 
     total_envs = n * world
     value = total_envs * K / wall

@@ -87,6 +87,7 @@ EXPORTS = [
     "he_seed", "he_reset", "he_step", "he_rollout", "he_num_envs", "he_episode_length",
     "he_num_episodes", "he_get_config", "he_state_size", "he_get_state", "he_set_state",
     "he_pcg64_seed_state", "he_host_episode_draws", "he_host_philox", "he_time_next_step",
+    "he_sync_market",
 ]
 
 _lib = None
@@ -133,6 +134,7 @@ def load(path=LIB_PATH):
         "he_host_episode_draws": (i32, [u64, u64, i64, vp]),
         "he_host_philox": (i32, [u64, u64, u64, ctypes.POINTER(ctypes.c_uint32 * 4)]),
         "he_time_next_step": (i32, [vp, vp, vp]),
+        "he_sync_market": (i32, [vp, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

@@ -55,7 +55,7 @@ struct Params {
     int32_t mt, maxh;
     float mt_f, maxh_f, T_f;
     float init_cash_f;
-    double tcpc, slip_frac, lam, w, initial_cash;
+    double tcpc, slip_frac, lam, w, theta, initial_cash;
     double shares_d;
     float shares_f;
     int32_t shares_zero;
@@ -488,7 +488,8 @@ __device__ __forceinline__ void step_env(const Params& p, Env& e, const Mkt& pre
     double tcp = p.lam * tc;
     double thp = 0.0, reward;
     if (p.variant == 2) {
-        thp = p.thp_tab[e.t > (uint32_t)p.T ? p.T : e.t];
+        // computed, not looked up: a table load indexed by t is a dependent round trip
+        thp = p.theta * ((double)(p.T - (int32_t)e.t) / 252.0);
         reward = (rpc - tcp) - thp;
     } else {
         reward = rpc - tcp;
@@ -586,6 +587,9 @@ __device__ __forceinline__ void env_reset_common(const Params& p, Env& e) {
 template <int MODE, bool INFO>
 __global__ __launch_bounds__(kBlock) void step_kernel(Params p, State s, Io io, int k_steps, int slot0) {
     constexpr bool REPLAY = (MODE == HE_MODE_REPLAY);
+    // latency-critical: win VALU/memory issue arbitration against the prefetching
+    // market_kernel waves that share the SIMDs (they run at the default priority 0)
+    __builtin_amdgcn_s_setprio(3);
     __shared__ __attribute__((aligned(16))) float tile[kBlock * kObs];
     const int64_t row0 = (int64_t)blockIdx.x * kBlock;
     const int64_t i = row0 + threadIdx.x;
@@ -611,8 +615,9 @@ __global__ __launch_bounds__(kBlock) void step_kernel(Params p, State s, Io io, 
             float s0f = p.rst[0];
             e.s0_small = s0f < 1e-6f;
             e.s0 = e.s0_small ? 1.0f : s0f;
-            pre = (e.t == 0) ? Mkt{p.rst[0], p.rst[1], p.rst[2], p.rst[3]}
-                             : as_mkt(p.tileA[(int64_t)slot0 * N + i]);
+            // unconditional load (no t -> load dependency), select afterwards
+            Mkt tp = as_mkt(p.tileA[(int64_t)slot0 * N + i]);
+            pre = (e.t == 0) ? Mkt{p.rst[0], p.rst[1], p.rst[2], p.rst[3]} : tp;
         }
     }
     bool reset_any = false;
@@ -807,17 +812,23 @@ struct he_env {
     he_config cfg;
     Params p;
     State s;
-    Market cur, bak;
+    Market cur;               // market position after the newest generated block
+    Market bak[2];            // start position of the block held in tile buffer b
     std::string err;
     void* state_mem = nullptr;
     size_t state_bytes = 0;
     float4* rec = nullptr;
     float4* recg = nullptr;
-    float4* tile = nullptr;   // tileA | tileB
+    float4* tile = nullptr;   // 2 buffers x (tileA | tileB)
     double* thp = nullptr;    // theta table [T+1]
     float* rst = nullptr;     // reset market + obs (generate)
     int64_t n_paths = 0;
     int32_t block_pos = 0;    // generate: next slot to consume; M = tile exhausted/invalid
+    int32_t cur_buf = 0;      // tile buffer of the block being consumed
+    int32_t next_state = 0;   // next block: 0 none, 1 generating on `xs` (ev_next), 2 ready
+    bool prefetch = true;     // generate block b+1 on `xs` while block b is stepped
+    hipStream_t xs = nullptr; // library side stream for market prefetch
+    hipEvent_t ev_fork = nullptr, ev_next = nullptr;
     bool ready = false;       // a reset happened since create/seed
     void* ev_start = nullptr; // he_time_next_step events (hipEvent_t)
     void* ev_stop = nullptr;
@@ -863,6 +874,7 @@ static void fill_params(he_env* env) {
     p.slip_frac = c.slippage_bps / 10000.0;
     p.lam = c.lambda_cost;
     p.w = c.pnl_penalty_weight;
+    p.theta = c.theta_weight;
     p.initial_cash = c.initial_cash;
     p.shares_d = (double)c.shares_to_hedge;
     p.shares_f = (float)c.shares_to_hedge;
@@ -907,10 +919,7 @@ static void fill_params(he_env* env) {
     p.T = c.episode_length;
     p.T_f = (float)c.episode_length;
     p.M = c.market_block;
-    if (env->tile) {
-        p.tileA = env->tile;
-        p.tileB = env->tile + (size_t)(c.market_block + 1) * (size_t)c.n_envs;
-    }
+    p.tileA = p.tileB = nullptr;  // set per launch (tile_params)
     p.rst = env->rst;
     p.rec = env->rec;
     p.recg = env->recg;
@@ -941,41 +950,67 @@ static he_status upload_tables(he_env* env) {
     return HE_OK;
 }
 
-template <int MODE>
-static void launch_market(he_env* env, int32_t advance_only, hipStream_t st) {
-    int64_t blocks = (env->cfg.n_envs + kMktEnvs - 1) / kMktEnvs;
-    hipLaunchKernelGGL(market_kernel<MODE>, dim3((unsigned)blocks), dim3(kMktEnvs * kMktLanes), 0, st, env->p,
-                       env->cur, env->bak, advance_only);
+// Params with the tile pointers of buffer b.
+static Params tile_params(const he_env* env, int b) {
+    Params p = env->p;
+    const size_t slots = (size_t)(env->cfg.market_block + 1) * (size_t)env->cfg.n_envs;
+    p.tileA = env->tile + (size_t)b * 2 * slots;
+    p.tileB = p.tileA + slots;
+    return p;
 }
 
-static he_status market(he_env* env, int32_t advance_only, hipStream_t st) {
-    if (env->cfg.mode == HE_MODE_GBM) launch_market<HE_MODE_GBM>(env, advance_only, st);
-    else launch_market<HE_MODE_HESTON>(env, advance_only, st);
+template <int MODE>
+static void launch_market(he_env* env, int32_t advance_only, int buf, hipStream_t st) {
+    int64_t blocks = (env->cfg.n_envs + kMktEnvs - 1) / kMktEnvs;
+    hipLaunchKernelGGL(market_kernel<MODE>, dim3((unsigned)blocks), dim3(kMktEnvs * kMktLanes), 0, st,
+                       tile_params(env, buf), env->cur, env->bak[buf], advance_only);
+}
+
+// generate the block that follows `cur` into tile buffer `buf` (advance_only = 0),
+// or rewind `cur` to `advance_only` steps past the start of buffer `buf`'s block.
+static he_status market(he_env* env, int32_t advance_only, int buf, hipStream_t st) {
+    if (env->cfg.mode == HE_MODE_GBM) launch_market<HE_MODE_GBM>(env, advance_only, buf, st);
+    else launch_market<HE_MODE_HESTON>(env, advance_only, buf, st);
     HE_HIP(env, hipGetLastError());
     return HE_OK;
 }
 
+// Make stream st wait for a pending prefetch on the side stream (join).
+static he_status join_prefetch(he_env* env, hipStream_t st) {
+    if (env->next_state == 1) {
+        HE_HIP(env, hipStreamWaitEvent(st, env->ev_next, 0));
+        env->next_state = 2;
+    }
+    return HE_OK;
+}
+
 // Bring `cur` to the position the envs are actually at (mid-block rewind) and
-// invalidate the tile.  Needed before partial resets and checkpoints.
+// drop every generated block.  Needed before partial resets and checkpoints.
 static he_status materialize_market(he_env* env, hipStream_t st) {
     const int32_t M = env->cfg.market_block;
-    if (env->block_pos < M) {
-        if (env->block_pos > 0) {
-            he_status s = market(env, env->block_pos, st);
+    he_status s = join_prefetch(env, st);
+    if (s != HE_OK) return s;
+    const bool generated_ahead = env->next_state != 0;
+    if (env->block_pos < M || generated_ahead) {
+        const int b = env->cur_buf;
+        if (env->block_pos < M && env->block_pos > 0) {
+            s = market(env, env->block_pos, b, st);
             if (s != HE_OK) return s;
         } else {
-            // no step consumed yet: the current position is the block start
+            // the current position is a block start: restore it from that block's bak
+            const int bb = (env->block_pos >= M) ? (b ^ 1) : b;
+            const Market& src = env->bak[bb];
             const int64_t N = env->cfg.n_envs;
-            HE_HIP(env, hipMemcpyAsync(env->cur.ep, env->bak.ep, N * 4, hipMemcpyDeviceToDevice, st));
-            HE_HIP(env, hipMemcpyAsync(env->cur.t, env->bak.t, N * 4, hipMemcpyDeviceToDevice, st));
-            HE_HIP(env, hipMemcpyAsync(env->cur.S, env->bak.S, N * 8, hipMemcpyDeviceToDevice, st));
-            HE_HIP(env, hipMemcpyAsync(env->cur.C, env->bak.C, N * 4, hipMemcpyDeviceToDevice, st));
-            HE_HIP(env, hipMemcpyAsync(env->cur.P, env->bak.P, N * 4, hipMemcpyDeviceToDevice, st));
-            if (env->cur.v)
-                HE_HIP(env, hipMemcpyAsync(env->cur.v, env->bak.v, N * 8, hipMemcpyDeviceToDevice, st));
+            HE_HIP(env, hipMemcpyAsync(env->cur.ep, src.ep, N * 4, hipMemcpyDeviceToDevice, st));
+            HE_HIP(env, hipMemcpyAsync(env->cur.t, src.t, N * 4, hipMemcpyDeviceToDevice, st));
+            HE_HIP(env, hipMemcpyAsync(env->cur.S, src.S, N * 8, hipMemcpyDeviceToDevice, st));
+            HE_HIP(env, hipMemcpyAsync(env->cur.C, src.C, N * 4, hipMemcpyDeviceToDevice, st));
+            HE_HIP(env, hipMemcpyAsync(env->cur.P, src.P, N * 4, hipMemcpyDeviceToDevice, st));
+            if (env->cur.v) HE_HIP(env, hipMemcpyAsync(env->cur.v, src.v, N * 8, hipMemcpyDeviceToDevice, st));
         }
     }
     env->block_pos = M;
+    env->next_state = 0;
     return HE_OK;
 }
 
@@ -987,25 +1022,53 @@ static void launch_reset(he_env* env, const int64_t* ids, int64_t count, float* 
 }
 
 template <int MODE>
-static void launch_step(he_env* env, const Io& io, bool info, int k, int slot0, hipStream_t st) {
+static void launch_step(he_env* env, const Params& p, const Io& io, bool info, int k, int slot0,
+                        hipStream_t st) {
     int64_t blocks = (env->cfg.n_envs + kBlock - 1) / kBlock;
     if (env->ev_start) {  // one-shot: bracket exactly this dispatch (hipExtLaunchKernelGGL)
         hipEvent_t a = (hipEvent_t)env->ev_start, b = (hipEvent_t)env->ev_stop;
         env->ev_start = env->ev_stop = nullptr;
         if (info)
             hipExtLaunchKernelGGL((step_kernel<MODE, true>), dim3((unsigned)blocks), dim3(kBlock), 0, st, a, b,
-                                  0, env->p, env->s, io, k, slot0);
+                                  0, p, env->s, io, k, slot0);
         else
             hipExtLaunchKernelGGL((step_kernel<MODE, false>), dim3((unsigned)blocks), dim3(kBlock), 0, st, a, b,
-                                  0, env->p, env->s, io, k, slot0);
+                                  0, p, env->s, io, k, slot0);
         return;
     }
     if (info)
-        hipLaunchKernelGGL((step_kernel<MODE, true>), dim3((unsigned)blocks), dim3(kBlock), 0, st, env->p,
-                           env->s, io, k, slot0);
+        hipLaunchKernelGGL((step_kernel<MODE, true>), dim3((unsigned)blocks), dim3(kBlock), 0, st, p, env->s,
+                           io, k, slot0);
     else
-        hipLaunchKernelGGL((step_kernel<MODE, false>), dim3((unsigned)blocks), dim3(kBlock), 0, st, env->p,
-                           env->s, io, k, slot0);
+        hipLaunchKernelGGL((step_kernel<MODE, false>), dim3((unsigned)blocks), dim3(kBlock), 0, st, p, env->s,
+                           io, k, slot0);
+}
+
+// Start the next block: make its market tile current (generated ahead on the side
+// stream, or now on `st`), then prefetch the block after it on the side stream so
+// that market_kernel(b+1) runs concurrently with the step kernels of block b.
+static he_status advance_block(he_env* env, hipStream_t st) {
+    const int nb = env->cur_buf ^ 1;
+    if (env->next_state == 0) {
+        he_status s = market(env, 0, nb, st);
+        if (s != HE_OK) return s;
+    } else {
+        he_status s = join_prefetch(env, st);
+        if (s != HE_OK) return s;
+    }
+    env->cur_buf = nb;
+    env->block_pos = 0;
+    env->next_state = 0;
+    if (env->prefetch) {
+        // fork: the side stream starts after everything already enqueued on st
+        HE_HIP(env, hipEventRecord(env->ev_fork, st));
+        HE_HIP(env, hipStreamWaitEvent(env->xs, env->ev_fork, 0));
+        he_status s = market(env, 0, nb ^ 1, env->xs);
+        if (s != HE_OK) return s;
+        HE_HIP(env, hipEventRecord(env->ev_next, env->xs));
+        env->next_state = 1;
+    }
+    return HE_OK;
 }
 
 static he_status launch_steps(he_env* env, Io io, bool info, int k_total, void* stream) {
@@ -1015,7 +1078,7 @@ static he_status launch_steps(he_env* env, Io io, bool info, int k_total, void* 
     DeviceGuard dg(c.device);
     hipStream_t st = (hipStream_t)stream;
     if (c.mode == HE_MODE_REPLAY) {
-        launch_step<HE_MODE_REPLAY>(env, io, info, k_total, 0, st);
+        launch_step<HE_MODE_REPLAY>(env, env->p, io, info, k_total, 0, st);
         HE_HIP(env, hipGetLastError());
         return HE_OK;
     }
@@ -1024,9 +1087,8 @@ static he_status launch_steps(he_env* env, Io io, bool info, int k_total, void* 
     int done = 0;
     while (done < k_total) {
         if (env->block_pos >= M) {
-            he_status s = market(env, 0, st);
+            he_status s = advance_block(env, st);
             if (s != HE_OK) return s;
-            env->block_pos = 0;
         }
         int k = k_total - done;
         if (k > M - env->block_pos) k = M - env->block_pos;
@@ -1035,8 +1097,9 @@ static he_status launch_steps(he_env* env, Io io, bool info, int k_total, void* 
         if (io.obs) sub.obs = io.obs + (int64_t)done * N * kObs;
         if (io.rew) sub.rew = io.rew + (int64_t)done * N;
         if (io.term) sub.term = io.term + (int64_t)done * N;
-        if (c.mode == HE_MODE_GBM) launch_step<HE_MODE_GBM>(env, sub, info, k, env->block_pos, st);
-        else launch_step<HE_MODE_HESTON>(env, sub, info, k, env->block_pos, st);
+        Params p = tile_params(env, env->cur_buf);
+        if (c.mode == HE_MODE_GBM) launch_step<HE_MODE_GBM>(env, p, sub, info, k, env->block_pos, st);
+        else launch_step<HE_MODE_HESTON>(env, p, sub, info, k, env->block_pos, st);
         HE_HIP(env, hipGetLastError());
         env->block_pos += k;
         done += k;
@@ -1134,8 +1197,8 @@ he_status he_create(const he_config* cfg, he_env** out) {
         fs.push_back({(size_t)N * 32, (void**)&env->s.pcg, true});
         fs.push_back({(size_t)N * 8, (void**)&env->s.pcgb, true});
     } else {
-        Market* ms[2] = {&env->cur, &env->bak};
-        for (int k = 0; k < 2; ++k) {
+        Market* ms[3] = {&env->cur, &env->bak[0], &env->bak[1]};
+        for (int k = 0; k < 3; ++k) {
             fs.push_back({(size_t)N * 4, (void**)&ms[k]->ep, k == 0});
             fs.push_back({(size_t)N * 4, (void**)&ms[k]->t, k == 0});
             fs.push_back({(size_t)N * 8, (void**)&ms[k]->S, k == 0});
@@ -1159,11 +1222,15 @@ he_status he_create(const he_config* cfg, he_env** out) {
     }
     HE_HIP(env, hipMemset(mem, 0, total));
     if (is_generate(env)) {
-        size_t tb = (size_t)2 * (size_t)(c.market_block + 1) * (size_t)N * sizeof(float4);
+        size_t tb = (size_t)4 * (size_t)(c.market_block + 1) * (size_t)N * sizeof(float4);
         e = hipMalloc(&env->tile, tb);
         if (e != hipSuccess) return fail(env, HE_ENOMEM, "hipMalloc(tile %zu) failed: %s", tb, hipGetErrorString(e));
         HE_HIP(env, hipMalloc(&env->rst, 32 * sizeof(float)));
         env->block_pos = c.market_block;
+        env->prefetch = c.reserved_i == 0;  // market_prefetch: on unless disabled
+        HE_HIP(env, hipStreamCreateWithFlags(&env->xs, hipStreamNonBlocking));
+        HE_HIP(env, hipEventCreateWithFlags(&env->ev_fork, hipEventDisableTiming));
+        HE_HIP(env, hipEventCreateWithFlags(&env->ev_next, hipEventDisableTiming));
     }
     he_status st = upload_tables(env);
     if (st != HE_OK) return st;
@@ -1187,6 +1254,12 @@ he_status he_destroy(he_env* env) {
         if (env->tile) (void)hipFree(env->tile);
         if (env->thp) (void)hipFree(env->thp);
         if (env->rst) (void)hipFree(env->rst);
+        if (env->xs) {
+            (void)hipStreamSynchronize(env->xs);
+            (void)hipStreamDestroy(env->xs);
+        }
+        if (env->ev_fork) (void)hipEventDestroy(env->ev_fork);
+        if (env->ev_next) (void)hipEventDestroy(env->ev_next);
     }
     delete env;
     return HE_OK;
@@ -1330,11 +1403,12 @@ he_status he_reset(he_env* env, const int64_t* env_ids, int64_t count, float* ob
     if (c.mode == HE_MODE_REPLAY) {
         launch_reset<HE_MODE_REPLAY>(env, env_ids, count, obs_out, st);
     } else {
-        if (env_ids) {
-            he_status s = materialize_market(env, st);
-            if (s != HE_OK) return s;
-        }
-        env->block_pos = c.market_block;  // tile regenerated on the next step
+        // partial reset: every other env keeps its market position (rewind); full
+        // reset: only wait for a pending prefetch, which writes `cur` too
+        he_status s = env_ids ? materialize_market(env, st) : join_prefetch(env, st);
+        if (s != HE_OK) return s;
+        env->block_pos = c.market_block;  // tiles regenerated on the next step
+        env->next_state = 0;
         if (c.mode == HE_MODE_GBM) launch_reset<HE_MODE_GBM>(env, env_ids, count, obs_out, st);
         else launch_reset<HE_MODE_HESTON>(env, env_ids, count, obs_out, st);
     }
@@ -1377,6 +1451,13 @@ he_status he_rollout(he_env* env, int32_t k_steps, const float* actions, float* 
     io.rew = reward;
     io.term = terminated;
     return launch_steps(env, io, false, k_steps, stream);
+}
+
+he_status he_sync_market(he_env* env, void* stream) {
+    if (!env) return HE_EINVAL;
+    if (!is_generate(env)) return HE_OK;
+    DeviceGuard dg(env->cfg.device);
+    return join_prefetch(env, (hipStream_t)stream);
 }
 
 he_status he_time_next_step(he_env* env, void* start_event, void* stop_event) {

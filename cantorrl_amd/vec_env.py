@@ -11,6 +11,7 @@ env_method, env_is_wrapped) with SB3's auto-reset semantics
 Every env's state lives on the device; one `he_step` launch advances all of
 them.  `step_tensors` is the zero-copy path for GPU-resident learners.
 """
+import os
 import time
 
 import numpy as np
@@ -71,7 +72,7 @@ class HedgingVecEnv:
     def __init__(self, n_envs, data_file_path=None, *, tables=None, variant=2, mode=None,
                  generate=None, device=None, seed=None, global_env_offset=0, autoreset=True,
                  return_numpy=True, info_keys=MONITOR_KEYWORDS, monitor_keywords=None,
-                 **env_kwargs):
+                 market_block=64, market_prefetch=True, **env_kwargs):
         self.lib = _lib.load()
         self.num_envs = int(n_envs)
         self.variant = int(variant)
@@ -121,6 +122,10 @@ class HedgingVecEnv:
         cfg.heston_theta = float(gen["heston_theta"])
         cfg.heston_xi = float(gen["heston_xi"])
         cfg.heston_rho = float(gen["heston_rho"])
+        cfg.market_block = int(market_block)
+        if os.environ.get("CANTORRL_NO_PREFETCH"):
+            market_prefetch = False
+        cfg.reserved_i = 0 if market_prefetch else 1
         base_seed = int(seed if seed is not None else gen.get("seed", 42))
         cfg.seed = base_seed
         self._cfg = cfg
@@ -284,6 +289,11 @@ class HedgingVecEnv:
     def step(self, actions):
         self.step_async(actions)
         return self.step_wait()
+
+    def sync_market(self):
+        """Join the library's market prefetch into the current stream (call before
+        ending a hipGraph capture that contains steps)."""
+        _lib.check(self.lib, self._h, self.lib.he_sync_market(self._h, self.stream), "he_sync_market")
 
     def rollout(self, actions, obs=None, reward=None, terminated=None):
         """K fused steps: actions [K,N,2] device tensor -> writes obs [K,N,13],

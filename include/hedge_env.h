@@ -103,7 +103,7 @@ typedef struct he_config {
     double heston_rho;
     int32_t market_block;       /* generate modes: steps of market data generated per
                                    market_kernel launch (1..64, default 64)          */
-    int32_t reserved_i;
+    int32_t reserved_i;         /* 1: disable market prefetch on the side stream     */
     double reserved[7];
 } he_config;
 
@@ -180,6 +180,12 @@ he_status he_step(he_env* env, const float* actions, float* obs, float* reward,
  * be NULL to skip).  Per-env state stays in registers across the K steps. */
 he_status he_rollout(he_env* env, int32_t k_steps, const float* actions, float* obs,
                      float* reward, uint8_t* terminated, void* stream);
+
+/* Generate modes run market_kernel for block b+1 on a library-owned side stream
+ * while the step kernels of block b run on `stream`.  he_sync_market makes `stream`
+ * wait for that prefetch (a join): call it before ending a hipGraph capture that
+ * contains he_step/he_rollout calls.  No-op in replay mode. */
+he_status he_sync_market(he_env* env, void* stream);
 
 /* Measurement: the next step_kernel dispatch (he_step / he_rollout) records
  * start_event / stop_event (opaque hipEvent_t) around exactly that dispatch
