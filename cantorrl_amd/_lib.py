@@ -75,6 +75,7 @@ INFO_FIELDS = [
     ("initial_S0_for_episode", "f4"),
     ("current_stock_price", "f4"), ("current_volatility", "f4"),
     ("current_call_price", "f4"), ("current_put_price", "f4"), ("current_step", "i4"),
+    ("current_episode_idx", "i4"),
 ]
 
 
@@ -120,7 +121,7 @@ def load(path=LIB_PATH):
         "he_version": (ctypes.c_char_p, []),
         "he_load_paths": (i32, [vp, vp, vp, vp, vp, i64, i64]),
         "he_seed": (i32, [vp, vp, vp, i64]),
-        "he_reset": (i32, [vp, vp, i64, vp, vp]),
+        "he_reset": (i32, [vp, vp, i64, vp, ctypes.POINTER(HeInfo), vp]),
         "he_step": (i32, [vp, vp, vp, vp, vp, vp, vp, ctypes.POINTER(HeInfo), vp]),
         "he_rollout": (i32, [vp, i32, vp, vp, vp, vp, vp]),
         "he_num_envs": (i64, [vp]),

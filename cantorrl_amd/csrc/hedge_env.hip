@@ -542,6 +542,7 @@ __device__ __forceinline__ void write_info(const he_info& inf, int64_t i, const 
     if (inf.current_call_price) inf.current_call_price[i] = m.C;
     if (inf.current_put_price) inf.current_put_price[i] = m.P;
     if (inf.current_step) inf.current_step[i] = (int32_t)e.t;
+    if (inf.current_episode_idx) inf.current_episode_idx[i] = e.path;
 }
 
 // Write a [rows][13] tile staged in LDS to out (row-major [N][13]) with 16-B stores.
@@ -615,6 +616,7 @@ __global__ __launch_bounds__(kBlock) void step_kernel(Params p, State s, Io io, 
             float s0f = p.rst[0];
             e.s0_small = s0f < 1e-6f;
             e.s0 = e.s0_small ? 1.0f : s0f;
+            e.path = -1;
             // unconditional load (no t -> load dependency), select afterwards
             Mkt tp = as_mkt(p.tileA[(int64_t)slot0 * N + i]);
             pre = (e.t == 0) ? Mkt{p.rst[0], p.rst[1], p.rst[2], p.rst[3]} : tp;
@@ -697,7 +699,7 @@ __global__ __launch_bounds__(kBlock) void step_kernel(Params p, State s, Io io, 
 // reset env moves to the start of its next episode.
 template <int MODE>
 __global__ __launch_bounds__(kBlock) void reset_kernel(Params p, State s, Market cur, const int64_t* ids,
-                                                       int64_t count, float* obs) {
+                                                       int64_t count, float* obs, he_info inf) {
     const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (j >= count) return;
     const int64_t i = ids ? ids[j] : j;
@@ -705,10 +707,11 @@ __global__ __launch_bounds__(kBlock) void reset_kernel(Params p, State s, Market
     Env e;
     env_reset_common(p, e);
     float o[kObs];
+    Mkt m;
     if (MODE == HE_MODE_REPLAY) {
         replay_reset(p, s, i, e);
         int64_t r = (int64_t)e.path * (p.T + 1);
-        Mkt m = as_mkt(p.rec[r]);
+        m = as_mkt(p.rec[r]);
         make_obs(p, e, m, p.recg[r], m.S, m.v, o);
         s.path[i] = e.path;
         s.s0[i] = e.s0_small ? -1.0f : e.s0;
@@ -719,6 +722,10 @@ __global__ __launch_bounds__(kBlock) void reset_kernel(Params p, State s, Market
         if (MODE == HE_MODE_HESTON) cur.v[i] = p.var;
         cur.C[i] = p.rst[2];
         cur.P[i] = p.rst[3];
+        m = Mkt{p.rst[0], p.rst[1], p.rst[2], p.rst[3]};
+        e.s0_small = m.S < 1e-6f;
+        e.s0 = e.s0_small ? 1.0f : m.S;
+        e.path = -1;
 #pragma unroll
         for (int c = 0; c < kObs; ++c) o[c] = p.rst[4 + c];
     }
@@ -729,6 +736,16 @@ __global__ __launch_bounds__(kBlock) void reset_kernel(Params p, State s, Market
 #pragma unroll
         for (int c = 0; c < kObs; ++c) obs[i * kObs + c] = o[c];
     }
+    if (inf.cash) inf.cash[i] = e.cash;
+    if (inf.call_contracts) inf.call_contracts[i] = 0;
+    if (inf.put_contracts) inf.put_contracts[i] = 0;
+    if (inf.initial_S0_for_episode) inf.initial_S0_for_episode[i] = e.s0;
+    if (inf.current_stock_price) inf.current_stock_price[i] = m.S;
+    if (inf.current_volatility) inf.current_volatility[i] = m.v;
+    if (inf.current_call_price) inf.current_call_price[i] = m.C;
+    if (inf.current_put_price) inf.current_put_price[i] = m.P;
+    if (inf.current_step) inf.current_step[i] = 0;
+    if (inf.current_episode_idx) inf.current_episode_idx[i] = e.path;
 }
 
 // ------------------------------------------------------------------ host side
@@ -1015,10 +1032,11 @@ static he_status materialize_market(he_env* env, hipStream_t st) {
 }
 
 template <int MODE>
-static void launch_reset(he_env* env, const int64_t* ids, int64_t count, float* obs, hipStream_t st) {
+static void launch_reset(he_env* env, const int64_t* ids, int64_t count, float* obs, const he_info& inf,
+                         hipStream_t st) {
     int64_t blocks = (count + kBlock - 1) / kBlock;
     hipLaunchKernelGGL(reset_kernel<MODE>, dim3((unsigned)blocks), dim3(kBlock), 0, st, env->p, env->s,
-                       env->cur, ids, count, obs);
+                       env->cur, ids, count, obs, inf);
 }
 
 template <int MODE>
@@ -1390,8 +1408,12 @@ he_status he_seed(he_env* env, const int64_t* env_ids, const uint64_t* seeds, in
     return HE_OK;
 }
 
-he_status he_reset(he_env* env, const int64_t* env_ids, int64_t count, float* obs_out, void* stream) {
+he_status he_reset(he_env* env, const int64_t* env_ids, int64_t count, float* obs_out, const he_info* info,
+                   void* stream) {
     if (!env) return HE_EINVAL;
+    he_info inf;
+    if (info) inf = *info;
+    else memset(&inf, 0, sizeof(inf));
     const he_config& c = env->cfg;
     if (c.mode == HE_MODE_REPLAY && !env->rec) return fail(env, HE_ESTATE, "no paths loaded (he_load_paths)");
     if (!env_ids) count = c.n_envs;
@@ -1401,7 +1423,7 @@ he_status he_reset(he_env* env, const int64_t* env_ids, int64_t count, float* ob
     DeviceGuard dg(c.device);
     hipStream_t st = (hipStream_t)stream;
     if (c.mode == HE_MODE_REPLAY) {
-        launch_reset<HE_MODE_REPLAY>(env, env_ids, count, obs_out, st);
+        launch_reset<HE_MODE_REPLAY>(env, env_ids, count, obs_out, inf, st);
     } else {
         // partial reset: every other env keeps its market position (rewind); full
         // reset: only wait for a pending prefetch, which writes `cur` too
@@ -1409,8 +1431,8 @@ he_status he_reset(he_env* env, const int64_t* env_ids, int64_t count, float* ob
         if (s != HE_OK) return s;
         env->block_pos = c.market_block;  // tiles regenerated on the next step
         env->next_state = 0;
-        if (c.mode == HE_MODE_GBM) launch_reset<HE_MODE_GBM>(env, env_ids, count, obs_out, st);
-        else launch_reset<HE_MODE_HESTON>(env, env_ids, count, obs_out, st);
+        if (c.mode == HE_MODE_GBM) launch_reset<HE_MODE_GBM>(env, env_ids, count, obs_out, inf, st);
+        else launch_reset<HE_MODE_HESTON>(env, env_ids, count, obs_out, inf, st);
     }
     HE_HIP(env, hipGetLastError());
     env->ready = true;

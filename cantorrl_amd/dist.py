@@ -1,0 +1,53 @@
+"""Multi-GPU plumbing: one process per GPU, envs sharded by global id.
+
+Envs are independent, so a step needs no collective.  Each rank owns the
+contiguous global ids [rank*N, (rank+1)*N) (he_config.global_env_offset); the
+Philox subsequence of an env is its global id, so every trajectory is identical
+for any GPU count.  Ranks exchange data only at rollout-buffer boundaries
+(n_steps = 256 in train_ppo_v2.py:48): `gather_rollout` all-gathers per-env
+tensors over RCCL (backend "nccl") on MI355X / gloo on CPU.
+"""
+import os
+
+import torch
+
+
+def world_info():
+    """(rank, local_rank, world_size) from the torch.distributed.run environment."""
+    return (int(os.environ.get("RANK", "0")), int(os.environ.get("LOCAL_RANK", "0")),
+            int(os.environ.get("WORLD_SIZE", "1")))
+
+
+def shard_offset(n_per_rank, rank):
+    """Global id of this rank's first env (weak scaling: n_per_rank envs per GPU)."""
+    if n_per_rank < 1 or rank < 0:
+        raise ValueError("n_per_rank >= 1 and rank >= 0 required")
+    return n_per_rank * rank
+
+
+def init(backend=None):
+    """Initialise the default process group for this process's device."""
+    import torch.distributed as dist
+    rank, local, world = world_info()
+    if world == 1 or dist.is_initialized():
+        return rank, local, world
+    if backend is None:
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+    if backend == "nccl":
+        torch.cuda.set_device(local)
+        dist.init_process_group(backend, device_id=torch.device("cuda", local))
+    else:
+        dist.init_process_group(backend)
+    return rank, local, world
+
+
+def gather_rollout(t, group=None):
+    """All-gather a per-env tensor [N, ...] from every rank -> [world*N, ...] in
+    global-id order (rank-major, matching shard_offset)."""
+    import torch.distributed as dist
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return t
+    w = dist.get_world_size(group)
+    out = torch.empty((w * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+    dist.all_gather_into_tensor(out, t.contiguous(), group=group)
+    return out

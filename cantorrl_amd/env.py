@@ -1,0 +1,195 @@
+"""HedgingEnv: the reference's single-env gym API on top of libhedgeenv.
+
+Same constructor signature and defaults as bcosm/CantorRL's
+`src/env/hedging_env_v2.py:10-22` (`HedgingEnv`) and `src/env/hedging_env.py:10-20`
+(`HedgingEnvV1`), same `reset(seed, options) -> (obs, {})` /
+`step(action) -> (obs, reward, terminated, truncated, info)` contract
+(hedging_env_v2.py:145-294), same attribute names read by the reference's
+baseline and benchmark scripts (src/agents/baselines.py:74-103,
+src/benchmark/delta_and_nothing.py:70-88).  The env is a 1-env handle on the GPU
+(no auto-reset: the caller resets, as with any gym env); use HedgingVecEnv for
+batches.
+
+Superset: `max_trade_per_step` is exposed as an attribute (the reference only
+has `_max_trade_per_step_internal`, so its delta baseline raises AttributeError).
+"""
+import numpy as np
+import torch
+
+from . import _lib
+from .vec_env import (HedgingVecEnv, OBS_HIGH, OBS_LOW)
+from .spaces import Box
+
+_INFO_F64 = ["step_pnl_total", "per_share_step_pnl", "raw_pnl_deviation_abs", "transaction_costs_total",
+             "commission_cost", "slippage_cost", "reward_pnl_component", "transaction_cost_penalty",
+             "theta_penalty", "reward_step", "portfolio_value"]
+
+
+class HedgingEnv:
+    """hedging_env_v2.HedgingEnv, GPU-backed.  Extra keyword-only arguments select
+    the market source: `data_file_path` (replay, reference semantics) or
+    `mode="gbm"|"heston"` with `generate=dict(...)`."""
+
+    metadata = {"render_modes": [], "render_fps": 1}
+    _variant = 2
+
+    def __init__(self, data_file_path=None,
+                 transaction_cost_per_contract=0.65,
+                 lambda_cost=1.0,
+                 pnl_penalty_weight=0.01,
+                 theta_weight=0.0,
+                 slippage_bps=0.0,
+                 loss_type="abs",
+                 initial_cash=0.0,
+                 shares_to_hedge=10000,
+                 max_contracts_held_per_type=200,
+                 max_trade_per_step=15,
+                 profile_print_interval=0,
+                 record_metrics=True,
+                 *, mode=None, generate=None, device=None, tables=None):
+        kw = dict(transaction_cost_per_contract=transaction_cost_per_contract, lambda_cost=lambda_cost,
+                  pnl_penalty_weight=pnl_penalty_weight, theta_weight=theta_weight,
+                  slippage_bps=slippage_bps, loss_type=loss_type, initial_cash=initial_cash,
+                  shares_to_hedge=shares_to_hedge, max_contracts_held_per_type=max_contracts_held_per_type,
+                  max_trade_per_step=max_trade_per_step, profile_print_interval=profile_print_interval,
+                  record_metrics=record_metrics)
+        self._init(data_file_path, kw, mode, generate, device, tables)
+
+    def _init(self, data_file_path, kw, mode, generate, device, tables):
+        keys = [k for k, _ in _lib.INFO_FIELDS]
+        self._venv = HedgingVecEnv(1, data_file_path, tables=tables, variant=self._variant, mode=mode,
+                                   generate=generate, device=device, autoreset=False, return_numpy=False,
+                                   info_keys=keys, **kw)
+        v = self._venv
+        self.pnl_penalty_weight = kw["pnl_penalty_weight"]
+        self.lambda_cost = kw["lambda_cost"]
+        if self._variant == 2:
+            self.theta_weight = kw["theta_weight"]
+            self.slippage_bps = kw["slippage_bps"]
+        self.loss_type = kw["loss_type"]
+        self.record_metrics = kw["record_metrics"]
+        self.initial_cash = kw["initial_cash"]
+        self._max_trade_per_step_internal = kw["max_trade_per_step"]
+        self.max_trade_per_step = kw["max_trade_per_step"]
+        self.num_episodes = v.num_episodes
+        self.episode_length = v.episode_length
+        self.transaction_cost_per_contract = kw["transaction_cost_per_contract"]
+        self.max_contracts_held = kw["max_contracts_held_per_type"]
+        self.shares_held_fixed = kw["shares_to_hedge"]
+        self.option_contract_multiplier = 100
+        self.risk_free_rate = 0.04
+        self.option_tenor_years = 30 / 252
+        self.action_space = Box(low=-1.0, high=1.0, shape=(2,), dtype=np.float32)
+        self.observation_space = Box(low=OBS_LOW, high=OBS_HIGH, shape=(13,), dtype=np.float32)
+        self.current_episode_idx = -1
+        self.current_step = 0
+        self.initial_S0_for_episode = 1.0
+        self._needs_reset = True
+        self._terminated = False
+        self._act = torch.zeros((1, 2), dtype=torch.float32, device=v.device)
+
+    # ------------------------------------------------------------------ helpers
+    def _pull(self):
+        v = self._venv
+        h = {k: t.cpu().numpy()[0] for k, t in v._info_t.items()}
+        self.current_stock_price = np.float32(h["current_stock_price"])
+        self.current_volatility = np.float32(h["current_volatility"])
+        self.current_call_price = np.float32(h["current_call_price"])
+        self.current_put_price = np.float32(h["current_put_price"])
+        self.current_step = int(h["current_step"])
+        self.call_contracts_held = np.int64(h["call_contracts"])
+        self.put_contracts_held = np.int64(h["put_contracts"])
+        self.cash_balance = np.float64(h["cash"])
+        s0 = np.float32(h["initial_S0_for_episode"])
+        return h, s0
+
+    # ------------------------------------------------------------------ gym API
+    def reset(self, seed=None, options=None):
+        v = self._venv
+        if seed is not None:
+            v.seed_envs([int(seed)])
+        obs = v.reset_tensors()
+        o = obs.cpu().numpy()[0].copy()
+        h, s0 = self._pull()
+        small = bool(s0 == np.float32(1.0) and self.current_stock_price < np.float32(1e-6))
+        self.initial_S0_for_episode = 1.0 if small else s0
+        self.current_episode_idx = int(h["current_episode_idx"])
+        self.S_t_minus_1 = self.current_stock_price
+        self.v_t_minus_1 = self.current_volatility
+        self.portfolio_value_t_minus_1 = (self.shares_held_fixed * self.current_stock_price) + 0 + \
+            self.initial_cash
+        self._needs_reset = False
+        self._terminated = False
+        return o, {}
+
+    def step(self, action: np.ndarray):
+        if self._needs_reset:
+            raise RuntimeError("call reset() before step()")
+        if self._terminated:
+            # the reference indexes past the end of its path (hedging_env_v2.py:223)
+            raise IndexError(f"index {self.episode_length + 1} is out of bounds for axis 0 with size "
+                             f"{self.episode_length + 1}")
+        a = np.asarray(action, dtype=np.float32).reshape(2)
+        self._act.copy_(torch.from_numpy(a).reshape(1, 2))
+        prev_S, prev_v = self.current_stock_price, self.current_volatility
+        obs, rew, term, trunc = self._venv.step_tensors(self._act)
+        o = obs.cpu().numpy()[0].copy()
+        h, s0 = self._pull()
+        terminated = bool(term.cpu().numpy()[0])
+        self._terminated = terminated
+        self.S_t_minus_1, self.v_t_minus_1 = prev_S, prev_v
+        self.portfolio_value_t_minus_1 = np.float64(h["portfolio_value"])
+        reward = np.float64(h["reward_step"])
+        info = {k: np.float64(h[k]) for k in _INFO_F64}
+        if self._variant == 2:
+            info["theta_penalty"] = float(h["theta_penalty"])
+        else:
+            for k in ("commission_cost", "slippage_cost", "theta_penalty"):
+                info.pop(k)
+        info.update({
+            "call_contracts": np.int64(h["call_contracts"]),
+            "put_contracts": np.int64(h["put_contracts"]),
+            "cash": np.float64(h["cash"]),
+            "raw_action_call": a[0],
+            "raw_action_put": a[1],
+            "scaled_float_call": np.float32(h["scaled_float_call"]),
+            "scaled_float_put": np.float32(h["scaled_float_put"]),
+            "requested_calls_rounded_clipped": np.int64(h["requested_calls_rounded_clipped"]),
+            "requested_puts_rounded_clipped": np.int64(h["requested_puts_rounded_clipped"]),
+            "actual_calls_traded": np.int64(h["actual_calls_traded"]),
+            "actual_puts_traded": np.int64(h["actual_puts_traded"]),
+            "loss_type_used": self.loss_type,
+            "initial_S0_for_episode": self.initial_S0_for_episode,
+        })
+        return o, reward, terminated, False, info
+
+    def render(self):
+        pass
+
+    def close(self):
+        self._venv.close()
+
+
+class HedgingEnvV1(HedgingEnv):
+    """hedging_env.HedgingEnv (v1): no theta/slippage, $0.05 per contract."""
+
+    _variant = 1
+
+    def __init__(self, data_file_path=None,
+                 transaction_cost_per_contract=0.05,
+                 lambda_cost=1.0,
+                 pnl_penalty_weight=0.01,
+                 loss_type="abs",
+                 initial_cash=0.0,
+                 shares_to_hedge=10000,
+                 max_contracts_held_per_type=200,
+                 max_trade_per_step=15,
+                 profile_print_interval=0,
+                 record_metrics=True,
+                 *, mode=None, generate=None, device=None, tables=None):
+        kw = dict(transaction_cost_per_contract=transaction_cost_per_contract, lambda_cost=lambda_cost,
+                  pnl_penalty_weight=pnl_penalty_weight, loss_type=loss_type, initial_cash=initial_cash,
+                  shares_to_hedge=shares_to_hedge, max_contracts_held_per_type=max_contracts_held_per_type,
+                  max_trade_per_step=max_trade_per_step, profile_print_interval=profile_print_interval,
+                  record_metrics=record_metrics)
+        self._init(data_file_path, kw, mode, generate, device, tables)

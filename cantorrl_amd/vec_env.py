@@ -231,11 +231,13 @@ class HedgingVecEnv:
         if self._pending_seeds is not None:
             self.seed_envs(self._pending_seeds)
             self._pending_seeds = None
+        info = _lib.ctypes.byref(self._info) if self._info_t else None
         if env_ids is None:
-            st = self.lib.he_reset(self._h, None, self.num_envs, self._obs.data_ptr(), self.stream)
+            st = self.lib.he_reset(self._h, None, self.num_envs, self._obs.data_ptr(), info, self.stream)
         else:
             ids = torch.as_tensor(env_ids, dtype=torch.int64, device=self.device)
-            st = self.lib.he_reset(self._h, ids.data_ptr(), ids.numel(), self._obs.data_ptr(), self.stream)
+            st = self.lib.he_reset(self._h, ids.data_ptr(), ids.numel(), self._obs.data_ptr(), info,
+                                   self.stream)
         _lib.check(self.lib, self._h, st, "he_reset")
         if env_ids is None:
             self._ep_ret[:] = 0.0

@@ -138,6 +138,7 @@ typedef struct he_info {
     float* current_call_price;
     float* current_put_price;
     int32_t* current_step;
+    int32_t* current_episode_idx;   /* replay: path row of the episode; generate: -1 */
 } he_info;
 
 typedef struct he_env he_env;
@@ -163,9 +164,11 @@ he_status he_load_paths(he_env* env, const float* S, const float* v, const float
 he_status he_seed(he_env* env, const int64_t* env_ids, const uint64_t* seeds, int64_t count);
 
 /* Reset envs (env_ids: DEVICE int64 list, NULL = all) and write their obs rows
- * into obs_out[N][13] (device; rows of other envs untouched; may be NULL). */
+ * into obs_out[N][13] (device; rows of other envs untouched; may be NULL).  If
+ * info is not NULL its position fields (cash, call/put contracts, current_*,
+ * initial_S0_for_episode, current_episode_idx) receive the post-reset values. */
 he_status he_reset(he_env* env, const int64_t* env_ids, int64_t count, float* obs_out,
-                   void* stream);
+                   const he_info* info, void* stream);
 
 /* One step of every env.  actions [N][2] f32 in, obs [N][13] f32 out (the reset
  * obs for envs that terminated when autoreset=1), reward [N] f32 (f64 reward cast
