@@ -120,11 +120,14 @@ def philox_normals(seed, env_ids, step_index):
 # --------------------------------------------------------------------------- #
 # Black-Scholes (quantconnect/option_calculator.py:11-27), vectorized f64       #
 # --------------------------------------------------------------------------- #
-def bs_price(S, K, T, r, sigma):
+def bs_price(S, K, T, r, sigma, square=None):
+    """`square` = how sigma**2 is formed: python-scalar pow (default, the reference's
+    scalar call) or x*x (`square=np.square`, the per-env sigma of Heston marks)."""
     S, K, T, sigma = np.broadcast_arrays(*(np.asarray(x, np.float64) for x in (S, K, T, sigma)))
     with np.errstate(all="ignore"):
         sqT = np.sqrt(T)
-        d1 = (np.log(S / K) + (r + 0.5 * spow2(sigma)) * T) / (sigma * sqT)
+        sig2 = spow2(sigma) if square is None else sigma * sigma
+        d1 = (np.log(S / K) + (r + 0.5 * sig2) * T) / (sigma * sqT)
         d2 = d1 - sigma * sqT
         disc = np.exp(-r * T)
         call = S * ndtr(d1) - K * disc * ndtr(d2)
@@ -202,7 +205,7 @@ class OracleVecEnv:
                 raise ValueError("Data shapes are inconsistent.")
             self.num_episodes = self.S_tab.shape[0]
             self.episode_length = self.S_tab.shape[1] - 1
-        elif mode == "gbm":
+        elif mode in ("gbm", "heston"):
             g = dict(gen)
             self.g_s0 = float(g["s0"])
             self.g_v = float(g["variance"])
@@ -210,10 +213,15 @@ class OracleVecEnv:
             self.g_dt = float(g.get("dt", 1 / 252))
             self.g_seed = int(g.get("seed", 42))
             self.g_offset = int(g.get("env_offset", 0))
+            self.h_kappa = float(g.get("heston_kappa", 2.0))
+            self.h_theta = float(g.get("heston_theta", 0.029028))
+            self.h_xi = float(g.get("heston_xi", 0.3))
+            self.h_rho = float(g.get("heston_rho", -0.7))
             self.episode_length = int(g.get("episode_length", 252))
             self.num_episodes = None
             self.g_ep = np.full(self.n, -1, np.int64)  # next reset starts episode 0
             self.S64 = np.zeros(self.n, np.float64)
+            self.V64 = np.zeros(self.n, np.float64)
         else:
             raise ValueError(mode)
         self.rngs = [None] * self.n
@@ -234,23 +242,41 @@ class OracleVecEnv:
         self.pv_prev = z.astype(np.float64)
 
     # ------------------------------------------------------------------ market
-    def _gbm_marks(self, S64):
+    def _gbm_marks(self, S64, V64=None):
         K = np.round(S64)
-        sig = np.sqrt(self.g_v)
-        C, P = bs_price(S64, K, self.tenor, self.r, sig)
+        if self.mode == "heston":
+            sig = np.sqrt(np.maximum(V64, 0.0))
+            C, P = bs_price(S64, K, self.tenor, self.r, sig, square=np.square)
+        else:
+            sig = np.sqrt(self.g_v)
+            C, P = bs_price(S64, K, self.tenor, self.r, sig)
         return C, P
 
     def _gbm_advance(self, mask):
-        """S_{t+1} from S_t for masked envs (rbergomi_sim.py:454-464, v constant)."""
+        """S_{t+1} from S_t for masked envs (rbergomi_sim.py:454-464).
+
+        GBM: constant v, one normal.  Heston: full-truncation Euler on v driven by
+        dw1, price driven by dW = rho*dw1 + sqrt(1-rho^2)*dw2 (rbergomi_sim.py:457)."""
         ids = np.nonzero(mask)[0]
         n_idx = (self.g_ep[ids] * self.episode_length + self.t[ids]).astype(np.uint64)
-        z0, _ = philox_normals(self.g_seed, np.uint64(self.g_offset) + ids.astype(np.uint64), n_idx)
-        v = self.g_v
+        z0, z1 = philox_normals(self.g_seed, np.uint64(self.g_offset) + ids.astype(np.uint64), n_idx)
         sqrt_dt = np.sqrt(self.g_dt)
-        dW = sqrt_dt * z0
-        drift = (self.g_mu - 0.5 * v) * self.g_dt
-        diff = np.sqrt(np.maximum(0.0, v)) * dW
-        Snew = self.S64[ids] * np.exp(drift + diff)
+        if self.mode == "heston":
+            v = self.V64[ids]
+            vp = np.maximum(v, 0.0)
+            dw1 = sqrt_dt * z0
+            dw2 = sqrt_dt * z1
+            dW = self.h_rho * dw1 + np.sqrt(max(0.0, 1.0 - self.h_rho * self.h_rho)) * dw2
+            drift = (self.g_mu - 0.5 * vp) * self.g_dt
+            diff = np.sqrt(vp) * dW
+            Snew = self.S64[ids] * np.exp(drift + diff)
+            self.V64[ids] = (v + self.h_kappa * (self.h_theta - vp) * self.g_dt) + self.h_xi * np.sqrt(vp) * dw1
+        else:
+            v = self.g_v
+            dW = sqrt_dt * z0
+            drift = (self.g_mu - 0.5 * v) * self.g_dt
+            diff = np.sqrt(np.maximum(0.0, v)) * dW
+            Snew = self.S64[ids] * np.exp(drift + diff)
         self.S64[ids] = np.maximum(Snew, 1e-8)
 
     # ------------------------------------------------------------------ reset
@@ -273,7 +299,7 @@ class OracleVecEnv:
         for i, s in zip(ids, seeds):
             if self.mode == "replay":
                 self.rngs[i] = np.random.Generator(np.random.PCG64(np.random.SeedSequence(int(s))))
-        if self.mode == "gbm":
+        if self.mode in ("gbm", "heston"):
             # generate mode: seed selects the Philox key for the whole batch
             self.g_seed = int(seeds[0])
             self.g_ep[:] = -1
@@ -293,9 +319,10 @@ class OracleVecEnv:
         else:
             self.g_ep[ids] += 1  # every reset starts the next episode of the env
             self.S64[ids] = self.g_s0
+            self.V64[ids] = self.g_v
             S = self.S64[ids].astype(np.float32)
             v = np.full(len(ids), self.g_v).astype(np.float32)
-            Cd, Pd = self._gbm_marks(self.S64[ids])
+            Cd, Pd = self._gbm_marks(self.S64[ids], self.V64[ids])
             C = Cd.astype(np.float32)
             P = Pd.astype(np.float32)
         self.t[ids] = 0
@@ -417,7 +444,9 @@ class OracleVecEnv:
             self._gbm_advance(np.ones(self.n, bool))
             self.t = self.t + 1
             self.S = self.S64.astype(np.float32)
-            Cd, Pd = self._gbm_marks(self.S64)
+            if self.mode == "heston":
+                self.v = self.V64.astype(np.float32)
+            Cd, Pd = self._gbm_marks(self.S64, self.V64)
             self.C = np.where(term, self.C, Cd.astype(np.float32))
             self.P = np.where(term, self.P, Pd.astype(np.float32))
         with np.errstate(all="ignore"):

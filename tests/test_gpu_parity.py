@@ -81,13 +81,13 @@ def test_replay_matches_reference_golden(fname):
     env.close()
 
 
-def run_gbm_pair(n, steps, seed, cfg, gen, offset=0):
+def run_gbm_pair(n, steps, seed, cfg, gen, offset=0, mode="gbm"):
     from cantorrl_amd.vec_env import HedgingVecEnv
     rng = np.random.default_rng(seed)
     acts = rng.uniform(-1.05, 1.05, size=(steps, n, 2)).astype(np.float32)
-    venv = HedgingVecEnv(n, mode="gbm", generate=gen, seed=seed, global_env_offset=offset,
+    venv = HedgingVecEnv(n, mode=mode, generate=gen, seed=seed, global_env_offset=offset,
                          info_keys=all_info_keys(), return_numpy=False, **cfg)
-    orc = OracleVecEnv(n, mode="gbm", gen=dict(gen, seed=seed, env_offset=offset), **cfg)
+    orc = OracleVecEnv(n, mode=mode, gen=dict(gen, seed=seed, env_offset=offset), **cfg)
     orc.seed_envs_at(np.arange(n), [seed] * n)
     o_obs = orc.reset()
     g_obs = venv.reset_tensors().cpu().numpy()
@@ -199,3 +199,37 @@ def test_odd_sizes_and_bounds(n):
     c = env.info_tensor("call_contracts")
     assert int(c.abs().max()) <= 200
     env.close()
+
+
+def test_heston_matches_oracle():
+    """Config 5's market (extension): Heston full-truncation Euler, rho=-0.7."""
+    cfg = dict(loss_type="abs", pnl_penalty_weight=0.001, lambda_cost=0.0001, theta_weight=0.0002,
+               slippage_bps=1.0)
+    gen = dict(s0=496.48001098632812, variance=0.04, mu=0.04, dt=1 / 252, episode_length=30,
+               heston_kappa=1.5, heston_theta=0.035, heston_xi=0.6, heston_rho=-0.7)
+    stats = run_gbm_pair(256, 75, 11, cfg, gen, mode="heston")
+    assert stats["pnl_exact"] >= 0.95 * stats["pnl_total"], stats
+
+
+def test_partial_reset_keeps_other_envs_on_their_paths():
+    """he_reset(env_ids) mid-block rewinds the market of the untouched envs: their
+    trajectories equal a run without the partial reset."""
+    from cantorrl_amd.vec_env import HedgingVecEnv
+    n, K = 512, 100
+    acts = torch.rand((K, n, 2), device="cuda") * 2 - 1
+    a = HedgingVecEnv(n, mode="gbm", seed=4, return_numpy=False, info_keys=())
+    b = HedgingVecEnv(n, mode="gbm", seed=4, return_numpy=False, info_keys=())
+    a.reset_tensors()
+    b.reset_tensors()
+    for k in range(K):
+        if k == 37:
+            b.reset_tensors(env_ids=[3, 200, 511])
+        oa, ra, _, _ = a.step_tensors(acts[k], terminal_obs=False)
+        ob, rb, _, _ = b.step_tensors(acts[k], terminal_obs=False)
+        keep = torch.ones(n, dtype=torch.bool, device="cuda")
+        if k >= 37:
+            keep[[3, 200, 511]] = False
+        assert torch.equal(oa[keep], ob[keep]), k
+        assert torch.equal(ra[keep], rb[keep]), k
+        if k == 37:  # a reset env restarts at t=0: obs[6] (time to end) of the next step
+            assert torch.all(ob[[3, 200, 511], 6] == (252 - 1) / 252)
