@@ -70,6 +70,31 @@ HE_HD double u01(uint32_t hi, uint32_t lo) {
 }
 
 // ---------------------------------------------------------------- normal cdf/pdf
+// erf on |x| < 1/sqrt2 (the branch ndtr uses): Maclaurin series
+// 2/sqrt(pi) * sum_n (-1)^n x^(2n+1) / (n! (2n+1)) to n = 15 -- alternating, so the
+// truncation error < the n=16 term < 3e-20 |x|; 16 FMAs instead of ocml's
+// ranged rational approximation (~2-3x the instructions).
+HE_HD double erf_small(double x) {
+    const double z = x * x;
+    double p = -2.783516207210921354903762e-14;
+    p = fma(p, z, 4.463224263286477344931894e-13);
+    p = fma(p, z, -6.711366855164110377934626e-12);
+    p = fma(p, z, 9.422759064650410970620214e-11);
+    p = fma(p, z, -1.229055530171792735298289e-9);
+    p = fma(p, z, 1.480719281587921723954605e-8);
+    p = fma(p, z, -0.00000016365844691234924317393);
+    p = fma(p, z, 0.000001646211436588924740161296);
+    p = fma(p, z, -0.00001492565035840625097746242);
+    p = fma(p, z, 0.0001205533298178966425102734);
+    p = fma(p, z, -0.0008548327023450852832546658);
+    p = fma(p, z, 0.005223977625442187842111847);
+    p = fma(p, z, -0.02686617064513125175943235);
+    p = fma(p, z, 0.1128379167095512573896159);
+    p = fma(p, z, -0.376126389031837524632053);
+    p = fma(p, z, 1.128379167095512573896159);
+    return x * p;
+}
+
 // scipy.special.ndtr (cephes ndtr.c): erf branch inside |x| < 1/sqrt2.
 HE_HD double ndtr(double a) {
     if (a != a) return a;
@@ -78,7 +103,7 @@ HE_HD double ndtr(double a) {
     double z = fabs(x);
     double y;
     if (z < SQRT1_2) {
-        y = 0.5 + 0.5 * erf(x);
+        y = 0.5 + 0.5 * erf_small(x);
     } else {
         y = 0.5 * erfc(z);
         if (x > 0) y = 1.0 - y;
@@ -87,9 +112,10 @@ HE_HD double ndtr(double a) {
 }
 
 // scipy.stats.norm.pdf: exp(-x**2/2.0) / sqrt(2*pi)  (x**2 on an array = x*x)
-// (division by 2.0 is exact scaling, so *0.5 is bit-identical)
+// (division by 2.0 is exact scaling, so *0.5 is bit-identical; the division by
+// sqrt(2 pi) becomes a multiply by 1/sqrt(2 pi): <= 1 ulp, far below the f32 cast)
 HE_HD double norm_pdf(double x) {
-    return exp(-(x * x) * 0.5) / 2.5066282746310002;
+    return exp(-(x * x) * 0.5) * 0.3989422804014327;
 }
 
 // ---------------------------------------------------------------- Black-Scholes
@@ -98,6 +124,7 @@ HE_HD double norm_pdf(double x) {
 // precomputed with python-float semantics when sigma is constant.
 struct BSConst {
     double a, b, disc;
+    double inv_b;   // 1/b: the constant-sigma division becomes a multiply (<= 1 ulp)
     int intrinsic;  // T <= 0 or sigma <= 0
 };
 
@@ -108,7 +135,7 @@ HE_HD void bs_call_put(double S, double K, const BSConst& c, double* call, doubl
         *put = (ip < 0.0) ? 0.0 : ip;
         return;
     }
-    double d1 = (log(S / K) + c.a) / c.b;
+    double d1 = (log(S / K) + c.a) * c.inv_b;
     double d2 = d1 - c.b;
     double Kd = K * c.disc;
     double n1 = ndtr(d1), n2 = ndtr(d2);

@@ -73,6 +73,7 @@ struct Params {
     BSConst bs;             // constant-sigma BS constants (GBM)
     float g_sigma, g_num_drift;  // constant-variance greeks: sigma, (r+0.5 sigma**2)*T (f32)
     double g_sst;                // sigma*sqrt(T) (f64)
+    double g_inv_sst;            // 1/(sigma*sqrt(T))
     double h_kappa, h_theta, h_xi, h_rho, h_sqrt1mrho2;
     int32_t M;              // market block length
     float4* tileA;          // [M+1][N] {S, v, C, P}
@@ -170,7 +171,7 @@ __device__ __forceinline__ float4 greeks(const Params& p, float S, float v) {
                 float sg = (num > 0.0f) ? 1.0f : ((num < 0.0f) ? -1.0f : num);  // np.sign
                 d1 = (double)(sg * 10.0f);
             } else {
-                d1 = (double)num / sst;
+                d1 = CONST_VAR ? (double)num * p.g_inv_sst : (double)num / sst;
             }
             double n1 = ndtr(d1);
             cd = n1;
@@ -232,6 +233,7 @@ __device__ __forceinline__ void marks(const Params& p, double S64, double var64,
         h.intrinsic = (p.tenor_d <= 0.0) || (sig <= 0.0);
         h.a = (p.r_d + 0.5 * (sig * sig)) * p.tenor_d;
         h.b = sig * p.sqrt_tenor;
+        h.inv_b = 1.0 / h.b;
         h.disc = p.bs.disc;
         bs_call_put(S64, K, h, &c, &q);
     } else {
@@ -242,21 +244,16 @@ __device__ __forceinline__ void marks(const Params& p, double S64, double var64,
 }
 
 // Box-Muller pair of the Philox block of (seed, global env id, env-step index n).
-__device__ __forceinline__ void normals(const Params& p, int64_t gid, uint64_t n, double* z1, double* z2,
-                                        bool both) {
+__device__ __forceinline__ void normals(const Params& p, int64_t gid, uint64_t n, double* z1, double* z2) {
     u32x4 ctr = {(uint32_t)n, (uint32_t)(n >> 32), (uint32_t)gid, (uint32_t)((uint64_t)gid >> 32)};
     u32x4 x = philox4x32_10(ctr, p.key0, p.key1);
     double u1 = u01(x.x, x.y), u2 = u01(x.z, x.w);
     double rad = sqrt(-2.0 * log(u1));
     double ang = 6.283185307179586 * u2;
-    if (both) {
-        double sn, cs;
-        sincos(ang, &sn, &cs);
-        *z1 = rad * cs;
-        *z2 = rad * sn;
-    } else {
-        *z1 = rad * cos(ang);
-    }
+    double sn, cs;
+    sincos(ang, &sn, &cs);
+    *z1 = rad * cs;
+    *z2 = rad * sn;
 }
 
 // ------------------------------------------------------------------ market kernel
@@ -295,19 +292,33 @@ __global__ __launch_bounds__(kMktEnvs * kMktLanes) void market_kernel(Params p, 
     const uint32_t t0m = (t0 >= T) ? 0u : t0;  // position modulo T
     const uint64_t a0 = (uint64_t)ep0 * T + t0m + ((t0 >= T) ? T : 0u);
     // phase 1 (all lanes, time-parallel): the random part of every step
-    for (int j = 1 + sub; j <= nsteps; j += kMktLanes) {
-        if (!live) break;
-        uint64_t n = a0 + (uint64_t)(j - 1);
-        double z1, z2;
-        if (HESTON) {
-            normals(p, gid, n, &z1, &z2, true);
+    if (HESTON) {
+        // two normals per step: Philox block n -> (z1, z2)
+        for (int j = 1 + sub; j <= nsteps; j += kMktLanes) {
+            if (!live) break;
+            uint64_t n = a0 + (uint64_t)(j - 1);
+            double z1, z2;
+            normals(p, gid, n, &z1, &z2);
             double dw1 = p.sqrt_dt * z1, dw2 = p.sqrt_dt * z2;
             shV[lane][j] = dw1;
             shS[lane][j] = p.h_rho * dw1 + p.h_sqrt1mrho2 * dw2;  // rbergomi_sim.py:457
-        } else {
-            normals(p, gid, n, &z1, &z2, false);
-            double dW = p.sqrt_dt * z1;
-            shS[lane][j] = exp(p.drift + p.sqrt_var * dW);      // rbergomi_sim.py:459-463
+        }
+    } else {
+        // one normal per step: Philox block m = n/2 gives the Box-Muller pair of
+        // steps 2m (cos branch) and 2m+1 (sin branch)
+        const uint64_t m0 = a0 >> 1, m1 = (a0 + (uint64_t)nsteps - 1) >> 1;
+        for (uint64_t m = m0 + (uint64_t)sub; m <= m1; m += kMktLanes) {
+            if (!live) break;
+            double z[2];
+            normals(p, gid, m, &z[0], &z[1]);
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                uint64_t n = 2 * m + (uint64_t)h;
+                if (n < a0 || n >= a0 + (uint64_t)nsteps) continue;
+                int j = (int)(n - a0) + 1;
+                double dW = p.sqrt_dt * z[h];
+                shS[lane][j] = exp(p.drift + p.sqrt_var * dW);  // rbergomi_sim.py:459-463
+            }
         }
     }
     __syncthreads();
@@ -920,6 +931,7 @@ static void fill_params(he_env* env) {
     p.bs.intrinsic = (T <= 0.0) || (sig <= 0.0);
     p.bs.a = (r + 0.5 * pow(sig, 2.0)) * T;
     p.bs.b = sig * sqrt(T);
+    p.bs.inv_b = 1.0 / p.bs.b;
     p.bs.disc = exp(-r * T);
     // hedging_env_v2.py:84,95-99 for a constant f32 variance (numpy scalar powf)
     float vf = (float)c.variance;
@@ -927,6 +939,7 @@ static void fill_params(he_env* env) {
     p.g_sigma = sqrtf(vmax);
     p.g_num_drift = ((float)r + 0.5f * powf(p.g_sigma, 2.0f)) * (float)T;
     p.g_sst = (double)p.g_sigma * sqrt(T);
+    p.g_inv_sst = 1.0 / p.g_sst;
     p.h_kappa = c.heston_kappa;
     p.h_theta = c.heston_theta;
     p.h_xi = c.heston_xi;

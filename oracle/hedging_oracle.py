@@ -255,11 +255,18 @@ class OracleVecEnv:
     def _gbm_advance(self, mask):
         """S_{t+1} from S_t for masked envs (rbergomi_sim.py:454-464).
 
-        GBM: constant v, one normal.  Heston: full-truncation Euler on v driven by
-        dw1, price driven by dW = rho*dw1 + sqrt(1-rho^2)*dw2 (rbergomi_sim.py:457)."""
+        GBM: constant v, one normal per step -- env-step n takes the cos (n even) or
+        sin (n odd) half of the Box-Muller pair of Philox block n//2.  Heston:
+        both halves of block n; full-truncation Euler on v driven by dw1, price
+        driven by dW = rho*dw1 + sqrt(1-rho^2)*dw2 (rbergomi_sim.py:457)."""
         ids = np.nonzero(mask)[0]
         n_idx = (self.g_ep[ids] * self.episode_length + self.t[ids]).astype(np.uint64)
-        z0, z1 = philox_normals(self.g_seed, np.uint64(self.g_offset) + ids.astype(np.uint64), n_idx)
+        gids = np.uint64(self.g_offset) + ids.astype(np.uint64)
+        if self.mode == "heston":
+            z0, z1 = philox_normals(self.g_seed, gids, n_idx)
+        else:
+            c, s = philox_normals(self.g_seed, gids, n_idx >> np.uint64(1))
+            z0 = np.where((n_idx & np.uint64(1)) == 1, s, c)
         sqrt_dt = np.sqrt(self.g_dt)
         if self.mode == "heston":
             v = self.V64[ids]
