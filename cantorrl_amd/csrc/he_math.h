@@ -111,6 +111,33 @@ HE_HD double ndtr(double a) {
     return y;
 }
 
+// (ndtr(a), ndtr(-a)) from one erf/erfc evaluation, each bit-identical to a
+// separate ndtr() call: erf_small is odd (x * P(x^2)), and for |x| >= 1/sqrt2 both
+// branches evaluate erfc(|x|).
+HE_HD void ndtr_pair(double a, double* pos, double* neg) {
+    if (a != a) {
+        *pos = *neg = a;
+        return;
+    }
+    const double SQRT1_2 = 0.70710678118654752440;
+    double x = a * SQRT1_2;
+    double z = fabs(x);
+    if (z < SQRT1_2) {
+        double e = erf_small(x);
+        *pos = 0.5 + 0.5 * e;
+        *neg = 0.5 + 0.5 * (-e);
+    } else {
+        double y = 0.5 * erfc(z);
+        if (x > 0) {
+            *pos = 1.0 - y;
+            *neg = y;
+        } else {
+            *pos = y;
+            *neg = 1.0 - y;
+        }
+    }
+}
+
 // scipy.stats.norm.pdf: exp(-x**2/2.0) / sqrt(2*pi)  (x**2 on an array = x*x)
 // (division by 2.0 is exact scaling, so *0.5 is bit-identical; the division by
 // sqrt(2 pi) becomes a multiply by 1/sqrt(2 pi): <= 1 ulp, far below the f32 cast)
@@ -138,11 +165,11 @@ HE_HD void bs_call_put(double S, double K, const BSConst& c, double* call, doubl
     double d1 = (log(S / K) + c.a) * c.inv_b;
     double d2 = d1 - c.b;
     double Kd = K * c.disc;
-    double n1 = ndtr(d1), n2 = ndtr(d2);
+    double n1, m1, n2, m2;
+    ndtr_pair(d1, &n1, &m1);
+    ndtr_pair(d2, &n2, &m2);
     double cv = S * n1 - Kd * n2;
-    // ndtr(-x) taken as 1 - ndtr(x): |difference| <= 2^-53 absolute; C/P are
-    // handed to the env as f32 (hedging_env_v2.py:40-41), far above that.
-    double pv = Kd * (1.0 - n2) - S * (1.0 - n1);
+    double pv = Kd * m2 - S * m1;
     *call = (cv < 0.0) ? 0.0 : cv;   // python max(price, 0): NaN stays NaN
     *put = (pv < 0.0) ? 0.0 : pv;
 }

@@ -59,7 +59,6 @@ struct Params {
     double shares_d;
     float shares_f;
     int32_t shares_zero;
-    const double* thp_tab;  // theta_weight * ((T - t) / 252.0), t = 0..T (hedging_env_v2.py:259-260)
     // observation / greeks constants (hedging_env_v2.py:57-58)
     float r_f, tenor_f;
     double r_d, tenor_d, sqrt_tenor;
@@ -78,7 +77,7 @@ struct Params {
     int32_t M;              // market block length
     float4* tileA;          // [M+1][N] {S, v, C, P}
     float4* tileB;          // [M+1][N] {call_delta, gamma, put_delta, 0}
-    const float* rst;       // reset market + obs: {S0, v0, C0, P0, obs0[13]} (generate)
+    float rstv[4 + kObs];   // reset market + obs (generate): {S0, v0, C0, P0, obs0[13]}, by value
     // replay
     const float4* rec;      // [n_paths][T+1] {S, v, C, P}; C/P at T hold row T-1
     const float4* recg;     // [n_paths][T+1] {call_delta, gamma, put_delta, 0}
@@ -377,8 +376,8 @@ __global__ __launch_bounds__(kMktEnvs * kMktLanes) void market_kernel(Params p, 
         if (tj < T) {
             marks<MODE>(p, S64, v64, &C, &P);
         } else if (T == 1u) {  // lagged marks of t = T-1 = 0: the reset marks
-            C = p.rst[2];
-            P = p.rst[3];
+            C = p.rstv[2];
+            P = p.rstv[3];
         } else if (j == 1) {   // lagged marks of the block start
             C = C0v;
             P = P0v;
@@ -596,6 +595,9 @@ __device__ __forceinline__ void env_reset_common(const Params& p, Env& e) {
 }
 
 // K fused steps from market slot `slot0` (generate) / the env's own path row (replay).
+// Every load of step 0 is issued in a straight-line prologue before its first use
+// (one memory round trip instead of two), and in generate mode the loads of step
+// k+1 go out before the arithmetic of step k (software pipelining for rollouts).
 template <int MODE, bool INFO>
 __global__ __launch_bounds__(kBlock) void step_kernel(Params p, State s, Io io, int k_steps, int slot0) {
     constexpr bool REPLAY = (MODE == HE_MODE_REPLAY);
@@ -608,30 +610,46 @@ __global__ __launch_bounds__(kBlock) void step_kernel(Params p, State s, Io io, 
     const bool live = i < p.n;
     const int rows = (int)((p.n - row0) < kBlock ? (p.n - row0) : kBlock);
     const int64_t N = p.n;
+    const float2* act = reinterpret_cast<const float2*>(io.act);
+    const Mkt rst{p.rstv[0], p.rstv[1], p.rstv[2], p.rstv[3]};
     Env e;
     Mkt pre;
+    float4 postA, postB;
+    float2 a;
     if (live) {
-        e.t = s.t[i];
-        uint32_t pk = s.pos[i];
-        e.call = unpack_lo(pk);
-        e.put = unpack_hi(pk);
-        e.cash = s.cash[i];
+        const uint32_t t0 = s.t[i];
+        const uint32_t pk = s.pos[i];
+        const double cash = s.cash[i];
+        a = act[i];
         if (REPLAY) {
-            e.path = s.path[i];
-            float s0 = s.s0[i];
+            const int32_t path = s.path[i];
+            const float s0 = s.s0[i];
+            const uint32_t tt = t0 > (uint32_t)p.T ? (uint32_t)p.T : t0;
+            const uint32_t tn = t0 + 1 > (uint32_t)p.T ? (uint32_t)p.T : t0 + 1;
+            const int64_t r0 = (int64_t)path * (p.T + 1);
+            pre = as_mkt(p.rec[r0 + tt]);
+            postA = p.rec[r0 + tn];
+            postB = p.recg[r0 + tn];
+            e.path = path;
             e.s0_small = (s0 == -1.0f);
             e.s0 = e.s0_small ? 1.0f : s0;
-            uint32_t tt = e.t > (uint32_t)p.T ? (uint32_t)p.T : e.t;
-            pre = as_mkt(p.rec[(int64_t)e.path * (p.T + 1) + tt]);
         } else {
-            float s0f = p.rst[0];
-            e.s0_small = s0f < 1e-6f;
-            e.s0 = e.s0_small ? 1.0f : s0f;
+            float4 preA = p.tileA[(int64_t)slot0 * N + i];
+            postA = p.tileA[(int64_t)(slot0 + 1) * N + i];
+            postB = p.tileB[(int64_t)(slot0 + 1) * N + i];
+            // pin the loads here: otherwise preA is sunk into the t != 0 branch and
+            // becomes a second, dependent memory round trip
+            asm volatile("" : "+v"(preA.x), "+v"(preA.y), "+v"(preA.z), "+v"(preA.w), "+v"(postA.x),
+                         "+v"(postB.x));
             e.path = -1;
-            // unconditional load (no t -> load dependency), select afterwards
-            Mkt tp = as_mkt(p.tileA[(int64_t)slot0 * N + i]);
-            pre = (e.t == 0) ? Mkt{p.rst[0], p.rst[1], p.rst[2], p.rst[3]} : tp;
+            e.s0_small = rst.S < 1e-6f;
+            e.s0 = e.s0_small ? 1.0f : rst.S;
+            pre = (t0 == 0) ? rst : as_mkt(preA);  // select of values, not addresses
         }
+        e.t = t0;
+        e.call = unpack_lo(pk);
+        e.put = unpack_hi(pk);
+        e.cash = cash;
     }
     bool reset_any = false;
     for (int k = 0; k < k_steps; ++k) {
@@ -639,21 +657,17 @@ __global__ __launch_bounds__(kBlock) void step_kernel(Params p, State s, Io io, 
         float* orow = tile + threadIdx.x * kObs;
         bool term = false;
         if (live) {
-            Mkt post;
-            float4 g;
-            if (REPLAY) {
-                uint32_t tn = e.t + 1 > (uint32_t)p.T ? (uint32_t)p.T : e.t + 1;
-                int64_t r = (int64_t)e.path * (p.T + 1) + tn;
-                post = as_mkt(p.rec[r]);
-                g = p.recg[r];
-            } else {
-                int64_t r = (int64_t)(slot0 + k + 1) * N + i;
-                post = as_mkt(p.tileA[r]);
-                g = p.tileB[r];
+            const Mkt post = as_mkt(postA);
+            const float4 g = postB;
+            const float2 ak = a;
+            if (!REPLAY && k + 1 < k_steps) {
+                const int64_t r = (int64_t)(slot0 + k + 2) * N + i;
+                a = act[koff + N + i];
+                postA = p.tileA[r];
+                postB = p.tileB[r];
             }
-            float2 a = reinterpret_cast<const float2*>(io.act)[koff + i];
             StepOut so;
-            step_env(p, e, pre, post, a.x, a.y, so);
+            step_env(p, e, pre, post, ak.x, ak.y, so);
             term = so.term;
             if (INFO) write_info(io.info, i, so, e, post, p.variant);
             float o[kObs];
@@ -681,12 +695,19 @@ __global__ __launch_bounds__(kBlock) void step_kernel(Params p, State s, Io io, 
 #pragma unroll
                     for (int c = 0; c < kObs; ++c) orow[c] = o[c];
                 } else {
-                    pre = Mkt{p.rst[0], p.rst[1], p.rst[2], p.rst[3]};
+                    pre = rst;
 #pragma unroll
-                    for (int c = 0; c < kObs; ++c) orow[c] = p.rst[4 + c];
+                    for (int c = 0; c < kObs; ++c) orow[c] = p.rstv[4 + c];
                 }
                 reset_any = true;
             }
+        }
+        if (REPLAY && live && k + 1 < k_steps) {
+            const uint32_t tn = e.t + 1 > (uint32_t)p.T ? (uint32_t)p.T : e.t + 1;
+            const int64_t r = (int64_t)e.path * (p.T + 1) + tn;
+            a = act[koff + N + i];
+            postA = p.rec[r];
+            postB = p.recg[r];
         }
         if (io.obs) {
             __syncthreads();
@@ -731,14 +752,14 @@ __global__ __launch_bounds__(kBlock) void reset_kernel(Params p, State s, Market
         cur.t[i] = 0;
         cur.S[i] = p.s0;
         if (MODE == HE_MODE_HESTON) cur.v[i] = p.var;
-        cur.C[i] = p.rst[2];
-        cur.P[i] = p.rst[3];
-        m = Mkt{p.rst[0], p.rst[1], p.rst[2], p.rst[3]};
+        cur.C[i] = p.rstv[2];
+        cur.P[i] = p.rstv[3];
+        m = Mkt{p.rstv[0], p.rstv[1], p.rstv[2], p.rstv[3]};
         e.s0_small = m.S < 1e-6f;
         e.s0 = e.s0_small ? 1.0f : m.S;
         e.path = -1;
 #pragma unroll
-        for (int c = 0; c < kObs; ++c) o[c] = p.rst[4 + c];
+        for (int c = 0; c < kObs; ++c) o[c] = p.rstv[4 + c];
     }
     s.t[i] = 0;
     s.pos[i] = 0;
@@ -848,7 +869,7 @@ struct he_env {
     float4* rec = nullptr;
     float4* recg = nullptr;
     float4* tile = nullptr;   // 2 buffers x (tileA | tileB)
-    double* thp = nullptr;    // theta table [T+1]
+    float rstv[4 + kObs] = {};  // host copy of the reset market + obs (generate)
     float* rst = nullptr;     // reset market + obs (generate)
     int64_t n_paths = 0;
     int32_t block_pos = 0;    // generate: next slot to consume; M = tile exhausted/invalid
@@ -907,7 +928,6 @@ static void fill_params(he_env* env) {
     p.shares_d = (double)c.shares_to_hedge;
     p.shares_f = (float)c.shares_to_hedge;
     p.shares_zero = c.shares_to_hedge == 0;
-    p.thp_tab = env->thp;
     p.r_f = (float)c.risk_free_rate;
     p.tenor_f = (float)c.option_tenor_years;
     p.r_d = c.risk_free_rate;
@@ -950,7 +970,7 @@ static void fill_params(he_env* env) {
     p.T_f = (float)c.episode_length;
     p.M = c.market_block;
     p.tileA = p.tileB = nullptr;  // set per launch (tile_params)
-    p.rst = env->rst;
+    memcpy(p.rstv, env->rstv, sizeof(p.rstv));
     p.rec = env->rec;
     p.recg = env->recg;
     p.n_paths = env->n_paths;
@@ -961,21 +981,17 @@ static void launch_init_reset(he_env* env) {
     hipLaunchKernelGGL(init_reset_kernel<MODE>, dim3(1), dim3(64), 0, 0, env->p, env->rst);
 }
 
-// theta table + (generate) reset constants; re-run whenever T or the config changes.
+// (generate) reset market + reset obs, computed once on the device with the same
+// device functions as the step path, then handed to every kernel by value.
 static he_status upload_tables(he_env* env) {
-    const int32_t T = env->cfg.episode_length;
-    std::vector<double> h((size_t)T + 1);
-    for (int32_t t = 0; t <= T; ++t) h[(size_t)t] = env->cfg.theta_weight * ((double)(T - t) / 252.0);
-    if (env->thp) (void)hipFree(env->thp);
-    env->thp = nullptr;
-    HE_HIP(env, hipMalloc(&env->thp, h.size() * sizeof(double)));
-    HE_HIP(env, hipMemcpy(env->thp, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice));
     fill_params(env);
     if (is_generate(env)) {
         if (env->cfg.mode == HE_MODE_GBM) launch_init_reset<HE_MODE_GBM>(env);
         else launch_init_reset<HE_MODE_HESTON>(env);
         HE_HIP(env, hipGetLastError());
         HE_HIP(env, hipDeviceSynchronize());
+        HE_HIP(env, hipMemcpy(env->rstv, env->rst, sizeof(env->rstv), hipMemcpyDeviceToHost));
+        fill_params(env);
     }
     return HE_OK;
 }
@@ -1078,7 +1094,7 @@ static void launch_step(he_env* env, const Params& p, const Io& io, bool info, i
 // Start the next block: make its market tile current (generated ahead on the side
 // stream, or now on `st`), then prefetch the block after it on the side stream so
 // that market_kernel(b+1) runs concurrently with the step kernels of block b.
-static he_status advance_block(he_env* env, hipStream_t st) {
+static he_status advance_block(he_env* env, hipStream_t st, bool prefetch) {
     const int nb = env->cur_buf ^ 1;
     if (env->next_state == 0) {
         he_status s = market(env, 0, nb, st);
@@ -1090,7 +1106,7 @@ static he_status advance_block(he_env* env, hipStream_t st) {
     env->cur_buf = nb;
     env->block_pos = 0;
     env->next_state = 0;
-    if (env->prefetch) {
+    if (prefetch) {
         // fork: the side stream starts after everything already enqueued on st
         HE_HIP(env, hipEventRecord(env->ev_fork, st));
         HE_HIP(env, hipStreamWaitEvent(env->xs, env->ev_fork, 0));
@@ -1118,7 +1134,10 @@ static he_status launch_steps(he_env* env, Io io, bool info, int k_total, void* 
     int done = 0;
     while (done < k_total) {
         if (env->block_pos >= M) {
-            he_status s = advance_block(env, st);
+            // prefetch only under fused rollouts: beside single-step launches the
+            // background market waves cost the latency-bound step_kernel more than
+            // they save (MI355X, 65,536 envs: 6.94 vs 6.05 us/step)
+            he_status s = advance_block(env, st, env->prefetch && k_total > 1);
             if (s != HE_OK) return s;
         }
         int k = k_total - done;
@@ -1283,7 +1302,6 @@ he_status he_destroy(he_env* env) {
         if (env->rec) (void)hipFree(env->rec);
         if (env->recg) (void)hipFree(env->recg);
         if (env->tile) (void)hipFree(env->tile);
-        if (env->thp) (void)hipFree(env->thp);
         if (env->rst) (void)hipFree(env->rst);
         if (env->xs) {
             (void)hipStreamSynchronize(env->xs);
