@@ -149,6 +149,25 @@ HE_HD double norm_pdf(double x) {
 // OptionCalculator.black_scholes_price (quantconnect/option_calculator.py:11-27),
 // f64.  `a` = (r + 0.5*sigma**2)*T, `b` = sigma*sqrt(T), `disc` = exp(-r*T) are
 // precomputed with python-float semantics when sigma is constant.
+// log(S / K) for the rolling-ATM strike K = round(S): the quotient is within
+// 2^-7 of 1 whenever S >= 64, where log1p of y = q - 1 (exact, Sterbenz) is a
+// 9-term alternating series (truncation < y^10/10); elsewhere ocml log.
+HE_HD double log_ratio(double S, double K) {
+    const double q = S / K;
+    const double y = q - 1.0;
+    if (!(fabs(y) < 0.0078125)) return log(q);
+    double p = 1.0 / 9.0;
+    p = fma(p, y, -1.0 / 8.0);
+    p = fma(p, y, 1.0 / 7.0);
+    p = fma(p, y, -1.0 / 6.0);
+    p = fma(p, y, 1.0 / 5.0);
+    p = fma(p, y, -1.0 / 4.0);
+    p = fma(p, y, 1.0 / 3.0);
+    p = fma(p, y, -0.5);
+    p = fma(p, y, 1.0);
+    return y * p;
+}
+
 struct BSConst {
     double a, b, disc;
     double inv_b;   // 1/b: the constant-sigma division becomes a multiply (<= 1 ulp)
@@ -162,7 +181,7 @@ HE_HD void bs_call_put(double S, double K, const BSConst& c, double* call, doubl
         *put = (ip < 0.0) ? 0.0 : ip;
         return;
     }
-    double d1 = (log(S / K) + c.a) * c.inv_b;
+    double d1 = (log_ratio(S, K) + c.a) * c.inv_b;
     double d2 = d1 - c.b;
     double Kd = K * c.disc;
     double n1, m1, n2, m2;

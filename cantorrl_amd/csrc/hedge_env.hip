@@ -42,8 +42,8 @@ namespace {
 
 constexpr int kBlock = 256;      // step kernel: envs per workgroup
 constexpr int kObs = HE_OBS_DIM;
-constexpr int kMktEnvs = 64;     // market kernel: envs per workgroup (one wave wide)
-constexpr int kMktLanes = 4;     //                slot-lanes per env (4 waves)
+constexpr int kMktEnvs = 32;     // market kernel: envs per workgroup (half a wave wide)
+constexpr int kMktLanes = 8;     //                slot-lanes per env (4 waves, 16.6 KB LDS)
 constexpr int kMaxBlock = 64;    // max market block length M
 
 // ------------------------------------------------------------------ parameters
