@@ -45,13 +45,29 @@ TRAIN_KW = dict(loss_type="abs", pnl_penalty_weight=0.001, lambda_cost=0.0001, t
                 slippage_bps=1.0)  # train_ppo_v2.py:74-80
 GEN = dict(s0=496.48001098632812, variance=0.029028, mu=0.04, dt=1 / 252, episode_length=252)
 
+# BASELINE.json configs (configs[0] is the CPU case = cpu_baseline below)
+CONFIGS = {
+    2: dict(envs=65536, mode="gbm", gen=GEN, kw=TRAIN_KW,
+            workload="configs[1]: 65,536 parallel envs/GPU, European call (BS rolling-ATM marks), GBM, "
+                     "v2 env, train_ppo_v2 reward"),
+    3: dict(envs=1048576, mode="gbm", gen=GEN, kw=dict(TRAIN_KW, slippage_bps=5.0),
+            workload="configs[2]: 1,048,576 parallel envs/GPU, European call, GBM, proportional costs "
+                     "(5 bp slippage + $0.65 commission)"),
+    5: dict(envs=131072, mode="heston",
+            gen=dict(GEN, heston_kappa=2.0, heston_theta=0.029028, heston_xi=0.3, heston_rho=-0.7),
+            kw=TRAIN_KW,
+            workload="configs[4] market: Heston full-truncation Euler (rho=-0.7), 131,072 envs/GPU "
+                     "(1M over 8 GPUs)"),
+}
+
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2520)
     ap.add_argument("--warmup", type=int, default=256)
-    ap.add_argument("--envs", type=int, default=65536, help="envs per GPU")
+    ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS), help="BASELINE.json config")
+    ap.add_argument("--envs", type=int, default=None, help="envs per GPU (default: the config's)")
     ap.add_argument("--mode", choices=["graph", "eager", "rollout"], default="graph")
     ap.add_argument("--graph-chunk", type=int, default=64)
     ap.add_argument("--rollout-k", type=int, default=64)
@@ -91,9 +107,10 @@ def probe(args):
     """Short run for counter collection: 2 market blocks of eager he_step."""
     torch.cuda.set_device(0)
     from cantorrl_amd.vec_env import HedgingVecEnv
+    cfg = CONFIGS[args.config]
     n = args.envs
-    env = HedgingVecEnv(n, mode="gbm", generate=GEN, seed=args.seed, return_numpy=False, info_keys=(),
-                        **TRAIN_KW)
+    env = HedgingVecEnv(n, mode=cfg["mode"], generate=cfg["gen"], seed=args.seed, return_numpy=False,
+                        info_keys=(), **cfg["kw"])
     env.reset_tensors()
     acts = torch.rand((64, n, 2), device="cuda:0") * 2 - 1
     for k in range(128):
@@ -118,7 +135,8 @@ def pmc_traffic(args):
     for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
         with tempfile.TemporaryDirectory(dir="/tmp") as td:
             cmd = ["rocprofv3", "--pmc", ctr, "--output-format", "csv", "-d", td, "-o", "pmc", "--",
-                   sys.executable, os.path.abspath(__file__), "--probe", "--envs", str(args.envs)]
+                   sys.executable, os.path.abspath(__file__), "--probe", "--envs", str(args.envs),
+                   "--config", str(args.config)]
             try:
                 subprocess.run(cmd, check=True, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
                                timeout=240, cwd="/tmp", env=dict(os.environ, TMPDIR="/tmp"))
@@ -139,6 +157,8 @@ def pmc_traffic(args):
 
 def main():
     args = parse()
+    if args.envs is None:
+        args.envs = CONFIGS[args.config]["envs"]
     if args.probe:
         probe(args)
         return
@@ -158,9 +178,10 @@ def main():
     dev = torch.device("cuda", torch.cuda.current_device())
 
     from cantorrl_amd.vec_env import HedgingVecEnv
+    cfg = CONFIGS[args.config]
     n = args.envs
-    env = HedgingVecEnv(n, mode="gbm", generate=GEN, seed=args.seed, global_env_offset=rank * n,
-                        device=dev, return_numpy=False, info_keys=(), **TRAIN_KW)
+    env = HedgingVecEnv(n, mode=cfg["mode"], generate=cfg["gen"], seed=args.seed, global_env_offset=rank * n,
+                        device=dev, return_numpy=False, info_keys=(), **cfg["kw"])
     env.reset_tensors()
     ring = 256
     g = torch.Generator(device=dev)
@@ -313,8 +334,8 @@ def main():
         kern_ms = float(np.mean(kd[idx]))
         # market_kernel is prefetched on the library's side stream here; time it on a
         # handle without prefetch, where it runs inside the he_step of a block boundary
-        env2 = HedgingVecEnv(n, mode="gbm", generate=GEN, seed=args.seed, device=dev, return_numpy=False,
-                             info_keys=(), market_prefetch=False, **TRAIN_KW)
+        env2 = HedgingVecEnv(n, mode=cfg["mode"], generate=cfg["gen"], seed=args.seed, device=dev,
+                             return_numpy=False, info_keys=(), market_prefetch=False, **cfg["kw"])
         env2.reset_tensors()
         m = []
         with torch.cuda.stream(stream):
@@ -373,9 +394,8 @@ def main():
             "vs_baseline": None,
             "dtype": "f64+f32",
             "data": "synthetic (GBM paths from Philox4x32-10, U(-1,1) actions pre-generated on device)",
-            "config": {"workload": "configs[1]: 65,536 parallel envs/GPU, European call (BS rolling-ATM marks), "
-                                   "GBM fp32 env view, v2 env, train_ppo_v2 reward", "envs_per_gpu": n,
-                       "episode_length": GEN["episode_length"], "mode": args.mode,
+            "config": {"workload": cfg["workload"], "config_index": args.config, "envs_per_gpu": n,
+                       "episode_length": cfg["gen"]["episode_length"], "mode": args.mode,
                        "parallelism": f"env-shard x{world}"},
             "device_ms_per_step": round(dev_ms / K, 6),
             "roofline": roof,
