@@ -46,6 +46,7 @@ constexpr int kObs = HE_OBS_DIM;
 constexpr int kMktEnvs = 32;     // market kernel: envs per workgroup (half a wave wide)
 constexpr int kMktLanes = 8;     //                slot-lanes per env (4 waves, 16.6 KB LDS)
 constexpr int kMaxBlock = 64;    // max market block length M
+constexpr int64_t kPrefetchMinEnvs = 131072;  // auto prefetch for single steps from here
 
 // ------------------------------------------------------------------ parameters
 struct Params {
@@ -878,7 +879,7 @@ struct he_env {
     int32_t block_pos = 0;    // generate: next slot to consume; M = tile exhausted/invalid
     int32_t cur_buf = 0;      // tile buffer of the block being consumed
     int32_t next_state = 0;   // next block: 0 none, 1 generating on `xs` (ev_next), 2 ready
-    bool prefetch = true;     // generate block b+1 on `xs` while block b is stepped
+    int32_t prefetch_mode = 0; // 0 auto, 1 never, 2 always: market_kernel(b+1) on `xs` during block b
     hipStream_t xs = nullptr; // library side stream for market prefetch
     hipEvent_t ev_fork = nullptr, ev_next = nullptr;
     bool ready = false;       // a reset happened since create/seed
@@ -1140,7 +1141,13 @@ static he_status launch_steps(he_env* env, Io io, bool info, int k_total, void* 
             // prefetch only under fused rollouts: beside single-step launches the
             // background market waves cost the latency-bound step_kernel more than
             // they save (MI355X, 65,536 envs: 6.94 vs 6.05 us/step)
-            he_status s = advance_block(env, st, env->prefetch && k_total > 1);
+            // auto policy (MI355X, graph-mode he_step, GBM): at 65,536 envs the
+            // background market waves slow the latency-bound step_kernel more than
+            // they save (6.94 vs 6.05 us/step); from 2^18 envs the step_kernel is
+            // bandwidth-bound and overlap wins (+5% at 262k, +14% at 524k, +19% at 1M)
+            bool want = env->prefetch_mode == 2 ||
+                        (env->prefetch_mode == 0 && (k_total > 1 || c.n_envs >= kPrefetchMinEnvs));
+            he_status s = advance_block(env, st, want);
             if (s != HE_OK) return s;
         }
         int k = k_total - done;
@@ -1280,7 +1287,7 @@ he_status he_create(const he_config* cfg, he_env** out) {
         if (e != hipSuccess) return fail(env, HE_ENOMEM, "hipMalloc(tile %zu) failed: %s", tb, hipGetErrorString(e));
         HE_HIP(env, hipMalloc(&env->rst, 32 * sizeof(float)));
         env->block_pos = c.market_block;
-        env->prefetch = c.reserved_i == 0;  // market_prefetch: on unless disabled
+        env->prefetch_mode = c.reserved_i;  // market_prefetch mode (0 auto, 1 never, 2 always)
         HE_HIP(env, hipStreamCreateWithFlags(&env->xs, hipStreamNonBlocking));
         HE_HIP(env, hipEventCreateWithFlags(&env->ev_fork, hipEventDisableTiming));
         HE_HIP(env, hipEventCreateWithFlags(&env->ev_next, hipEventDisableTiming));

@@ -72,7 +72,7 @@ class HedgingVecEnv:
     def __init__(self, n_envs, data_file_path=None, *, tables=None, variant=2, mode=None,
                  generate=None, device=None, seed=None, global_env_offset=0, autoreset=True,
                  return_numpy=True, info_keys=MONITOR_KEYWORDS, monitor_keywords=None,
-                 market_block=64, market_prefetch=True, **env_kwargs):
+                 market_block=64, market_prefetch="auto", **env_kwargs):
         self.lib = _lib.load()
         self.num_envs = int(n_envs)
         self.variant = int(variant)
@@ -125,7 +125,8 @@ class HedgingVecEnv:
         cfg.market_block = int(market_block)
         if os.environ.get("CANTORRL_NO_PREFETCH"):
             market_prefetch = False
-        cfg.reserved_i = 0 if market_prefetch else 1
+        # 0 auto (rollouts, or single steps from 131,072 envs), 1 never, 2 always
+        cfg.reserved_i = 0 if market_prefetch == "auto" else (2 if market_prefetch else 1)
         base_seed = int(seed if seed is not None else gen.get("seed", 42))
         cfg.seed = base_seed
         self._cfg = cfg

@@ -103,7 +103,9 @@ typedef struct he_config {
     double heston_rho;
     int32_t market_block;       /* generate modes: steps of market data generated per
                                    market_kernel launch (1..64, default 64)          */
-    int32_t reserved_i;         /* 1: disable market prefetch on the side stream     */
+    int32_t reserved_i;         /* market prefetch on the side stream: 0 auto (fused
+                                   rollouts, or he_step from 131,072 envs), 1 never,
+                                   2 always                                          */
     double reserved[7];
 } he_config;
 
