@@ -41,6 +41,18 @@ using namespace he;
 
 namespace {
 
+#define GLOBAL __attribute__((address_space(1)))
+typedef float v2f __attribute__((ext_vector_type(2)));
+typedef float v4f __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 ld4(const GLOBAL v4f* p, int64_t k) {
+    v4f x = p[k];
+    return make_float4(x.x, x.y, x.z, x.w);
+}
+__device__ __forceinline__ float2 ld2(const GLOBAL v2f* p, int64_t k) {
+    v2f x = p[k];
+    return make_float2(x.x, x.y);
+}
+
 constexpr int kBlock = 256;      // step kernel: envs per workgroup
 constexpr int kObs = HE_OBS_DIM;
 constexpr int kMktEnvs = 32;     // market kernel: envs per workgroup (half a wave wide)
@@ -557,15 +569,28 @@ __device__ __forceinline__ void write_info(const he_info& inf, int64_t i, const 
     if (inf.current_episode_idx) inf.current_episode_idx[i] = e.path;
 }
 
-// Write a [rows][13] tile staged in LDS to out (row-major [N][13]) with 16-B stores.
-__device__ __forceinline__ void flush_obs_tile(const float* tile, float* out, int64_t row0, int rows) {
-    float* dst = out + row0 * kObs;
-    const int nf = rows * kObs;
-    const int nv = nf >> 2;  // row0*13*4 is 16-B aligned because row0 % 4 == 0
-    float4* d4 = reinterpret_cast<float4*>(dst);
-    const float4* s4 = reinterpret_cast<const float4*>(tile);
-    for (int k = threadIdx.x; k < nv; k += kBlock) d4[k] = s4[k];
-    for (int k = (nv << 2) + threadIdx.x; k < nf; k += kBlock) dst[k] = tile[k];
+// Write one wave's obs rows [wrow0, wrow0 + rows), staged in LDS as [64][13] at
+// wtile, to out (row-major [N][13]) with 16-B stores.  Wave-local: the lanes of a
+// wave issue their LDS writes and reads in program order, so no workgroup barrier.
+// (compiler-only barriers around it: no hardware wait is needed)
+__device__ __forceinline__ void flush_obs_wave(const float* wtile, float* out, int64_t wrow0, int rows, int lane) {
+    asm volatile("" ::: "memory");
+    GLOBAL float* dst = (GLOBAL float*)out + wrow0 * kObs;  // 16-B aligned: wrow0 % 64 == 0
+    GLOBAL v4f* d4 = (GLOBAL v4f*)dst;
+    const v4f* s4 = reinterpret_cast<const v4f*>(wtile);
+    if (rows == 64) {
+        // 64 rows = 208 float4: three per lane, a fourth on lanes 0-15
+        d4[lane] = s4[lane];
+        d4[lane + 64] = s4[lane + 64];
+        d4[lane + 128] = s4[lane + 128];
+        if (lane < 16) d4[lane + 192] = s4[lane + 192];
+    } else if (rows > 0) {
+        const int nf = rows * kObs;
+        const int nv = nf >> 2;
+        for (int k = lane; k < nv; k += 64) d4[k] = s4[k];
+        for (int k = (nv << 2) + lane; k < nf; k += 64) dst[k] = wtile[k];
+    }
+    asm volatile("" ::: "memory");
 }
 
 // replay reset (hedging_env_v2.py:145-173): draw the episode row from the env's
@@ -600,9 +625,12 @@ __device__ __forceinline__ void env_reset_common(const Params& p, Env& e) {
 // Every load of step 0 is issued in a straight-line prologue before its first use
 // (one memory round trip instead of two), and in generate mode the loads of step
 // k+1 go out before the arithmetic of step k (software pipelining for rollouts).
-template <int MODE, bool INFO>
-__global__ __launch_bounds__(kBlock) void step_kernel(Params p, State s, Io io, int k_steps, int slot0) {
+// SINGLE: the he_step instance (k_steps == 1 at compile time, straight-line code).
+template <int MODE, bool INFO, bool SINGLE>
+__global__ __launch_bounds__(kBlock) void step_kernel(Params pk, State s, Io io, int k_steps_arg, int slot0) {
     constexpr bool REPLAY = (MODE == HE_MODE_REPLAY);
+    const int k_steps = SINGLE ? 1 : k_steps_arg;
+    Params p = pk;
     // latency-critical: win VALU/memory issue arbitration against the prefetching
     // market_kernel waves that share the SIMDs (they run at the default priority 0)
     __builtin_amdgcn_s_setprio(3);
@@ -614,35 +642,55 @@ __global__ __launch_bounds__(kBlock) void step_kernel(Params p, State s, Io io, 
     const int64_t N = p.n;
     const float2* act = reinterpret_cast<const float2*>(io.act);
     const Mkt rst{p.rstv[0], p.rstv[1], p.rstv[2], p.rstv[3]};
+    // Every kernel argument of the prologue's addresses and of the step arithmetic,
+    // pinned in SGPRs by ONE asm: one scalar round trip to the kernarg segment.  Left
+    // alone, the backend sinks some of these loads into the `live` branch or after
+    // the first vector loads return, each a further serialized round trip (measured
+    // 0.3 us apiece at 65,536 envs).  The pointers are laundered as global-address-
+    // space pointers, or their loads would turn into flat loads.
+    auto s_t = (const GLOBAL uint32_t*)s.t;
+    auto s_pos = (const GLOBAL uint32_t*)s.pos;
+    auto s_cash = (const GLOBAL double*)s.cash;
+    auto gact = (const GLOBAL v2f*)act;
+    auto mA = (const GLOBAL v4f*)(REPLAY ? p.rec : p.tileA);
+    auto mB = (const GLOBAL v4f*)(REPLAY ? p.recg : p.tileB);
+    auto s_path = (const GLOBAL int32_t*)s.path;
+    auto s_s0 = (const GLOBAL float*)s.s0;
+    int32_t hot_i = REPLAY ? p.T : slot0;
+    asm volatile("" : "+s"(s_t), "+s"(s_pos), "+s"(s_cash), "+s"(gact), "+s"(mA), "+s"(mB), "+s"(hot_i));
+    if (REPLAY) asm volatile("" : "+s"(s_path), "+s"(s_s0));
     Env e;
     Mkt pre;
     float4 postA, postB;
     float2 a;
     if (live) {
-        const uint32_t t0 = s.t[i];
-        const uint32_t pk = s.pos[i];
-        const double cash = s.cash[i];
-        a = act[i];
+        const uint32_t t0 = s_t[i];
+        const uint32_t pk = s_pos[i];
+        double cash = s_cash[i];
+        a = ld2(gact, i);
         if (REPLAY) {
-            const int32_t path = s.path[i];
-            const float s0 = s.s0[i];
-            const uint32_t tt = t0 > (uint32_t)p.T ? (uint32_t)p.T : t0;
-            const uint32_t tn = t0 + 1 > (uint32_t)p.T ? (uint32_t)p.T : t0 + 1;
-            const int64_t r0 = (int64_t)path * (p.T + 1);
-            pre = as_mkt(p.rec[r0 + tt]);
-            postA = p.rec[r0 + tn];
-            postB = p.recg[r0 + tn];
+            const int32_t T = hot_i;
+            const int32_t path = s_path[i];
+            const float s0 = s_s0[i];
+            const uint32_t tt = t0 > (uint32_t)T ? (uint32_t)T : t0;
+            const uint32_t tn = t0 + 1 > (uint32_t)T ? (uint32_t)T : t0 + 1;
+            const int64_t r0 = (int64_t)path * (T + 1);
+            pre = as_mkt(ld4(mA, r0 + tt));
+            postA = ld4(mA, r0 + tn);
+            postB = ld4(mB, r0 + tn);
             e.path = path;
             e.s0_small = (s0 == -1.0f);
             e.s0 = e.s0_small ? 1.0f : s0;
         } else {
-            float4 preA = p.tileA[(int64_t)slot0 * N + i];
-            postA = p.tileA[(int64_t)(slot0 + 1) * N + i];
-            postB = p.tileB[(int64_t)(slot0 + 1) * N + i];
-            // pin the loads here: otherwise preA is sunk into the t != 0 branch and
-            // becomes a second, dependent memory round trip
+            float4 preA = ld4(mA, (int64_t)hot_i * N + i);
+            postA = ld4(mA, (int64_t)(hot_i + 1) * N + i);
+            postB = ld4(mB, (int64_t)(hot_i + 1) * N + i);
+            // pin every prologue load here: otherwise preA is sunk into the t != 0
+            // branch (a second, dependent memory round trip), and a load still
+            // pending at a branch merge makes the waitcnt pass drain every later
+            // store with vmcnt(0) before the final state stores
             asm volatile("" : "+v"(preA.x), "+v"(preA.y), "+v"(preA.z), "+v"(preA.w), "+v"(postA.x),
-                         "+v"(postB.x));
+                         "+v"(postB.x), "+v"(cash), "+v"(a.x), "+v"(a.y));
             e.path = -1;
             e.s0_small = rst.S < 1e-6f;
             e.s0 = e.s0_small ? 1.0f : rst.S;
@@ -676,8 +724,8 @@ __global__ __launch_bounds__(kBlock) void step_kernel(Params p, State s, Io io, 
             make_obs(p, e, post, g, pre.S, pre.v, o);
 #pragma unroll
             for (int c = 0; c < kObs; ++c) orow[c] = o[c];
-            if (io.rew) io.rew[koff + i] = (float)so.reward;
-            if (io.term) io.term[koff + i] = term ? 1 : 0;
+            if (io.rew) ((GLOBAL float*)io.rew)[koff + i] = (float)so.reward;
+            if (io.term) ((GLOBAL uint8_t*)io.term)[koff + i] = term ? 1 : 0;
             pre = post;
         }
         // wave-level done mask: waves without a terminating env skip the reset path
@@ -714,9 +762,9 @@ __global__ __launch_bounds__(kBlock) void step_kernel(Params p, State s, Io io, 
         if (io.obs) {
             // LDS-staged 16-B stores: measured 6.45 vs 7.14 us/step against per-lane
             // 4-B stores of the 52-B rows (MI355X, 65,536 envs, graph mode)
-            __syncthreads();
-            flush_obs_tile(tile, io.obs + koff * kObs, row0, rows);
-            __syncthreads();
+            const int wave = threadIdx.x >> 6;
+            const int wrows = rows - wave * 64 < 64 ? rows - wave * 64 : 64;
+            flush_obs_wave(tile + wave * 64 * kObs, io.obs + koff * kObs, row0 + wave * 64, wrows, threadIdx.x & 63);
         }
     }
     if (live) {
@@ -727,7 +775,7 @@ __global__ __launch_bounds__(kBlock) void step_kernel(Params p, State s, Io io, 
             s.path[i] = e.path;
             s.s0[i] = e.s0_small ? -1.0f : e.s0;
         }
-        if (io.trunc) io.trunc[i] = 0;
+        if (io.trunc) ((GLOBAL uint8_t*)io.trunc)[i] = 0;
     }
 }
 
@@ -1076,23 +1124,16 @@ template <int MODE>
 static void launch_step(he_env* env, const Params& p, const Io& io, bool info, int k, int slot0,
                         hipStream_t st) {
     int64_t blocks = (env->cfg.n_envs + kBlock - 1) / kBlock;
+    void (*kern)(Params, State, Io, int, int);
+    if (k == 1) kern = info ? step_kernel<MODE, true, true> : step_kernel<MODE, false, true>;
+    else kern = info ? step_kernel<MODE, true, false> : step_kernel<MODE, false, false>;
     if (env->ev_start) {  // one-shot: bracket exactly this dispatch (hipExtLaunchKernelGGL)
         hipEvent_t a = (hipEvent_t)env->ev_start, b = (hipEvent_t)env->ev_stop;
         env->ev_start = env->ev_stop = nullptr;
-        if (info)
-            hipExtLaunchKernelGGL((step_kernel<MODE, true>), dim3((unsigned)blocks), dim3(kBlock), 0, st, a, b,
-                                  0, p, env->s, io, k, slot0);
-        else
-            hipExtLaunchKernelGGL((step_kernel<MODE, false>), dim3((unsigned)blocks), dim3(kBlock), 0, st, a, b,
-                                  0, p, env->s, io, k, slot0);
+        hipExtLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kBlock), 0, st, a, b, 0, p, env->s, io, k, slot0);
         return;
     }
-    if (info)
-        hipLaunchKernelGGL((step_kernel<MODE, true>), dim3((unsigned)blocks), dim3(kBlock), 0, st, p, env->s,
-                           io, k, slot0);
-    else
-        hipLaunchKernelGGL((step_kernel<MODE, false>), dim3((unsigned)blocks), dim3(kBlock), 0, st, p, env->s,
-                           io, k, slot0);
+    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kBlock), 0, st, p, env->s, io, k, slot0);
 }
 
 // Start the next block: make its market tile current (generated ahead on the side
@@ -1138,9 +1179,6 @@ static he_status launch_steps(he_env* env, Io io, bool info, int k_total, void* 
     int done = 0;
     while (done < k_total) {
         if (env->block_pos >= M) {
-            // prefetch only under fused rollouts: beside single-step launches the
-            // background market waves cost the latency-bound step_kernel more than
-            // they save (MI355X, 65,536 envs: 6.94 vs 6.05 us/step)
             // auto policy (MI355X, graph-mode he_step, GBM): at 65,536 envs the
             // background market waves slow the latency-bound step_kernel more than
             // they save (6.94 vs 6.05 us/step); from 2^18 envs the step_kernel is
