@@ -46,5 +46,12 @@ def build(force=False, verbose=False):
     return OUT
 
 
+def build_variant(out, extra_flags):
+    """Diagnostic / A-B builds (e.g. -DHE_TIMING) outside the package directory."""
+    os.makedirs(os.path.dirname(os.path.abspath(out)), exist_ok=True)
+    subprocess.run([HIPCC, *FLAGS, *extra_flags, "-o", out, SRC], check=True)
+    return out
+
+
 if __name__ == "__main__":
     print(build(force="--force" in sys.argv, verbose=True))

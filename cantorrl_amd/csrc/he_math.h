@@ -22,6 +22,19 @@ HE_HD double np_max(double a, double b) { return (a != a) ? a : ((b != b) ? b : 
 // np.clip(x, lo, hi) for f32 with NaN propagation.
 HE_HD float np_clipf(float x, float lo, float hi) { return x < lo ? lo : (x > hi ? hi : x); }
 
+// a / b, correctly rounded, from y = RN(1/b) precomputed on the host (Markstein:
+// q = RN(a*y), r = a - b*q is exact by FMA, and RN(q + r*y) = RN(a/b) whenever the
+// quotient is clear of overflow and underflow).  Zero, subnormal, huge and
+// non-finite quotients take the IEEE division.  Checked against a / b on 1.05e9
+// pairs, 210 divisors (tests/test_lib_cpu.py repeats a sample through the host build).
+HE_HD double div_by(double a, double b, double y) {
+    double q = a * y;
+    double aq = fabs(q);
+    if (!(aq > 0x1p-960 && aq < 0x1p+960)) return a / b;
+    double r = fma(-q, b, a);
+    return fma(r, y, q);
+}
+
 // np.rint(f32).astype(int64) then np.clip(., -mt, mt)  (hedging_env_v2.py:184-188).
 // x86 cvttss2si maps NaN and |x| >= 2^63 to INT64_MIN, which the clip sends to -mt.
 HE_HD int32_t trade_round(float f, int32_t mt) {

@@ -70,7 +70,7 @@ struct Params {
     float mt_f, maxh_f, T_f;
     float init_cash_f;
     double tcpc, slip_frac, lam, w, theta, initial_cash;
-    double shares_d;
+    double shares_d, inv_shares;  // inv_*: RN(1/x) for div_by
     float shares_f;
     int32_t shares_zero;
     // observation / greeks constants (hedging_env_v2.py:57-58)
@@ -88,6 +88,8 @@ struct Params {
     double g_sst;                // sigma*sqrt(T) (f64)
     double g_inv_sst;            // 1/(sigma*sqrt(T))
     double h_kappa, h_theta, h_xi, h_rho, h_sqrt1mrho2;
+    int32_t den_const;      // generate: reward denominator of the shared S0 (all envs)
+    double den, inv_den;
     int32_t M;              // market block length
     float4* tileA;          // [M+1][N] {S, v, C, P}
     float4* tileB;          // [M+1][N] {call_delta, gamma, put_delta, 0}
@@ -96,6 +98,9 @@ struct Params {
     const float4* rec;      // [n_paths][T+1] {S, v, C, P}; C/P at T hold row T-1
     const float4* recg;     // [n_paths][T+1] {call_delta, gamma, put_delta, 0}
     int64_t n_paths;
+#ifdef HE_TIMING
+    uint64_t* tim;          // [5][8192][2]
+#endif
 };
 
 struct State {
@@ -497,23 +502,26 @@ __device__ __forceinline__ void step_env(const Params& p, Env& e, const Mkt& pre
     double optv = ((double)e.call * (double)post.C) * 100.0 + ((double)e.put * (double)post.P) * 100.0;
     double pv = ((double)(p.shares_f * post.S) + optv) + e.cash;
     double pnl = pv - pv_prev;
-    double ps = p.shares_zero ? pnl : pnl / p.shares_d;
+    double ps = p.shares_zero ? pnl : div_by(pnl, p.shares_d, p.inv_shares);
     // (vii) reward (:243-262)
-    float f = np_maxf(e.s0, 25.0f);
     double term_v;
-    if (p.loss == HE_LOSS_MSE) {
-        double den = e.s0_small ? (625.0 + 1e-9) : (double)(f * f + 1e-9f);
-        term_v = (ps * ps) / den;
+    const double num = (p.loss == HE_LOSS_MSE) ? ps * ps : fabs(ps);
+    if (p.den_const) {
+        term_v = div_by(num, p.den, p.inv_den);
     } else {
-        double den = e.s0_small ? (25.0 + 1e-9) : (double)(f + 1e-9f);
-        term_v = fabs(ps) / den;
+        float f = np_maxf(e.s0, 25.0f);
+        double den;
+        if (p.loss == HE_LOSS_MSE) den = e.s0_small ? (625.0 + 1e-9) : (double)(f * f + 1e-9f);
+        else den = e.s0_small ? (25.0 + 1e-9) : (double)(f + 1e-9f);
+        term_v = num / den;
     }
     double rpc = (-p.w) * term_v;
     double tcp = p.lam * tc;
     double thp = 0.0, reward;
     if (p.variant == 2) {
-        // computed, not looked up: a table load indexed by t is a dependent round trip
-        thp = p.theta * ((double)(p.T - (int32_t)e.t) / 252.0);
+        // computed, not looked up: a table load indexed by t is a dependent round trip.
+        // theta_weight 0 (the default): 0 * finite = +0 and x - +0 == x bit for bit
+        if (p.theta != 0.0) thp = p.theta * div_by((double)(p.T - (int32_t)e.t), 252.0, 1.0 / 252.0);
         reward = (rpc - tcp) - thp;
     } else {
         reward = rpc - tcp;
@@ -625,21 +633,47 @@ __device__ __forceinline__ void env_reset_common(const Params& p, Env& e) {
 // Every load of step 0 is issued in a straight-line prologue before its first use
 // (one memory round trip instead of two), and in generate mode the loads of step
 // k+1 go out before the arithmetic of step k (software pipelining for rollouts).
+#ifdef HE_TIMING
+// Diagnostic builds (tools/step_ab.sh): per-wave timestamps of the last step_kernel
+// at fixed points into p.tim[point][wave][2] = {s_memrealtime (100 MHz, points 0
+// and 4 only), s_memtime (shader clock)}.
+#define HE_TIM(k)                                                                          \
+    do {                                                                                   \
+        uint64_t rt_ = ((k) == 0 || (k) == 4) ? __builtin_amdgcn_s_memrealtime() : 0;       \
+        uint64_t ct_ = __builtin_amdgcn_s_memtime();                                        \
+        if ((threadIdx.x & 63) == 0) {                                                     \
+            size_t w_ = (size_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);            \
+            if (w_ < 8192) {                                                               \
+                p.tim[((size_t)(k) * 8192 + w_) * 2] = rt_;                                \
+                p.tim[((size_t)(k) * 8192 + w_) * 2 + 1] = ct_;                            \
+            }                                                                              \
+        }                                                                                  \
+    } while (0)
+#else
+#define HE_TIM(k) \
+    do {          \
+    } while (0)
+#endif
+
 // SINGLE: the he_step instance (k_steps == 1 at compile time, straight-line code).
+// tA/tB: the market source, tile buffer {S,v,C,P} / greeks (generate) or the
+// replay table rec / recg.
 template <int MODE, bool INFO, bool SINGLE>
-__global__ __launch_bounds__(kBlock) void step_kernel(Params pk, State s, Io io, int k_steps_arg, int slot0) {
+__device__ __forceinline__ void step_body(const Params& pk, int64_t n_envs, const float4* tA, const float4* tB,
+                                          State s, Io io, int k_steps_arg, int slot0) {
     constexpr bool REPLAY = (MODE == HE_MODE_REPLAY);
     const int k_steps = SINGLE ? 1 : k_steps_arg;
     Params p = pk;
+    HE_TIM(0);
     // latency-critical: win VALU/memory issue arbitration against the prefetching
     // market_kernel waves that share the SIMDs (they run at the default priority 0)
     __builtin_amdgcn_s_setprio(3);
     __shared__ __attribute__((aligned(16))) float tile[kBlock * kObs];
     const int64_t row0 = (int64_t)blockIdx.x * kBlock;
     const int64_t i = row0 + threadIdx.x;
-    const bool live = i < p.n;
-    const int rows = (int)((p.n - row0) < kBlock ? (p.n - row0) : kBlock);
-    const int64_t N = p.n;
+    const int64_t N = n_envs;
+    const bool live = i < N;
+    const int rows = (int)((N - row0) < kBlock ? (N - row0) : kBlock);
     const float2* act = reinterpret_cast<const float2*>(io.act);
     const Mkt rst{p.rstv[0], p.rstv[1], p.rstv[2], p.rstv[3]};
     // Every kernel argument of the prologue's addresses and of the step arithmetic,
@@ -652,13 +686,14 @@ __global__ __launch_bounds__(kBlock) void step_kernel(Params pk, State s, Io io,
     auto s_pos = (const GLOBAL uint32_t*)s.pos;
     auto s_cash = (const GLOBAL double*)s.cash;
     auto gact = (const GLOBAL v2f*)act;
-    auto mA = (const GLOBAL v4f*)(REPLAY ? p.rec : p.tileA);
-    auto mB = (const GLOBAL v4f*)(REPLAY ? p.recg : p.tileB);
+    auto mA = (const GLOBAL v4f*)tA;
+    auto mB = (const GLOBAL v4f*)tB;
     auto s_path = (const GLOBAL int32_t*)s.path;
     auto s_s0 = (const GLOBAL float*)s.s0;
     int32_t hot_i = REPLAY ? p.T : slot0;
     asm volatile("" : "+s"(s_t), "+s"(s_pos), "+s"(s_cash), "+s"(gact), "+s"(mA), "+s"(mB), "+s"(hot_i));
     if (REPLAY) asm volatile("" : "+s"(s_path), "+s"(s_s0));
+    HE_TIM(1);
     Env e;
     Mkt pre;
     float4 postA, postB;
@@ -691,6 +726,7 @@ __global__ __launch_bounds__(kBlock) void step_kernel(Params pk, State s, Io io,
             // store with vmcnt(0) before the final state stores
             asm volatile("" : "+v"(preA.x), "+v"(preA.y), "+v"(preA.z), "+v"(preA.w), "+v"(postA.x),
                          "+v"(postB.x), "+v"(cash), "+v"(a.x), "+v"(a.y));
+            HE_TIM(2);
             e.path = -1;
             e.s0_small = rst.S < 1e-6f;
             e.s0 = e.s0_small ? 1.0f : rst.S;
@@ -713,8 +749,8 @@ __global__ __launch_bounds__(kBlock) void step_kernel(Params pk, State s, Io io,
             if (!REPLAY && k + 1 < k_steps) {
                 const int64_t r = (int64_t)(slot0 + k + 2) * N + i;
                 a = act[koff + N + i];
-                postA = p.tileA[r];
-                postB = p.tileB[r];
+                postA = tA[r];
+                postB = tB[r];
             }
             StepOut so;
             step_env(p, e, pre, post, ak.x, ak.y, so);
@@ -739,9 +775,9 @@ __global__ __launch_bounds__(kBlock) void step_kernel(Params pk, State s, Io io,
                 if (REPLAY) {
                     replay_reset(p, s, i, e);
                     int64_t r = (int64_t)e.path * (p.T + 1);
-                    pre = as_mkt(p.rec[r]);
+                    pre = as_mkt(tA[r]);
                     float o[kObs];
-                    make_obs(p, e, pre, p.recg[r], pre.S, pre.v, o);
+                    make_obs(p, e, pre, tB[r], pre.S, pre.v, o);
 #pragma unroll
                     for (int c = 0; c < kObs; ++c) orow[c] = o[c];
                 } else {
@@ -756,9 +792,10 @@ __global__ __launch_bounds__(kBlock) void step_kernel(Params pk, State s, Io io,
             const uint32_t tn = e.t + 1 > (uint32_t)p.T ? (uint32_t)p.T : e.t + 1;
             const int64_t r = (int64_t)e.path * (p.T + 1) + tn;
             a = act[koff + N + i];
-            postA = p.rec[r];
-            postB = p.recg[r];
+            postA = tA[r];
+            postB = tB[r];
         }
+        HE_TIM(3);
         if (io.obs) {
             // LDS-staged 16-B stores: measured 6.45 vs 7.14 us/step against per-lane
             // 4-B stores of the 52-B rows (MI355X, 65,536 envs, graph mode)
@@ -777,6 +814,39 @@ __global__ __launch_bounds__(kBlock) void step_kernel(Params pk, State s, Io io,
         }
         if (io.trunc) ((GLOBAL uint8_t*)io.trunc)[i] = 0;
     }
+    HE_TIM(4);
+}
+
+// Every step path: Params by value in the kernel arguments.
+template <int MODE, bool INFO, bool SINGLE>
+__global__ __launch_bounds__(kBlock) void step_kernel(Params pk, State s, Io io, int k_steps, int slot0) {
+    constexpr bool REPLAY = (MODE == HE_MODE_REPLAY);
+    step_body<MODE, INFO, SINGLE>(pk, pk.n, REPLAY ? pk.rec : pk.tileA, REPLAY ? pk.recg : pk.tileB, s, io,
+                                  k_steps, slot0);
+}
+
+// he_step without info: Params from a device-resident copy; the kernel arguments carry
+// only the pointers the first loads need (132 B instead of ~850 B of kernarg segment).
+struct StepIo {
+    const float* act;
+    float* obs;
+    float* rew;
+    uint8_t* term;
+    uint8_t* trunc;
+    float* tobs;
+};
+template <int MODE>
+__global__ __launch_bounds__(kBlock) void step1_kernel(const Params* __restrict__ pc, int64_t n, const float4* tA,
+                                                       const float4* tB, State s, StepIo sio, int slot0) {
+    Io io;
+    io.act = sio.act;
+    io.obs = sio.obs;
+    io.rew = sio.rew;
+    io.term = sio.term;
+    io.trunc = sio.trunc;
+    io.tobs = sio.tobs;
+    io.info = he_info{};
+    step_body<MODE, false, true>(*pc, n, tA, tB, s, io, 1, slot0);
 }
 
 // Explicit reset of envs `ids` (NULL: all).  Generate: the market position of a
@@ -923,6 +993,7 @@ struct he_env {
     float4* tile = nullptr;   // 2 buffers x (tileA | tileB)
     float rstv[4 + kObs] = {};  // host copy of the reset market + obs (generate)
     float* rst = nullptr;     // reset market + obs (generate)
+    Params* dparams = nullptr;  // device copies of tile_params(env, 0 / 1) for step1_kernel
     int64_t n_paths = 0;
     int32_t block_pos = 0;    // generate: next slot to consume; M = tile exhausted/invalid
     int32_t cur_buf = 0;      // tile buffer of the block being consumed
@@ -955,6 +1026,10 @@ static he_status fail(he_env* env, he_status st, const char* fmt, ...) {
 
 static bool is_generate(const he_env* env) { return env->cfg.mode != HE_MODE_REPLAY; }
 
+#ifdef HE_TIMING
+static uint64_t* g_tim = nullptr;
+#endif
+
 static void fill_params(he_env* env) {
     const he_config& c = env->cfg;
     Params& p = env->p;
@@ -978,6 +1053,7 @@ static void fill_params(he_env* env) {
     p.theta = c.theta_weight;
     p.initial_cash = c.initial_cash;
     p.shares_d = (double)c.shares_to_hedge;
+    p.inv_shares = 1.0 / p.shares_d;
     p.shares_f = (float)c.shares_to_hedge;
     p.shares_zero = c.shares_to_hedge == 0;
     p.r_f = (float)c.risk_free_rate;
@@ -1023,14 +1099,40 @@ static void fill_params(he_env* env) {
     p.M = c.market_block;
     p.tileA = p.tileB = nullptr;  // set per launch (tile_params)
     memcpy(p.rstv, env->rstv, sizeof(p.rstv));
+    if (is_generate(env)) {
+        // every generate-mode episode starts at the same S0 = rstv[0] (f32), so the
+        // reward denominator (hedging_env_v2.py:243-253) is one host constant
+        float s0 = p.rstv[0];
+        bool small = s0 < 1e-6f;
+        float f = small ? 25.0f : (s0 > 25.0f || s0 != s0 ? s0 : 25.0f);
+        if (c.loss_type == HE_LOSS_MSE) p.den = small ? (625.0 + 1e-9) : (double)(f * f + 1e-9f);
+        else p.den = small ? (25.0 + 1e-9) : (double)(f + 1e-9f);
+        p.inv_den = 1.0 / p.den;
+        p.den_const = 1;
+    }
     p.rec = env->rec;
     p.recg = env->recg;
+#ifdef HE_TIMING
+    if (!g_tim && hipMalloc(&g_tim, (size_t)5 * 8192 * 2 * 8) != hipSuccess) g_tim = nullptr;
+    p.tim = g_tim;
+#endif
     p.n_paths = env->n_paths;
 }
 
 template <int MODE>
 static void launch_init_reset(he_env* env) {
     hipLaunchKernelGGL(init_reset_kernel<MODE>, dim3(1), dim3(64), 0, 0, env->p, env->rst);
+}
+
+static Params tile_params(const he_env* env, int b);
+
+// Refresh the device copies of Params after fill_params.  Not stream-ordered, so the
+// device is drained first (configuration calls only, never on the step path).
+static he_status sync_dparams(he_env* env) {
+    Params h[2] = {tile_params(env, 0), tile_params(env, 1)};
+    HE_HIP(env, hipDeviceSynchronize());
+    HE_HIP(env, hipMemcpy(env->dparams, h, sizeof(h), hipMemcpyHostToDevice));
+    return HE_OK;
 }
 
 // (generate) reset market + reset obs, computed once on the device with the same
@@ -1045,12 +1147,13 @@ static he_status upload_tables(he_env* env) {
         HE_HIP(env, hipMemcpy(env->rstv, env->rst, sizeof(env->rstv), hipMemcpyDeviceToHost));
         fill_params(env);
     }
-    return HE_OK;
+    return sync_dparams(env);
 }
 
 // Params with the tile pointers of buffer b.
 static Params tile_params(const he_env* env, int b) {
     Params p = env->p;
+    if (!env->tile) return p;  // replay
     const size_t slots = (size_t)(env->cfg.market_block + 1) * (size_t)env->cfg.n_envs;
     p.tileA = env->tile + (size_t)b * 2 * slots;
     p.tileB = p.tileA + slots;
@@ -1124,6 +1227,23 @@ template <int MODE>
 static void launch_step(he_env* env, const Params& p, const Io& io, bool info, int k, int slot0,
                         hipStream_t st) {
     int64_t blocks = (env->cfg.n_envs + kBlock - 1) / kBlock;
+    if (k == 1 && !info) {
+        constexpr bool REPLAY = (MODE == HE_MODE_REPLAY);
+        const Params* pc = env->dparams + (REPLAY ? 0 : env->cur_buf);
+        const float4* tA = REPLAY ? p.rec : p.tileA;
+        const float4* tB = REPLAY ? p.recg : p.tileB;
+        StepIo sio{io.act, io.obs, io.rew, io.term, io.trunc, io.tobs};
+        if (env->ev_start) {
+            hipEvent_t a = (hipEvent_t)env->ev_start, b = (hipEvent_t)env->ev_stop;
+            env->ev_start = env->ev_stop = nullptr;
+            hipExtLaunchKernelGGL(step1_kernel<MODE>, dim3((unsigned)blocks), dim3(kBlock), 0, st, a, b, 0, pc,
+                                  p.n, tA, tB, env->s, sio, slot0);
+            return;
+        }
+        hipLaunchKernelGGL(step1_kernel<MODE>, dim3((unsigned)blocks), dim3(kBlock), 0, st, pc, p.n, tA, tB, env->s,
+                           sio, slot0);
+        return;
+    }
     void (*kern)(Params, State, Io, int, int);
     if (k == 1) kern = info ? step_kernel<MODE, true, true> : step_kernel<MODE, false, true>;
     else kern = info ? step_kernel<MODE, true, false> : step_kernel<MODE, false, false>;
@@ -1330,6 +1450,7 @@ he_status he_create(const he_config* cfg, he_env** out) {
         HE_HIP(env, hipEventCreateWithFlags(&env->ev_fork, hipEventDisableTiming));
         HE_HIP(env, hipEventCreateWithFlags(&env->ev_next, hipEventDisableTiming));
     }
+    HE_HIP(env, hipMalloc(&env->dparams, 2 * sizeof(Params)));
     he_status st = upload_tables(env);
     if (st != HE_OK) return st;
     // default streams: env i seeded with (seed + global id) until he_seed is called
@@ -1351,6 +1472,7 @@ he_status he_destroy(he_env* env) {
         if (env->recg) (void)hipFree(env->recg);
         if (env->tile) (void)hipFree(env->tile);
         if (env->rst) (void)hipFree(env->rst);
+        if (env->dparams) (void)hipFree(env->dparams);
         if (env->xs) {
             (void)hipStreamSynchronize(env->xs);
             (void)hipStreamDestroy(env->xs);
@@ -1453,6 +1575,21 @@ he_status he_host_philox(uint64_t seed, uint64_t env_id, uint64_t n, uint32_t ou
     return HE_OK;
 }
 
+#ifdef HE_TIMING
+he_status he_debug_timing(void* host, size_t bytes) {
+    const size_t cap = (size_t)5 * 8192 * 2 * 8;
+    if (bytes > cap) bytes = cap;
+    return hipMemcpy(host, g_tim, bytes, hipMemcpyDeviceToHost) == hipSuccess ? HE_OK : HE_EHIP;
+}
+#endif
+
+he_status he_host_div_by(const double* a, int64_t count, double b, double* out) {
+    if ((!a || !out) && count > 0) return HE_EINVAL;
+    const double y = 1.0 / b;
+    for (int64_t k = 0; k < count; ++k) out[k] = div_by(a[k], b, y);
+    return HE_OK;
+}
+
 he_status he_seed(he_env* env, const int64_t* env_ids, const uint64_t* seeds, int64_t count) {
     if (!env) return HE_EINVAL;
     if (!seeds || count < 1) return fail(env, HE_EINVAL, "he_seed needs >= 1 seed");
@@ -1479,6 +1616,8 @@ he_status he_seed(he_env* env, const int64_t* env_ids, const uint64_t* seeds, in
     } else {
         env->cfg.seed = seeds[0];
         fill_params(env);
+        he_status s = sync_dparams(env);
+        if (s != HE_OK) return s;
         // episode counters restart: the next reset starts episode 0 of every env
         HE_HIP(env, hipMemset(env->cur.ep, 0xFF, (size_t)N * 4));
         env->block_pos = env->cfg.market_block;

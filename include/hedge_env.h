@@ -218,6 +218,9 @@ he_status he_pcg64_seed_state(uint64_t seed, uint64_t state[4]);
  * and the 4 Philox4x32-10 words of (seed, global env id, env-step index n). */
 he_status he_host_episode_draws(uint64_t seed, uint64_t n_paths, int64_t count, int64_t* out);
 he_status he_host_philox(uint64_t seed, uint64_t env_id, uint64_t n, uint32_t out[4]);
+/* out[k] = a[k] / b through the reciprocal-multiply division the step kernel uses
+ * for its constant divisors (must equal IEEE a[k] / b bit for bit). */
+he_status he_host_div_by(const double* a, int64_t count, double b, double* out);
 
 #ifdef __cplusplus
 }

@@ -88,3 +88,22 @@ def test_host_philox_matches_oracle_and_kat():
         seed, g, n = (int(x) for x in rng.integers(0, 2 ** 62, 3))
         exp = tuple(int(np.asarray(w).item()) for w in philox_words(seed, g, n))
         assert _lib.host_philox(seed, g, n) == exp
+
+
+@pytest.mark.parametrize("b", [10000.0, 252.0, 25.0 + 1e-9, 625.0 + 1e-9, 496.4800109863281 + 1e-9, 1.0, 3.0,
+                               0.1, 7.5e-3])
+def test_reciprocal_division_is_ieee_division(b):
+    # step_kernel divides P&L by shares_to_hedge, the reward term by its constant
+    # denominator and (T - t) by 252 through q + (a - b q) / b with q = a * RN(1/b)
+    rng = np.random.default_rng(int(b * 1000) % 2 ** 32)
+    a = np.concatenate([
+        rng.standard_normal(200_000) * 10.0 ** rng.integers(-12, 12, 200_000),
+        np.round(rng.uniform(-1e6, 1e6, 100_000), 2),             # cent-valued P&L
+        np.arange(0, 253, dtype=np.float64),                       # T - t
+        [0.0, -0.0, np.inf, -np.inf, np.nan, 5e-324, -5e-324, 1e-310, 1.7e308, -1.7e308],
+    ])
+    got = _lib.host_div_by(a, b)
+    with np.errstate(over="ignore"):
+        exp = a / b
+    assert_same(got, exp, "div_by")
+    assert np.array_equal(np.signbit(got), np.signbit(exp))

@@ -9,6 +9,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 
+#include <algorithm>
 #include <vector>
 
 #include "../include/hedge_env.h"
@@ -23,12 +24,14 @@ struct Api {
     decltype(&he_step) step;
     decltype(&he_sync_market) sync_market;
     decltype(&he_last_error) last_error;
+    void* handle;
 };
 
 static Api load(const char* path) {
     void* h = dlopen(path, RTLD_NOW | RTLD_LOCAL);
     if (!h) { fprintf(stderr, "dlopen %s: %s\n", path, dlerror()); exit(1); }
     Api a;
+    a.handle = h;
     a.config_init = (decltype(a.config_init))dlsym(h, "he_config_init");
     a.create = (decltype(a.create))dlsym(h, "he_create");
     a.destroy = (decltype(a.destroy))dlsym(h, "he_destroy");
@@ -93,6 +96,34 @@ int main(int argc, char** argv) {
         CK(hipEventElapsedTime(&ms, a, b));
         double us = ms * 1000.0 / (reps * 64.0);
         printf("%-24s%s%s N=%lld  %.3f us/step  %.4e env-steps/s\n", argv[li], o ? "" : " (no obs)", c.reserved_i == 2 ? " (prefetch)" : "", (long long)N, us, N / us * 1e6);
+        typedef he_status (*tim_fn)(void*, size_t);
+        tim_fn tim = (tim_fn)dlsym(api.handle, "he_debug_timing");
+        if (tim) {
+            // per-wave timestamps of the last step_kernel: {realtime 100 MHz, shader clock}
+            const int W = 8192, P = 5;  // [5][8192][2]
+            std::vector<uint64_t> t((size_t)5 * W * 2);
+            tim(t.data(), t.size() * 8);
+            const int nw = (int)((N + 63) / 64);
+            auto at = [&](int k, int w, int c) { return t[((size_t)k * W + w) * 2 + c]; };
+            uint64_t rt0 = ~0ull, rt0max = 0, rtend = 0;
+            double dc[P] = {0};
+            for (int w = 0; w < nw; ++w) {
+                rt0 = std::min(rt0, at(0, w, 0));
+                rt0max = std::max(rt0max, at(0, w, 0));
+                rtend = std::max(rtend, at(4, w, 0));
+                for (int k = 1; k < P; ++k) dc[k] += (double)(at(k, w, 1) - at(k - 1, w, 1));
+            }
+            printf("   waves %d: start spread %.2f us, first start -> last end %.2f us\n", nw, (rt0max - rt0) * 0.01,
+                   (rtend - rt0) * 0.01);
+            printf("   mean shader cycles: entry->scalar %.0f, ->vector %.0f, ->compute %.0f, ->end %.0f\n",
+                   dc[1] / nw, dc[2] / nw, dc[3] / nw, dc[4] / nw);
+            // histogram of wave start offsets (realtime ticks of 10 ns)
+            int hist[12] = {0};
+            for (int w = 0; w < nw; ++w) { int b = (int)((at(0, w, 0) - rt0) / 25); hist[b > 11 ? 11 : b]++; }
+            printf("   start histogram (0.25 us bins):");
+            for (int b = 0; b < 12; ++b) printf(" %d", hist[b]);
+            printf("\n");
+        }
         for (int gi = 0; gi < 4; ++gi) { hipGraphExecDestroy(ge[gi]); hipGraphDestroy(g[gi]); }
         api.destroy(env);
     }
