@@ -125,6 +125,7 @@ def pmc_traffic(args):
     gfx950, so bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024).  Runs BEFORE this process
     touches the GPU; the profiled program is a child (`rocprofv3 ... -- python3`)."""
     import csv
+    import re
     import glob
     import shutil
     import subprocess
@@ -146,7 +147,7 @@ def pmc_traffic(args):
             for f in glob.glob(os.path.join(td, "**", "*counter_collection.csv"), recursive=True):
                 with open(f) as fh:
                     for r in csv.DictReader(fh):
-                        if "step_kernel" in r.get("Kernel_Name", "") and r.get("Counter_Name") == ctr:
+                        if re.search(r"step1?_kernel", r.get("Kernel_Name", "")) and r.get("Counter_Name") == ctr:
                             rows.append(float(r["Counter_Value"]))
             if not rows:
                 return None, f"no {ctr} rows for step_kernel"
