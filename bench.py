@@ -1,23 +1,29 @@
 #!/usr/bin/env python3
 """Headline benchmark: env-steps/s of the batched hedging env on MI355X.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--envs E] [--mode graph|eager|rollout]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config C] [--envs E]
+                    [--mode rollout|graph|eager]
 
 Workload = BASELINE.json configs[1]: 65,536 parallel envs per GPU, GBM price
 advance (Philox4x32-10 normals), Black-Scholes rolling-ATM marks, v2 env with
 the train_ppo_v2.py reward settings (abs loss, w=1e-3, lambda=1e-4,
 theta=2e-4, 1 bp slippage).  One "step" = one env-step of every env: actions
 [N,2] in (pre-generated, HBM-resident), obs [N,13] / reward [N] / done flags
-out, auto-reset inside the kernel.
+out, auto-reset inside the kernel, plus the market generation of that step.
 
-Modes: `graph` (default) replays he_step launches captured into a hipGraph,
-one kernel per step; `eager` calls he_step from Python every step; `rollout`
-fuses 64 steps per launch (he_rollout).  For N>1 the script runs under
-torch.distributed.run, one rank per GPU (weak scaling: E envs per rank, env
-ids offset by rank), and all-gathers per-env rewards over RCCL every 256 steps
-(the rollout-buffer boundary of train_ppo_v2.py:48).
+Modes: `rollout` (default) fuses 64 steps per launch (he_rollout: actions
+[64,N,2] in, obs [64,N,13] / reward / terminated out, the collect_rollouts
+inner loop of train_ppo_v2.py:48 with actions supplied up front); `graph`
+replays he_step launches captured into hipGraphs, one kernel per step (the
+Gym step API path); `eager` calls he_step from Python every step.  At N=1 the
+JSON line also carries the graph-mode he_step measurement under "step_api".
+For N>1 the script runs under torch.distributed.run, one rank per GPU (weak
+scaling: E envs per rank, env ids offset by rank), and all-gathers per-env
+rewards over RCCL every 256 steps (the rollout-buffer boundary of
+train_ppo_v2.py:48).
 """
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -29,17 +35,21 @@ import torch
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
-# algorithmic HBM bytes per env-step of step_kernel<GBM> (DESIGN.md "Roofline"):
+# Algorithmic HBM bytes per env-step:
+# he_step (step1_kernel, one launch per step):
 #   reads : state (t 4, pos 4, cash 8) 16 + action 8 + market tile slots
-#           (pre {S,v,C,P} 16, post {S,v,C,P} 16, post greeks 16) 48            = 72
+#           (pre {S,v,C,P} 16, post {S,v,C,P} 16, post greeks+lag 16) 48            = 72
 #   writes: state 16 + obs 52 + reward 4 + terminated 1 + truncated 1             = 74
 STEP_BYTES_PER_ENV = 146
-# market_kernel per env-step: tile {S,v,C,P} + greeks written (32) + per-block state
-MARKET_BYTES_PER_ENV = 32
-# he_rollout per env-step: action 8 + obs 52 + reward 4 + terminated 1 + tile read 32
+# he_rollout (step_kernel, K steps per launch, state in registers):
+#   per step: action 8 + tile post slots 32 (read) + obs 52 + reward 4 + terminated 1 = 97
+#   per launch: state 16 read + 16 written + pre slot 16 read                         = 48
 ROLLOUT_BYTES_PER_ENV = 97
-ROLLOUT_STATE_BYTES = 16 + 16 + 16
-HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+ROLLOUT_STATE_BYTES = 48
+# market_kernel per env-step: tile {S,v,C,P} + {greeks, lag} written (32)
+MARKET_BYTES_PER_ENV = 32
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
+M_BLOCK = 64           # market block (he_config.market_block)
 
 TRAIN_KW = dict(loss_type="abs", pnl_penalty_weight=0.001, lambda_cost=0.0001, theta_weight=0.0002,
                 slippage_bps=1.0)  # train_ppo_v2.py:74-80
@@ -64,13 +74,13 @@ CONFIGS = {
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=2520)
+    ap.add_argument("--steps", type=int, default=2560)
     ap.add_argument("--warmup", type=int, default=256)
     ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS), help="BASELINE.json config")
     ap.add_argument("--envs", type=int, default=None, help="envs per GPU (default: the config's)")
-    ap.add_argument("--mode", choices=["graph", "eager", "rollout"], default="graph")
-    ap.add_argument("--graph-chunk", type=int, default=64)
+    ap.add_argument("--mode", choices=["rollout", "graph", "eager"], default="rollout")
     ap.add_argument("--rollout-k", type=int, default=64)
+    ap.add_argument("--no-step-api", action="store_true", help="skip the secondary graph-mode he_step run")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--seed", type=int, default=42)
@@ -103,30 +113,109 @@ def cpu_baseline(seconds):
                        f"({el:.1f} s, 1 thread, NumPy)")
 
 
-def probe(args):
-    """Short run for counter collection: 2 market blocks of eager he_step."""
-    torch.cuda.set_device(0)
+def make_env(args, dev, rank=0, prefetch="auto"):
     from cantorrl_amd.vec_env import HedgingVecEnv
     cfg = CONFIGS[args.config]
-    n = args.envs
-    env = HedgingVecEnv(n, mode=cfg["mode"], generate=cfg["gen"], seed=args.seed, return_numpy=False,
-                        info_keys=(), **cfg["kw"])
+    env = HedgingVecEnv(args.envs, mode=cfg["mode"], generate=cfg["gen"], seed=args.seed,
+                        global_env_offset=rank * args.envs, device=dev, return_numpy=False, info_keys=(),
+                        market_prefetch=prefetch, **cfg["kw"])
     env.reset_tensors()
-    acts = torch.rand((64, n, 2), device="cuda:0") * 2 - 1
-    for k in range(128):
-        env.step_tensors(acts[k % 64])
+    return env
+
+
+class Runner:
+    """Enqueues env-steps of one handle in one mode (rollout / graph / eager)."""
+
+    def __init__(self, args, env, mode, acts, stream, dist=None, gathered=None):
+        self.args, self.env, self.mode, self.acts, self.stream = args, env, mode, acts, stream
+        self.dist, self.gathered = dist, gathered
+        self.lib, self.h = env.lib, env._h
+        self.ring = acts.shape[0]
+        n = args.envs
+        dev = acts.device
+        self.chunk = args.rollout_k if mode == "rollout" else (M_BLOCK if mode == "graph" else 1)
+        if mode == "rollout":
+            RK = args.rollout_k
+            self.ro = torch.empty((RK, n, 13), dtype=torch.float32, device=dev)
+            self.rr = torch.empty((RK, n), dtype=torch.float32, device=dev)
+            self.rt = torch.empty((RK, n), dtype=torch.uint8, device=dev)
+        self.graphs = []
+        self.replays = 0
+        if mode == "graph":
+            with torch.cuda.stream(stream):
+                # one eager block first, so each captured graph is the steady state
+                # [fork: market_kernel(b+1) on the side stream || 64 x step1_kernel(b)] + join
+                for j in range(M_BLOCK):
+                    self.step(j, stream.cuda_stream)
+                env.sync_market()
+                torch.cuda.synchronize()
+                for gi in range(self.ring // M_BLOCK):
+                    gr = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(gr, stream=stream):
+                        cs = torch.cuda.current_stream().cuda_stream
+                        for j in range(M_BLOCK):
+                            self.step(gi * M_BLOCK + j, cs)
+                        env.sync_market()
+                    self.graphs.append(gr)
+            torch.cuda.synchronize()
+
+    def step(self, k, s):
+        e = self.env
+        st = self.lib.he_step(self.h, self.acts[k % self.ring].data_ptr(), e._obs.data_ptr(), e._rew.data_ptr(),
+                              e._term.data_ptr(), e._trunc.data_ptr(), e._tobs.data_ptr(), None, s)
+        if st:
+            raise RuntimeError(self.lib.he_last_error(self.h).decode())
+
+    def rollout(self, done, s):
+        RK = self.args.rollout_k
+        a0 = done % self.ring
+        a = self.acts[a0:a0 + RK] if a0 + RK <= self.ring else self.acts[:RK]
+        st = self.lib.he_rollout(self.h, RK, a.data_ptr(), self.ro.data_ptr(), self.rr.data_ptr(),
+                                 self.rt.data_ptr(), s)
+        if st:
+            raise RuntimeError(self.lib.he_last_error(self.h).decode())
+
+    def run(self, steps):
+        """Enqueue `steps` env-steps (a multiple of the chunk) on self.stream."""
+        done = 0
+        cs = self.stream.cuda_stream
+        while done < steps:
+            if self.mode == "graph":
+                self.graphs[self.replays % len(self.graphs)].replay()
+                self.replays += 1
+            elif self.mode == "eager":
+                self.step(done, cs)
+            else:
+                self.rollout(done, cs)
+            done += self.chunk
+            if self.dist is not None and done % 256 == 0:
+                # per-env summary gather at the rollout-buffer boundary (train_ppo_v2.py:48)
+                src = self.rr[-1] if self.mode == "rollout" else self.env._rew
+                self.dist.all_gather_into_tensor(self.gathered, src)
+
+
+def probe(args):
+    """Short run for counter collection (the headline mode's kernel)."""
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    env = make_env(args, dev)
+    acts = torch.rand((256, args.envs, 2), device=dev) * 2 - 1
+    stream = torch.cuda.Stream(device=dev)
+    r = Runner(args, env, "eager" if args.mode == "graph" else args.mode, acts, stream)
+    with torch.cuda.stream(stream):
+        r.run(r.chunk * (8 if args.mode == "rollout" else 128))
     torch.cuda.synchronize()
     env.close()
 
 
 def pmc_traffic(args):
-    """HBM bytes per step_kernel launch from rocprofv3 PMC counters, one counter per
+    """HBM bytes per step-kernel launch from rocprofv3 PMC counters, one counter per
     pass (MI355X_MICROARCH.md "HBM": FETCH_SIZE reads 1/2 of a wide coalesced read on
     gfx950, so bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024).  Runs BEFORE this process
     touches the GPU; the profiled program is a child (`rocprofv3 ... -- python3`)."""
     import csv
-    import re
     import glob
+    import re
     import shutil
     import subprocess
     import tempfile
@@ -137,7 +226,7 @@ def pmc_traffic(args):
         with tempfile.TemporaryDirectory(dir="/tmp") as td:
             cmd = ["rocprofv3", "--pmc", ctr, "--output-format", "csv", "-d", td, "-o", "pmc", "--",
                    sys.executable, os.path.abspath(__file__), "--probe", "--envs", str(args.envs),
-                   "--config", str(args.config)]
+                   "--config", str(args.config), "--mode", args.mode, "--rollout-k", str(args.rollout_k)]
             try:
                 subprocess.run(cmd, check=True, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
                                timeout=240, cwd="/tmp", env=dict(os.environ, TMPDIR="/tmp"))
@@ -150,22 +239,138 @@ def pmc_traffic(args):
                         if re.search(r"step1?_kernel", r.get("Kernel_Name", "")) and r.get("Counter_Name") == ctr:
                             rows.append(float(r["Counter_Value"]))
             if not rows:
-                return None, f"no {ctr} rows for step_kernel"
-            vals[ctr] = float(np.mean(rows[8:] if len(rows) > 16 else rows))
+                return None, f"no {ctr} rows for the step kernel"
+            skip = 2 if args.mode == "rollout" else 8
+            vals[ctr] = float(np.mean(rows[skip:] if len(rows) > 2 * skip else rows))
     traffic = (2.0 * vals["FETCH_SIZE"] + vals["WRITE_SIZE"]) * 1024.0
     return traffic, vals
+
+
+class HipEvents:
+    """hipEvent_t pairs from the HIP runtime torch (and libhedgeenv) use."""
+
+    def __init__(self):
+        self.hip = ctypes.CDLL("libamdhip64.so.7")
+
+    def create(self):
+        e = ctypes.c_void_p()
+        if self.hip.hipEventCreate(ctypes.byref(e)) != 0:
+            raise RuntimeError("hipEventCreate failed")
+        return e
+
+    def record(self, e, stream):
+        self.hip.hipEventRecord(e, ctypes.c_void_p(stream.cuda_stream))
+
+    def elapsed_ms(self, a, b):
+        ms = ctypes.c_float()
+        if self.hip.hipEventElapsedTime(ctypes.byref(ms), a, b) != 0:
+            raise RuntimeError("hipEventElapsedTime failed")
+        return ms.value
+
+    def destroy(self, *evs):
+        for e in evs:
+            self.hip.hipEventDestroy(e)
+
+
+def kernel_time_ms(hev, runner, nprobe):
+    """Live duration of the step kernel: he_time_next_step brackets exactly the next
+    step-kernel dispatch with HIP events on `runner.stream` (hipExtLaunchKernelGGL)."""
+    env, lib, h, stream = runner.env, runner.lib, runner.h, runner.stream
+    kev = [(hev.create(), hev.create()) for _ in range(nprobe)]
+    env.reset_tensors()
+    torch.cuda.synchronize()
+    with torch.cuda.stream(stream):
+        for k in range(nprobe):
+            lib.he_time_next_step(h, kev[k][0], kev[k][1])
+            if runner.mode == "rollout":
+                runner.rollout(k * runner.chunk, stream.cuda_stream)
+            else:
+                runner.step(k, stream.cuda_stream)
+    torch.cuda.synchronize()
+    kd = np.array([hev.elapsed_ms(a, b) for a, b in kev])
+    for a, b in kev:
+        hev.destroy(a, b)
+    skip = 4 if runner.mode == "rollout" else 8
+    return float(np.mean(kd[skip:]))
+
+
+def market_time_ms(hev, args, dev, acts, stream):
+    """market_kernel duration per block of M_BLOCK steps: he_step on a handle without
+    prefetch, where it runs inside the he_step call of every block boundary."""
+    env2 = make_env(args, dev, prefetch=False)
+    m = []
+    with torch.cuda.stream(stream):
+        for k in range(4 * M_BLOCK):
+            a, b = hev.create(), hev.create()
+            hev.record(a, stream)
+            st = env2.lib.he_step(env2._h, acts[k % acts.shape[0]].data_ptr(), env2._obs.data_ptr(),
+                                  env2._rew.data_ptr(), env2._term.data_ptr(), env2._trunc.data_ptr(), None,
+                                  None, stream.cuda_stream)
+            hev.record(b, stream)
+            if st:
+                raise RuntimeError(env2.lib.he_last_error(env2._h).decode())
+            m.append((a, b))
+    torch.cuda.synchronize()
+    d2 = np.array([hev.elapsed_ms(a, b) for a, b in m])
+    for a, b in m:
+        hev.destroy(a, b)
+    env2.close()
+    return float(np.median(d2[M_BLOCK::M_BLOCK])) - float(np.median(np.delete(d2, np.arange(0, 4 * M_BLOCK, M_BLOCK))))
+
+
+def timed(runner, K, W, dist):
+    """W untimed warm-up steps, then exactly K timed steps between barriers; returns
+    (max-over-ranks wall seconds, device ms on the stream)."""
+    stream = runner.stream
+    with torch.cuda.stream(stream):
+        runner.run(W)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    with torch.cuda.stream(stream):
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev1 = torch.cuda.Event(enable_timing=True)
+        ev0.record(stream)
+        runner.run(K)
+        ev1.record(stream)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    t = torch.tensor([wall], dtype=torch.float64, device=torch.device("cuda", torch.cuda.current_device()))
+    if dist is not None:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item()), ev0.elapsed_time(ev1)
+
+
+def roofline(mode, n, kern_ms, rk):
+    if mode == "rollout":
+        bytes_launch = n * rk * (ROLLOUT_BYTES_PER_ENV + ROLLOUT_STATE_BYTES / rk)
+        kname = "step_kernel<GBM> (he_rollout, K=%d fused steps)" % rk
+    else:
+        bytes_launch = n * STEP_BYTES_PER_ENV
+        kname = "step1_kernel<GBM> (he_step, K=1)"
+    achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
+    return dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
+                frac=round(achieved / HBM_PEAK_GBS, 4), traffic=None, kernel=kname,
+                kernel_us=round(kern_ms * 1e3, 3), bytes_per_launch=int(bytes_launch))
 
 
 def main():
     args = parse()
     if args.envs is None:
         args.envs = CONFIGS[args.config]["envs"]
+    if args.mode == "rollout" and (args.rollout_k < 1 or args.rollout_k > M_BLOCK):
+        raise SystemExit("--rollout-k must be in [1, 64]")
     if args.probe:
         probe(args)
         return
     world = int(os.environ.get("WORLD_SIZE", "1"))
     pmc = (None, "skipped")
-    if world == 1 and not args.no_pmc and args.mode != "rollout":
+    if world == 1 and not args.no_pmc:
         pmc = pmc_traffic(args)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -177,214 +382,55 @@ def main():
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
-
-    from cantorrl_amd.vec_env import HedgingVecEnv
     cfg = CONFIGS[args.config]
     n = args.envs
-    env = HedgingVecEnv(n, mode=cfg["mode"], generate=cfg["gen"], seed=args.seed, global_env_offset=rank * n,
-                        device=dev, return_numpy=False, info_keys=(), **cfg["kw"])
-    env.reset_tensors()
-    ring = 256
+
     g = torch.Generator(device=dev)
     g.manual_seed(1234 + rank)
-    acts = torch.rand((ring, n, 2), device=dev, generator=g) * 2 - 1
+    acts = torch.rand((256, n, 2), device=dev, generator=g) * 2 - 1
     stream = torch.cuda.Stream(device=dev)
     gathered = torch.empty((world, n), dtype=torch.float32, device=dev) if world > 1 else None
 
-    lib = env.lib
-    h = env._h
-    obs, rew, term, trunc, tobs = env._obs, env._rew, env._term, env._trunc, env._tobs
+    env = make_env(args, dev, rank)
+    runner = Runner(args, env, args.mode, acts, stream, dist, gathered)
+    K = -(-args.steps // runner.chunk) * runner.chunk
+    W = -(-args.warmup // runner.chunk) * runner.chunk
+    wall, dev_ms = timed(runner, K, W, dist)
+    hev = HipEvents()
+    kern_ms = kernel_time_ms(hev, runner, 64 if args.mode == "rollout" else 256)
+    env.close()
 
-    def launch(k, s):
-        st = lib.he_step(h, acts[k % ring].data_ptr(), obs.data_ptr(), rew.data_ptr(), term.data_ptr(),
-                         trunc.data_ptr(), tobs.data_ptr(), None, s)
-        if st:
-            raise RuntimeError(lib.he_last_error(h).decode())
-
-    K = args.steps
-    W = args.warmup
-    graphs = []
-    if args.mode == "graph":
-        C = args.graph_chunk  # == market block: every graph = one block of steps
-        K = -(-K // C) * C
-        W = -(-W // C) * C
-        with torch.cuda.stream(stream):
-            # one eager block first, so each captured graph is the steady state
-            # [fork: market_kernel(b+1) on the side stream || C x step_kernel(b)] + join
-            for j in range(C):
-                launch(j, stream.cuda_stream)
-            env.sync_market()
-            torch.cuda.synchronize()
-            for gi in range(ring // C):
-                gr = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(gr, stream=stream):
-                    cs = torch.cuda.current_stream().cuda_stream
-                    for j in range(C):
-                        launch(gi * C + j, cs)
-                    env.sync_market()
-                graphs.append(gr)
-        torch.cuda.synchronize()
-        # device state = after the eager block; graphs replay in capture order from here
-
-    roll_obs = roll_rew = roll_term = None
-    if args.mode == "rollout":
-        RK = args.rollout_k
-        roll_obs = torch.empty((RK, n, 13), dtype=torch.float32, device=dev)
-        roll_rew = torch.empty((RK, n), dtype=torch.float32, device=dev)
-        roll_term = torch.empty((RK, n), dtype=torch.uint8, device=dev)
-
-    replays = [0]
-
-    def run(steps, s):
-        """Enqueue `steps` env-steps on stream s."""
-        done = 0
-        cs = s.cuda_stream
-        while done < steps:
-            if args.mode == "graph":
-                # K, W are multiples of the chunk; graphs replay in capture order
-                graphs[replays[0] % len(graphs)].replay()
-                replays[0] += 1
-                done += args.graph_chunk
-            elif args.mode == "eager":
-                launch(done, cs)
-                done += 1
-            else:
-                RK = min(args.rollout_k, steps - done)
-                a0 = (done % ring)
-                a = acts[a0:a0 + RK] if a0 + RK <= ring else acts[:RK]
-                st = lib.he_rollout(h, RK, a.data_ptr(), roll_obs.data_ptr(), roll_rew.data_ptr(),
-                                    roll_term.data_ptr(), cs)
-                if st:
-                    raise RuntimeError(lib.he_last_error(h).decode())
-                done += RK
-            if dist is not None and done % 256 == 0:
-                dist.all_gather_into_tensor(gathered, rew)
-
-    with torch.cuda.stream(stream):
-        run(W, stream)
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    with torch.cuda.stream(stream):
-        ev0 = torch.cuda.Event(enable_timing=True)
-        ev1 = torch.cuda.Event(enable_timing=True)
-        ev0.record(stream)
-        run(K, stream)
-        ev1.record(stream)
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
-    wall = time.perf_counter() - t0
-    t = torch.tensor([wall], dtype=torch.float64, device=dev)
-    if dist is not None:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    wall = float(t.item())
-    dev_ms = ev0.elapsed_time(ev1)
-
-    # live per-launch kernel duration: HIP events bracketing single launches on `stream`
-    # (the he_step of every 64th step also launches market_kernel for the next 64 steps)
-    # `kev` brackets exactly the step_kernel dispatch (he_time_next_step ->
-    # hipExtLaunchKernelGGL), `oev` the whole call (+ market_kernel every 64 steps)
-    nprobe = 256
-    import ctypes
-    hip = ctypes.CDLL("libamdhip64.so.7")  # the HIP runtime torch (and libhedgeenv) use
-
-    def mk():
-        e = ctypes.c_void_p()
-        if hip.hipEventCreate(ctypes.byref(e)) != 0:
-            raise RuntimeError("hipEventCreate failed")
-        return e
-
-    def elapsed(a, b):
-        ms = ctypes.c_float()
-        if hip.hipEventElapsedTime(ctypes.byref(ms), a, b) != 0:
-            raise RuntimeError("hipEventElapsedTime failed")
-        return ms.value
-
-    kev = [(mk(), mk()) for _ in range(nprobe)]
-    oev = [(mk(), mk()) for _ in range(nprobe)]
-    env.reset_tensors()
-    torch.cuda.synchronize()
-    sh = ctypes.c_void_p(stream.cuda_stream)
-    with torch.cuda.stream(stream):
-        for k in range(nprobe):
-            hip.hipEventRecord(oev[k][0], sh)
-            lib.he_time_next_step(h, kev[k][0], kev[k][1])
-            if args.mode == "rollout":
-                RK = args.rollout_k
-                lib.he_rollout(h, RK, acts[:RK].data_ptr(), roll_obs.data_ptr(), roll_rew.data_ptr(),
-                               roll_term.data_ptr(), stream.cuda_stream)
-            else:
-                launch(k, stream.cuda_stream)
-            hip.hipEventRecord(oev[k][1], sh)
-    torch.cuda.synchronize()
-    kd = np.array([elapsed(a, b) for a, b in kev])  # ms
-    od = np.array([elapsed(a, b) for a, b in oev])
-    for a, b in kev + oev:
-        hip.hipEventDestroy(a)
-        hip.hipEventDestroy(b)
-    M = 64
-    if args.mode == "rollout":
-        kern_ms = float(np.mean(kd[4:]))
-        mkt_ms = None  # prefetched on the side stream (see graph-mode probe)
-    else:
-        idx = np.arange(8, nprobe)
-        kern_ms = float(np.mean(kd[idx]))
-        # market_kernel is prefetched on the library's side stream here; time it on a
-        # handle without prefetch, where it runs inside the he_step of a block boundary
-        env2 = HedgingVecEnv(n, mode=cfg["mode"], generate=cfg["gen"], seed=args.seed, device=dev,
-                             return_numpy=False, info_keys=(), market_prefetch=False, **cfg["kw"])
-        env2.reset_tensors()
-        m = []
-        with torch.cuda.stream(stream):
-            for k in range(4 * M):
-                a, b = mk(), mk()
-                hip.hipEventRecord(a, sh)
-                st2 = lib.he_step(env2._h, acts[k % ring].data_ptr(), env2._obs.data_ptr(), env2._rew.data_ptr(),
-                                  env2._term.data_ptr(), env2._trunc.data_ptr(), None, None, stream.cuda_stream)
-                hip.hipEventRecord(b, sh)
-                if st2:
-                    raise RuntimeError(lib.he_last_error(env2._h).decode())
-                m.append((a, b))
-        torch.cuda.synchronize()
-        d2 = np.array([elapsed(a, b) for a, b in m])
-        for a, b in m:
-            hip.hipEventDestroy(a)
-            hip.hipEventDestroy(b)
-        mkt_ms = float(np.median(d2[M::M])) - float(np.median(np.delete(d2, np.arange(0, 4 * M, M))))
-        env2.close()
-
-    total_envs = n * world
-    value = total_envs * K / wall
-    if args.mode == "rollout":
-        RK = args.rollout_k
-        bytes_launch = n * RK * (ROLLOUT_BYTES_PER_ENV + ROLLOUT_STATE_BYTES / RK)
-        kname = "step_kernel<GBM> (K=%d fused) + market_kernel" % RK
-    else:
-        bytes_launch = n * STEP_BYTES_PER_ENV
-        kname = "step_kernel<GBM> (K=1)"
-    achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
-    roof = dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
-                frac=round(achieved / HBM_PEAK_GBS, 4), traffic=None, kernel=kname,
-                kernel_us=round(kern_ms * 1e3, 3), bytes_per_launch=int(bytes_launch))
-    if mkt_ms is not None:
-        roof["market_kernel_us_per_64_steps"] = round(mkt_ms * 1e3, 3)
-        roof["market_kernel_us_per_step"] = round(mkt_ms * 1e3 / M, 3)
+    roof = roofline(args.mode, n, kern_ms, args.rollout_k)
+    mkt_ms = market_time_ms(hev, args, dev, acts, stream)
+    roof["market_kernel_us_per_64_steps"] = round(mkt_ms * 1e3, 3)
+    roof["market_kernel_us_per_step"] = round(mkt_ms * 1e3 / M_BLOCK, 3)
     if pmc[0] is not None:
         roof["traffic"] = int(pmc[0])
         roof["traffic_counters_kb"] = {k: round(v, 1) for k, v in pmc[1].items()}
     else:
         roof["traffic_note"] = pmc[1]
+
+    step_api = None
+    if world == 1 and args.mode != "graph" and not args.no_step_api:
+        # secondary: the Gym step API path, one he_step launch per step in hipGraphs
+        env_g = make_env(args, dev)
+        rg = Runner(args, env_g, "graph", acts, stream)
+        Kg = -(-min(K, 2560) // M_BLOCK) * M_BLOCK
+        wall_g, _ = timed(rg, Kg, M_BLOCK * 4, None)
+        kg = kernel_time_ms(hev, rg, 256)
+        env_g.close()
+        rf = roofline("graph", n, kg, 1)
+        step_api = dict(mode="graph (he_step, one launch per step)", value=round(n * Kg / wall_g, 1),
+                        ms_per_step=round(wall_g * 1e3 / Kg, 6), kernel=rf["kernel"], kernel_us=rf["kernel_us"],
+                        achieved_gbs=rf["achieved"], frac=rf["frac"], bytes_per_launch=rf["bytes_per_launch"])
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args.cpu_seconds)
     if rank == 0:
         line = {
             "metric": "env-steps/sec (batched episodes)",
-            "value": round(value, 1),
+            "value": round(n * world * K / wall, 1),
             "unit": "env-steps/s",
             "n_gpus": world,
             "steps": K,
@@ -397,13 +443,14 @@ def main():
             "data": "synthetic (GBM paths from Philox4x32-10, U(-1,1) actions pre-generated on device)",
             "config": {"workload": cfg["workload"], "config_index": args.config, "envs_per_gpu": n,
                        "episode_length": cfg["gen"]["episode_length"], "mode": args.mode,
+                       "rollout_k": args.rollout_k if args.mode == "rollout" else None,
                        "parallelism": f"env-shard x{world}"},
             "device_ms_per_step": round(dev_ms / K, 6),
             "roofline": roof,
+            "step_api": step_api,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
-    env.close()
     if dist is not None:
         dist.destroy_process_group()
 

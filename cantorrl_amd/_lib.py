@@ -87,7 +87,7 @@ EXPORTS = [
     "he_config_init", "he_create", "he_destroy", "he_last_error", "he_version", "he_load_paths",
     "he_seed", "he_reset", "he_step", "he_rollout", "he_num_envs", "he_episode_length",
     "he_num_episodes", "he_get_config", "he_state_size", "he_get_state", "he_set_state",
-    "he_pcg64_seed_state", "he_host_episode_draws", "he_host_philox", "he_host_div_by", "he_time_next_step",
+    "he_pcg64_seed_state", "he_host_episode_draws", "he_host_philox", "he_host_div_by", "he_host_div_byf", "he_time_next_step",
     "he_sync_market",
 ]
 
@@ -135,6 +135,7 @@ def load(path=LIB_PATH):
         "he_host_episode_draws": (i32, [u64, u64, i64, vp]),
         "he_host_philox": (i32, [u64, u64, u64, ctypes.POINTER(ctypes.c_uint32 * 4)]),
         "he_host_div_by": (i32, [ctypes.c_void_p, i64, ctypes.c_double, ctypes.c_void_p]),
+        "he_host_div_byf": (i32, [ctypes.c_void_p, i64, ctypes.c_float, ctypes.c_void_p]),
         "he_time_next_step": (i32, [vp, vp, vp]),
         "he_sync_market": (i32, [vp, vp]),
     }
@@ -185,4 +186,14 @@ def host_div_by(a, b):
     a = np.ascontiguousarray(a, np.float64)
     out = np.empty_like(a)
     check(lib, None, lib.he_host_div_by(a.ctypes.data, a.size, float(b), out.ctypes.data), "he_host_div_by")
+    return out
+
+
+def host_div_byf(a, b):
+    """Host build of the obs kernels' f32 reciprocal-multiply division, for tests."""
+    import numpy as np
+    lib = load()
+    a = np.ascontiguousarray(a, np.float32)
+    out = np.empty_like(a)
+    check(lib, None, lib.he_host_div_byf(a.ctypes.data, a.size, float(b), out.ctypes.data), "he_host_div_byf")
     return out

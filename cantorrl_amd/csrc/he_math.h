@@ -24,15 +24,29 @@ HE_HD float np_clipf(float x, float lo, float hi) { return x < lo ? lo : (x > hi
 
 // a / b, correctly rounded, from y = RN(1/b) precomputed on the host (Markstein:
 // q = RN(a*y), r = a - b*q is exact by FMA, and RN(q + r*y) = RN(a/b) whenever the
-// quotient is clear of overflow and underflow).  Zero, subnormal, huge and
-// non-finite quotients take the IEEE division.  Checked against a / b on 1.05e9
+// quotient and the dividend are clear of overflow and underflow).  Zero, tiny, huge
+// and non-finite operands take the IEEE division.  Checked against a / b on 1.05e9
 // pairs, 210 divisors (tests/test_lib_cpu.py repeats a sample through the host build).
 HE_HD double div_by(double a, double b, double y) {
     double q = a * y;
-    double aq = fabs(q);
-    if (!(aq > 0x1p-960 && aq < 0x1p+960)) return a / b;
+    double aq = fabs(q), aa = fabs(a);
+    // r = a - b q must be exact: keep q and a (so r ~ ulp(a)) clear of subnormals
+    if (!(aq > 0x1p-960 && aq < 0x1p+960 && aa > 0x1p-960)) return a / b;
     double r = fma(-q, b, a);
     return fma(r, y, q);
+}
+
+// f32 a / b, correctly rounded, by the same Markstein step with y = RN_f32(1/b): the
+// obs quotients by per-handle constants (max(S0, 25), max_contracts_held, T).  A
+// true f32 division is ~11 instructions with two quarter-rate reciprocals; this is 3.
+// Exhaustively checked over all 2^32 numerators for the default divisors
+// (tools/div_check.c), sampled for random divisors in tests/test_lib_cpu.py.
+HE_HD float div_byf(float a, float b, float y) {
+    float q = a * y;
+    float aq = fabsf(q), aa = fabsf(a);
+    if (!(aq > 0x1p-100f && aq < 0x1p+100f && aa > 0x1p-100f)) return a / b;
+    float r = fmaf(-q, b, a);
+    return fmaf(r, y, q);
 }
 
 // np.rint(f32).astype(int64) then np.clip(., -mt, mt)  (hedging_env_v2.py:184-188).
@@ -64,8 +78,11 @@ HE_HD u32x4 philox4x32_10(u32x4 c, uint32_t k0, uint32_t k1) {
 #pragma unroll
     for (int r = 0; r < 10; ++r) {
         if (r) { k0 += W0; k1 += W1; }
-        uint32_t hi0 = mulhi32(M0, c.x), lo0 = M0 * c.x;
-        uint32_t hi1 = mulhi32(M1, c.z), lo1 = M1 * c.z;
+        // one 32x32->64 product per multiplier (v_mad_u64_u32) instead of separate
+        // quarter-rate mul_hi / mul_lo instructions
+        const uint64_t p0 = (uint64_t)M0 * c.x, p1 = (uint64_t)M1 * c.z;
+        uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+        uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
         u32x4 o;
         o.x = hi1 ^ c.y ^ k0;
         o.y = lo1;

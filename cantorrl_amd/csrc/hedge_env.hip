@@ -58,6 +58,13 @@ constexpr int kObs = HE_OBS_DIM;
 constexpr int kMktEnvs = 32;     // market kernel: envs per workgroup (half a wave wide)
 constexpr int kMktLanes = 8;     //                slot-lanes per env (4 waves, 16.6 KB LDS)
 constexpr int kMaxBlock = 64;    // max market block length M
+#ifndef HE_ROLLOUT_PREFETCH
+#define HE_ROLLOUT_PREFETCH 4
+#endif
+constexpr int kRolloutPrefetch = HE_ROLLOUT_PREFETCH;  // rollout: steps of inputs in flight
+#ifndef HE_MKT_WAVES
+#define HE_MKT_WAVES 2  // market_kernel: min waves per SIMD (3 is faster alone, slower beside rollouts)
+#endif
 constexpr int64_t kPrefetchMinEnvs = 131072;  // auto prefetch for single steps from here
 
 // ------------------------------------------------------------------ parameters
@@ -68,6 +75,9 @@ struct Params {
     int32_t variant, loss, record_metrics, autoreset, mode;
     int32_t mt, maxh;
     float mt_f, maxh_f, T_f;
+    float inv_maxh_f, inv_T_f;  // RN_f32(1/x) for div_byf
+    int32_t s0s_const;          // generate: max(S0, 25) is one constant for every env
+    float s0s_f, inv_s0s_f;
     float init_cash_f;
     double tcpc, slip_frac, lam, w, theta, initial_cash;
     double shares_d, inv_shares;  // inv_*: RN(1/x) for div_by
@@ -202,25 +212,39 @@ __device__ __forceinline__ float4 greeks(const Params& p, float S, float v) {
 }
 
 // ------------------------------------------------------------------ observation
-// hedging_env_v2.py:109-143.  m = market after the step, g = its greeks,
-// Sp/vp = S_t_minus_1 / v_t_minus_1.
+// S_t / S_{t-1} - 1 clipped to +-1, 0 when S_{t-1} == 0 (hedging_env_v2.py:129-136):
+// a function of the market alone, so it is computed where the market is (market_kernel
+// slots, replay table load) and travels in the .w lane of the greeks record.
+__device__ __forceinline__ float lag_return(float S, float Sp) {
+    return (Sp == 0.0f) ? 0.0f : np_clipf((S - Sp) / Sp, -1.0f, 1.0f);
+}
+
+// hedging_env_v2.py:109-143.  m = market after the step, g = its greeks and, in g.w,
+// lag_return(m.S, Sp); Sp/vp = S_t_minus_1 / v_t_minus_1.  Quotients by per-handle
+// constants use div_byf (correctly rounded, 3 instructions).
 __device__ __forceinline__ void make_obs(const Params& p, const Env& e, const Mkt& m, float4 g, float Sp,
                                          float vp, float* o) {
-    float s0s = np_maxf(e.s0, 25.0f);
-    o[0] = m.S / s0s;
-    o[1] = m.C / s0s;
-    o[2] = m.P / s0s;
+    if (p.s0s_const) {
+        o[0] = div_byf(m.S, p.s0s_f, p.inv_s0s_f);
+        o[1] = div_byf(m.C, p.s0s_f, p.inv_s0s_f);
+        o[2] = div_byf(m.P, p.s0s_f, p.inv_s0s_f);
+    } else {
+        float s0s = np_maxf(e.s0, 25.0f);
+        o[0] = m.S / s0s;
+        o[1] = m.C / s0s;
+        o[2] = m.P / s0s;
+    }
     // int64/int -> f64 quotient cast to f32 == correctly rounded f32 quotient when
     // both operands are exact in f32 (|x| < 2^24) and 53 >= 2*24+2 (no double rounding)
     if (p.maxh != 0) {
-        o[3] = (float)e.call / p.maxh_f;
-        o[4] = (float)e.put / p.maxh_f;
+        o[3] = div_byf((float)e.call, p.maxh_f, p.inv_maxh_f);
+        o[4] = div_byf((float)e.put, p.maxh_f, p.inv_maxh_f);
     } else {
         o[3] = 0.0f;
         o[4] = 0.0f;
     }
     o[5] = m.v;
-    o[6] = (p.T != 0) ? (float)(p.T - (int32_t)e.t) / p.T_f : 0.0f;
+    o[6] = (p.T != 0) ? div_byf((float)(p.T - (int32_t)e.t), p.T_f, p.inv_T_f) : 0.0f;
     if (p.record_metrics) {
         o[7] = g.x;
         o[8] = g.y;
@@ -229,13 +253,9 @@ __device__ __forceinline__ void make_obs(const Params& p, const Env& e, const Mk
     } else {
         o[7] = o[8] = o[9] = o[10] = 0.0f;
     }
-    float ls = 0.0f, lv = 0.0f;
-    if (!(e.t == 0 || Sp == 0.0f)) {
-        ls = (m.S - Sp) / Sp;
-        lv = m.v - vp;
-    }
-    o[11] = np_clipf(ls, -1.0f, 1.0f);
-    o[12] = np_clipf(lv, -1.0f, 1.0f);
+    const bool first = e.t == 0;  // reset obs
+    o[11] = first ? 0.0f : g.w;
+    o[12] = (first || Sp == 0.0f) ? 0.0f : np_clipf(m.v - vp, -1.0f, 1.0f);
 }
 
 // ------------------------------------------------------------------ marks
@@ -281,7 +301,7 @@ __device__ __forceinline__ void normals(const Params& p, int64_t gid, uint64_t n
 // from S0 when t in {0, T} (autoreset), so every slot is a pure function of the
 // block-start state.
 template <int MODE>
-__global__ __launch_bounds__(kMktEnvs * kMktLanes) void market_kernel(Params p, Market cur, Market bak,
+__global__ __launch_bounds__(kMktEnvs * kMktLanes, HE_MKT_WAVES) void market_kernel(Params p, Market cur, Market bak,
                                                                        int32_t advance_only) {
     constexpr bool HESTON = (MODE == HE_MODE_HESTON);
     __shared__ double shS[kMktEnvs][kMaxBlock + 1];
@@ -412,6 +432,10 @@ __global__ __launch_bounds__(kMktEnvs * kMktLanes) void market_kernel(Params p, 
         float v32 = HESTON ? (float)v64 : p.var_f;
         p.tileA[(int64_t)j * N + i] = make_float4(S32, v32, C, P);
         float4 g = p.record_metrics ? greeks<!HESTON>(p, S32, v32) : make_float4(0.f, 0.f, 0.f, 0.f);
+        // the step into slot j starts from the reset market (first step of an
+        // episode) or from slot j-1
+        const float Sp32 = (tj == 1u) ? p.rstv[0] : (float)shS[lane][j - 1];
+        g.w = lag_return(S32, Sp32);
         p.tileB[(int64_t)j * N + i] = g;
     }
     if (!advance_only && sub == 0 && live) {
@@ -424,6 +448,7 @@ __global__ __launch_bounds__(kMktEnvs * kMktLanes) void market_kernel(Params p, 
 template <int MODE>
 __global__ void init_reset_kernel(Params p, float* rst) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    p.s0s_const = 0;  // S0 is what this kernel computes: divide by the env's own max(S0, 25)
     float C, P;
     marks<MODE>(p, p.s0, p.var, &C, &P);
     Mkt m{(float)p.s0, p.var_f, C, P};
@@ -446,7 +471,11 @@ __global__ __launch_bounds__(kBlock) void table_greeks_kernel(Params p, float4* 
     int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (k >= count) return;
     float4 r = p.rec[k];
-    recg[k] = p.record_metrics ? greeks<false>(p, r.x, r.y) : make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 g = p.record_metrics ? greeks<false>(p, r.x, r.y) : make_float4(0.f, 0.f, 0.f, 0.f);
+    // row t >= 1 is stepped into from row t-1 of the same path; row 0 is only a reset obs
+    const int64_t t = k % (int64_t)(p.T + 1);
+    g.w = (t == 0) ? 0.0f : lag_return(r.x, p.rec[k - 1].x);
+    recg[k] = g;
 }
 
 // ------------------------------------------------------------------ step
@@ -738,20 +767,13 @@ __device__ __forceinline__ void step_body(const Params& pk, int64_t n_envs, cons
         e.cash = cash;
     }
     bool reset_any = false;
-    for (int k = 0; k < k_steps; ++k) {
+    float* const orow = tile + threadIdx.x * kObs;
+    // step k of every env from market `post` (greeks + lag return `g`) with action ak:
+    // state update, reward/done stores, the obs row into the wave's LDS tile, auto-reset
+    auto step_part = [&](int k, const Mkt post, const float4 g, const float2 ak) {
         const int64_t koff = (int64_t)k * N;
-        float* orow = tile + threadIdx.x * kObs;
         bool term = false;
         if (live) {
-            const Mkt post = as_mkt(postA);
-            const float4 g = postB;
-            const float2 ak = a;
-            if (!REPLAY && k + 1 < k_steps) {
-                const int64_t r = (int64_t)(slot0 + k + 2) * N + i;
-                a = act[koff + N + i];
-                postA = tA[r];
-                postB = tB[r];
-            }
             StepOut so;
             step_env(p, e, pre, post, ak.x, ak.y, so);
             term = so.term;
@@ -788,20 +810,64 @@ __device__ __forceinline__ void step_body(const Params& pk, int64_t n_envs, cons
                 reset_any = true;
             }
         }
-        if (REPLAY && live && k + 1 < k_steps) {
-            const uint32_t tn = e.t + 1 > (uint32_t)p.T ? (uint32_t)p.T : e.t + 1;
-            const int64_t r = (int64_t)e.path * (p.T + 1) + tn;
-            a = act[koff + N + i];
-            postA = tA[r];
-            postB = tB[r];
-        }
+    };
+    auto flush_part = [&](int k) {
         HE_TIM(3);
         if (io.obs) {
             // LDS-staged 16-B stores: measured 6.45 vs 7.14 us/step against per-lane
             // 4-B stores of the 52-B rows (MI355X, 65,536 envs, graph mode)
             const int wave = threadIdx.x >> 6;
             const int wrows = rows - wave * 64 < 64 ? rows - wave * 64 : 64;
-            flush_obs_wave(tile + wave * 64 * kObs, io.obs + koff * kObs, row0 + wave * 64, wrows, threadIdx.x & 63);
+            flush_obs_wave(tile + wave * 64 * kObs, io.obs + (int64_t)k * N * kObs, row0 + wave * 64, wrows,
+                           threadIdx.x & 63);
+        }
+    };
+    if constexpr (!REPLAY && !SINGLE) {
+        // generate-mode rollout: the market and action inputs of step k+D are issued
+        // before step k's stores.  vmcnt retires in issue order, so with D = 1 the
+        // wait for step k+1's inputs also waits for step k-1's stores; at D = 4 those
+        // stores were issued 4 steps earlier.  Every lane issues every load (clamped
+        // index / step), so the wait counts are the same on every path.
+        constexpr int D = kRolloutPrefetch;
+        const int64_t ic = live ? i : N - 1;
+        float2 ra[D];
+        float4 rA[D], rB[D];
+        ra[0] = a;
+        rA[0] = postA;
+        rB[0] = postB;
+        auto load = [&](int d, int kk) {
+            kk = kk < k_steps ? kk : k_steps - 1;
+            const int64_t r = (int64_t)(slot0 + kk + 1) * N + ic;
+            ra[d] = ld2(gact, (int64_t)kk * N + ic);
+            rA[d] = ld4(mA, r);
+            rB[d] = ld4(mB, r);
+        };
+#pragma unroll
+        for (int d = 1; d < D; ++d) load(d, d);
+        for (int kb = 0; kb < k_steps; kb += D) {
+#pragma unroll
+            for (int d = 0; d < D; ++d) {
+                const int k = kb + d;
+                if (k >= k_steps) break;
+                const Mkt post = as_mkt(rA[d]);
+                const float4 g = rB[d];
+                const float2 ak = ra[d];
+                load(d, k + D);
+                step_part(k, post, g, ak);
+                flush_part(k);
+            }
+        }
+    } else {
+        for (int k = 0; k < k_steps; ++k) {
+            step_part(k, as_mkt(postA), postB, a);
+            if (REPLAY && live && k + 1 < k_steps) {
+                const uint32_t tn = e.t + 1 > (uint32_t)p.T ? (uint32_t)p.T : e.t + 1;
+                const int64_t r = (int64_t)e.path * (p.T + 1) + tn;
+                a = act[(int64_t)(k + 1) * N + i];
+                postA = tA[r];
+                postB = tB[r];
+            }
+            flush_part(k);
         }
     }
     if (live) {
@@ -1096,6 +1162,8 @@ static void fill_params(he_env* env) {
     p.h_sqrt1mrho2 = sqrt(omr < 0.0 ? 0.0 : omr);
     p.T = c.episode_length;
     p.T_f = (float)c.episode_length;
+    p.inv_maxh_f = 1.0f / p.maxh_f;
+    p.inv_T_f = 1.0f / p.T_f;
     p.M = c.market_block;
     p.tileA = p.tileB = nullptr;  // set per launch (tile_params)
     memcpy(p.rstv, env->rstv, sizeof(p.rstv));
@@ -1109,6 +1177,9 @@ static void fill_params(he_env* env) {
         else p.den = small ? (25.0 + 1e-9) : (double)(f + 1e-9f);
         p.inv_den = 1.0 / p.den;
         p.den_const = 1;
+        p.s0s_const = 1;
+        p.s0s_f = f;
+        p.inv_s0s_f = 1.0f / f;
     }
     p.rec = env->rec;
     p.recg = env->recg;
@@ -1587,6 +1658,13 @@ he_status he_host_div_by(const double* a, int64_t count, double b, double* out) 
     if ((!a || !out) && count > 0) return HE_EINVAL;
     const double y = 1.0 / b;
     for (int64_t k = 0; k < count; ++k) out[k] = div_by(a[k], b, y);
+    return HE_OK;
+}
+
+he_status he_host_div_byf(const float* a, int64_t count, float b, float* out) {
+    if ((!a || !out) && count > 0) return HE_EINVAL;
+    const float y = 1.0f / b;
+    for (int64_t k = 0; k < count; ++k) out[k] = div_byf(a[k], b, y);
     return HE_OK;
 }
 

@@ -221,6 +221,8 @@ he_status he_host_philox(uint64_t seed, uint64_t env_id, uint64_t n, uint32_t ou
 /* out[k] = a[k] / b through the reciprocal-multiply division the step kernel uses
  * for its constant divisors (must equal IEEE a[k] / b bit for bit). */
 he_status he_host_div_by(const double* a, int64_t count, double b, double* out);
+/* f32 twin for the obs quotients by per-handle constants (must equal IEEE a[k] / b). */
+he_status he_host_div_byf(const float* a, int64_t count, float b, float* out);
 
 #ifdef __cplusplus
 }

@@ -107,3 +107,23 @@ def test_reciprocal_division_is_ieee_division(b):
         exp = a / b
     assert_same(got, exp, "div_by")
     assert np.array_equal(np.signbit(got), np.signbit(exp))
+
+
+@pytest.mark.parametrize("b", [25.0, 496.48001098632812, 200.0, 252.0, 40.0, 7.0, 0.3, 1.99999988, 1e-3, 3e5])
+def test_reciprocal_division_f32_is_ieee_division(b):
+    # obs quotients by per-handle constants (max(S0, 25), max_contracts_held, T) go
+    # through div_byf; tools/div_check.c checks all 2^32 numerators for the defaults
+    b = np.float32(b)
+    rng = np.random.default_rng(int(b * 1000) % 2 ** 32)
+    bits = rng.integers(0, 2 ** 32, 1_000_000, dtype=np.uint64).astype(np.uint32)
+    a = np.concatenate([
+        bits.view(np.float32),
+        np.arange(-400, 401, dtype=np.float32),                    # positions, T - t
+        rng.uniform(0, 2000, 200_000).astype(np.float32),           # prices
+        np.array([0.0, -0.0, np.inf, -np.inf, np.nan, 1e-45, -1e-45, 1e-38, 3.4e38], np.float32),
+    ])
+    got = _lib.host_div_byf(a, b)
+    with np.errstate(over="ignore", under="ignore", invalid="ignore"):
+        exp = a / b
+    assert_same(got, exp, "div_byf")
+    assert np.array_equal(np.signbit(got), np.signbit(exp))

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Measurement pass on the GPU box: GPU parity suite, smoke, default bench (PMC traffic +
-# CPU baseline), rollout mode, and a rocprofv3 kernel-trace summary of the default bench.
+# CPU baseline, graph-mode step API), and a rocprofv3 kernel-trace summary of the default bench.
 #   gpurun --timeout 1100 -- bash tools/gpu/round.sh <tag>
 set -o pipefail
 TAG=${1:-run}
@@ -16,12 +16,9 @@ tail -1 $O/smoke.log
 echo "[$(date +%T)] bench default"
 timeout -k 10 400 python -u bench.py > $O/b_default.log 2>&1 || { tail -20 $O/b_default.log; exit 1; }
 grep "^{" $O/b_default.log
-echo "[$(date +%T)] bench rollout"
-timeout -k 10 300 python -u bench.py --mode rollout --no-cpu-baseline --no-pmc > $O/b_rollout.log 2>&1 || { tail -20 $O/b_rollout.log; exit 1; }
-grep "^{" $O/b_rollout.log
 echo "[$(date +%T)] rocprofv3 kernel trace"
 cd /tmp
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $R/$O/prof -o run --output-format csv -- python3 $R/bench.py --no-cpu-baseline --no-pmc > $R/$O/b_prof.log 2>&1 || { tail -20 $R/$O/b_prof.log; exit 1; }
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $R/$O/prof -o run --output-format csv -- python3 $R/bench.py --no-cpu-baseline --no-pmc --no-step-api > $R/$O/b_prof.log 2>&1 || { tail -20 $R/$O/b_prof.log; exit 1; }
 grep "^{" $R/$O/b_prof.log
 find $R/$O/prof -name "*kernel_stats.csv"
 echo "[$(date +%T)] done"

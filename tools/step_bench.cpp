@@ -22,6 +22,7 @@ struct Api {
     decltype(&he_destroy) destroy;
     decltype(&he_reset) reset;
     decltype(&he_step) step;
+    decltype(&he_rollout) rollout;
     decltype(&he_sync_market) sync_market;
     decltype(&he_last_error) last_error;
     void* handle;
@@ -37,6 +38,7 @@ static Api load(const char* path) {
     a.destroy = (decltype(a.destroy))dlsym(h, "he_destroy");
     a.reset = (decltype(a.reset))dlsym(h, "he_reset");
     a.step = (decltype(a.step))dlsym(h, "he_step");
+    a.rollout = (decltype(a.rollout))dlsym(h, "he_rollout");
     a.sync_market = (decltype(a.sync_market))dlsym(h, "he_sync_market");
     a.last_error = (decltype(a.last_error))dlsym(h, "he_last_error");
     return a;
@@ -46,16 +48,19 @@ int main(int argc, char** argv) {
     setvbuf(stdout, nullptr, _IONBF, 0);
     if (argc < 3) { fprintf(stderr, "usage: step_bench N lib.so...\n"); return 2; }
     const int64_t N = atoll(argv[1]);
+    // STEP_BENCH_ROLLOUT=K: he_rollout of K fused steps per launch instead of he_step
+    const int RK = getenv("STEP_BENCH_ROLLOUT") ? atoi(getenv("STEP_BENCH_ROLLOUT")) : 0;
+    const int64_t KK = RK > 0 ? RK : 1;
     float *act, *obs, *rew;
     uint8_t *term, *trunc;
-    CK(hipMalloc(&act, N * 8));
-    CK(hipMalloc(&obs, N * 52));
-    CK(hipMalloc(&rew, N * 4));
-    CK(hipMalloc(&term, N));
+    CK(hipMalloc(&act, KK * N * 8));
+    CK(hipMalloc(&obs, KK * N * 52));
+    CK(hipMalloc(&rew, KK * N * 4));
+    CK(hipMalloc(&term, KK * N));
     CK(hipMalloc(&trunc, N));
-    std::vector<float> ha(N * 2);
-    for (int64_t i = 0; i < N * 2; ++i) ha[i] = (float)((i * 2654435761u) % 2001) / 1000.0f - 1.0f;
-    CK(hipMemcpy(act, ha.data(), N * 8, hipMemcpyHostToDevice));
+    std::vector<float> ha(KK * N * 2);
+    for (int64_t i = 0; i < KK * N * 2; ++i) ha[i] = (float)((i * 2654435761u) % 2001) / 1000.0f - 1.0f;
+    CK(hipMemcpy(act, ha.data(), KK * N * 8, hipMemcpyHostToDevice));
     hipStream_t st;
     CK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
     hipEvent_t a, b;
@@ -67,35 +72,41 @@ int main(int argc, char** argv) {
         api.config_init(&c, 2);
         c.n_envs = N;
         c.mode = HE_MODE_GBM;
-        c.reserved_i = getenv("STEP_BENCH_PREFETCH") ? 2 : 1;  // always / never
+        c.reserved_i = getenv("STEP_BENCH_PREFETCH") ? 2 : (RK > 0 ? 0 : 1);  // always / (auto) / never
         he_env* env;
         if (api.create(&c, &env) != HE_OK) { fprintf(stderr, "create: %s\n", api.last_error(env)); return 1; }
         if (api.reset(env, nullptr, 0, obs, nullptr, st) != HE_OK) return 1;
         float* o = getenv("STEP_BENCH_NO_OBS") ? nullptr : obs;
-        for (int k = 0; k < 64; ++k)
-            if (api.step(env, act, o, rew, term, trunc, nullptr, nullptr, st) != HE_OK) return 1;
+        auto one = [&]() {
+            if (RK > 0) return api.rollout(env, RK, act, o, rew, term, st);
+            return api.step(env, act, o, rew, term, trunc, nullptr, nullptr, st);
+        };
+        const int per_graph = RK > 0 ? (64 / RK > 0 ? 64 / RK : 1) : 64;
+        for (int k = 0; k < per_graph; ++k)
+            if (one() != HE_OK) { fprintf(stderr, "step: %s\n", api.last_error(env)); return 1; }
         api.sync_market(env, st);
         CK(hipStreamSynchronize(st));
         hipGraph_t g[4];
         hipGraphExec_t ge[4];
         for (int gi = 0; gi < 4; ++gi) {
             CK(hipStreamBeginCapture(st, hipStreamCaptureModeGlobal));
-            for (int k = 0; k < 64; ++k) api.step(env, act, o, rew, term, trunc, nullptr, nullptr, st);
+            for (int k = 0; k < per_graph; ++k) one();
             api.sync_market(env, st);
             CK(hipStreamEndCapture(st, &g[gi]));
             CK(hipGraphInstantiate(&ge[gi], g[gi], nullptr, nullptr, 0));
         }
-        for (int r = 0; r < 8; ++r) CK(hipGraphLaunch(ge[r & 3], st));
+        const int warm = getenv("STEP_BENCH_REPS") ? 1 : 8;
+        for (int r = 0; r < warm; ++r) CK(hipGraphLaunch(ge[r & 3], st));
         CK(hipStreamSynchronize(st));
-        const int reps = 160;
+        const int reps = getenv("STEP_BENCH_REPS") ? atoi(getenv("STEP_BENCH_REPS")) : 160;
         CK(hipEventRecord(a, st));
         for (int r = 0; r < reps; ++r) CK(hipGraphLaunch(ge[r & 3], st));
         CK(hipEventRecord(b, st));
         CK(hipEventSynchronize(b));
         float ms;
         CK(hipEventElapsedTime(&ms, a, b));
-        double us = ms * 1000.0 / (reps * 64.0);
-        printf("%-24s%s%s N=%lld  %.3f us/step  %.4e env-steps/s\n", argv[li], o ? "" : " (no obs)", c.reserved_i == 2 ? " (prefetch)" : "", (long long)N, us, N / us * 1e6);
+        double us = ms * 1000.0 / (reps * (double)per_graph * KK);
+        printf("%-24s%s%s%s N=%lld  %.3f us/step  %.4e env-steps/s\n", argv[li], o ? "" : " (no obs)", c.reserved_i == 2 ? " (prefetch)" : "", RK > 0 ? " (rollout)" : "", (long long)N, us, N / us * 1e6);
         typedef he_status (*tim_fn)(void*, size_t);
         tim_fn tim = (tim_fn)dlsym(api.handle, "he_debug_timing");
         if (tim) {
