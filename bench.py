@@ -55,6 +55,12 @@ TRAIN_KW = dict(loss_type="abs", pnl_penalty_weight=0.001, lambda_cost=0.0001, t
                 slippage_bps=1.0)  # train_ppo_v2.py:74-80
 GEN = dict(s0=496.48001098632812, variance=0.029028, mu=0.04, dt=1 / 252, episode_length=252)
 
+# liability books (extension, include/hedge_env.h he_book_option): short options on S0 = 496.48
+BOOK8 = [dict(type=t, strike=k, expiry=e, quantity=q) for t, k, e, q in (
+    ("call", 500.0, 63, -20.0), ("put", 480.0, 63, -15.0), ("call", 520.0, 126, -10.0), ("put", 500.0, 126, -25.0),
+    ("call", 470.0, 189, -5.0), ("put", 530.0, 189, -5.0), ("call", 496.0, 252, -40.0), ("put", 450.0, 252, -30.0))]
+BARRIER_BOOK = [dict(type="uo_call", strike=496.0, barrier=570.0, expiry=252, quantity=-50.0)]
+
 # BASELINE.json configs (configs[0] is the CPU case = cpu_baseline below)
 CONFIGS = {
     2: dict(envs=65536, mode="gbm", gen=GEN, kw=TRAIN_KW,
@@ -63,11 +69,14 @@ CONFIGS = {
     3: dict(envs=1048576, mode="gbm", gen=GEN, kw=dict(TRAIN_KW, slippage_bps=5.0),
             workload="configs[2]: 1,048,576 parallel envs/GPU, European call, GBM, proportional costs "
                      "(5 bp slippage + $0.65 commission)"),
+    4: dict(envs=524288, mode="gbm", gen=dict(GEN, book=BOOK8), kw=TRAIN_KW,
+            workload="configs[3]: 524,288 envs/GPU (4M over 8 GPUs), GBM, liability book of 8 European "
+                     "options per env marked every step"),
     5: dict(envs=131072, mode="heston",
-            gen=dict(GEN, heston_kappa=2.0, heston_theta=0.029028, heston_xi=0.3, heston_rho=-0.7),
+            gen=dict(GEN, heston_kappa=2.0, heston_theta=0.029028, heston_xi=0.3, heston_rho=-0.7, book=BARRIER_BOOK),
             kw=TRAIN_KW,
-            workload="configs[4] market: Heston full-truncation Euler (rho=-0.7), 131,072 envs/GPU "
-                     "(1M over 8 GPUs)"),
+            workload="configs[4]: Heston full-truncation Euler (rho=-0.7) + up-and-out barrier call book, "
+                     "131,072 envs/GPU (1M over 8 GPUs)"),
 }
 
 
@@ -346,13 +355,14 @@ def timed(runner, K, W, dist):
     return float(t.item()), ev0.elapsed_time(ev1)
 
 
-def roofline(mode, n, kern_ms, rk):
+def roofline(mode, n, kern_ms, rk, book=False):
+    """book: + the f64 book slot per env-step (post; he_step also reads the pre slot)."""
     if mode == "rollout":
-        bytes_launch = n * rk * (ROLLOUT_BYTES_PER_ENV + ROLLOUT_STATE_BYTES / rk)
-        kname = "step_kernel<GBM> (he_rollout, K=%d fused steps)" % rk
+        bytes_launch = n * rk * (ROLLOUT_BYTES_PER_ENV + (8 if book else 0) + ROLLOUT_STATE_BYTES / rk)
+        kname = "step_kernel (he_rollout, K=%d fused steps)" % rk
     else:
-        bytes_launch = n * STEP_BYTES_PER_ENV
-        kname = "step1_kernel<GBM> (he_step, K=1)"
+        bytes_launch = n * (STEP_BYTES_PER_ENV + (16 if book else 0))
+        kname = "step1_kernel (he_step, K=1)"
     achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
     return dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
                 frac=round(achieved / HBM_PEAK_GBS, 4), traffic=None, kernel=kname,
@@ -400,7 +410,8 @@ def main():
     kern_ms = kernel_time_ms(hev, runner, 64 if args.mode == "rollout" else 256)
     env.close()
 
-    roof = roofline(args.mode, n, kern_ms, args.rollout_k)
+    has_book = bool(cfg["gen"].get("book"))
+    roof = roofline(args.mode, n, kern_ms, args.rollout_k, has_book)
     mkt_ms = market_time_ms(hev, args, dev, acts, stream)
     roof["market_kernel_us_per_64_steps"] = round(mkt_ms * 1e3, 3)
     roof["market_kernel_us_per_step"] = round(mkt_ms * 1e3 / M_BLOCK, 3)
@@ -419,7 +430,7 @@ def main():
         wall_g, _ = timed(rg, Kg, M_BLOCK * 4, None)
         kg = kernel_time_ms(hev, rg, 256)
         env_g.close()
-        rf = roofline("graph", n, kg, 1)
+        rf = roofline("graph", n, kg, 1, has_book)
         step_api = dict(mode="graph (he_step, one launch per step)", value=round(n * Kg / wall_g, 1),
                         ms_per_step=round(wall_g * 1e3 / Kg, 6), kernel=rf["kernel"], kernel_us=rf["kernel_us"],
                         achieved_gbs=rf["achieved"], frac=rf["frac"], bytes_per_launch=rf["bytes_per_launch"])

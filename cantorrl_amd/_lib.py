@@ -12,7 +12,9 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "lib", "libhedgeenv.so")
 
-HE_ABI_VERSION = 1
+HE_ABI_VERSION = 2
+HE_BOOK_MAX = 8
+BOOK_TYPES = {"call": 0, "put": 1, "uo_call": 2}
 HE_OK, HE_EINVAL, HE_ESHAPE, HE_EHIP, HE_ENOMEM, HE_ESTATE = range(6)
 HE_MODE_REPLAY, HE_MODE_GBM, HE_MODE_HESTON = range(3)
 HE_LOSS_MSE, HE_LOSS_ABS, HE_LOSS_CVAR, HE_LOSS_OTHER = range(4)
@@ -22,6 +24,16 @@ MODES = {"replay": HE_MODE_REPLAY, "gbm": HE_MODE_GBM, "heston": HE_MODE_HESTON}
 def loss_code(loss_type):
     """hedging_env_v2.py:246-253: "mse", "abs", "cvar", anything else = |x| branch."""
     return {"mse": HE_LOSS_MSE, "abs": HE_LOSS_ABS, "cvar": HE_LOSS_CVAR}.get(loss_type, HE_LOSS_OTHER)
+
+
+class HeBookOption(ctypes.Structure):
+    _fields_ = [
+        ("type", ctypes.c_int32),
+        ("expiry", ctypes.c_int32),
+        ("strike", ctypes.c_double),
+        ("barrier", ctypes.c_double),
+        ("quantity", ctypes.c_double),
+    ]
 
 
 class HeConfig(ctypes.Structure):
@@ -57,7 +69,10 @@ class HeConfig(ctypes.Structure):
         ("heston_xi", ctypes.c_double),
         ("heston_rho", ctypes.c_double),
         ("market_block", ctypes.c_int32),
+        ("market_prefetch", ctypes.c_int32),
+        ("book_size", ctypes.c_int32),
         ("reserved_i", ctypes.c_int32),
+        ("book", HeBookOption * HE_BOOK_MAX),
         ("reserved", ctypes.c_double * 7),
     ]
 

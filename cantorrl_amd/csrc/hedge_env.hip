@@ -68,6 +68,12 @@ constexpr int kRolloutPrefetch = HE_ROLLOUT_PREFETCH;  // rollout: steps of inpu
 constexpr int64_t kPrefetchMinEnvs = 131072;  // auto prefetch for single steps from here
 
 // ------------------------------------------------------------------ parameters
+// One option of the liability book (he_book_option), device copy: q100 = quantity*100.
+struct BookOpt {
+    int32_t type, expiry;
+    double K, H, q100;
+};
+
 struct Params {
     int64_t n;
     int64_t goff;
@@ -106,8 +112,13 @@ struct Params {
     float rstv[4 + kObs];   // reset market + obs (generate): {S0, v0, C0, P0, obs0[13]}, by value
     // replay
     const float4* rec;      // [n_paths][T+1] {S, v, C, P}; C/P at T hold row T-1
-    const float4* recg;     // [n_paths][T+1] {call_delta, gamma, put_delta, 0}
+    const float4* recg;     // [n_paths][T+1] {call_delta, gamma, put_delta, lag return}
     int64_t n_paths;
+    // liability book (generate modes)
+    int32_t book_n;
+    const BookOpt* book;    // device copy [book_n], read through the scalar cache
+    double book_rst;        // book value of the reset market (t = 0, S0, v0)
+    double* tileC;          // [M+1][N] f64 book value of every slot
 #ifdef HE_TIMING
     uint64_t* tim;          // [5][8192][2]
 #endif
@@ -132,6 +143,7 @@ struct Market {
     double* v;         // f64 variance (Heston)
     float* C;          // f32 marks at this position
     float* P;
+    double* M;         // book: running max of S over the episode (barrier monitor)
 };
 
 struct Io {
@@ -146,6 +158,7 @@ struct Io {
 
 struct Mkt {
     float S, v, C, P;
+    double B;          // liability book value (0 without a book)
 };
 
 struct Env {
@@ -281,6 +294,67 @@ __device__ __forceinline__ void marks(const Params& p, double S64, double var64,
     *P = (float)q;
 }
 
+// ------------------------------------------------------------------ liability book
+// Extension (he_book_option, BASELINE.json configs[3]/[4]).  Option o at the env's
+// market S with volatility sig, tau years to expiry, runmax = max S over the episode
+// at the step dates so far.  Europeans: the OptionCalculator.black_scholes_price form
+// (option_calculator.py:11-27, intrinsic when tau <= 0 or sig <= 0).  Up-and-out call
+// (q = 0, Hull, "Options, Futures and Other Derivatives", barrier options):
+// c_uo = c - c_ui, worthless once S touched H at a step date or when H <= K.
+__device__ __forceinline__ double book_option(const BookOpt& o, double S, double sig, double tau, double r,
+                                              double runmax) {
+    if (o.type == HE_BOOK_UO_CALL && runmax >= o.H) return 0.0;
+    const double K = o.K;
+    if (tau <= 0.0 || sig <= 0.0) {
+        const double ic = S - K, ip = K - S;
+        if (o.type == HE_BOOK_PUT) return (ip < 0.0) ? 0.0 : ip;
+        return (ic < 0.0) ? 0.0 : ic;
+    }
+    if (o.type == HE_BOOK_UO_CALL && o.H <= K) return 0.0;
+    const double s2 = sig * sig;
+    const double sst = sig * sqrt(tau);
+    const double d1 = (log(S / K) + (r + 0.5 * s2) * tau) / sst;
+    const double d2 = d1 - sst;
+    const double Kd = K * exp(-r * tau);
+    double n1, m1, n2, m2;
+    ndtr_pair(d1, &n1, &m1);
+    ndtr_pair(d2, &n2, &m2);
+    double v;
+    if (o.type == HE_BOOK_PUT) {
+        v = Kd * m2 - S * m1;
+    } else {
+        v = S * n1 - Kd * n2;
+        if (o.type == HE_BOOK_UO_CALL) {
+            const double H = o.H;
+            const double lam = (r + 0.5 * s2) / s2;
+            const double ls = lam * sst;
+            const double lhs = log(H / S);
+            const double x1 = log(S / H) / sst + ls;
+            const double y = log((H * H) / (S * K)) / sst + ls;
+            const double y1 = lhs / sst + ls;
+            const double p2l = exp((2.0 * lam) * lhs);          // (H/S)^(2 lam)
+            const double p2l2 = exp((2.0 * lam - 2.0) * lhs);   // (H/S)^(2 lam - 2)
+            const double cui = S * ndtr(x1) - Kd * ndtr(x1 - sst) - S * p2l * (ndtr(-y) - ndtr(-y1)) +
+                               Kd * p2l2 * (ndtr(-y + sst) - ndtr(-y1 + sst));
+            v = v - cui;
+        }
+    }
+    return (v < 0.0) ? 0.0 : v;   // python max(price, 0)
+}
+
+// sum_k q_k * 100 * V_k after step t of the episode (variance var: GBM constant,
+// Heston the env's v_t).
+__device__ __forceinline__ double book_value(const Params& p, double S, double var, int32_t t, double runmax) {
+    const double sig = sqrt(var < 0.0 ? 0.0 : var);
+    double B = 0.0;
+    for (int k = 0; k < p.book_n; ++k) {
+        const BookOpt o = p.book[k];
+        const double tau = (double)(o.expiry - t) * p.dt;
+        B = B + o.q100 * book_option(o, S, sig, tau, p.r_d, runmax);
+    }
+    return B;
+}
+
 // Box-Muller pair of the Philox block of (seed, global env id, env-step index n).
 __device__ __forceinline__ void normals(const Params& p, int64_t gid, uint64_t n, double* z1, double* z2) {
     u32x4 ctr = {(uint32_t)n, (uint32_t)(n >> 32), (uint32_t)gid, (uint32_t)((uint64_t)gid >> 32)};
@@ -300,12 +374,13 @@ __device__ __forceinline__ void normals(const Params& p, int64_t gid, uint64_t n
 // a = ep*T + t the step from position a uses Philox counter n = a and starts
 // from S0 when t in {0, T} (autoreset), so every slot is a pure function of the
 // block-start state.
-template <int MODE>
+template <int MODE, bool BOOK>
 __global__ __launch_bounds__(kMktEnvs * kMktLanes, HE_MKT_WAVES) void market_kernel(Params p, Market cur, Market bak,
                                                                        int32_t advance_only) {
     constexpr bool HESTON = (MODE == HE_MODE_HESTON);
     __shared__ double shS[kMktEnvs][kMaxBlock + 1];
     __shared__ double shV[HESTON ? kMktEnvs : 1][HESTON ? kMaxBlock + 1 : 1];
+    __shared__ double shM[BOOK ? kMktEnvs : 1][BOOK ? kMaxBlock + 1 : 1];  // running max of S
     const int lane = threadIdx.x & (kMktEnvs - 1);
     const int sub = threadIdx.x / kMktEnvs;
     const int64_t i = (int64_t)blockIdx.x * kMktEnvs + lane;
@@ -316,13 +391,14 @@ __global__ __launch_bounds__(kMktEnvs * kMktLanes, HE_MKT_WAVES) void market_ker
     // block-start position (advance_only: rewind from `bak`, else continue from `cur`)
     Market src = advance_only ? bak : cur;
     uint32_t ep0 = 0, t0 = 0;
-    double S0v = 0.0, v0v = 0.0;
+    double S0v = 0.0, v0v = 0.0, M0v = 0.0;
     float C0v = 0.0f, P0v = 0.0f;
     if (live) {
         ep0 = src.ep[i];
         t0 = src.t[i];
         S0v = src.S[i];
         if (HESTON) v0v = src.v[i];
+        if (BOOK) M0v = src.M[i];
         C0v = src.C[i];
         P0v = src.P[i];
     }
@@ -362,16 +438,18 @@ __global__ __launch_bounds__(kMktEnvs * kMktLanes, HE_MKT_WAVES) void market_ker
     __syncthreads();
     // phase 2 (one lane per env): the sequential f64 chain
     if (sub == 0 && live) {
-        double S = S0v, v = v0v;
+        double S = S0v, v = v0v, Mx = M0v;
         uint32_t tt = t0;
         uint32_t ep = ep0;
         shS[lane][0] = S;
         if (HESTON) shV[lane][0] = v;
+        if (BOOK) shM[lane][0] = Mx;
         for (int j = 1; j <= nsteps; ++j) {
             if (tt == 0 || tt >= T) {  // autoreset: a new episode starts from S0
                 if (tt >= T) ep += 1u;
                 S = p.s0;
                 if (HESTON) v = p.var;
+                if (BOOK) Mx = p.s0;
                 tt = 0;
             }
             if (HESTON) {
@@ -388,6 +466,10 @@ __global__ __launch_bounds__(kMktEnvs * kMktLanes, HE_MKT_WAVES) void market_ker
                 S = (Sn < 1e-8) ? 1e-8 : Sn;  // np.maximum(., 1e-8), NaN kept
             }
             shS[lane][j] = S;
+            if (BOOK) {
+                Mx = np_max(Mx, S);
+                shM[lane][j] = Mx;
+            }
             tt += 1u;
         }
         if (!advance_only) {  // keep the block start for rewinds
@@ -397,11 +479,13 @@ __global__ __launch_bounds__(kMktEnvs * kMktLanes, HE_MKT_WAVES) void market_ker
             if (HESTON) bak.v[i] = v0v;
             bak.C[i] = C0v;
             bak.P[i] = P0v;
+            if (BOOK) bak.M[i] = M0v;
         }
         cur.ep[i] = ep;
         cur.t[i] = tt;
         cur.S[i] = S;
         if (HESTON) cur.v[i] = v;
+        if (BOOK) cur.M[i] = Mx;
     }
     __syncthreads();
     // phase 3 (time-parallel): marks + greeks of every slot
@@ -437,10 +521,16 @@ __global__ __launch_bounds__(kMktEnvs * kMktLanes, HE_MKT_WAVES) void market_ker
         const float Sp32 = (tj == 1u) ? p.rstv[0] : (float)shS[lane][j - 1];
         g.w = lag_return(S32, Sp32);
         p.tileB[(int64_t)j * N + i] = g;
+        if (BOOK) p.tileC[(int64_t)j * N + i] = book_value(p, S64, v64, (int32_t)tj, shM[lane][j]);
     }
     if (!advance_only && sub == 0 && live) {
         float v32 = HESTON ? (float)v0v : p.var_f;
         p.tileA[i] = make_float4((float)S0v, v32, C0v, P0v);
+        // slot 0 = the block start; at t0 in {0, T} the next step starts from the reset
+        // market and reads book_rst instead
+        if (BOOK)
+            p.tileC[i] = (t0 == 0u || t0 >= T) ? p.book_rst
+                                                : book_value(p, S0v, HESTON ? v0v : p.var, (int32_t)t0, M0v);
     }
 }
 
@@ -464,6 +554,7 @@ __global__ void init_reset_kernel(Params p, float* rst) {
     rst[2] = C;
     rst[3] = P;
     make_obs(p, e, m, g, m.S, m.v, rst + 4);
+    if (p.book_n) reinterpret_cast<double*>(rst)[10] = book_value(p, p.s0, p.var, 0, p.s0);  // rst[20..21]
 }
 
 // Replay: obs greeks of every table entry, once at load time.
@@ -489,6 +580,7 @@ struct StepOut {
 
 // hedging_env_v2.py:175-262 (v1: hedging_env.py:171-245).  pre/post: market before
 // and after the advance (post C/P already lagged on the terminal step).
+template <bool BOOK>
 __device__ __forceinline__ void step_env(const Params& p, Env& e, const Mkt& pre, const Mkt& post, float a0,
                                          float a1, StepOut& o) {
     // portfolio_value_t_minus_1 is a pure function of the pre-step state
@@ -500,6 +592,7 @@ __device__ __forceinline__ void step_env(const Params& p, Env& e, const Mkt& pre
         double optv = ((double)e.call * (double)pre.C) * 100.0 + ((double)e.put * (double)pre.P) * 100.0;
         pv_prev = ((double)(p.shares_f * pre.S) + optv) + e.cash;
     }
+    if (BOOK) pv_prev = pv_prev + pre.B;  // liability book (extension): after cash
     // (i)-(ii) integer trade logic (:181-200)
     float fc = a0 * p.mt_f;
     float fp = a1 * p.mt_f;
@@ -530,6 +623,7 @@ __device__ __forceinline__ void step_env(const Params& p, Env& e, const Mkt& pre
     // (vi) mark-to-market (:233-238)
     double optv = ((double)e.call * (double)post.C) * 100.0 + ((double)e.put * (double)post.P) * 100.0;
     double pv = ((double)(p.shares_f * post.S) + optv) + e.cash;
+    if (BOOK) pv = pv + post.B;
     double pnl = pv - pv_prev;
     double ps = p.shares_zero ? pnl : div_by(pnl, p.shares_d, p.inv_shares);
     // (vii) reward (:243-262)
@@ -687,9 +781,9 @@ __device__ __forceinline__ void env_reset_common(const Params& p, Env& e) {
 // SINGLE: the he_step instance (k_steps == 1 at compile time, straight-line code).
 // tA/tB: the market source, tile buffer {S,v,C,P} / greeks (generate) or the
 // replay table rec / recg.
-template <int MODE, bool INFO, bool SINGLE>
+template <int MODE, bool INFO, bool SINGLE, bool BOOK>
 __device__ __forceinline__ void step_body(const Params& pk, int64_t n_envs, const float4* tA, const float4* tB,
-                                          State s, Io io, int k_steps_arg, int slot0) {
+                                          const double* tC, State s, Io io, int k_steps_arg, int slot0) {
     constexpr bool REPLAY = (MODE == HE_MODE_REPLAY);
     const int k_steps = SINGLE ? 1 : k_steps_arg;
     Params p = pk;
@@ -704,7 +798,7 @@ __device__ __forceinline__ void step_body(const Params& pk, int64_t n_envs, cons
     const bool live = i < N;
     const int rows = (int)((N - row0) < kBlock ? (N - row0) : kBlock);
     const float2* act = reinterpret_cast<const float2*>(io.act);
-    const Mkt rst{p.rstv[0], p.rstv[1], p.rstv[2], p.rstv[3]};
+    const Mkt rst{p.rstv[0], p.rstv[1], p.rstv[2], p.rstv[3], BOOK ? p.book_rst : 0.0};
     // Every kernel argument of the prologue's addresses and of the step arithmetic,
     // pinned in SGPRs by ONE asm: one scalar round trip to the kernarg segment.  Left
     // alone, the backend sinks some of these loads into the `live` branch or after
@@ -717,15 +811,18 @@ __device__ __forceinline__ void step_body(const Params& pk, int64_t n_envs, cons
     auto gact = (const GLOBAL v2f*)act;
     auto mA = (const GLOBAL v4f*)tA;
     auto mB = (const GLOBAL v4f*)tB;
+    auto mC = (const GLOBAL double*)tC;
     auto s_path = (const GLOBAL int32_t*)s.path;
     auto s_s0 = (const GLOBAL float*)s.s0;
     int32_t hot_i = REPLAY ? p.T : slot0;
     asm volatile("" : "+s"(s_t), "+s"(s_pos), "+s"(s_cash), "+s"(gact), "+s"(mA), "+s"(mB), "+s"(hot_i));
+    if (BOOK) asm volatile("" : "+s"(mC));
     if (REPLAY) asm volatile("" : "+s"(s_path), "+s"(s_s0));
     HE_TIM(1);
     Env e;
     Mkt pre;
     float4 postA, postB;
+    double postC = 0.0;
     float2 a;
     if (live) {
         const uint32_t t0 = s_t[i];
@@ -749,6 +846,12 @@ __device__ __forceinline__ void step_body(const Params& pk, int64_t n_envs, cons
             float4 preA = ld4(mA, (int64_t)hot_i * N + i);
             postA = ld4(mA, (int64_t)(hot_i + 1) * N + i);
             postB = ld4(mB, (int64_t)(hot_i + 1) * N + i);
+            double preC = 0.0;
+            if (BOOK) {
+                preC = mC[(int64_t)hot_i * N + i];
+                postC = mC[(int64_t)(hot_i + 1) * N + i];
+                asm volatile("" : "+v"(preC), "+v"(postC));
+            }
             // pin every prologue load here: otherwise preA is sunk into the t != 0
             // branch (a second, dependent memory round trip), and a load still
             // pending at a branch merge makes the waitcnt pass drain every later
@@ -760,6 +863,7 @@ __device__ __forceinline__ void step_body(const Params& pk, int64_t n_envs, cons
             e.s0_small = rst.S < 1e-6f;
             e.s0 = e.s0_small ? 1.0f : rst.S;
             pre = (t0 == 0) ? rst : as_mkt(preA);  // select of values, not addresses
+            if (BOOK) pre.B = (t0 == 0) ? p.book_rst : preC;
         }
         e.t = t0;
         e.call = unpack_lo(pk);
@@ -775,7 +879,7 @@ __device__ __forceinline__ void step_body(const Params& pk, int64_t n_envs, cons
         bool term = false;
         if (live) {
             StepOut so;
-            step_env(p, e, pre, post, ak.x, ak.y, so);
+            step_env<BOOK>(p, e, pre, post, ak.x, ak.y, so);
             term = so.term;
             if (INFO) write_info(io.info, i, so, e, post, p.variant);
             float o[kObs];
@@ -832,15 +936,18 @@ __device__ __forceinline__ void step_body(const Params& pk, int64_t n_envs, cons
         const int64_t ic = live ? i : N - 1;
         float2 ra[D];
         float4 rA[D], rB[D];
+        double rC[D];
         ra[0] = a;
         rA[0] = postA;
         rB[0] = postB;
+        rC[0] = postC;
         auto load = [&](int d, int kk) {
             kk = kk < k_steps ? kk : k_steps - 1;
             const int64_t r = (int64_t)(slot0 + kk + 1) * N + ic;
             ra[d] = ld2(gact, (int64_t)kk * N + ic);
             rA[d] = ld4(mA, r);
             rB[d] = ld4(mB, r);
+            if (BOOK) rC[d] = mC[r];
         };
 #pragma unroll
         for (int d = 1; d < D; ++d) load(d, d);
@@ -849,7 +956,8 @@ __device__ __forceinline__ void step_body(const Params& pk, int64_t n_envs, cons
             for (int d = 0; d < D; ++d) {
                 const int k = kb + d;
                 if (k >= k_steps) break;
-                const Mkt post = as_mkt(rA[d]);
+                Mkt post = as_mkt(rA[d]);
+                if (BOOK) post.B = rC[d];
                 const float4 g = rB[d];
                 const float2 ak = ra[d];
                 load(d, k + D);
@@ -859,7 +967,9 @@ __device__ __forceinline__ void step_body(const Params& pk, int64_t n_envs, cons
         }
     } else {
         for (int k = 0; k < k_steps; ++k) {
-            step_part(k, as_mkt(postA), postB, a);
+            Mkt post = as_mkt(postA);
+            if (BOOK) post.B = postC;
+            step_part(k, post, postB, a);
             if (REPLAY && live && k + 1 < k_steps) {
                 const uint32_t tn = e.t + 1 > (uint32_t)p.T ? (uint32_t)p.T : e.t + 1;
                 const int64_t r = (int64_t)e.path * (p.T + 1) + tn;
@@ -884,11 +994,11 @@ __device__ __forceinline__ void step_body(const Params& pk, int64_t n_envs, cons
 }
 
 // Every step path: Params by value in the kernel arguments.
-template <int MODE, bool INFO, bool SINGLE>
+template <int MODE, bool INFO, bool SINGLE, bool BOOK>
 __global__ __launch_bounds__(kBlock) void step_kernel(Params pk, State s, Io io, int k_steps, int slot0) {
     constexpr bool REPLAY = (MODE == HE_MODE_REPLAY);
-    step_body<MODE, INFO, SINGLE>(pk, pk.n, REPLAY ? pk.rec : pk.tileA, REPLAY ? pk.recg : pk.tileB, s, io,
-                                  k_steps, slot0);
+    step_body<MODE, INFO, SINGLE, BOOK>(pk, pk.n, REPLAY ? pk.rec : pk.tileA, REPLAY ? pk.recg : pk.tileB,
+                                        pk.tileC, s, io, k_steps, slot0);
 }
 
 // he_step without info: Params from a device-resident copy; the kernel arguments carry
@@ -901,9 +1011,10 @@ struct StepIo {
     uint8_t* trunc;
     float* tobs;
 };
-template <int MODE>
+template <int MODE, bool BOOK>
 __global__ __launch_bounds__(kBlock) void step1_kernel(const Params* __restrict__ pc, int64_t n, const float4* tA,
-                                                       const float4* tB, State s, StepIo sio, int slot0) {
+                                                       const float4* tB, const double* tC, State s, StepIo sio,
+                                                       int slot0) {
     Io io;
     io.act = sio.act;
     io.obs = sio.obs;
@@ -912,7 +1023,7 @@ __global__ __launch_bounds__(kBlock) void step1_kernel(const Params* __restrict_
     io.trunc = sio.trunc;
     io.tobs = sio.tobs;
     io.info = he_info{};
-    step_body<MODE, false, true>(*pc, n, tA, tB, s, io, 1, slot0);
+    step_body<MODE, false, true, BOOK>(*pc, n, tA, tB, tC, s, io, 1, slot0);
 }
 
 // Explicit reset of envs `ids` (NULL: all).  Generate: the market position of a
@@ -942,7 +1053,8 @@ __global__ __launch_bounds__(kBlock) void reset_kernel(Params p, State s, Market
         if (MODE == HE_MODE_HESTON) cur.v[i] = p.var;
         cur.C[i] = p.rstv[2];
         cur.P[i] = p.rstv[3];
-        m = Mkt{p.rstv[0], p.rstv[1], p.rstv[2], p.rstv[3]};
+        if (cur.M) cur.M[i] = p.s0;
+        m = Mkt{p.rstv[0], p.rstv[1], p.rstv[2], p.rstv[3], 0.0};
         e.s0_small = m.S < 1e-6f;
         e.s0 = e.s0_small ? 1.0f : m.S;
         e.path = -1;
@@ -1060,6 +1172,8 @@ struct he_env {
     float rstv[4 + kObs] = {};  // host copy of the reset market + obs (generate)
     float* rst = nullptr;     // reset market + obs (generate)
     Params* dparams = nullptr;  // device copies of tile_params(env, 0 / 1) for step1_kernel
+    BookOpt* dbook = nullptr;   // liability book, device copy (generate modes)
+    double book_rst = 0.0;      // book value of the reset market (host copy)
     int64_t n_paths = 0;
     int32_t block_pos = 0;    // generate: next slot to consume; M = tile exhausted/invalid
     int32_t cur_buf = 0;      // tile buffer of the block being consumed
@@ -1183,6 +1297,10 @@ static void fill_params(he_env* env) {
     }
     p.rec = env->rec;
     p.recg = env->recg;
+    p.book_n = is_generate(env) ? c.book_size : 0;
+    p.book = env->dbook;
+    p.book_rst = env->book_rst;
+    p.tileC = nullptr;
 #ifdef HE_TIMING
     if (!g_tim && hipMalloc(&g_tim, (size_t)5 * 8192 * 2 * 8) != hipSuccess) g_tim = nullptr;
     p.tim = g_tim;
@@ -1215,7 +1333,10 @@ static he_status upload_tables(he_env* env) {
         else launch_init_reset<HE_MODE_HESTON>(env);
         HE_HIP(env, hipGetLastError());
         HE_HIP(env, hipDeviceSynchronize());
-        HE_HIP(env, hipMemcpy(env->rstv, env->rst, sizeof(env->rstv), hipMemcpyDeviceToHost));
+        float rec[32];
+        HE_HIP(env, hipMemcpy(rec, env->rst, sizeof(rec), hipMemcpyDeviceToHost));
+        memcpy(env->rstv, rec, sizeof(env->rstv));
+        if (env->cfg.book_size > 0) memcpy(&env->book_rst, rec + 20, sizeof(double));
         fill_params(env);
     }
     return sync_dparams(env);
@@ -1228,21 +1349,28 @@ static Params tile_params(const he_env* env, int b) {
     const size_t slots = (size_t)(env->cfg.market_block + 1) * (size_t)env->cfg.n_envs;
     p.tileA = env->tile + (size_t)b * 2 * slots;
     p.tileB = p.tileA + slots;
+    if (env->cfg.book_size > 0) p.tileC = reinterpret_cast<double*>(env->tile + 4 * slots) + (size_t)b * slots;
     return p;
 }
 
-template <int MODE>
+template <int MODE, bool BOOK>
 static void launch_market(he_env* env, int32_t advance_only, int buf, hipStream_t st) {
     int64_t blocks = (env->cfg.n_envs + kMktEnvs - 1) / kMktEnvs;
-    hipLaunchKernelGGL(market_kernel<MODE>, dim3((unsigned)blocks), dim3(kMktEnvs * kMktLanes), 0, st,
+    hipLaunchKernelGGL((market_kernel<MODE, BOOK>), dim3((unsigned)blocks), dim3(kMktEnvs * kMktLanes), 0, st,
                        tile_params(env, buf), env->cur, env->bak[buf], advance_only);
 }
 
 // generate the block that follows `cur` into tile buffer `buf` (advance_only = 0),
 // or rewind `cur` to `advance_only` steps past the start of buffer `buf`'s block.
 static he_status market(he_env* env, int32_t advance_only, int buf, hipStream_t st) {
-    if (env->cfg.mode == HE_MODE_GBM) launch_market<HE_MODE_GBM>(env, advance_only, buf, st);
-    else launch_market<HE_MODE_HESTON>(env, advance_only, buf, st);
+    const bool book = env->cfg.book_size > 0;
+    if (env->cfg.mode == HE_MODE_GBM) {
+        if (book) launch_market<HE_MODE_GBM, true>(env, advance_only, buf, st);
+        else launch_market<HE_MODE_GBM, false>(env, advance_only, buf, st);
+    } else {
+        if (book) launch_market<HE_MODE_HESTON, true>(env, advance_only, buf, st);
+        else launch_market<HE_MODE_HESTON, false>(env, advance_only, buf, st);
+    }
     HE_HIP(env, hipGetLastError());
     return HE_OK;
 }
@@ -1279,6 +1407,7 @@ static he_status materialize_market(he_env* env, hipStream_t st) {
             HE_HIP(env, hipMemcpyAsync(env->cur.C, src.C, N * 4, hipMemcpyDeviceToDevice, st));
             HE_HIP(env, hipMemcpyAsync(env->cur.P, src.P, N * 4, hipMemcpyDeviceToDevice, st));
             if (env->cur.v) HE_HIP(env, hipMemcpyAsync(env->cur.v, src.v, N * 8, hipMemcpyDeviceToDevice, st));
+            if (env->cur.M) HE_HIP(env, hipMemcpyAsync(env->cur.M, src.M, N * 8, hipMemcpyDeviceToDevice, st));
         }
     }
     env->block_pos = M;
@@ -1294,7 +1423,7 @@ static void launch_reset(he_env* env, const int64_t* ids, int64_t count, float* 
                        env->cur, ids, count, obs, inf);
 }
 
-template <int MODE>
+template <int MODE, bool BOOK>
 static void launch_step(he_env* env, const Params& p, const Io& io, bool info, int k, int slot0,
                         hipStream_t st) {
     int64_t blocks = (env->cfg.n_envs + kBlock - 1) / kBlock;
@@ -1307,17 +1436,17 @@ static void launch_step(he_env* env, const Params& p, const Io& io, bool info, i
         if (env->ev_start) {
             hipEvent_t a = (hipEvent_t)env->ev_start, b = (hipEvent_t)env->ev_stop;
             env->ev_start = env->ev_stop = nullptr;
-            hipExtLaunchKernelGGL(step1_kernel<MODE>, dim3((unsigned)blocks), dim3(kBlock), 0, st, a, b, 0, pc,
-                                  p.n, tA, tB, env->s, sio, slot0);
+            hipExtLaunchKernelGGL((step1_kernel<MODE, BOOK>), dim3((unsigned)blocks), dim3(kBlock), 0, st, a, b, 0,
+                                  pc, p.n, tA, tB, (const double*)p.tileC, env->s, sio, slot0);
             return;
         }
-        hipLaunchKernelGGL(step1_kernel<MODE>, dim3((unsigned)blocks), dim3(kBlock), 0, st, pc, p.n, tA, tB, env->s,
-                           sio, slot0);
+        hipLaunchKernelGGL((step1_kernel<MODE, BOOK>), dim3((unsigned)blocks), dim3(kBlock), 0, st, pc, p.n, tA, tB,
+                           (const double*)p.tileC, env->s, sio, slot0);
         return;
     }
     void (*kern)(Params, State, Io, int, int);
-    if (k == 1) kern = info ? step_kernel<MODE, true, true> : step_kernel<MODE, false, true>;
-    else kern = info ? step_kernel<MODE, true, false> : step_kernel<MODE, false, false>;
+    if (k == 1) kern = info ? step_kernel<MODE, true, true, BOOK> : step_kernel<MODE, false, true, BOOK>;
+    else kern = info ? step_kernel<MODE, true, false, BOOK> : step_kernel<MODE, false, false, BOOK>;
     if (env->ev_start) {  // one-shot: bracket exactly this dispatch (hipExtLaunchKernelGGL)
         hipEvent_t a = (hipEvent_t)env->ev_start, b = (hipEvent_t)env->ev_stop;
         env->ev_start = env->ev_stop = nullptr;
@@ -1361,7 +1490,7 @@ static he_status launch_steps(he_env* env, Io io, bool info, int k_total, void* 
     DeviceGuard dg(c.device);
     hipStream_t st = (hipStream_t)stream;
     if (c.mode == HE_MODE_REPLAY) {
-        launch_step<HE_MODE_REPLAY>(env, env->p, io, info, k_total, 0, st);
+        launch_step<HE_MODE_REPLAY, false>(env, env->p, io, info, k_total, 0, st);
         HE_HIP(env, hipGetLastError());
         return HE_OK;
     }
@@ -1387,8 +1516,14 @@ static he_status launch_steps(he_env* env, Io io, bool info, int k_total, void* 
         if (io.rew) sub.rew = io.rew + (int64_t)done * N;
         if (io.term) sub.term = io.term + (int64_t)done * N;
         Params p = tile_params(env, env->cur_buf);
-        if (c.mode == HE_MODE_GBM) launch_step<HE_MODE_GBM>(env, p, sub, info, k, env->block_pos, st);
-        else launch_step<HE_MODE_HESTON>(env, p, sub, info, k, env->block_pos, st);
+        const bool book = c.book_size > 0;
+        if (c.mode == HE_MODE_GBM) {
+            if (book) launch_step<HE_MODE_GBM, true>(env, p, sub, info, k, env->block_pos, st);
+            else launch_step<HE_MODE_GBM, false>(env, p, sub, info, k, env->block_pos, st);
+        } else {
+            if (book) launch_step<HE_MODE_HESTON, true>(env, p, sub, info, k, env->block_pos, st);
+            else launch_step<HE_MODE_HESTON, false>(env, p, sub, info, k, env->block_pos, st);
+        }
         HE_HIP(env, hipGetLastError());
         env->block_pos += k;
         done += k;
@@ -1464,6 +1599,13 @@ he_status he_create(const he_config* cfg, he_env** out) {
         return fail(env, HE_EINVAL, "max_trade_per_step must be in [0, 32767]");
     if (c.mode != HE_MODE_REPLAY && (c.episode_length < 1 || c.episode_length > (1 << 30)))
         return fail(env, HE_EINVAL, "episode_length must be >= 1");
+    if (c.book_size < 0 || c.book_size > HE_BOOK_MAX)
+        return fail(env, HE_EINVAL, "book_size must be in [0, %d]", HE_BOOK_MAX);
+    if (c.book_size > 0 && c.mode == HE_MODE_REPLAY)
+        return fail(env, HE_EINVAL, "the liability book needs a generate mode (GBM / Heston)");
+    for (int k = 0; k < c.book_size; ++k)
+        if (c.book[k].type < HE_BOOK_CALL || c.book[k].type > HE_BOOK_UO_CALL)
+            return fail(env, HE_EINVAL, "book[%d].type %d is not an he_book_type", k, c.book[k].type);
     if (c.market_block == 0) c.market_block = 64;
     if (c.market_block < 1 || c.market_block > kMaxBlock)
         return fail(env, HE_EINVAL, "market_block must be in [1, %d]", kMaxBlock);
@@ -1494,6 +1636,7 @@ he_status he_create(const he_config* cfg, he_env** out) {
             fs.push_back({(size_t)N * 4, (void**)&ms[k]->C, k == 0});
             fs.push_back({(size_t)N * 4, (void**)&ms[k]->P, k == 0});
             if (c.mode == HE_MODE_HESTON) fs.push_back({(size_t)N * 8, (void**)&ms[k]->v, k == 0});
+            if (c.book_size > 0) fs.push_back({(size_t)N * 8, (void**)&ms[k]->M, k == 0});
         }
     }
     size_t total = 0;
@@ -1511,17 +1654,31 @@ he_status he_create(const he_config* cfg, he_env** out) {
     }
     HE_HIP(env, hipMemset(mem, 0, total));
     if (is_generate(env)) {
+        // 2 buffers x ({S,v,C,P} | {greeks, lag}) float4 slots (+ 2 x f64 book slots)
         size_t tb = (size_t)4 * (size_t)(c.market_block + 1) * (size_t)N * sizeof(float4);
+        if (c.book_size > 0) tb += (size_t)2 * (size_t)(c.market_block + 1) * (size_t)N * sizeof(double);
         e = hipMalloc(&env->tile, tb);
         if (e != hipSuccess) return fail(env, HE_ENOMEM, "hipMalloc(tile %zu) failed: %s", tb, hipGetErrorString(e));
         HE_HIP(env, hipMalloc(&env->rst, 32 * sizeof(float)));
         env->block_pos = c.market_block;
-        env->prefetch_mode = c.reserved_i;  // market_prefetch mode (0 auto, 1 never, 2 always)
+        env->prefetch_mode = c.market_prefetch;  // 0 auto, 1 never, 2 always
         HE_HIP(env, hipStreamCreateWithFlags(&env->xs, hipStreamNonBlocking));
         HE_HIP(env, hipEventCreateWithFlags(&env->ev_fork, hipEventDisableTiming));
         HE_HIP(env, hipEventCreateWithFlags(&env->ev_next, hipEventDisableTiming));
     }
     HE_HIP(env, hipMalloc(&env->dparams, 2 * sizeof(Params)));
+    if (c.book_size > 0) {
+        BookOpt hb[HE_BOOK_MAX];
+        for (int k = 0; k < c.book_size; ++k) {
+            hb[k].type = c.book[k].type;
+            hb[k].expiry = c.book[k].expiry;
+            hb[k].K = c.book[k].strike;
+            hb[k].H = c.book[k].barrier;
+            hb[k].q100 = c.book[k].quantity * 100.0;
+        }
+        HE_HIP(env, hipMalloc(&env->dbook, HE_BOOK_MAX * sizeof(BookOpt)));
+        HE_HIP(env, hipMemcpy(env->dbook, hb, c.book_size * sizeof(BookOpt), hipMemcpyHostToDevice));
+    }
     he_status st = upload_tables(env);
     if (st != HE_OK) return st;
     // default streams: env i seeded with (seed + global id) until he_seed is called
@@ -1544,6 +1701,7 @@ he_status he_destroy(he_env* env) {
         if (env->tile) (void)hipFree(env->tile);
         if (env->rst) (void)hipFree(env->rst);
         if (env->dparams) (void)hipFree(env->dparams);
+        if (env->dbook) (void)hipFree(env->dbook);
         if (env->xs) {
             (void)hipStreamSynchronize(env->xs);
             (void)hipStreamDestroy(env->xs);

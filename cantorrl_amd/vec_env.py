@@ -65,7 +65,10 @@ class HedgingVecEnv:
 
     Replay mode (reference semantics): pass `data_file_path` (NPZ with paths,
     volatilities, call_prices_atm, put_prices_atm) or `tables=(S, v, C, P)`.
-    Generate modes: `mode="gbm"` / `"heston"`, market in `generate=dict(...)`.
+    Generate modes: `mode="gbm"` / `"heston"`, market in `generate=dict(...)`;
+    `generate["book"]` = list of up to 8 dicts {type: "call"|"put"|"uo_call",
+    strike, expiry (steps), quantity (contracts, < 0 short), barrier} is the
+    per-env liability book (extension, include/hedge_env.h he_book_option).
     Remaining keywords are the reference HedgingEnv ctor keywords.
     """
 
@@ -86,7 +89,9 @@ class HedgingVecEnv:
         kw = dict(base, **env_kwargs)
         self.env_kwargs = kw
         gen = dict(GENERATE_DEFAULTS, **(generate or {}))
+        book = list(gen.pop("book", None) or ())
         self.generate = gen
+        self.book = book
         self.device = torch.device(device if device is not None else "cuda:0")
         if self.device.type != "cuda":
             raise _lib.HedgeEnvError("HedgingVecEnv runs on a HIP device (cuda:N); there is no CPU path")
@@ -123,10 +128,23 @@ class HedgingVecEnv:
         cfg.heston_xi = float(gen["heston_xi"])
         cfg.heston_rho = float(gen["heston_rho"])
         cfg.market_block = int(market_block)
+        if book:
+            if mode == "replay":
+                raise ValueError("the liability book needs a generate mode (gbm / heston)")
+            if len(book) > _lib.HE_BOOK_MAX:
+                raise ValueError(f"at most {_lib.HE_BOOK_MAX} book options")
+            cfg.book_size = len(book)
+            for k, o in enumerate(book):
+                typ = o["type"]
+                cfg.book[k].type = _lib.BOOK_TYPES[typ] if isinstance(typ, str) else int(typ)
+                cfg.book[k].expiry = int(o["expiry"])
+                cfg.book[k].strike = float(o["strike"])
+                cfg.book[k].barrier = float(o.get("barrier", 0.0))
+                cfg.book[k].quantity = float(o["quantity"])
         if os.environ.get("CANTORRL_NO_PREFETCH"):
             market_prefetch = False
         # 0 auto (rollouts, or single steps from 131,072 envs), 1 never, 2 always
-        cfg.reserved_i = 0 if market_prefetch == "auto" else (2 if market_prefetch else 1)
+        cfg.market_prefetch = 0 if market_prefetch == "auto" else (2 if market_prefetch else 1)
         base_seed = int(seed if seed is not None else gen.get("seed", 42))
         cfg.seed = base_seed
         self._cfg = cfg

@@ -41,7 +41,8 @@
 extern "C" {
 #endif
 
-#define HE_ABI_VERSION 1
+#define HE_ABI_VERSION 2
+#define HE_BOOK_MAX 8
 #define HE_OBS_DIM 13
 #define HE_ACT_DIM 2
 
@@ -66,6 +67,25 @@ typedef enum he_loss {
     HE_LOSS_CVAR = 2,    /* identical to ABS inside the env (hedging_env_v2.py:250-253) */
     HE_LOSS_OTHER = 3    /* any other string: |x| branch (:252-253)                    */
 } he_loss;
+
+/* Liability book (extension, generate modes; BASELINE.json configs[3]/[4]): options
+ * every env carries besides the hedged shares.  The book is marked at every step
+ * from the env's own market (S_t, v_t, t) and enters the portfolio value
+ * (hedging_env_v2.py:233-236): PV = shares*S + options + cash + sum_k q_k*100*V_k. */
+typedef enum he_book_type {
+    HE_BOOK_CALL = 0,      /* European call, Black-Scholes (option_calculator.py:11-27 form) */
+    HE_BOOK_PUT = 1,       /* European put                                                  */
+    HE_BOOK_UO_CALL = 2    /* up-and-out call: worthless once S_t >= barrier at a step date;
+                              alive: closed-form continuous-barrier price (Hull, q = 0)     */
+} he_book_type;
+
+typedef struct he_book_option {
+    int32_t type;          /* he_book_type                                                  */
+    int32_t expiry;        /* in env steps from the episode start: tau = (expiry - t) * dt  */
+    double strike;         /* K                                                             */
+    double barrier;        /* H (HE_BOOK_UO_CALL)                                           */
+    double quantity;       /* contracts (x100 shares); negative = short, i.e. a liability   */
+} he_book_option;
 
 typedef struct he_config {
     int32_t abi_version;        /* = HE_ABI_VERSION                                  */
@@ -103,9 +123,12 @@ typedef struct he_config {
     double heston_rho;
     int32_t market_block;       /* generate modes: steps of market data generated per
                                    market_kernel launch (1..64, default 64)          */
-    int32_t reserved_i;         /* market prefetch on the side stream: 0 auto (fused
+    int32_t market_prefetch;    /* market_kernel(b+1) on the side stream: 0 auto (fused
                                    rollouts, or he_step from 131,072 envs), 1 never,
                                    2 always                                          */
+    int32_t book_size;          /* generate modes: options in the liability book (0..8) */
+    int32_t reserved_i;
+    he_book_option book[HE_BOOK_MAX];
     double reserved[7];
 } he_config;
 

@@ -14,6 +14,10 @@ sequence of the reference (NumPy 2 / NEP 50 promotion, python scalars weak):
 * `OptionCalculator.black_scholes_price`
                            -- quantconnect/option_calculator.py:11-27
 * GBM price advance        -- src/sim/rbergomi_sim.py:454-464 (constant v)
+* liability book (extension, BASELINE.json configs[3]/[4]; include/hedge_env.h
+  he_book_option) -- Europeans in the option_calculator.py:11-27 form, the
+  up-and-out call in Hull's closed form; parity unpinned by the reference (it has
+  no book), checked against a Brownian-bridge Monte Carlo in tests/test_book_cpu.py
 
 Replay mode consumes NPZ-layout tables (`paths`, `volatilities`,
 `call_prices_atm`, `put_prices_atm`, hedging_env_v2.py:36-48) and draws the
@@ -160,6 +164,66 @@ def bs_greeks(S, K, T, r, sigma):
 
 
 # --------------------------------------------------------------------------- #
+# Liability book (extension): restates cantorrl_amd/csrc/hedge_env.hip        #
+# book_option / book_value                                                    #
+# --------------------------------------------------------------------------- #
+BOOK_TYPES = {"call": 0, "put": 1, "uo_call": 2}
+
+
+def book_option_value(o, S, sig, tau, r, runmax):
+    """One book option at (S, sig, tau) [f64 arrays]; runmax = episode max of S at the
+    step dates (up-and-out monitor).  Intrinsic when tau <= 0 or sig <= 0."""
+    typ = BOOK_TYPES[o["type"]] if isinstance(o["type"], str) else int(o["type"])
+    K = float(o["strike"])
+    H = float(o.get("barrier", 0.0))
+    S, sig, tau, runmax = np.broadcast_arrays(*(np.asarray(x, np.float64) for x in (S, sig, tau, runmax)))
+    with np.errstate(all="ignore"):
+        intrinsic = (tau <= 0) | (sig <= 0)
+        ic = np.where(S - K < 0, 0.0, S - K)
+        ip = np.where(K - S < 0, 0.0, K - S)
+        s2 = sig * sig
+        sst = sig * np.sqrt(tau)
+        d1 = (np.log(S / K) + (r + 0.5 * s2) * tau) / sst
+        d2 = d1 - sst
+        Kd = K * np.exp(-r * tau)
+        if typ == 1:
+            v = Kd * ndtr(-d2) - S * ndtr(-d1)
+            v = np.where(v < 0, 0.0, v)
+            return np.where(intrinsic, ip, v)
+        v = S * ndtr(d1) - Kd * ndtr(d2)
+        if typ == 2:
+            lam = (r + 0.5 * s2) / s2
+            ls = lam * sst
+            lhs = np.log(H / S)
+            x1 = np.log(S / H) / sst + ls
+            y = np.log((H * H) / (S * K)) / sst + ls
+            y1 = lhs / sst + ls
+            p2l = np.exp((2.0 * lam) * lhs)
+            p2l2 = np.exp((2.0 * lam - 2.0) * lhs)
+            cui = (S * ndtr(x1) - Kd * ndtr(x1 - sst) - S * p2l * (ndtr(-y) - ndtr(-y1))
+                   + Kd * p2l2 * (ndtr(-y + sst) - ndtr(-y1 + sst)))
+            v = v - cui
+        v = np.where(v < 0, 0.0, v)
+        if typ == 2:
+            v = np.where(H <= K, 0.0, v)
+        v = np.where(intrinsic, ic, v)
+        if typ == 2:
+            v = np.where(runmax >= H, 0.0, v)
+    return v
+
+
+def book_value(book, S, var, t, runmax, r, dt):
+    """sum_k q_k * 100 * V_k after step t of the episode (in book order, from 0.0)."""
+    S = np.asarray(S, np.float64)
+    sig = np.sqrt(np.maximum(np.asarray(var, np.float64), 0.0))
+    B = np.zeros(S.shape)
+    for o in book:
+        tau = (int(o["expiry"]) - np.asarray(t, np.int64)) * dt
+        B = B + (float(o["quantity"]) * 100.0) * book_option_value(o, S, sig, tau, r, runmax)
+    return B
+
+
+# --------------------------------------------------------------------------- #
 # The env batch                                                               #
 # --------------------------------------------------------------------------- #
 class OracleVecEnv:
@@ -222,6 +286,8 @@ class OracleVecEnv:
             self.g_ep = np.full(self.n, -1, np.int64)  # next reset starts episode 0
             self.S64 = np.zeros(self.n, np.float64)
             self.V64 = np.zeros(self.n, np.float64)
+            self.book = list(g.get("book", None) or ())
+            self.runmax = np.zeros(self.n, np.float64)
         else:
             raise ValueError(mode)
         self.rngs = [None] * self.n
@@ -345,6 +411,10 @@ class OracleVecEnv:
         self.pv_prev[ids] = pv0.astype(np.float32).astype(np.float64)
         self.S_prev[ids] = S
         self.v_prev[ids] = v
+        if self.mode != "replay" and self.book:
+            self.runmax[ids] = self.g_s0
+            self.pv_prev[ids] = self.pv_prev[ids] + book_value(self.book, np.full(len(ids), self.g_s0), self.g_v,
+                                                               0, self.g_s0, self.r, self.g_dt)
 
     # ------------------------------------------------------------------ obs
     def _greeks(self):
@@ -456,9 +526,15 @@ class OracleVecEnv:
             Cd, Pd = self._gbm_marks(self.S64, self.V64)
             self.C = np.where(term, self.C, Cd.astype(np.float32))
             self.P = np.where(term, self.P, Pd.astype(np.float32))
+            if self.book:
+                self.runmax = np.maximum(self.runmax, self.S64)
+                var = self.V64 if self.mode == "heston" else self.g_v
+                book = book_value(self.book, self.S64, var, self.t, self.runmax, self.r, self.g_dt)
         with np.errstate(all="ignore"):
             opt = (self.call * self.C * self.mult) + (self.put * self.P * self.mult)
             pv = (np.float32(self.shares) * self.S) + opt + self.cash
+            if self.mode != "replay" and self.book:
+                pv = pv + book
             pnl = pv - self.pv_prev
             ps = pnl / self.shares if self.shares != 0 else pnl
             raw = np.abs(ps)

@@ -233,3 +233,59 @@ def test_partial_reset_keeps_other_envs_on_their_paths():
         assert torch.equal(ra[keep], rb[keep]), k
         if k == 37:  # a reset env restarts at t=0: obs[6] (time to end) of the next step
             assert torch.all(ob[[3, 200, 511], 6] == (252 - 1) / 252)
+
+
+BOOK8 = [dict(type="call", strike=500.0, expiry=10, quantity=-20.0),
+         dict(type="put", strike=480.0, expiry=20, quantity=-15.0),
+         dict(type="call", strike=520.0, expiry=30, quantity=-10.0),
+         dict(type="put", strike=500.0, expiry=40, quantity=-25.0),
+         dict(type="call", strike=470.0, expiry=50, quantity=5.0),
+         dict(type="put", strike=530.0, expiry=35, quantity=-5.0),
+         dict(type="call", strike=496.0, expiry=5, quantity=-40.0),
+         dict(type="put", strike=450.0, expiry=60, quantity=-30.0)]
+
+
+def test_book_of_8_europeans_matches_oracle():
+    """Config 4's env (extension): 8-option liability book marked every step, expiries
+    inside and past the episode (intrinsic once expired)."""
+    cfg = dict(loss_type="abs", pnl_penalty_weight=0.001, lambda_cost=0.0001, theta_weight=0.0002,
+               slippage_bps=1.0)
+    gen = dict(s0=496.48001098632812, variance=0.029028, mu=0.04, dt=1 / 252, episode_length=40, book=BOOK8)
+    run_gbm_pair(256, 100, 21, cfg, gen)
+
+
+def test_book_heston_up_and_out_matches_oracle():
+    """Config 5's env (extension): Heston market + an up-and-out call close to the
+    money, so envs knock out at different steps (divergent branches)."""
+    cfg = dict(loss_type="abs", pnl_penalty_weight=0.001, lambda_cost=0.0001, theta_weight=0.0002,
+               slippage_bps=1.0)
+    book = [dict(type="uo_call", strike=490.0, barrier=515.0, expiry=30, quantity=-50.0),
+            dict(type="call", strike=500.0, expiry=30, quantity=10.0)]
+    gen = dict(s0=496.48001098632812, variance=0.04, mu=0.04, dt=1 / 252, episode_length=30,
+               heston_kappa=1.5, heston_theta=0.035, heston_xi=0.6, heston_rho=-0.7, book=book)
+    run_gbm_pair(256, 75, 13, cfg, gen, mode="heston")
+
+
+def test_book_rollout_equals_repeated_steps_and_checkpoint():
+    from cantorrl_amd.vec_env import HedgingVecEnv
+    n, K = 700, 70
+    gen = dict(episode_length=30, book=BOOK8[:3] + [dict(type="uo_call", strike=490.0, barrier=510.0, expiry=25,
+                                                        quantity=-10.0)])
+    acts = torch.rand((K, n, 2), device="cuda") * 2 - 1
+    a = HedgingVecEnv(n, mode="gbm", generate=gen, seed=5, return_numpy=False, info_keys=("portfolio_value",))
+    b = HedgingVecEnv(n, mode="gbm", generate=gen, seed=5, return_numpy=False, info_keys=("portfolio_value",))
+    a.reset_tensors()
+    b.reset_tensors()
+    obs_r, rew_r, term_r = a.rollout(acts[:40].contiguous())
+    for k in range(40):
+        obs, rew, term, _ = b.step_tensors(acts[k], terminal_obs=False)
+        assert torch.equal(obs, obs_r[k]), k
+        assert torch.equal(rew, rew_r[k]), k
+    blob = a.get_state()
+    o1, r1, _ = a.rollout(acts[40:].contiguous())
+    c = HedgingVecEnv(n, mode="gbm", generate=gen, seed=5, return_numpy=False, info_keys=())
+    c.set_state(blob)
+    o2, r2, _ = c.rollout(acts[40:].contiguous())
+    assert torch.equal(o1, o2) and torch.equal(r1, r2)
+    for e in (a, b, c):
+        e.close()

@@ -72,7 +72,7 @@ int main(int argc, char** argv) {
         api.config_init(&c, 2);
         c.n_envs = N;
         c.mode = HE_MODE_GBM;
-        c.reserved_i = getenv("STEP_BENCH_PREFETCH") ? 2 : (RK > 0 ? 0 : 1);  // always / (auto) / never
+        c.market_prefetch = getenv("STEP_BENCH_PREFETCH") ? 2 : (RK > 0 ? 0 : 1);  // always / (auto) / never
         he_env* env;
         if (api.create(&c, &env) != HE_OK) { fprintf(stderr, "create: %s\n", api.last_error(env)); return 1; }
         if (api.reset(env, nullptr, 0, obs, nullptr, st) != HE_OK) return 1;
@@ -106,7 +106,7 @@ int main(int argc, char** argv) {
         float ms;
         CK(hipEventElapsedTime(&ms, a, b));
         double us = ms * 1000.0 / (reps * (double)per_graph * KK);
-        printf("%-24s%s%s%s N=%lld  %.3f us/step  %.4e env-steps/s\n", argv[li], o ? "" : " (no obs)", c.reserved_i == 2 ? " (prefetch)" : "", RK > 0 ? " (rollout)" : "", (long long)N, us, N / us * 1e6);
+        printf("%-24s%s%s%s N=%lld  %.3f us/step  %.4e env-steps/s\n", argv[li], o ? "" : " (no obs)", c.market_prefetch == 2 ? " (prefetch)" : "", RK > 0 ? " (rollout)" : "", (long long)N, us, N / us * 1e6);
         typedef he_status (*tim_fn)(void*, size_t);
         tim_fn tim = (tim_fn)dlsym(api.handle, "he_debug_timing");
         if (tim) {
