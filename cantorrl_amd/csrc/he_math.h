@@ -49,6 +49,32 @@ HE_HD float div_byf(float a, float b, float y) {
     return fmaf(r, y, q);
 }
 
+// Integer-valued a (|a| <= 2^24) by a constant 1 <= b <= 2^30: the Markstein step with
+// no guard -- q = a*y can neither overflow nor fall near the subnormals, and a = 0
+// gives +0 like +0 / b.  f32 (obs positions / max held, (T - t) / T) and f64 ((T - t)
+// / 252) forms.
+HE_HD float div_int_byf(float a, float b, float y) {
+    const float q = a * y;
+    return fmaf(fmaf(-q, b, a), y, q);
+}
+HE_HD double div_int_by(double a, double b, double y) {
+    const double q = a * y;
+    return fma(fma(-q, b, a), y, q);
+}
+
+// f32 a / b for any f32 a, branch-free: the f64 Markstein step on the f32 operands
+// (an f32 quotient is never near the f64 subnormals or overflow, so RN64(a/b) is exact
+// by the theorem) rounded once more to f32 -- RN32(RN64(a/b)) = RN32(a/b) since
+// 53 >= 2*24 + 2.  Zero / inf / NaN dividends take a*y (same value and sign as a/b).
+// y64 = RN64(1/b).
+HE_HD float div_f32_by(float a, double b, double y64) {
+    const double ad = (double)a;
+    const double q = ad * y64;
+    const double r = fma(-q, b, ad);
+    const float res = (float)fma(r, y64, q);
+    return (a == 0.0f || !(fabsf(a) <= 3.4028234663852886e38f)) ? (float)q : res;
+}
+
 // np.rint(f32).astype(int64) then np.clip(., -mt, mt)  (hedging_env_v2.py:184-188).
 // x86 cvttss2si maps NaN and |x| >= 2^63 to INT64_MIN, which the clip sends to -mt.
 HE_HD int32_t trade_round(float f, int32_t mt) {

@@ -53,7 +53,12 @@ __device__ __forceinline__ float2 ld2(const GLOBAL v2f* p, int64_t k) {
     return make_float2(x.x, x.y);
 }
 
-constexpr int kBlock = 256;      // step kernel: envs per workgroup
+constexpr int kBlock = 256;      // step kernel: threads per workgroup (4 waves)
+#ifndef HE_STEP_EPW
+#define HE_STEP_EPW 64
+#endif
+constexpr int kEpw = HE_STEP_EPW;          // step kernel: envs per wave (64, or 32 = 2x the waves)
+constexpr int kEpb = (kBlock / 64) * kEpw; // step kernel: envs per workgroup
 constexpr int kObs = HE_OBS_DIM;
 constexpr int kMktEnvs = 32;     // market kernel: envs per workgroup (half a wave wide)
 constexpr int kMktLanes = 8;     //                slot-lanes per env (4 waves, 16.6 KB LDS)
@@ -84,6 +89,8 @@ struct Params {
     float inv_maxh_f, inv_T_f;  // RN_f32(1/x) for div_byf
     int32_t s0s_const;          // generate: max(S0, 25) is one constant for every env
     float s0s_f, inv_s0s_f;
+    double s0s_d, inv_s0s_d;    // the same as f64 (div_f32_by)
+    double inv_252;             // RN(1/252)
     float init_cash_f;
     double tcpc, slip_frac, lam, w, theta, initial_cash;
     double shares_d, inv_shares;  // inv_*: RN(1/x) for div_by
@@ -103,6 +110,8 @@ struct Params {
     float g_sigma, g_num_drift;  // constant-variance greeks: sigma, (r+0.5 sigma**2)*T (f32)
     double g_sst;                // sigma*sqrt(T) (f64)
     double g_inv_sst;            // 1/(sigma*sqrt(T))
+    float g_sst_f, g_inv_sst_f;  // f32 twins for greeks_fast
+    float sqrt_tenor_f;
     double h_kappa, h_theta, h_xi, h_rho, h_sqrt1mrho2;
     int32_t den_const;      // generate: reward denominator of the shared S0 (all envs)
     double den, inv_den;
@@ -224,6 +233,59 @@ __device__ __forceinline__ float4 greeks(const Params& p, float S, float v) {
     return make_float4((float)cd, (float)gam, (float)pd, 0.0f);
 }
 
+// Generate-mode obs greeks (market_kernel): same branches and the same f32 d1
+// numerator as greeks(), the rest in f32 instead of f64-then-cast.  N(d1) - 1 is
+// taken as -N(-d1) (no cancellation), 1/(S sigma sqrt T) through v_rcp_f32.  Within
+// 4 f32 ulp of the reference's f64 values (tests: OBS_RTOL 1e-6 on columns 7-10) at
+// about a third of the cost of the f64 chain (measured: greeks were 32% of
+// market_kernel).  Replay tables and the reset obs keep greeks().
+template <bool CONST_VAR>
+__device__ __forceinline__ float4 greeks_fast(const Params& p, float S, float v) {
+    float cd, gam, pd;
+    const float K = rintf(S);
+    if (S <= 1e-6f) {
+        cd = (K == 0.0f) ? 0.5f : ((K > 0.0f) ? 0.0f : 1.0f);
+        pd = (K == 0.0f) ? -0.5f : ((K < 0.0f) ? 0.0f : -1.0f);
+        gam = 0.0f;
+    } else {
+        float sigma, num_drift, sstf;
+        double sst;
+        if (CONST_VAR) {
+            sigma = p.g_sigma;
+            num_drift = p.g_num_drift;
+            sst = p.g_sst;
+            sstf = p.g_sst_f;
+        } else {
+            sigma = sqrtf(np_maxf(v, 1e-8f));
+            num_drift = (p.r_f + 0.5f * (sigma * sigma)) * p.tenor_f;
+            sst = (double)sigma * p.sqrt_tenor;
+            sstf = (float)sst;
+        }
+        if (p.tenor_small || sigma <= 1e-6f) {
+            cd = (S > K) ? 1.0f : ((S == K) ? 0.5f : 0.0f);
+            pd = (S < K) ? -1.0f : ((S == K) ? -0.5f : 0.0f);
+            gam = 0.0f;
+        } else {
+            const float Kc = np_maxf(K, 1e-6f);
+            const float num = logf(S / Kc) + num_drift;   // f32 in the reference too
+            float d1;
+            if (sst < 1e-9) {
+                const float sg = (num > 0.0f) ? 1.0f : ((num < 0.0f) ? -1.0f : num);
+                d1 = sg * 10.0f;
+            } else {
+                d1 = CONST_VAR ? num * p.g_inv_sst_f : num * __builtin_amdgcn_rcpf(sstf);
+            }
+            const float x = d1 * 0.70710678118654752f;
+            cd = 0.5f * erfcf(-x);
+            pd = -0.5f * erfcf(x);
+            const float gd = S * sstf;
+            gam = (fabsf(gd) < 1e-9f) ? 0.0f
+                                      : (expf(-0.5f * (d1 * d1)) * 0.398942280401432678f) * __builtin_amdgcn_rcpf(gd);
+        }
+    }
+    return make_float4(cd, gam, pd, 0.0f);
+}
+
 // ------------------------------------------------------------------ observation
 // S_t / S_{t-1} - 1 clipped to +-1, 0 when S_{t-1} == 0 (hedging_env_v2.py:129-136):
 // a function of the market alone, so it is computed where the market is (market_kernel
@@ -235,12 +297,15 @@ __device__ __forceinline__ float lag_return(float S, float Sp) {
 // hedging_env_v2.py:109-143.  m = market after the step, g = its greeks and, in g.w,
 // lag_return(m.S, Sp); Sp/vp = S_t_minus_1 / v_t_minus_1.  Quotients by per-handle
 // constants use div_byf (correctly rounded, 3 instructions).
+// FAST: the hot configuration is known at compile time (see fast_config()):
+// generate mode, record_metrics, max_contracts_held > 0, T > 0.
+template <bool FAST = false>
 __device__ __forceinline__ void make_obs(const Params& p, const Env& e, const Mkt& m, float4 g, float Sp,
                                          float vp, float* o) {
-    if (p.s0s_const) {
-        o[0] = div_byf(m.S, p.s0s_f, p.inv_s0s_f);
-        o[1] = div_byf(m.C, p.s0s_f, p.inv_s0s_f);
-        o[2] = div_byf(m.P, p.s0s_f, p.inv_s0s_f);
+    if (FAST || p.s0s_const) {
+        o[0] = div_f32_by(m.S, p.s0s_d, p.inv_s0s_d);
+        o[1] = div_f32_by(m.C, p.s0s_d, p.inv_s0s_d);
+        o[2] = div_f32_by(m.P, p.s0s_d, p.inv_s0s_d);
     } else {
         float s0s = np_maxf(e.s0, 25.0f);
         o[0] = m.S / s0s;
@@ -249,16 +314,16 @@ __device__ __forceinline__ void make_obs(const Params& p, const Env& e, const Mk
     }
     // int64/int -> f64 quotient cast to f32 == correctly rounded f32 quotient when
     // both operands are exact in f32 (|x| < 2^24) and 53 >= 2*24+2 (no double rounding)
-    if (p.maxh != 0) {
-        o[3] = div_byf((float)e.call, p.maxh_f, p.inv_maxh_f);
-        o[4] = div_byf((float)e.put, p.maxh_f, p.inv_maxh_f);
+    if (FAST || p.maxh != 0) {
+        o[3] = div_int_byf((float)e.call, p.maxh_f, p.inv_maxh_f);
+        o[4] = div_int_byf((float)e.put, p.maxh_f, p.inv_maxh_f);
     } else {
         o[3] = 0.0f;
         o[4] = 0.0f;
     }
     o[5] = m.v;
-    o[6] = (p.T != 0) ? div_byf((float)(p.T - (int32_t)e.t), p.T_f, p.inv_T_f) : 0.0f;
-    if (p.record_metrics) {
+    o[6] = (FAST || p.T != 0) ? div_int_byf((float)(p.T - (int32_t)e.t), p.T_f, p.inv_T_f) : 0.0f;
+    if (FAST || p.record_metrics) {
         o[7] = g.x;
         o[8] = g.y;
         o[9] = g.z;
@@ -424,7 +489,16 @@ __global__ __launch_bounds__(kMktEnvs * kMktLanes, HE_MKT_WAVES) void market_ker
         for (uint64_t m = m0 + (uint64_t)sub; m <= m1; m += kMktLanes) {
             if (!live) break;
             double z[2];
+#if defined(HE_MKT_SKIP) && (HE_MKT_SKIP & 4)
+            {   // diagnostic build: no Box-Muller (timing A/B only)
+                u32x4 ctr = {(uint32_t)m, (uint32_t)(m >> 32), (uint32_t)gid, (uint32_t)((uint64_t)gid >> 32)};
+                u32x4 x = philox4x32_10(ctr, p.key0, p.key1);
+                z[0] = u01(x.x, x.y) - 0.5;
+                z[1] = u01(x.z, x.w) - 0.5;
+            }
+#else
             normals(p, gid, m, &z[0], &z[1]);
+#endif
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
                 uint64_t n = 2 * m + (uint64_t)h;
@@ -497,7 +571,11 @@ __global__ __launch_bounds__(kMktEnvs * kMktLanes, HE_MKT_WAVES) void market_ker
         double v64 = HESTON ? shV[lane][j] : p.var;
         float C, P;
         if (tj < T) {
+#if defined(HE_MKT_SKIP) && (HE_MKT_SKIP & 2)
+            C = (float)S64; P = (float)v64;  // diagnostic build: no marks
+#else
             marks<MODE>(p, S64, v64, &C, &P);
+#endif
         } else if (T == 1u) {  // lagged marks of t = T-1 = 0: the reset marks
             C = p.rstv[2];
             P = p.rstv[3];
@@ -515,7 +593,11 @@ __global__ __launch_bounds__(kMktEnvs * kMktLanes, HE_MKT_WAVES) void market_ker
         float S32 = (float)S64;
         float v32 = HESTON ? (float)v64 : p.var_f;
         p.tileA[(int64_t)j * N + i] = make_float4(S32, v32, C, P);
-        float4 g = p.record_metrics ? greeks<!HESTON>(p, S32, v32) : make_float4(0.f, 0.f, 0.f, 0.f);
+#if defined(HE_MKT_SKIP) && (HE_MKT_SKIP & 1)
+        float4 g = make_float4(S32, v32, 0.f, 0.f);  // diagnostic build: no greeks
+#else
+        float4 g = p.record_metrics ? greeks_fast<!HESTON>(p, S32, v32) : make_float4(0.f, 0.f, 0.f, 0.f);
+#endif
         // the step into slot j starts from the reset market (first step of an
         // episode) or from slot j-1
         const float Sp32 = (tj == 1u) ? p.rstv[0] : (float)shS[lane][j - 1];
@@ -580,19 +662,30 @@ struct StepOut {
 
 // hedging_env_v2.py:175-262 (v1: hedging_env.py:171-245).  pre/post: market before
 // and after the advance (post C/P already lagged on the terminal step).
+// portfolio value of the pre-step state (hedging_env_v2.py:233-236): the previous
+// step's pv, recomputed bit for bit (same operands, same order)
 template <bool BOOK>
+__device__ __forceinline__ double portfolio_value(const Params& p, const Env& e, const Mkt& m) {
+    double optv = ((double)e.call * (double)m.C) * 100.0 + ((double)e.put * (double)m.P) * 100.0;
+    double pv = ((double)(p.shares_f * m.S) + optv) + e.cash;
+    if (BOOK) pv = pv + m.B;  // liability book (extension): after cash
+    return pv;
+}
+
+// FAST: variant 2, loss != mse, shares_to_hedge != 0, generate mode (constant reward
+// denominator) -- the branches on those flags compiled out (fast_config()).
+// pv_last = portfolio_value(pre-step state), carried in registers across fused steps.
+template <bool BOOK, bool FAST = false>
 __device__ __forceinline__ void step_env(const Params& p, Env& e, const Mkt& pre, const Mkt& post, float a0,
-                                         float a1, StepOut& o) {
-    // portfolio_value_t_minus_1 is a pure function of the pre-step state
+                                         float a1, double pv_last, StepOut& o) {
     double pv_prev;
     if (e.t == 0) {
         float pv0 = (p.shares_f * pre.S + 0.0f) + p.init_cash_f;  // f32 (:167-168)
         pv_prev = (double)pv0;
+        if (BOOK) pv_prev = pv_prev + pre.B;
     } else {
-        double optv = ((double)e.call * (double)pre.C) * 100.0 + ((double)e.put * (double)pre.P) * 100.0;
-        pv_prev = ((double)(p.shares_f * pre.S) + optv) + e.cash;
+        pv_prev = pv_last;
     }
-    if (BOOK) pv_prev = pv_prev + pre.B;  // liability book (extension): after cash
     // (i)-(ii) integer trade logic (:181-200)
     float fc = a0 * p.mt_f;
     float fp = a1 * p.mt_f;
@@ -608,7 +701,7 @@ __device__ __forceinline__ void step_env(const Params& p, Env& e, const Mkt& pre
     int32_t adc = dc < 0 ? -dc : dc, adp = dp < 0 ? -dp : dp;
     double commission = (double)(adc + adp) * p.tcpc;
     double slippage = 0.0, tc;
-    if (p.variant == 2) {
+    if (FAST || p.variant == 2) {
         double sc = (((double)adc * (double)pre.C) * 100.0) * p.slip_frac;
         double sp = (((double)adp * (double)pre.P) * 100.0) * p.slip_frac;
         slippage = sc + sp;
@@ -621,15 +714,13 @@ __device__ __forceinline__ void step_env(const Params& p, Env& e, const Mkt& pre
     e.t = e.t + 1;
     bool term = (int32_t)e.t >= p.T;
     // (vi) mark-to-market (:233-238)
-    double optv = ((double)e.call * (double)post.C) * 100.0 + ((double)e.put * (double)post.P) * 100.0;
-    double pv = ((double)(p.shares_f * post.S) + optv) + e.cash;
-    if (BOOK) pv = pv + post.B;
+    double pv = portfolio_value<BOOK>(p, e, post);
     double pnl = pv - pv_prev;
-    double ps = p.shares_zero ? pnl : div_by(pnl, p.shares_d, p.inv_shares);
+    double ps = (!FAST && p.shares_zero) ? pnl : div_by(pnl, p.shares_d, p.inv_shares);
     // (vii) reward (:243-262)
     double term_v;
-    const double num = (p.loss == HE_LOSS_MSE) ? ps * ps : fabs(ps);
-    if (p.den_const) {
+    const double num = (!FAST && p.loss == HE_LOSS_MSE) ? ps * ps : fabs(ps);
+    if (FAST || p.den_const) {
         term_v = div_by(num, p.den, p.inv_den);
     } else {
         float f = np_maxf(e.s0, 25.0f);
@@ -641,10 +732,10 @@ __device__ __forceinline__ void step_env(const Params& p, Env& e, const Mkt& pre
     double rpc = (-p.w) * term_v;
     double tcp = p.lam * tc;
     double thp = 0.0, reward;
-    if (p.variant == 2) {
+    if (FAST || p.variant == 2) {
         // computed, not looked up: a table load indexed by t is a dependent round trip.
         // theta_weight 0 (the default): 0 * finite = +0 and x - +0 == x bit for bit
-        if (p.theta != 0.0) thp = p.theta * div_by((double)(p.T - (int32_t)e.t), 252.0, 1.0 / 252.0);
+        if (FAST || p.theta != 0.0) thp = p.theta * div_int_by((double)(p.T - (int32_t)e.t), 252.0, p.inv_252);
         reward = (rpc - tcp) - thp;
     } else {
         reward = rpc - tcp;
@@ -700,13 +791,13 @@ __device__ __forceinline__ void write_info(const he_info& inf, int64_t i, const 
     if (inf.current_episode_idx) inf.current_episode_idx[i] = e.path;
 }
 
-// Write one wave's obs rows [wrow0, wrow0 + rows), staged in LDS as [64][13] at
-// wtile, to out (row-major [N][13]) with 16-B stores.  Wave-local: the lanes of a
+// Write one wave's obs rows [wrow0, wrow0 + rows), staged in LDS as [rows][13] at
+// wtile, to out (row-major [N][13]) with 16-B stores (wrow0 % 32 == 0: 16-B aligned).  Wave-local: the lanes of a
 // wave issue their LDS writes and reads in program order, so no workgroup barrier.
 // (compiler-only barriers around it: no hardware wait is needed)
 __device__ __forceinline__ void flush_obs_wave(const float* wtile, float* out, int64_t wrow0, int rows, int lane) {
     asm volatile("" ::: "memory");
-    GLOBAL float* dst = (GLOBAL float*)out + wrow0 * kObs;  // 16-B aligned: wrow0 % 64 == 0
+    GLOBAL float* dst = (GLOBAL float*)out + wrow0 * kObs;
     GLOBAL v4f* d4 = (GLOBAL v4f*)dst;
     const v4f* s4 = reinterpret_cast<const v4f*>(wtile);
     if (rows == 64) {
@@ -781,7 +872,7 @@ __device__ __forceinline__ void env_reset_common(const Params& p, Env& e) {
 // SINGLE: the he_step instance (k_steps == 1 at compile time, straight-line code).
 // tA/tB: the market source, tile buffer {S,v,C,P} / greeks (generate) or the
 // replay table rec / recg.
-template <int MODE, bool INFO, bool SINGLE, bool BOOK>
+template <int MODE, bool INFO, bool SINGLE, bool BOOK, bool FAST>
 __device__ __forceinline__ void step_body(const Params& pk, int64_t n_envs, const float4* tA, const float4* tB,
                                           const double* tC, State s, Io io, int k_steps_arg, int slot0) {
     constexpr bool REPLAY = (MODE == HE_MODE_REPLAY);
@@ -791,12 +882,13 @@ __device__ __forceinline__ void step_body(const Params& pk, int64_t n_envs, cons
     // latency-critical: win VALU/memory issue arbitration against the prefetching
     // market_kernel waves that share the SIMDs (they run at the default priority 0)
     __builtin_amdgcn_s_setprio(3);
-    __shared__ __attribute__((aligned(16))) float tile[kBlock * kObs];
-    const int64_t row0 = (int64_t)blockIdx.x * kBlock;
-    const int64_t i = row0 + threadIdx.x;
+    __shared__ __attribute__((aligned(16))) float tile[kEpb * kObs];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t wrow0 = (int64_t)blockIdx.x * kEpb + wave * kEpw;  // first env of this wave
+    const int64_t i = wrow0 + lane;
     const int64_t N = n_envs;
-    const bool live = i < N;
-    const int rows = (int)((N - row0) < kBlock ? (N - row0) : kBlock);
+    const bool live = lane < kEpw && i < N;
+    const int wrows = (int)((N - wrow0) < kEpw ? (N - wrow0 > 0 ? N - wrow0 : 0) : kEpw);
     const float2* act = reinterpret_cast<const float2*>(io.act);
     const Mkt rst{p.rstv[0], p.rstv[1], p.rstv[2], p.rstv[3], BOOK ? p.book_rst : 0.0};
     // Every kernel argument of the prologue's addresses and of the step arithmetic,
@@ -870,8 +962,11 @@ __device__ __forceinline__ void step_body(const Params& pk, int64_t n_envs, cons
         e.put = unpack_hi(pk);
         e.cash = cash;
     }
+    // pv of the pre-step state; afterwards each step's pv (the reference carries
+    // portfolio_value_t_minus_1 the same way, hedging_env_v2.py:268)
+    double pv_last = live ? portfolio_value<BOOK>(p, e, pre) : 0.0;
     bool reset_any = false;
-    float* const orow = tile + threadIdx.x * kObs;
+    float* const orow = tile + (wave * kEpw + (lane < kEpw ? lane : 0)) * kObs;
     // step k of every env from market `post` (greeks + lag return `g`) with action ak:
     // state update, reward/done stores, the obs row into the wave's LDS tile, auto-reset
     auto step_part = [&](int k, const Mkt post, const float4 g, const float2 ak) {
@@ -879,11 +974,12 @@ __device__ __forceinline__ void step_body(const Params& pk, int64_t n_envs, cons
         bool term = false;
         if (live) {
             StepOut so;
-            step_env<BOOK>(p, e, pre, post, ak.x, ak.y, so);
+            step_env<BOOK, FAST>(p, e, pre, post, ak.x, ak.y, pv_last, so);
+            pv_last = so.pv;
             term = so.term;
             if (INFO) write_info(io.info, i, so, e, post, p.variant);
             float o[kObs];
-            make_obs(p, e, post, g, pre.S, pre.v, o);
+            make_obs<FAST>(p, e, post, g, pre.S, pre.v, o);
 #pragma unroll
             for (int c = 0; c < kObs; ++c) orow[c] = o[c];
             if (io.rew) ((GLOBAL float*)io.rew)[koff + i] = (float)so.reward;
@@ -920,10 +1016,7 @@ __device__ __forceinline__ void step_body(const Params& pk, int64_t n_envs, cons
         if (io.obs) {
             // LDS-staged 16-B stores: measured 6.45 vs 7.14 us/step against per-lane
             // 4-B stores of the 52-B rows (MI355X, 65,536 envs, graph mode)
-            const int wave = threadIdx.x >> 6;
-            const int wrows = rows - wave * 64 < 64 ? rows - wave * 64 : 64;
-            flush_obs_wave(tile + wave * 64 * kObs, io.obs + (int64_t)k * N * kObs, row0 + wave * 64, wrows,
-                           threadIdx.x & 63);
+            flush_obs_wave(tile + wave * kEpw * kObs, io.obs + (int64_t)k * N * kObs, wrow0, wrows, lane);
         }
     };
     if constexpr (!REPLAY && !SINGLE) {
@@ -933,7 +1026,9 @@ __device__ __forceinline__ void step_body(const Params& pk, int64_t n_envs, cons
         // stores were issued 4 steps earlier.  Every lane issues every load (clamped
         // index / step), so the wait counts are the same on every path.
         constexpr int D = kRolloutPrefetch;
-        const int64_t ic = live ? i : N - 1;
+        // dead lanes load a live lane's address of the same wave (no extra cache lines)
+        const int64_t icl = wrow0 + (lane % kEpw);
+        const int64_t ic = icl < N ? icl : N - 1;
         float2 ra[D];
         float4 rA[D], rB[D];
         double rC[D];
@@ -994,11 +1089,11 @@ __device__ __forceinline__ void step_body(const Params& pk, int64_t n_envs, cons
 }
 
 // Every step path: Params by value in the kernel arguments.
-template <int MODE, bool INFO, bool SINGLE, bool BOOK>
+template <int MODE, bool INFO, bool SINGLE, bool BOOK, bool FAST>
 __global__ __launch_bounds__(kBlock) void step_kernel(Params pk, State s, Io io, int k_steps, int slot0) {
     constexpr bool REPLAY = (MODE == HE_MODE_REPLAY);
-    step_body<MODE, INFO, SINGLE, BOOK>(pk, pk.n, REPLAY ? pk.rec : pk.tileA, REPLAY ? pk.recg : pk.tileB,
-                                        pk.tileC, s, io, k_steps, slot0);
+    step_body<MODE, INFO, SINGLE, BOOK, FAST>(pk, pk.n, REPLAY ? pk.rec : pk.tileA, REPLAY ? pk.recg : pk.tileB,
+                                              pk.tileC, s, io, k_steps, slot0);
 }
 
 // he_step without info: Params from a device-resident copy; the kernel arguments carry
@@ -1011,7 +1106,7 @@ struct StepIo {
     uint8_t* trunc;
     float* tobs;
 };
-template <int MODE, bool BOOK>
+template <int MODE, bool BOOK, bool FAST>
 __global__ __launch_bounds__(kBlock) void step1_kernel(const Params* __restrict__ pc, int64_t n, const float4* tA,
                                                        const float4* tB, const double* tC, State s, StepIo sio,
                                                        int slot0) {
@@ -1023,7 +1118,7 @@ __global__ __launch_bounds__(kBlock) void step1_kernel(const Params* __restrict_
     io.trunc = sio.trunc;
     io.tobs = sio.tobs;
     io.info = he_info{};
-    step_body<MODE, false, true, BOOK>(*pc, n, tA, tB, tC, s, io, 1, slot0);
+    step_body<MODE, false, true, BOOK, FAST>(*pc, n, tA, tB, tC, s, io, 1, slot0);
 }
 
 // Explicit reset of envs `ids` (NULL: all).  Generate: the market position of a
@@ -1268,6 +1363,9 @@ static void fill_params(he_env* env) {
     p.g_num_drift = ((float)r + 0.5f * powf(p.g_sigma, 2.0f)) * (float)T;
     p.g_sst = (double)p.g_sigma * sqrt(T);
     p.g_inv_sst = 1.0 / p.g_sst;
+    p.g_sst_f = (float)p.g_sst;
+    p.g_inv_sst_f = (float)p.g_inv_sst;
+    p.sqrt_tenor_f = (float)p.sqrt_tenor;
     p.h_kappa = c.heston_kappa;
     p.h_theta = c.heston_theta;
     p.h_xi = c.heston_xi;
@@ -1278,6 +1376,7 @@ static void fill_params(he_env* env) {
     p.T_f = (float)c.episode_length;
     p.inv_maxh_f = 1.0f / p.maxh_f;
     p.inv_T_f = 1.0f / p.T_f;
+    p.inv_252 = 1.0 / 252.0;
     p.M = c.market_block;
     p.tileA = p.tileB = nullptr;  // set per launch (tile_params)
     memcpy(p.rstv, env->rstv, sizeof(p.rstv));
@@ -1294,6 +1393,8 @@ static void fill_params(he_env* env) {
         p.s0s_const = 1;
         p.s0s_f = f;
         p.inv_s0s_f = 1.0f / f;
+        p.s0s_d = (double)f;
+        p.inv_s0s_d = 1.0 / (double)f;
     }
     p.rec = env->rec;
     p.recg = env->recg;
@@ -1423,10 +1524,10 @@ static void launch_reset(he_env* env, const int64_t* ids, int64_t count, float* 
                        env->cur, ids, count, obs, inf);
 }
 
-template <int MODE, bool BOOK>
+template <int MODE, bool BOOK, bool FAST>
 static void launch_step(he_env* env, const Params& p, const Io& io, bool info, int k, int slot0,
                         hipStream_t st) {
-    int64_t blocks = (env->cfg.n_envs + kBlock - 1) / kBlock;
+    int64_t blocks = (env->cfg.n_envs + kEpb - 1) / kEpb;
     if (k == 1 && !info) {
         constexpr bool REPLAY = (MODE == HE_MODE_REPLAY);
         const Params* pc = env->dparams + (REPLAY ? 0 : env->cur_buf);
@@ -1436,17 +1537,17 @@ static void launch_step(he_env* env, const Params& p, const Io& io, bool info, i
         if (env->ev_start) {
             hipEvent_t a = (hipEvent_t)env->ev_start, b = (hipEvent_t)env->ev_stop;
             env->ev_start = env->ev_stop = nullptr;
-            hipExtLaunchKernelGGL((step1_kernel<MODE, BOOK>), dim3((unsigned)blocks), dim3(kBlock), 0, st, a, b, 0,
+            hipExtLaunchKernelGGL((step1_kernel<MODE, BOOK, FAST>), dim3((unsigned)blocks), dim3(kBlock), 0, st, a, b, 0,
                                   pc, p.n, tA, tB, (const double*)p.tileC, env->s, sio, slot0);
             return;
         }
-        hipLaunchKernelGGL((step1_kernel<MODE, BOOK>), dim3((unsigned)blocks), dim3(kBlock), 0, st, pc, p.n, tA, tB,
+        hipLaunchKernelGGL((step1_kernel<MODE, BOOK, FAST>), dim3((unsigned)blocks), dim3(kBlock), 0, st, pc, p.n, tA, tB,
                            (const double*)p.tileC, env->s, sio, slot0);
         return;
     }
     void (*kern)(Params, State, Io, int, int);
-    if (k == 1) kern = info ? step_kernel<MODE, true, true, BOOK> : step_kernel<MODE, false, true, BOOK>;
-    else kern = info ? step_kernel<MODE, true, false, BOOK> : step_kernel<MODE, false, false, BOOK>;
+    if (k == 1) kern = info ? step_kernel<MODE, true, true, BOOK, false> : step_kernel<MODE, false, true, BOOK, FAST>;
+    else kern = info ? step_kernel<MODE, true, false, BOOK, false> : step_kernel<MODE, false, false, BOOK, FAST>;
     if (env->ev_start) {  // one-shot: bracket exactly this dispatch (hipExtLaunchKernelGGL)
         hipEvent_t a = (hipEvent_t)env->ev_start, b = (hipEvent_t)env->ev_stop;
         env->ev_start = env->ev_stop = nullptr;
@@ -1483,6 +1584,14 @@ static he_status advance_block(he_env* env, hipStream_t st, bool prefetch) {
     return HE_OK;
 }
 
+// The configuration the FAST step kernels are specialised for (generate modes).
+static bool fast_config(const he_env* env) {
+    const he_config& c = env->cfg;
+    return c.mode != HE_MODE_REPLAY && c.variant == 2 && c.loss_type != HE_LOSS_MSE && c.shares_to_hedge != 0 &&
+           c.record_metrics && c.max_contracts_held_per_type > 0 && c.episode_length > 0 &&
+           env->p.s0s_const && env->p.den_const;
+}
+
 static he_status launch_steps(he_env* env, Io io, bool info, int k_total, void* stream) {
     const he_config& c = env->cfg;
     if (c.mode == HE_MODE_REPLAY && !env->rec) return fail(env, HE_ESTATE, "no paths loaded (he_load_paths)");
@@ -1490,7 +1599,7 @@ static he_status launch_steps(he_env* env, Io io, bool info, int k_total, void* 
     DeviceGuard dg(c.device);
     hipStream_t st = (hipStream_t)stream;
     if (c.mode == HE_MODE_REPLAY) {
-        launch_step<HE_MODE_REPLAY, false>(env, env->p, io, info, k_total, 0, st);
+        launch_step<HE_MODE_REPLAY, false, false>(env, env->p, io, info, k_total, 0, st);
         HE_HIP(env, hipGetLastError());
         return HE_OK;
     }
@@ -1517,12 +1626,23 @@ static he_status launch_steps(he_env* env, Io io, bool info, int k_total, void* 
         if (io.term) sub.term = io.term + (int64_t)done * N;
         Params p = tile_params(env, env->cur_buf);
         const bool book = c.book_size > 0;
+        const bool fast = fast_config(env);
         if (c.mode == HE_MODE_GBM) {
-            if (book) launch_step<HE_MODE_GBM, true>(env, p, sub, info, k, env->block_pos, st);
-            else launch_step<HE_MODE_GBM, false>(env, p, sub, info, k, env->block_pos, st);
+            if (book) {
+                if (fast) launch_step<HE_MODE_GBM, true, true>(env, p, sub, info, k, env->block_pos, st);
+                else launch_step<HE_MODE_GBM, true, false>(env, p, sub, info, k, env->block_pos, st);
+            } else {
+                if (fast) launch_step<HE_MODE_GBM, false, true>(env, p, sub, info, k, env->block_pos, st);
+                else launch_step<HE_MODE_GBM, false, false>(env, p, sub, info, k, env->block_pos, st);
+            }
         } else {
-            if (book) launch_step<HE_MODE_HESTON, true>(env, p, sub, info, k, env->block_pos, st);
-            else launch_step<HE_MODE_HESTON, false>(env, p, sub, info, k, env->block_pos, st);
+            if (book) {
+                if (fast) launch_step<HE_MODE_HESTON, true, true>(env, p, sub, info, k, env->block_pos, st);
+                else launch_step<HE_MODE_HESTON, true, false>(env, p, sub, info, k, env->block_pos, st);
+            } else {
+                if (fast) launch_step<HE_MODE_HESTON, false, true>(env, p, sub, info, k, env->block_pos, st);
+                else launch_step<HE_MODE_HESTON, false, false>(env, p, sub, info, k, env->block_pos, st);
+            }
         }
         HE_HIP(env, hipGetLastError());
         env->block_pos += k;
