@@ -77,6 +77,15 @@ class HeConfig(ctypes.Structure):
     ]
 
 
+POLICIES = {"no_hedge": 0, "delta_every_step": 1, "delta_threshold": 2}
+
+# he_episode_record as a numpy structured dtype (64 B, include/hedge_env.h)
+import numpy as _np  # noqa: E402
+EPISODE_RECORD = _np.dtype([("env_id", "<i8"), ("length", "<i4"), ("reserved", "<i4"), ("reward_sum", "<f8"),
+                            ("pnl_sum", "<f8"), ("abs_pnl_sum", "<f8"), ("cost_sum", "<f8"),
+                            ("pnl_penalty_sum", "<f8"), ("cost_penalty_sum", "<f8")])
+assert EPISODE_RECORD.itemsize == 64
+
 _P = ctypes.c_void_p
 INFO_FIELDS = [
     ("step_pnl_total", "f8"), ("per_share_step_pnl", "f8"), ("raw_pnl_deviation_abs", "f8"),
@@ -102,7 +111,7 @@ EXPORTS = [
     "he_config_init", "he_create", "he_destroy", "he_last_error", "he_version", "he_load_paths",
     "he_seed", "he_reset", "he_step", "he_rollout", "he_num_envs", "he_episode_length",
     "he_num_episodes", "he_get_config", "he_state_size", "he_get_state", "he_set_state",
-    "he_pcg64_seed_state", "he_host_episode_draws", "he_host_philox", "he_host_div_by", "he_host_div_byf", "he_time_next_step",
+    "he_pcg64_seed_state", "he_host_episode_draws", "he_host_philox", "he_host_div_by", "he_host_div_byf", "he_time_next_step", "he_rollout_policy",
     "he_sync_market",
 ]
 
@@ -139,6 +148,7 @@ def load(path=LIB_PATH):
         "he_reset": (i32, [vp, vp, i64, vp, ctypes.POINTER(HeInfo), vp]),
         "he_step": (i32, [vp, vp, vp, vp, vp, vp, vp, ctypes.POINTER(HeInfo), vp]),
         "he_rollout": (i32, [vp, i32, vp, vp, vp, vp, vp]),
+        "he_rollout_policy": (i32, [vp, i32, i32, vp, vp, vp, vp, vp, i64, vp, vp]),
         "he_num_envs": (i64, [vp]),
         "he_episode_length": (i32, [vp]),
         "he_num_episodes": (i64, [vp]),

@@ -141,6 +141,8 @@ struct State {
     float* s0;         // replay initial_S0_for_episode; -1 encodes the python 1.0 substitution
     uint64_t* pcg;     // replay [4][N]: state_hi, state_lo, inc_hi, inc_lo
     uint32_t* pcgb;    // replay [2][N]: has_uint32, uinteger
+    double* acc;       // policy rollouts: [6][N] episode sums (reward, pnl, |ps|, tc, rpc, tcp)
+    uint32_t* acc_len; // policy rollouts: [N] episode length so far
 };
 
 // Generate-mode market position of every env: `cur` = after the last generated
@@ -155,6 +157,15 @@ struct Market {
     double* M;         // book: running max of S over the episode (barrier monitor)
 };
 
+// he_rollout_policy: device policy instead of an action input, episode records out
+struct PolIo {
+    int32_t policy;                 // he_policy
+    float* act_out;                 // [K][N][2] or NULL
+    he_episode_record* rec;         // [cap]
+    int64_t cap;
+    unsigned long long* count;
+};
+
 struct Io {
     const float* act;  // [K][N][2]
     float* obs;        // [K][N][13]
@@ -163,6 +174,8 @@ struct Io {
     uint8_t* trunc;    // [N]
     float* tobs;       // [N][13]
     he_info info;
+    PolIo pol;
+    bool pol_on;
 };
 
 struct Mkt {
@@ -608,6 +621,9 @@ __global__ __launch_bounds__(kMktEnvs * kMktLanes, HE_MKT_WAVES) void market_ker
     if (!advance_only && sub == 0 && live) {
         float v32 = HESTON ? (float)v0v : p.var_f;
         p.tileA[i] = make_float4((float)S0v, v32, C0v, P0v);
+        // greeks of the block start (the obs policy rollouts resume from); equal to
+        // the previous block's last slot, same function of the same (S, v)
+        p.tileB[i] = p.record_metrics ? greeks_fast<!HESTON>(p, (float)S0v, v32) : make_float4(0.f, 0.f, 0.f, 0.f);
         // slot 0 = the block start; at t0 in {0, T} the next step starts from the reset
         // market and reads book_rst instead
         if (BOOK)
@@ -662,6 +678,48 @@ struct StepOut {
 
 // hedging_env_v2.py:175-262 (v1: hedging_env.py:171-245).  pre/post: market before
 // and after the advance (post C/P already lagged on the terminal step).
+// ------------------------------------------------------------------ baseline policies
+// The action of `policy` on the env's current obs (o3, o4, o7, o9 = obs[3], obs[4],
+// obs[7], obs[9]) and positions, with the reference's dtype sequence.
+__device__ __forceinline__ float2 policy_action(const Params& p, int policy, int32_t call, int32_t put, float o3,
+                                                float o4, float cd, float pd) {
+    const float mt = p.mt_f;
+    if (policy == HE_POLICY_DELTA_EVERY_STEP) {
+        // baselines.py:77-103, all f32 (numpy f32 scalars with weak python ints/floats)
+        const float cur_call = o3 * p.maxh_f;                       // obs[3] * max_contracts_held
+        const float cur_put = o4 * p.maxh_f;
+        const float opt_delta = (cur_call * cd + cur_put * pd) * 100.0f;
+        const float total = (float)p.shares_d + opt_delta;          // shares_held_fixed + ...
+        const float target = -total;
+        float tc = 0.0f, tp = 0.0f;
+        if (fabsf(cd * 100.0f) > 0.1f) tc = target / (cd * 100.0f);
+        else if (fabsf(pd * 100.0f) > 0.1f) tp = target / (pd * 100.0f);
+        return make_float2(np_clipf(tc, -mt, mt), np_clipf(tp, -mt, mt));
+    }
+    if (policy == HE_POLICY_DELTA_THRESHOLD) {
+        // delta_and_nothing.py:122-163: np.int64 positions x f32 deltas -> f64
+        const double cur = ((double)call * (double)cd + (double)put * (double)pd) * 100.0;
+        const double need = -p.shares_d - cur;                      // target - current
+        const float thr = (0.5f * fabsf(cd)) * 100.0f;
+        if (fabs(need) < (double)thr) return make_float2(0.0f, 0.0f);
+        double rc = 0.0, rp = 0.0;
+        const double mtd = (double)p.mt;
+        if (need > 0.0) {
+            if (fabsf(cd) > 1e-6f) {
+                const double n = need / (double)(cd * 100.0f);
+                rc = n < -mtd ? -mtd : (n > mtd ? mtd : n);
+            }
+        } else if (need < 0.0) {
+            if (fabsf(pd) > 1e-6f) {
+                const double n = need / (double)(pd * 100.0f);
+                rp = n < -mtd ? -mtd : (n > mtd ? mtd : n);
+            }
+        }
+        return make_float2((float)rc, (float)rp);
+    }
+    return make_float2(0.0f, 0.0f);  // HE_POLICY_NO_HEDGE (baselines.py:74-75)
+}
+
 // portfolio value of the pre-step state (hedging_env_v2.py:233-236): the previous
 // step's pv, recomputed bit for bit (same operands, same order)
 template <bool BOOK>
@@ -872,7 +930,7 @@ __device__ __forceinline__ void env_reset_common(const Params& p, Env& e) {
 // SINGLE: the he_step instance (k_steps == 1 at compile time, straight-line code).
 // tA/tB: the market source, tile buffer {S,v,C,P} / greeks (generate) or the
 // replay table rec / recg.
-template <int MODE, bool INFO, bool SINGLE, bool BOOK, bool FAST>
+template <int MODE, bool INFO, bool SINGLE, bool BOOK, bool FAST, bool POL>
 __device__ __forceinline__ void step_body(const Params& pk, int64_t n_envs, const float4* tA, const float4* tB,
                                           const double* tC, State s, Io io, int k_steps_arg, int slot0) {
     constexpr bool REPLAY = (MODE == HE_MODE_REPLAY);
@@ -920,7 +978,7 @@ __device__ __forceinline__ void step_body(const Params& pk, int64_t n_envs, cons
         const uint32_t t0 = s_t[i];
         const uint32_t pk = s_pos[i];
         double cash = s_cash[i];
-        a = ld2(gact, i);
+        a = POL ? make_float2(0.0f, 0.0f) : ld2(gact, i);
         if (REPLAY) {
             const int32_t T = hot_i;
             const int32_t path = s_path[i];
@@ -965,17 +1023,73 @@ __device__ __forceinline__ void step_body(const Params& pk, int64_t n_envs, cons
     // pv of the pre-step state; afterwards each step's pv (the reference carries
     // portfolio_value_t_minus_1 the same way, hedging_env_v2.py:268)
     double pv_last = live ? portfolio_value<BOOK>(p, e, pre) : 0.0;
+    // policy rollouts: the current obs columns the policies read, and the episode sums
+    float pol_o3 = 0.0f, pol_o4 = 0.0f, pol_cd = 0.0f, pol_pd = 0.0f;
+    double acc[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+    uint32_t acc_len = 0;
+    if (POL && live) {
+        float4 gpre;
+        if (REPLAY) {
+            const uint32_t tt = e.t > (uint32_t)p.T ? (uint32_t)p.T : e.t;
+            gpre = tB[(int64_t)e.path * (p.T + 1) + tt];
+        } else {
+            gpre = (e.t == 0) ? make_float4(p.rstv[4 + 7], 0.0f, p.rstv[4 + 9], 0.0f) : tB[(int64_t)slot0 * N + i];
+        }
+        const bool met = p.record_metrics != 0;
+        pol_cd = met ? gpre.x : 0.0f;
+        pol_pd = met ? gpre.z : 0.0f;
+        pol_o3 = (p.maxh != 0) ? div_int_byf((float)e.call, p.maxh_f, p.inv_maxh_f) : 0.0f;
+        pol_o4 = (p.maxh != 0) ? div_int_byf((float)e.put, p.maxh_f, p.inv_maxh_f) : 0.0f;
+#pragma unroll
+        for (int c = 0; c < 6; ++c) acc[c] = s.acc[(int64_t)c * N + i];
+        acc_len = s.acc_len[i];
+    }
     bool reset_any = false;
     float* const orow = tile + (wave * kEpw + (lane < kEpw ? lane : 0)) * kObs;
     // step k of every env from market `post` (greeks + lag return `g`) with action ak:
     // state update, reward/done stores, the obs row into the wave's LDS tile, auto-reset
-    auto step_part = [&](int k, const Mkt post, const float4 g, const float2 ak) {
+    auto step_part = [&](int k, const Mkt post, const float4 g, float2 ak) {
         const int64_t koff = (int64_t)k * N;
         bool term = false;
         if (live) {
+            if (POL) {
+                ak = policy_action(p, io.pol.policy, e.call, e.put, pol_o3, pol_o4, pol_cd, pol_pd);
+                if (io.pol.act_out) {
+                    v2f av = {ak.x, ak.y};
+                    ((GLOBAL v2f*)io.pol.act_out)[koff + i] = av;
+                }
+            }
             StepOut so;
             step_env<BOOK, FAST>(p, e, pre, post, ak.x, ak.y, pv_last, so);
             pv_last = so.pv;
+            if (POL) {  // the reference evaluation loops' sums, in step order
+                acc[0] = acc[0] + so.reward;
+                acc[1] = acc[1] + so.pnl;
+                acc[2] = acc[2] + fabs(so.ps);
+                acc[3] = acc[3] + so.tc;
+                acc[4] = acc[4] + so.rpc;
+                acc[5] = acc[5] + so.tcp;
+                acc_len += 1u;
+                if (so.term) {
+                    const unsigned long long r = atomicAdd(io.pol.count, 1ull);
+                    if ((int64_t)r < io.pol.cap) {
+                        he_episode_record rec;
+                        rec.env_id = p.goff + i;
+                        rec.length = (int32_t)acc_len;
+                        rec.reserved = 0;
+                        rec.reward_sum = acc[0];
+                        rec.pnl_sum = acc[1];
+                        rec.abs_pnl_sum = acc[2];
+                        rec.cost_sum = acc[3];
+                        rec.pnl_penalty_sum = acc[4];
+                        rec.cost_penalty_sum = acc[5];
+                        io.pol.rec[r] = rec;
+                    }
+#pragma unroll
+                    for (int c = 0; c < 6; ++c) acc[c] = 0.0;
+                    acc_len = 0;
+                }
+            }
             term = so.term;
             if (INFO) write_info(io.info, i, so, e, post, p.variant);
             float o[kObs];
@@ -1010,6 +1124,12 @@ __device__ __forceinline__ void step_body(const Params& pk, int64_t n_envs, cons
                 reset_any = true;
             }
         }
+        if (POL && live) {  // the obs row this step returns (post-reset for done envs)
+            pol_o3 = orow[3];
+            pol_o4 = orow[4];
+            pol_cd = orow[7];
+            pol_pd = orow[9];
+        }
     };
     auto flush_part = [&](int k) {
         HE_TIM(3);
@@ -1039,7 +1159,7 @@ __device__ __forceinline__ void step_body(const Params& pk, int64_t n_envs, cons
         auto load = [&](int d, int kk) {
             kk = kk < k_steps ? kk : k_steps - 1;
             const int64_t r = (int64_t)(slot0 + kk + 1) * N + ic;
-            ra[d] = ld2(gact, (int64_t)kk * N + ic);
+            if (!POL) ra[d] = ld2(gact, (int64_t)kk * N + ic);
             rA[d] = ld4(mA, r);
             rB[d] = ld4(mB, r);
             if (BOOK) rC[d] = mC[r];
@@ -1068,7 +1188,7 @@ __device__ __forceinline__ void step_body(const Params& pk, int64_t n_envs, cons
             if (REPLAY && live && k + 1 < k_steps) {
                 const uint32_t tn = e.t + 1 > (uint32_t)p.T ? (uint32_t)p.T : e.t + 1;
                 const int64_t r = (int64_t)e.path * (p.T + 1) + tn;
-                a = act[(int64_t)(k + 1) * N + i];
+                if (!POL) a = act[(int64_t)(k + 1) * N + i];
                 postA = tA[r];
                 postB = tB[r];
             }
@@ -1083,17 +1203,22 @@ __device__ __forceinline__ void step_body(const Params& pk, int64_t n_envs, cons
             s.path[i] = e.path;
             s.s0[i] = e.s0_small ? -1.0f : e.s0;
         }
+        if (POL) {
+#pragma unroll
+            for (int c = 0; c < 6; ++c) s.acc[(int64_t)c * N + i] = acc[c];
+            s.acc_len[i] = acc_len;
+        }
         if (io.trunc) ((GLOBAL uint8_t*)io.trunc)[i] = 0;
     }
     HE_TIM(4);
 }
 
 // Every step path: Params by value in the kernel arguments.
-template <int MODE, bool INFO, bool SINGLE, bool BOOK, bool FAST>
+template <int MODE, bool INFO, bool SINGLE, bool BOOK, bool FAST, bool POL = false>
 __global__ __launch_bounds__(kBlock) void step_kernel(Params pk, State s, Io io, int k_steps, int slot0) {
     constexpr bool REPLAY = (MODE == HE_MODE_REPLAY);
-    step_body<MODE, INFO, SINGLE, BOOK, FAST>(pk, pk.n, REPLAY ? pk.rec : pk.tileA, REPLAY ? pk.recg : pk.tileB,
-                                              pk.tileC, s, io, k_steps, slot0);
+    step_body<MODE, INFO, SINGLE, BOOK, FAST, POL>(pk, pk.n, REPLAY ? pk.rec : pk.tileA,
+                                                   REPLAY ? pk.recg : pk.tileB, pk.tileC, s, io, k_steps, slot0);
 }
 
 // he_step without info: Params from a device-resident copy; the kernel arguments carry
@@ -1118,7 +1243,7 @@ __global__ __launch_bounds__(kBlock) void step1_kernel(const Params* __restrict_
     io.trunc = sio.trunc;
     io.tobs = sio.tobs;
     io.info = he_info{};
-    step_body<MODE, false, true, BOOK, FAST>(*pc, n, tA, tB, tC, s, io, 1, slot0);
+    step_body<MODE, false, true, BOOK, FAST, false>(*pc, n, tA, tB, tC, s, io, 1, slot0);
 }
 
 // Explicit reset of envs `ids` (NULL: all).  Generate: the market position of a
@@ -1159,6 +1284,9 @@ __global__ __launch_bounds__(kBlock) void reset_kernel(Params p, State s, Market
     s.t[i] = 0;
     s.pos[i] = 0;
     s.cash[i] = e.cash;
+#pragma unroll
+    for (int c = 0; c < 6; ++c) s.acc[(int64_t)c * p.n + i] = 0.0;
+    s.acc_len[i] = 0;
     if (obs) {
 #pragma unroll
         for (int c = 0; c < kObs; ++c) obs[i * kObs + c] = o[c];
@@ -1268,6 +1396,7 @@ struct he_env {
     float* rst = nullptr;     // reset market + obs (generate)
     Params* dparams = nullptr;  // device copies of tile_params(env, 0 / 1) for step1_kernel
     BookOpt* dbook = nullptr;   // liability book, device copy (generate modes)
+    unsigned long long* scratch_count = nullptr;  // he_rollout_policy without records
     double book_rst = 0.0;      // book value of the reset market (host copy)
     int64_t n_paths = 0;
     int32_t block_pos = 0;    // generate: next slot to consume; M = tile exhausted/invalid
@@ -1528,6 +1657,11 @@ template <int MODE, bool BOOK, bool FAST>
 static void launch_step(he_env* env, const Params& p, const Io& io, bool info, int k, int slot0,
                         hipStream_t st) {
     int64_t blocks = (env->cfg.n_envs + kEpb - 1) / kEpb;
+    if (io.pol_on) {  // policy rollouts (any k)
+        void (*pk)(Params, State, Io, int, int) = step_kernel<MODE, false, false, BOOK, FAST, true>;
+        hipLaunchKernelGGL(pk, dim3((unsigned)blocks), dim3(kBlock), 0, st, p, env->s, io, k, slot0);
+        return;
+    }
     if (k == 1 && !info) {
         constexpr bool REPLAY = (MODE == HE_MODE_REPLAY);
         const Params* pc = env->dparams + (REPLAY ? 0 : env->cur_buf);
@@ -1620,7 +1754,8 @@ static he_status launch_steps(he_env* env, Io io, bool info, int k_total, void* 
         int k = k_total - done;
         if (k > M - env->block_pos) k = M - env->block_pos;
         Io sub = io;
-        sub.act = io.act + (int64_t)done * N * 2;
+        if (io.act) sub.act = io.act + (int64_t)done * N * 2;
+        if (io.pol.act_out) sub.pol.act_out = io.pol.act_out + (int64_t)done * N * 2;
         if (io.obs) sub.obs = io.obs + (int64_t)done * N * kObs;
         if (io.rew) sub.rew = io.rew + (int64_t)done * N;
         if (io.term) sub.term = io.term + (int64_t)done * N;
@@ -1742,6 +1877,8 @@ he_status he_create(const he_config* cfg, he_env** out) {
     fs.push_back({(size_t)N * 4, (void**)&env->s.t, true});
     fs.push_back({(size_t)N * 4, (void**)&env->s.pos, true});
     fs.push_back({(size_t)N * 8, (void**)&env->s.cash, true});
+    fs.push_back({(size_t)N * 48, (void**)&env->s.acc, true});
+    fs.push_back({(size_t)N * 4, (void**)&env->s.acc_len, true});
     if (c.mode == HE_MODE_REPLAY) {
         fs.push_back({(size_t)N * 4, (void**)&env->s.path, true});
         fs.push_back({(size_t)N * 4, (void**)&env->s.s0, true});
@@ -1822,6 +1959,7 @@ he_status he_destroy(he_env* env) {
         if (env->rst) (void)hipFree(env->rst);
         if (env->dparams) (void)hipFree(env->dparams);
         if (env->dbook) (void)hipFree(env->dbook);
+        if (env->scratch_count) (void)hipFree(env->scratch_count);
         if (env->xs) {
             (void)hipStreamSynchronize(env->xs);
             (void)hipStreamDestroy(env->xs);
@@ -2046,6 +2184,34 @@ he_status he_rollout(he_env* env, int32_t k_steps, const float* actions, float* 
     io.obs = obs;
     io.rew = reward;
     io.term = terminated;
+    return launch_steps(env, io, false, k_steps, stream);
+}
+
+he_status he_rollout_policy(he_env* env, int32_t k_steps, int32_t policy, float* actions_out, float* obs,
+                            float* reward, uint8_t* terminated, he_episode_record* records, int64_t record_capacity,
+                            unsigned long long* record_count, void* stream) {
+    if (!env) return HE_EINVAL;
+    if (k_steps < 1) return fail(env, HE_EINVAL, "k_steps must be >= 1");
+    if (policy < HE_POLICY_NO_HEDGE || policy > HE_POLICY_DELTA_THRESHOLD)
+        return fail(env, HE_EINVAL, "policy %d is not an he_policy", policy);
+    if (!env->cfg.autoreset) return fail(env, HE_ESTATE, "he_rollout_policy needs autoreset=1");
+    if (record_capacity < 0 || (record_capacity > 0 && (!records || !record_count)))
+        return fail(env, HE_EINVAL, "records / record_count must be device pointers when record_capacity > 0");
+    Io io;
+    memset(&io, 0, sizeof(io));
+    io.obs = obs;
+    io.rew = reward;
+    io.term = terminated;
+    io.pol_on = true;
+    io.pol.policy = policy;
+    io.pol.act_out = actions_out;
+    io.pol.rec = records;
+    io.pol.cap = record_capacity;
+    io.pol.count = record_count;
+    if (record_capacity == 0) {  // no records: the atomic still needs a valid counter
+        if (!env->scratch_count) HE_HIP(env, hipMalloc(&env->scratch_count, sizeof(unsigned long long)));
+        io.pol.count = env->scratch_count;
+    }
     return launch_steps(env, io, false, k_steps, stream);
 }
 

@@ -334,6 +334,41 @@ class HedgingVecEnv:
         _lib.check(self.lib, self._h, st, "he_rollout")
         return obs, reward, terminated
 
+    def rollout_policy(self, k_steps, policy, actions_out=None, obs=None, reward=None, terminated=None,
+                       records=None, record_count=None):
+        """k_steps fused steps driven by a baseline policy evaluated on the device
+        (he_rollout_policy): "no_hedge" / "delta_every_step" (baselines.py:74-103) or
+        "delta_threshold" (delta_and_nothing.py:122-163).  Finished episodes append
+        he_episode_record rows to `records` (uint8 device tensor [cap, 64]) at the
+        index taken from `record_count` (int64 device tensor [1])."""
+        pol = _lib.POLICIES[policy] if isinstance(policy, str) else int(policy)
+        K = int(k_steps)
+        cap = 0 if records is None else int(records.shape[0])
+        st = self.lib.he_rollout_policy(self._h, K, pol, self._ptr(actions_out), self._ptr(obs), self._ptr(reward),
+                                        self._ptr(terminated), self._ptr(records), cap, self._ptr(record_count),
+                                        self.stream)
+        _lib.check(self.lib, self._h, st, "he_rollout_policy")
+
+    def evaluate_policy(self, policy, num_episodes, chunk=64, max_steps=None):
+        """Run `policy` until `num_episodes` episodes finished (all envs stepping) and
+        return the per-episode records as a numpy structured array (he_episode_record):
+        the device-side evaluate_baseline_policy (baselines.py:32-72)."""
+        dev = self.device
+        cap = int(num_episodes) + self.num_envs
+        recs = torch.zeros((cap, _lib.EPISODE_RECORD.itemsize), dtype=torch.uint8, device=dev)
+        cnt = torch.zeros(1, dtype=torch.int64, device=dev)
+        steps = 0
+        limit = max_steps if max_steps is not None else (num_episodes // self.num_envs + 2) * (self.episode_length + 1)
+        while True:
+            self.rollout_policy(chunk, policy, records=recs, record_count=cnt)
+            steps += chunk
+            done = int(cnt.item())
+            if done >= num_episodes or steps >= limit:
+                break
+        n = min(int(cnt.item()), cap)
+        out = recs[:n].cpu().numpy().view(_lib.EPISODE_RECORD).reshape(n)
+        return out[:num_episodes]
+
     # ------------------------------------------------------------------ attrs
     def _indices(self, indices):
         if indices is None:

@@ -28,6 +28,11 @@
  *                                                             hedging_env_v2.py:175-294
  *   he_rollout      <- SB3 collect_rollouts' inner loop over VecEnv.step for n_steps
  *                      (train_ppo_v2.py:48,222-230) with actions supplied up front
+ *   he_rollout_policy <- evaluate_baseline_policy(policy_no_hedge / policy_delta_every_step)
+ *                      (src/agents/baselines.py:32-103) and run_benchmark_strategy(
+ *                      delta_hedging_action_selector) (src/benchmark/delta_and_nothing.py:33-163):
+ *                      the policy evaluated on the device from each step's obs, fused
+ *                      into the step kernel, with per-episode sums recorded on device
  *   he_get_state / he_set_state  <- env pickling by SubprocVecEnv / checkpoints (no
  *                      reference equivalent; state is otherwise lost across processes)
  */
@@ -208,6 +213,41 @@ he_status he_step(he_env* env, const float* actions, float* obs, float* reward,
  * be NULL to skip).  Per-env state stays in registers across the K steps. */
 he_status he_rollout(he_env* env, int32_t k_steps, const float* actions, float* obs,
                      float* reward, uint8_t* terminated, void* stream);
+
+/* Baseline policies evaluated inside the fused step kernel (no action input). */
+typedef enum he_policy {
+    HE_POLICY_NO_HEDGE = 0,          /* baselines.py:74-75 / delta_and_nothing.py:117-119: [0, 0]      */
+    HE_POLICY_DELTA_EVERY_STEP = 1,  /* baselines.py:77-103: trade calls (else puts) to offset the
+                                        portfolio delta from obs[3,4,7,9]; f32 as the reference       */
+    HE_POLICY_DELTA_THRESHOLD = 2    /* delta_and_nothing.py:122-163: calls for positive, puts for
+                                        negative delta needed, skipped under half a call's delta      */
+} he_policy;
+
+/* One finished episode of a policy rollout: sums over its steps, in step order, of the
+ * f64 reward and info fields the reference evaluation loops accumulate
+ * (baselines.py:47-54, delta_and_nothing.py:80-86). */
+typedef struct he_episode_record {
+    int64_t env_id;          /* global env id                                          */
+    int32_t length;          /* steps                                                   */
+    int32_t reserved;
+    double reward_sum;       /* sum reward                                              */
+    double pnl_sum;          /* sum info["step_pnl_total"]                              */
+    double abs_pnl_sum;      /* sum info["raw_pnl_deviation_abs"] (|per-share P&L|)     */
+    double cost_sum;         /* sum info["transaction_costs_total"]                     */
+    double pnl_penalty_sum;  /* sum info["reward_pnl_component"]                        */
+    double cost_penalty_sum; /* sum info["transaction_cost_penalty"]                    */
+} he_episode_record;
+
+/* k_steps fused steps with actions from `policy` (he_policy) computed on the device from
+ * each env's current obs; autoreset semantics as he_rollout.  actions_out [K][N][2],
+ * obs/reward/terminated as he_rollout (each may be NULL).  Every episode that ends
+ * appends one he_episode_record at records[atomicAdd(record_count, 1)] while that
+ * index is < record_capacity (DEVICE pointers; the caller zeroes *record_count).
+ * Episode sums run from the last he_reset of the env and are kept by this entry point
+ * only (he_step / he_rollout do not update them). */
+he_status he_rollout_policy(he_env* env, int32_t k_steps, int32_t policy, float* actions_out, float* obs,
+                            float* reward, uint8_t* terminated, he_episode_record* records,
+                            int64_t record_capacity, unsigned long long* record_count, void* stream);
 
 /* Generate modes run market_kernel for block b+1 on a library-owned side stream
  * while the step kernels of block b run on `stream`.  he_sync_market makes `stream`

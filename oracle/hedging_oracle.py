@@ -224,6 +224,51 @@ def book_value(book, S, var, t, runmax, r, dt):
 
 
 # --------------------------------------------------------------------------- #
+# Baseline policies (restating src/agents/baselines.py:74-103 and              #
+# src/benchmark/delta_and_nothing.py:122-163 over a batch, same dtypes)        #
+# --------------------------------------------------------------------------- #
+POLICIES = ("no_hedge", "delta_every_step", "delta_threshold")
+
+
+def policy_actions(policy, obs, call, put, max_held, shares, mt):
+    """Actions [N,2] f32 of `policy` on the current obs [N,13] f32 and positions."""
+    obs = np.asarray(obs, np.float32)
+    n = obs.shape[0]
+    if policy == "no_hedge":
+        return np.zeros((n, 2), np.float32)
+    cd, pd = obs[:, 7], obs[:, 9]
+    f100 = np.float32(100)
+    with np.errstate(all="ignore"):
+        if policy == "delta_every_step":
+            # baselines.py:77-103: numpy f32 scalars with weak python ints / floats
+            cur_call = obs[:, 3] * np.float32(max_held)
+            cur_put = obs[:, 4] * np.float32(max_held)
+            opt = (cur_call * cd + cur_put * pd) * f100
+            target = -(np.float32(shares) + opt)
+            use_c = np.abs(cd * f100) > np.float32(0.1)
+            use_p = (~use_c) & (np.abs(pd * f100) > np.float32(0.1))
+            tc = np.where(use_c, target / (cd * f100), np.float32(0))
+            tp = np.where(use_p, target / (pd * f100), np.float32(0))
+            m = np.float32(mt)
+            return np.stack([np.clip(tc, -m, m), np.clip(tp, -m, m)], axis=1).astype(np.float32)
+        if policy == "delta_threshold":
+            # delta_and_nothing.py:122-163: np.int64 positions x f32 deltas -> f64
+            cur = (np.asarray(call, np.int64) * cd.astype(np.float64)
+                   + np.asarray(put, np.int64) * pd.astype(np.float64)) * 100
+            need = -shares - cur
+            thr = (np.float32(0.5) * np.abs(cd)) * f100
+            skip = np.abs(need) < thr.astype(np.float64)
+            rc = np.where((need > 0) & (np.abs(cd) > np.float32(1e-6)),
+                          np.clip(need / (cd * f100).astype(np.float64), -mt, mt), 0.0)
+            rp = np.where((need < 0) & (np.abs(pd) > np.float32(1e-6)),
+                          np.clip(need / (pd * f100).astype(np.float64), -mt, mt), 0.0)
+            rc = np.where(skip, 0.0, rc)
+            rp = np.where(skip, 0.0, rp)
+            return np.stack([rc, rp], axis=1).astype(np.float32)
+    raise ValueError(policy)
+
+
+# --------------------------------------------------------------------------- #
 # The env batch                                                               #
 # --------------------------------------------------------------------------- #
 class OracleVecEnv:
@@ -366,7 +411,28 @@ class OracleVecEnv:
         mask = np.zeros(self.n, bool)
         mask[ids] = True
         self._reset_mask(mask)
-        return self._obs()[ids]
+        obs = self._obs()
+        self.last_obs = obs.copy()
+        self.ep_sums = np.zeros((self.n, 6))
+        self.ep_len = np.zeros(self.n, np.int64)
+        return obs[ids]
+
+    def step_policy(self, policy):
+        """One step with actions from a baseline policy on the current obs; returns the
+        step outputs plus the actions and the records (env, length, 6 sums) of the
+        episodes that ended (in env order)."""
+        a = policy_actions(policy, self.last_obs, self.call, self.put, self.max_held, self.shares, self.mt)
+        obs, rew, term, tobs, info = self.step(a)
+        vals = (rew, info["step_pnl_total"], info["raw_pnl_deviation_abs"], info["transaction_costs_total"],
+                info["reward_pnl_component"], info["transaction_cost_penalty"])
+        for c, v in enumerate(vals):
+            self.ep_sums[:, c] = self.ep_sums[:, c] + v
+        self.ep_len += 1
+        done = np.nonzero(term)[0]
+        recs = [(int(i), int(self.ep_len[i]), *self.ep_sums[i]) for i in done]
+        self.ep_sums[term] = 0.0
+        self.ep_len[term] = 0
+        return a, obs, rew, term, info, recs
 
     def seed_envs_at(self, ids, seeds):
         for i, s in zip(ids, seeds):
@@ -573,6 +639,7 @@ class OracleVecEnv:
             terminal_obs[term] = obs[term]
             self._reset_mask(term)
             obs[term] = self._obs()[term]
+        self.last_obs = obs.copy()
         return obs, reward, term, terminal_obs, info
 
 

@@ -289,3 +289,109 @@ def test_book_rollout_equals_repeated_steps_and_checkpoint():
     assert torch.equal(o1, o2) and torch.equal(r1, r2)
     for e in (a, b, c):
         e.close()
+
+
+G10 = sorted(f for f in os.listdir(GOLDEN) if f.startswith("g10_policy_"))
+
+
+def _episode_sums_from_golden(d):
+    """Per-env episode sums in step order from the golden infos (the reference
+    evaluation loops' accumulation, baselines.py:47-54 / delta_and_nothing.py:80-86)."""
+    n, S = int(d["n_envs"]), int(d["n_steps"])
+    acc = np.zeros((n, 6))
+    ln = np.zeros(n, np.int64)
+    out = {i: [] for i in range(n)}
+    cols = [d["reward"], d["info_step_pnl_total"], d["info_raw_pnl_deviation_abs"],
+            d["info_transaction_costs_total"], d["info_reward_pnl_component"], d["info_transaction_cost_penalty"]]
+    for s in range(S):
+        for c in range(6):
+            acc[:, c] = acc[:, c] + cols[c][s]
+        ln += 1
+        for i in np.nonzero(d["terminated"][s])[0]:
+            out[int(i)].append((int(ln[i]), *acc[i]))
+            acc[i] = 0.0
+            ln[i] = 0
+    return out
+
+
+@pytest.mark.parametrize("fname", G10)
+def test_policy_rollout_matches_reference_golden(fname):
+    """he_rollout_policy (policy evaluated in the step kernel) replays the reference's
+    own baseline-policy runs: actions, rewards, done flags and obs, and the device
+    episode records equal the reference loops' per-episode sums."""
+    import json
+    from cantorrl_amd import _lib
+    from cantorrl_amd.vec_env import HedgingVecEnv
+    z = np.load(os.path.join(GOLDEN, fname), allow_pickle=False)
+    d = {k: z[k] for k in z.files}
+    cfg = json.loads(str(d["config_json"]))
+    cfg.pop("profile_print_interval", None)
+    n, S = int(d["n_envs"]), int(d["n_steps"])
+    env = HedgingVecEnv(n, tables=(d["paths"], d["volatilities"], d["call_prices_atm"], d["put_prices_atm"]),
+                        variant=1, info_keys=(), return_numpy=False, **cfg)
+    env.seed_envs([int(d["seed_base"]) + i for i in range(n)])
+    compare_obs(env.reset_tensors().cpu().numpy(), d["reset_obs"], "reset_obs")
+    recs = torch.zeros((4 * n, 64), dtype=torch.uint8, device="cuda")
+    cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+    K = 37  # chunks that do not divide the episode length
+    for s0 in range(0, S, K):
+        k = min(K, S - s0)
+        a = torch.empty((k, n, 2), device="cuda")
+        o = torch.empty((k, n, 13), device="cuda")
+        r = torch.empty((k, n), device="cuda")
+        t = torch.empty((k, n), dtype=torch.uint8, device="cuda")
+        env.rollout_policy(k, str(d["policy"]), a, o, r, t, recs, cnt)
+        torch.cuda.synchronize()
+        # actions read obs[7]/obs[9]: the greeks carry OBS_RTOL (f32 log: ocml vs NumPy's
+        # SIMD log, which is not correctly rounded), amplified by the delta offset's
+        # cancellation; the integer trades and everything after them stay exact
+        assert_same(a.cpu().numpy(), d["actions"][s0:s0 + k], f"actions[{s0}:]", rtol=1e-4, atol=1e-6)
+        assert_same(t.cpu().numpy().astype(bool), d["terminated"][s0:s0 + k], f"terminated[{s0}:]")
+        assert_same(r.cpu().numpy(), d["reward"][s0:s0 + k].astype(np.float32), f"reward[{s0}:]")
+        compare_obs(o.cpu().numpy(), d["obs"][s0:s0 + k], f"obs[{s0}:]")
+    m = int(cnt.item())
+    got = recs[:m].cpu().numpy().view(_lib.EPISODE_RECORD).reshape(m)
+    exp = _episode_sums_from_golden(d)
+    assert m == sum(len(v) for v in exp.values())
+    for i in range(n):
+        mine = got[got["env_id"] == i]  # per env in finishing order (atomic index grows with time)
+        assert len(mine) == len(exp[i])
+        for rec, e in zip(mine, exp[i]):
+            assert rec["length"] == e[0]
+            for c, key in enumerate(("reward_sum", "pnl_sum", "abs_pnl_sum", "cost_sum", "pnl_penalty_sum",
+                                     "cost_penalty_sum")):
+                assert rec[key] == e[1 + c], (fname, i, key, rec[key], e[1 + c])
+    env.close()
+
+
+@pytest.mark.parametrize("policy", ["delta_every_step", "delta_threshold"])
+def test_policy_rollout_generate_equals_host_policy_steps(policy):
+    """Generate mode: the fused device policy takes exactly the actions the host-side
+    restatement computes from the env's own obs (he_step loop), step for step."""
+    from cantorrl_amd.vec_env import HedgingVecEnv
+    from oracle.hedging_oracle import policy_actions
+    n, K = 512, 90
+    gen = dict(episode_length=40)
+    kw = dict(loss_type="abs", pnl_penalty_weight=0.001, lambda_cost=0.0001, theta_weight=0.0002, slippage_bps=1.0)
+    a = HedgingVecEnv(n, mode="gbm", generate=gen, seed=8, return_numpy=False,
+                      info_keys=("call_contracts", "put_contracts"), **kw)
+    b = HedgingVecEnv(n, mode="gbm", generate=gen, seed=8, return_numpy=False, info_keys=(), **kw)
+    obs = a.reset_tensors().cpu().numpy().copy()
+    b.reset_tensors()
+    call = np.zeros(n, np.int64)
+    put = np.zeros(n, np.int64)
+    acts = torch.empty((K, n, 2), device="cuda")
+    o_r = torch.empty((K, n, 13), device="cuda")
+    b.rollout_policy(K, policy, acts, o_r)
+    torch.cuda.synchronize()
+    for k in range(K):
+        act = policy_actions(policy, obs, call, put, 200, 10000, 15)
+        assert_same(acts[k].cpu().numpy(), act, f"actions[{k}]")
+        o, _, t, _ = a.step_tensors(torch.from_numpy(act).cuda())
+        obs = o.cpu().numpy().copy()
+        assert_same(o_r[k].cpu().numpy(), obs, f"obs[{k}]")
+        done = t.cpu().numpy().astype(bool)  # info positions are pre-reset: a reset env holds 0
+        call = np.where(done, 0, a.info_tensor("call_contracts").cpu().numpy().astype(np.int64))
+        put = np.where(done, 0, a.info_tensor("put_contracts").cpu().numpy().astype(np.int64))
+    a.close()
+    b.close()
