@@ -83,8 +83,9 @@ POLICIES = {"no_hedge": 0, "delta_every_step": 1, "delta_threshold": 2}
 import numpy as _np  # noqa: E402
 EPISODE_RECORD = _np.dtype([("env_id", "<i8"), ("length", "<i4"), ("reserved", "<i4"), ("reward_sum", "<f8"),
                             ("pnl_sum", "<f8"), ("abs_pnl_sum", "<f8"), ("cost_sum", "<f8"),
-                            ("pnl_penalty_sum", "<f8"), ("cost_penalty_sum", "<f8")])
-assert EPISODE_RECORD.itemsize == 64
+                            ("pnl_penalty_sum", "<f8"), ("cost_penalty_sum", "<f8"),
+                            ("per_share_pnl_sum", "<f8"), ("reserved2", "<f8")])
+assert EPISODE_RECORD.itemsize == 80
 
 _P = ctypes.c_void_p
 INFO_FIELDS = [

@@ -141,7 +141,7 @@ struct State {
     float* s0;         // replay initial_S0_for_episode; -1 encodes the python 1.0 substitution
     uint64_t* pcg;     // replay [4][N]: state_hi, state_lo, inc_hi, inc_lo
     uint32_t* pcgb;    // replay [2][N]: has_uint32, uinteger
-    double* acc;       // policy rollouts: [6][N] episode sums (reward, pnl, |ps|, tc, rpc, tcp)
+    double* acc;       // policy rollouts: [7][N] episode sums (reward, pnl, |ps|, tc, rpc, tcp, ps)
     uint32_t* acc_len; // policy rollouts: [N] episode length so far
 };
 
@@ -1025,7 +1025,7 @@ __device__ __forceinline__ void step_body(const Params& pk, int64_t n_envs, cons
     double pv_last = live ? portfolio_value<BOOK>(p, e, pre) : 0.0;
     // policy rollouts: the current obs columns the policies read, and the episode sums
     float pol_o3 = 0.0f, pol_o4 = 0.0f, pol_cd = 0.0f, pol_pd = 0.0f;
-    double acc[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+    double acc[7] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
     uint32_t acc_len = 0;
     if (POL && live) {
         float4 gpre;
@@ -1041,7 +1041,7 @@ __device__ __forceinline__ void step_body(const Params& pk, int64_t n_envs, cons
         pol_o3 = (p.maxh != 0) ? div_int_byf((float)e.call, p.maxh_f, p.inv_maxh_f) : 0.0f;
         pol_o4 = (p.maxh != 0) ? div_int_byf((float)e.put, p.maxh_f, p.inv_maxh_f) : 0.0f;
 #pragma unroll
-        for (int c = 0; c < 6; ++c) acc[c] = s.acc[(int64_t)c * N + i];
+        for (int c = 0; c < 7; ++c) acc[c] = s.acc[(int64_t)c * N + i];
         acc_len = s.acc_len[i];
     }
     bool reset_any = false;
@@ -1069,6 +1069,7 @@ __device__ __forceinline__ void step_body(const Params& pk, int64_t n_envs, cons
                 acc[3] = acc[3] + so.tc;
                 acc[4] = acc[4] + so.rpc;
                 acc[5] = acc[5] + so.tcp;
+                acc[6] = acc[6] + so.ps;
                 acc_len += 1u;
                 if (so.term) {
                     const unsigned long long r = atomicAdd(io.pol.count, 1ull);
@@ -1083,10 +1084,12 @@ __device__ __forceinline__ void step_body(const Params& pk, int64_t n_envs, cons
                         rec.cost_sum = acc[3];
                         rec.pnl_penalty_sum = acc[4];
                         rec.cost_penalty_sum = acc[5];
+                        rec.per_share_pnl_sum = acc[6];
+                        rec.reserved2 = 0.0;
                         io.pol.rec[r] = rec;
                     }
 #pragma unroll
-                    for (int c = 0; c < 6; ++c) acc[c] = 0.0;
+                    for (int c = 0; c < 7; ++c) acc[c] = 0.0;
                     acc_len = 0;
                 }
             }
@@ -1205,7 +1208,7 @@ __device__ __forceinline__ void step_body(const Params& pk, int64_t n_envs, cons
         }
         if (POL) {
 #pragma unroll
-            for (int c = 0; c < 6; ++c) s.acc[(int64_t)c * N + i] = acc[c];
+            for (int c = 0; c < 7; ++c) s.acc[(int64_t)c * N + i] = acc[c];
             s.acc_len[i] = acc_len;
         }
         if (io.trunc) ((GLOBAL uint8_t*)io.trunc)[i] = 0;
@@ -1285,7 +1288,7 @@ __global__ __launch_bounds__(kBlock) void reset_kernel(Params p, State s, Market
     s.pos[i] = 0;
     s.cash[i] = e.cash;
 #pragma unroll
-    for (int c = 0; c < 6; ++c) s.acc[(int64_t)c * p.n + i] = 0.0;
+    for (int c = 0; c < 7; ++c) s.acc[(int64_t)c * p.n + i] = 0.0;
     s.acc_len[i] = 0;
     if (obs) {
 #pragma unroll
@@ -1877,7 +1880,7 @@ he_status he_create(const he_config* cfg, he_env** out) {
     fs.push_back({(size_t)N * 4, (void**)&env->s.t, true});
     fs.push_back({(size_t)N * 4, (void**)&env->s.pos, true});
     fs.push_back({(size_t)N * 8, (void**)&env->s.cash, true});
-    fs.push_back({(size_t)N * 48, (void**)&env->s.acc, true});
+    fs.push_back({(size_t)N * 56, (void**)&env->s.acc, true});
     fs.push_back({(size_t)N * 4, (void**)&env->s.acc_len, true});
     if (c.mode == HE_MODE_REPLAY) {
         fs.push_back({(size_t)N * 4, (void**)&env->s.path, true});

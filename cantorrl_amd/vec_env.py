@@ -339,7 +339,7 @@ class HedgingVecEnv:
         """k_steps fused steps driven by a baseline policy evaluated on the device
         (he_rollout_policy): "no_hedge" / "delta_every_step" (baselines.py:74-103) or
         "delta_threshold" (delta_and_nothing.py:122-163).  Finished episodes append
-        he_episode_record rows to `records` (uint8 device tensor [cap, 64]) at the
+        he_episode_record rows to `records` (uint8 device tensor [cap, 80]) at the
         index taken from `record_count` (int64 device tensor [1])."""
         pol = _lib.POLICIES[policy] if isinstance(policy, str) else int(policy)
         K = int(k_steps)

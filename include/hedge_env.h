@@ -236,6 +236,8 @@ typedef struct he_episode_record {
     double cost_sum;         /* sum info["transaction_costs_total"]                     */
     double pnl_penalty_sum;  /* sum info["reward_pnl_component"]                        */
     double cost_penalty_sum; /* sum info["transaction_cost_penalty"]                    */
+    double per_share_pnl_sum;/* sum info["per_share_step_pnl"] (train_ppo_v2.py:484)    */
+    double reserved2;
 } he_episode_record;
 
 /* k_steps fused steps with actions from `policy` (he_policy) computed on the device from

@@ -298,13 +298,14 @@ def _episode_sums_from_golden(d):
     """Per-env episode sums in step order from the golden infos (the reference
     evaluation loops' accumulation, baselines.py:47-54 / delta_and_nothing.py:80-86)."""
     n, S = int(d["n_envs"]), int(d["n_steps"])
-    acc = np.zeros((n, 6))
+    acc = np.zeros((n, 7))
     ln = np.zeros(n, np.int64)
     out = {i: [] for i in range(n)}
     cols = [d["reward"], d["info_step_pnl_total"], d["info_raw_pnl_deviation_abs"],
-            d["info_transaction_costs_total"], d["info_reward_pnl_component"], d["info_transaction_cost_penalty"]]
+            d["info_transaction_costs_total"], d["info_reward_pnl_component"], d["info_transaction_cost_penalty"],
+            d["info_per_share_step_pnl"]]
     for s in range(S):
-        for c in range(6):
+        for c in range(7):
             acc[:, c] = acc[:, c] + cols[c][s]
         ln += 1
         for i in np.nonzero(d["terminated"][s])[0]:
@@ -331,7 +332,7 @@ def test_policy_rollout_matches_reference_golden(fname):
                         variant=1, info_keys=(), return_numpy=False, **cfg)
     env.seed_envs([int(d["seed_base"]) + i for i in range(n)])
     compare_obs(env.reset_tensors().cpu().numpy(), d["reset_obs"], "reset_obs")
-    recs = torch.zeros((4 * n, 64), dtype=torch.uint8, device="cuda")
+    recs = torch.zeros((4 * n, 80), dtype=torch.uint8, device="cuda")
     cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
     K = 37  # chunks that do not divide the episode length
     for s0 in range(0, S, K):
@@ -359,7 +360,7 @@ def test_policy_rollout_matches_reference_golden(fname):
         for rec, e in zip(mine, exp[i]):
             assert rec["length"] == e[0]
             for c, key in enumerate(("reward_sum", "pnl_sum", "abs_pnl_sum", "cost_sum", "pnl_penalty_sum",
-                                     "cost_penalty_sum")):
+                                     "cost_penalty_sum", "per_share_pnl_sum")):
                 assert rec[key] == e[1 + c], (fname, i, key, rec[key], e[1 + c])
     env.close()
 

@@ -37,3 +37,39 @@ def test_oracle_policy_rollout_matches_reference(fname):
         for k in ("step_pnl_total", "raw_pnl_deviation_abs", "transaction_costs_total", "call_contracts"):
             assert_same(np.asarray(info[k]).astype(np.float64), d["info_" + k][s], f"{k}[{s}]")
         assert_same(obs, d["obs"][s], f"obs[{s}]")
+
+
+def test_evaluation_statistics_match_reference_reductions():
+    """baselines.py:56-72 and train_ppo_v2.py:515-531 reductions over records built
+    from a golden policy run (episode sums in step order)."""
+    from cantorrl_amd import _lib
+    from cantorrl_amd.evaluation import baseline_statistics, train_eval_statistics
+    d = load("g10_policy_delta_every_step.npz")
+    n, S = int(d["n_envs"]), int(d["n_steps"])
+    recs, abs_sum, cost_sum, ps_sum, ln = [], np.zeros(n), np.zeros(n), np.zeros(n), np.zeros(n, np.int64)
+    ep_abs, ep_cost, ep_ps = [], [], []
+    for s in range(S):
+        abs_sum += d["info_raw_pnl_deviation_abs"][s]
+        cost_sum += d["info_transaction_costs_total"][s]
+        ps_sum += d["info_per_share_step_pnl"][s]
+        ln += 1
+        for i in np.nonzero(d["terminated"][s])[0]:
+            r = np.zeros(1, _lib.EPISODE_RECORD)
+            r["env_id"], r["length"], r["abs_pnl_sum"], r["cost_sum"], r["per_share_pnl_sum"] = \
+                i, ln[i], abs_sum[i], cost_sum[i], ps_sum[i]
+            recs.append(r)
+            ep_abs.append(abs_sum[i] / ln[i])
+            ep_cost.append(cost_sum[i] / ln[i])
+            ep_ps.append(ps_sum[i])
+            abs_sum[i] = cost_sum[i] = ps_sum[i] = 0.0
+            ln[i] = 0
+    recs = np.concatenate(recs)
+    b = baseline_statistics(recs)
+    assert b["mean_abs_pnl"] == np.mean(ep_abs) and b["mean_cost"] == np.mean(ep_cost)
+    assert b["std_abs_pnl"] == np.std(ep_abs)
+    T = 252
+    t = train_eval_statistics(recs, T)
+    per = [abs(x) / T for x in ep_ps]
+    assert t["mean_abs_pnl"] == np.mean(per) and t["std_abs_pnl"] == np.std(per)
+    srt = sorted(per)
+    assert t["cvar95_abs_pnl"] == np.mean(srt[int(0.95 * len(srt)):])
