@@ -112,7 +112,7 @@ EXPORTS = [
     "he_config_init", "he_create", "he_destroy", "he_last_error", "he_version", "he_load_paths",
     "he_seed", "he_reset", "he_step", "he_rollout", "he_num_envs", "he_episode_length",
     "he_num_episodes", "he_get_config", "he_state_size", "he_get_state", "he_set_state",
-    "he_pcg64_seed_state", "he_host_episode_draws", "he_host_philox", "he_host_div_by", "he_host_div_byf", "he_time_next_step", "he_rollout_policy",
+    "he_pcg64_seed_state", "he_host_episode_draws", "he_host_philox", "he_host_div_by", "he_host_div_byf", "he_time_next_step", "he_rollout_policy", "he_host_box_muller",
     "he_sync_market",
 ]
 
@@ -162,6 +162,7 @@ def load(path=LIB_PATH):
         "he_host_philox": (i32, [u64, u64, u64, ctypes.POINTER(ctypes.c_uint32 * 4)]),
         "he_host_div_by": (i32, [ctypes.c_void_p, i64, ctypes.c_double, ctypes.c_void_p]),
         "he_host_div_byf": (i32, [ctypes.c_void_p, i64, ctypes.c_float, ctypes.c_void_p]),
+        "he_host_box_muller": (i32, [ctypes.c_void_p, ctypes.c_void_p, i64, ctypes.c_void_p, ctypes.c_void_p]),
         "he_time_next_step": (i32, [vp, vp, vp]),
         "he_sync_market": (i32, [vp, vp]),
     }
@@ -223,3 +224,16 @@ def host_div_byf(a, b):
     out = np.empty_like(a)
     check(lib, None, lib.he_host_div_byf(a.ctypes.data, a.size, float(b), out.ctypes.data), "he_host_div_byf")
     return out
+
+
+def host_box_muller(u1, u2):
+    """Host build of the generate-mode Box-Muller pair, for tests."""
+    import numpy as np
+    lib = load()
+    u1 = np.ascontiguousarray(u1, np.float64)
+    u2 = np.ascontiguousarray(u2, np.float64)
+    z1 = np.empty_like(u1)
+    z2 = np.empty_like(u1)
+    check(lib, None, lib.he_host_box_muller(u1.ctypes.data, u2.ctypes.data, u1.size, z1.ctypes.data, z2.ctypes.data),
+          "he_host_box_muller")
+    return z1, z2

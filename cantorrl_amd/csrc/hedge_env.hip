@@ -288,9 +288,12 @@ __device__ __forceinline__ float4 greeks_fast(const Params& p, float S, float v)
             } else {
                 d1 = CONST_VAR ? num * p.g_inv_sst_f : num * __builtin_amdgcn_rcpf(sstf);
             }
+            // N(d1) = erfc(-x)/2 and N(d1) - 1 = -erfc(x)/2: evaluate erfc at |x| (the
+            // small tail, accurate) and take the other as 1 - tail (>= 1/2, no cancellation)
             const float x = d1 * 0.70710678118654752f;
-            cd = 0.5f * erfcf(-x);
-            pd = -0.5f * erfcf(x);
+            const float tail = 0.5f * erfcf(fabsf(x));
+            cd = (x >= 0.0f) ? 1.0f - tail : tail;
+            pd = (x >= 0.0f) ? -tail : tail - 1.0f;
             const float gd = S * sstf;
             gam = (fabsf(gd) < 1e-9f) ? 0.0f
                                       : (expf(-0.5f * (d1 * d1)) * 0.398942280401432678f) * __builtin_amdgcn_rcpf(gd);
@@ -437,13 +440,7 @@ __device__ __forceinline__ double book_value(const Params& p, double S, double v
 __device__ __forceinline__ void normals(const Params& p, int64_t gid, uint64_t n, double* z1, double* z2) {
     u32x4 ctr = {(uint32_t)n, (uint32_t)(n >> 32), (uint32_t)gid, (uint32_t)((uint64_t)gid >> 32)};
     u32x4 x = philox4x32_10(ctr, p.key0, p.key1);
-    double u1 = u01(x.x, x.y), u2 = u01(x.z, x.w);
-    double rad = sqrt(-2.0 * log(u1));
-    double ang = 6.283185307179586 * u2;
-    double sn, cs;
-    sincos(ang, &sn, &cs);
-    *z1 = rad * cs;
-    *z2 = rad * sn;
+    box_muller(u01(x.x, x.y), u01(x.z, x.w), z1, z2);
 }
 
 // ------------------------------------------------------------------ market kernel
@@ -577,9 +574,12 @@ __global__ __launch_bounds__(kMktEnvs * kMktLanes, HE_MKT_WAVES) void market_ker
     __syncthreads();
     // phase 3 (time-parallel): marks + greeks of every slot
     const int64_t N = p.n;
-    for (int j = 1 + sub; j <= nsteps; j += kMktLanes) {
+    // episode step of slot j: (t0m + j - 1) % T + 1, stepped by kMktLanes without a
+    // divide per slot
+    uint32_t tj = (t0m + (uint32_t)sub) % T + 1u;  // 1..T
+    const uint32_t tstep = (uint32_t)kMktLanes % T;
+    for (int j = 1 + sub; j <= nsteps; j += kMktLanes, tj += tstep, tj = (tj > T) ? tj - T : tj) {
         if (!live) break;
-        uint32_t tj = (t0m + (uint32_t)(j - 1)) % T + 1u;  // 1..T
         double S64 = shS[lane][j];
         double v64 = HESTON ? shV[lane][j] : p.var;
         float C, P;
@@ -1586,23 +1586,34 @@ static Params tile_params(const he_env* env, int b) {
     return p;
 }
 
+// A market_kernel launched beside step kernels (the side-stream prefetch) is held to
+// 2 workgroups = 2 waves per SIMD by padding its LDS past a third of the CU's 160 KB:
+// at 3 waves/SIMD it finishes sooner alone (74 vs 91 us per 64 steps at 65,536 envs)
+// but takes issue slots from the latency-bound rollout wave (2.72 vs 2.27 us/step).
+constexpr size_t kCuLds = 160 * 1024;
+constexpr size_t kMktWgLds = kMktEnvs * (kMaxBlock + 1) * sizeof(double);  // one shS-sized array
+
 template <int MODE, bool BOOK>
-static void launch_market(he_env* env, int32_t advance_only, int buf, hipStream_t st) {
+static void launch_market(he_env* env, int32_t advance_only, int buf, hipStream_t st, bool beside_steps) {
     int64_t blocks = (env->cfg.n_envs + kMktEnvs - 1) / kMktEnvs;
-    hipLaunchKernelGGL((market_kernel<MODE, BOOK>), dim3((unsigned)blocks), dim3(kMktEnvs * kMktLanes), 0, st,
+    const size_t stat = kMktWgLds * (1 + (MODE == HE_MODE_HESTON ? 1 : 0) + (BOOK ? 1 : 0));
+    const size_t cap = kCuLds / 3 + 1024;  // > 1/3 of the CU: at most 2 workgroups
+    const size_t pad = (beside_steps && stat < cap) ? cap - stat : 0;
+    hipLaunchKernelGGL((market_kernel<MODE, BOOK>), dim3((unsigned)blocks), dim3(kMktEnvs * kMktLanes), pad, st,
                        tile_params(env, buf), env->cur, env->bak[buf], advance_only);
 }
 
 // generate the block that follows `cur` into tile buffer `buf` (advance_only = 0),
 // or rewind `cur` to `advance_only` steps past the start of buffer `buf`'s block.
-static he_status market(he_env* env, int32_t advance_only, int buf, hipStream_t st) {
+static he_status market(he_env* env, int32_t advance_only, int buf, hipStream_t st, bool beside_steps = false) {
     const bool book = env->cfg.book_size > 0;
+    const bool b = beside_steps;
     if (env->cfg.mode == HE_MODE_GBM) {
-        if (book) launch_market<HE_MODE_GBM, true>(env, advance_only, buf, st);
-        else launch_market<HE_MODE_GBM, false>(env, advance_only, buf, st);
+        if (book) launch_market<HE_MODE_GBM, true>(env, advance_only, buf, st, b);
+        else launch_market<HE_MODE_GBM, false>(env, advance_only, buf, st, b);
     } else {
-        if (book) launch_market<HE_MODE_HESTON, true>(env, advance_only, buf, st);
-        else launch_market<HE_MODE_HESTON, false>(env, advance_only, buf, st);
+        if (book) launch_market<HE_MODE_HESTON, true>(env, advance_only, buf, st, b);
+        else launch_market<HE_MODE_HESTON, false>(env, advance_only, buf, st, b);
     }
     HE_HIP(env, hipGetLastError());
     return HE_OK;
@@ -1713,7 +1724,7 @@ static he_status advance_block(he_env* env, hipStream_t st, bool prefetch) {
         // fork: the side stream starts after everything already enqueued on st
         HE_HIP(env, hipEventRecord(env->ev_fork, st));
         HE_HIP(env, hipStreamWaitEvent(env->xs, env->ev_fork, 0));
-        he_status s = market(env, 0, nb ^ 1, env->xs);
+        he_status s = market(env, 0, nb ^ 1, env->xs, true);
         if (s != HE_OK) return s;
         HE_HIP(env, hipEventRecord(env->ev_next, env->xs));
         env->next_state = 1;
@@ -2077,6 +2088,12 @@ he_status he_host_div_by(const double* a, int64_t count, double b, double* out) 
     if ((!a || !out) && count > 0) return HE_EINVAL;
     const double y = 1.0 / b;
     for (int64_t k = 0; k < count; ++k) out[k] = div_by(a[k], b, y);
+    return HE_OK;
+}
+
+he_status he_host_box_muller(const double* u1, const double* u2, int64_t count, double* z1, double* z2) {
+    if ((!u1 || !u2 || !z1 || !z2) && count > 0) return HE_EINVAL;
+    for (int64_t k = 0; k < count; ++k) box_muller(u1[k], u2[k], z1 + k, z2 + k);
     return HE_OK;
 }
 

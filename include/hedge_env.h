@@ -286,6 +286,8 @@ he_status he_host_philox(uint64_t seed, uint64_t env_id, uint64_t n, uint32_t ou
 /* out[k] = a[k] / b through the reciprocal-multiply division the step kernel uses
  * for its constant divisors (must equal IEEE a[k] / b bit for bit). */
 he_status he_host_div_by(const double* a, int64_t count, double b, double* out);
+/* The generate-mode Box-Muller pair (he_math.h box_muller) on host arrays, for tests. */
+he_status he_host_box_muller(const double* u1, const double* u2, int64_t count, double* z1, double* z2);
 /* f32 twin for the obs quotients by per-handle constants (must equal IEEE a[k] / b). */
 he_status he_host_div_byf(const float* a, int64_t count, float b, float* out);
 

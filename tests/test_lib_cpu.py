@@ -127,3 +127,19 @@ def test_reciprocal_division_f32_is_ieee_division(b):
         exp = a / b
     assert_same(got, exp, "div_byf")
     assert np.array_equal(np.signbit(got), np.signbit(exp))
+
+
+def test_box_muller_within_ulps_of_libm():
+    # generate-mode normals: fast log/sincos (he_math.h box_muller) vs NumPy's
+    # rad*cos(2 pi u2): the oracle's definition; the difference is the libm argument
+    # rounding of 2*pi*u2 plus a few ulp
+    rng = np.random.default_rng(1)
+    k1 = rng.integers(0, 2 ** 52, 400_000, dtype=np.uint64)
+    k2 = rng.integers(0, 2 ** 52, 400_000, dtype=np.uint64)
+    u1 = np.concatenate([(k1.astype(np.float64) + 0.5) * 2.0 ** -52, [0.5 * 2.0 ** -52, 1 - 0.5 * 2.0 ** -52, 0.5]])
+    u2 = np.concatenate([(k2.astype(np.float64) + 0.5) * 2.0 ** -52, [0.5 * 2.0 ** -52, 1 - 0.5 * 2.0 ** -52, 0.25]])
+    z1, z2 = _lib.host_box_muller(u1, u2)
+    rad = np.sqrt(-2.0 * np.log(u1))
+    ang = 2.0 * np.pi * u2
+    assert np.all(np.abs(z1 - rad * np.cos(ang)) <= 8 * np.spacing(rad))
+    assert np.all(np.abs(z2 - rad * np.sin(ang)) <= 8 * np.spacing(rad))

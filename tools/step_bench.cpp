@@ -72,7 +72,7 @@ int main(int argc, char** argv) {
         api.config_init(&c, 2);
         c.n_envs = N;
         c.mode = HE_MODE_GBM;
-        c.market_prefetch = getenv("STEP_BENCH_PREFETCH") ? 2 : (RK > 0 ? 0 : 1);  // always / (auto) / never
+        c.market_prefetch = getenv("STEP_BENCH_PREFETCH") ? 2 : ((RK > 0 && !getenv("STEP_BENCH_NOPF")) ? 0 : 1);  // always / (auto) / never
         he_env* env;
         if (api.create(&c, &env) != HE_OK) { fprintf(stderr, "create: %s\n", api.last_error(env)); return 1; }
         if (api.reset(env, nullptr, 0, obs, nullptr, st) != HE_OK) return 1;
