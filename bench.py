@@ -91,24 +91,26 @@ def parse():
     ap.add_argument("--rollout-k", type=int, default=64)
     ap.add_argument("--no-step-api", action="store_true", help="skip the secondary graph-mode he_step run")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC traffic pass")
     ap.add_argument("--probe", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args()
 
 
-def cpu_baseline(seconds):
-    """The oracle (NumPy restatement of the reference env) on host cores, N=256."""
+def _cpu_sample(seconds, seed=42, barrier=None):
+    """One host core: the oracle (NumPy restatement of the reference env) on 256 envs."""
     from oracle.hedging_oracle import OracleVecEnv
     n = 256
-    env = OracleVecEnv(n, mode="gbm", gen=dict(GEN, seed=42), **TRAIN_KW)
-    env.seed_envs_at(np.arange(n), [42] * n)
+    env = OracleVecEnv(n, mode="gbm", gen=dict(GEN, seed=seed), **TRAIN_KW)
+    env.seed_envs_at(np.arange(n), [seed] * n)
     env.reset()
-    rng = np.random.default_rng(0)
+    rng = np.random.default_rng(seed)
     acts = rng.uniform(-1, 1, size=(64, n, 2)).astype(np.float32)
     for k in range(8):
         env.step(acts[k])
+    if barrier is not None:
+        barrier.wait()
     steps = 0
     t0 = time.perf_counter()
     while True:
@@ -117,9 +119,44 @@ def cpu_baseline(seconds):
         el = time.perf_counter() - t0
         if el >= seconds:
             break
-    return dict(value=n * steps / el, unit="env-steps/s", cores=1, kind="port",
-                sample=f"oracle/hedging_oracle.py OracleVecEnv GBM, 256 envs x {steps} steps "
-                       f"({el:.1f} s, 1 thread, NumPy)")
+    return n * steps, el
+
+
+_BARRIER = None
+
+
+def _pool_init(b):
+    global _BARRIER
+    _BARRIER = b
+
+
+def _pool_task(a):
+    return _cpu_sample(a[0], a[1], _BARRIER)
+
+
+def cpu_baseline(seconds):
+    """the oracle at N=256 on the host, 1 thread and one process per core.
+
+    Must run before anything initialises the GPU: the all-core leg forks worker processes.
+    """
+    import multiprocessing as mp
+    steps1, el1 = _cpu_sample(seconds)
+    v1 = steps1 / el1
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count() or 1
+    procs = max(1, min(avail, 16))   # the GPU box grants 16 host cores per GPU
+    ctx = mp.get_context("fork")
+    b = ctx.Barrier(procs)
+    with ctx.Pool(procs, initializer=_pool_init, initargs=(b,)) as pool:
+        res = pool.map(_pool_task, [(seconds, 42 + i) for i in range(procs)])
+    vp = sum(s / e for s, e in res)
+    return dict(value=vp, unit="env-steps/s", cores=procs, kind="port",
+                sample=f"oracle/hedging_oracle.py OracleVecEnv GBM, 256 envs per process, {procs} processes "
+                       f"x {seconds:.0f} s (NumPy, 1 thread each; {avail} cores in affinity mask)",
+                single_core_value=v1,
+                single_core_sample=f"256 envs x {steps1 // 256} steps ({el1:.1f} s, 1 thread)")
 
 
 def make_env(args, dev, rank=0, prefetch="auto"):
@@ -384,6 +421,9 @@ def main():
         pmc = pmc_traffic(args)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args.cpu_seconds)   # before the GPU is touched (forks workers)
     dist = None
     if world > 1:
         import torch.distributed as dist
@@ -435,9 +475,6 @@ def main():
                         ms_per_step=round(wall_g * 1e3 / Kg, 6), kernel=rf["kernel"], kernel_us=rf["kernel_us"],
                         achieved_gbs=rf["achieved"], frac=rf["frac"], bytes_per_launch=rf["bytes_per_launch"])
 
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args.cpu_seconds)
     if rank == 0:
         line = {
             "metric": "env-steps/sec (batched episodes)",
