@@ -1,4 +1,5 @@
-"""Build libhedgeenv for gfx950 in-tree (cantorrl_amd/lib/libhedgeenv.so).
+"""Build the gfx950 libraries in-tree: cantorrl_amd/lib/libhedgeenv.so (the env) and
+cantorrl_amd/lib/librbergomi.so (the rough-Bergomi data generator).
 
     python -m cantorrl_amd.build [--force]
 
@@ -26,23 +27,31 @@ FLAGS = [
 ]
 
 
-def needs_build(out=OUT):
+RB_SRC = os.path.join(HERE, "csrc", "rbergomi.hip")
+RB_DEPS = [RB_SRC, os.path.join(HERE, "csrc", "he_math.h"), os.path.join(REPO, "include", "rbergomi.h")]
+RB_OUT = os.path.join(HERE, "lib", "librbergomi.so")
+TARGETS = [(SRC, DEPS, OUT), (RB_SRC, RB_DEPS, RB_OUT)]
+
+
+def needs_build(out=OUT, deps=DEPS):
     if not os.path.exists(out):
         return True
     t = os.path.getmtime(out)
-    return any(os.path.getmtime(d) > t for d in DEPS)
+    return any(os.path.getmtime(d) > t for d in deps)
 
 
 def build(force=False, verbose=False):
-    if not force and not needs_build():
-        return OUT
-    os.makedirs(os.path.dirname(OUT), exist_ok=True)
-    tmp = OUT + ".tmp"
-    cmd = [HIPCC, *FLAGS, "-o", tmp, SRC]
-    if verbose:
-        print(" ".join(cmd))
-    subprocess.run(cmd, check=True)
-    os.replace(tmp, OUT)
+    """Build every library that is missing or older than its sources; returns the env's."""
+    for src, deps, out in TARGETS:
+        if not force and not needs_build(out, deps):
+            continue
+        os.makedirs(os.path.dirname(out), exist_ok=True)
+        tmp = out + ".tmp"
+        cmd = [HIPCC, *FLAGS, "-o", tmp, src]
+        if verbose:
+            print(" ".join(cmd))
+        subprocess.run(cmd, check=True)
+        os.replace(tmp, out)
     return OUT
 
 

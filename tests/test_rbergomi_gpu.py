@@ -1,0 +1,192 @@
+"""rBergomi generator on the GPU: the HIP kernels fed the reference's own draws
+against the reference goldens, and the Philox path through size-independent
+properties (Black-Scholes limit, sharding identity, determinism, NPZ replay)."""
+import math
+import os
+
+import numpy as np
+import pytest
+
+from oracle import rbergomi_oracle as orc
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+DEV = "cuda:0"
+
+# Tolerances.  Same draws, same algorithm, different f64 libm (device exp / pow /
+# sqrt vs glibc), a direct convolution in place of two FFTs and the option price
+# chain in log space: ~1e-15 relative per value, ~1e-13 after 252 chained price
+# steps.  MC marks are means of max(S - K, 0) over 8-48 paths, where a 1e-13 change
+# of S moves a near-the-money payoff by 1e-13 S absolute: an absolute floor of
+# 1e-10 S0.
+PATH_RTOL = 1e-12
+MARK_RTOL = 1e-10
+
+
+def _rb():
+    from cantorrl_amd import rbergomi
+    return rbergomi
+
+
+def _history():
+    # data/historical_prices.csv of the reference, as recorded in the golden file
+    return np.load(os.path.join(GOLD, "rb_estimate.npz"))["hist__prices"]
+
+
+def _bs(S, K, T, r, sig):
+    d1 = (math.log(S / K) + (r + 0.5 * sig * sig) * T) / (sig * math.sqrt(T))
+    d2 = d1 - sig * math.sqrt(T)
+    N = lambda x: 0.5 * math.erfc(-x / math.sqrt(2))  # noqa: E731
+    c = S * N(d1) - K * math.exp(-r * T) * N(d2)
+    return c, c - S + K * math.exp(-r * T)
+
+
+def test_pricer_reference_draws_match_golden():
+    rb = _rb()
+    g = np.load(os.path.join(GOLD, "rb_price.npz"))
+    S0, K, xi, H, eta, rho = (g[k] for k in ("S0", "K", "xi", "H", "eta", "rho"))
+    n_mc, seed = int(g["n_mc"]), int(g["seed"])
+    for i, T in enumerate(g["tenors"]):
+        d = orc.ReferenceDraws(seed + i)
+        n = int(T / orc.DT)
+        Wc = Wp = np.zeros((len(S0), n_mc, 2, 2))
+        if n > 0:
+            Mo = orc.next_pow2(n + 1)
+            Wc = orc.z_to_w(d.complex_normal((len(S0), n_mc, Mo)))
+            Wp = orc.z_to_w(d.complex_normal((len(S0), n_mc, Mo)))
+        for kind, W in (("call", Wc), ("put", Wp)):
+            got = rb.price_rbergomi_option(S0, K, T, orc.R, xi, H, eta, rho, kind, n_mc, orc.DT, device=DEV, W=W)
+            ref = g[f"{kind}_{i}"]
+            np.testing.assert_allclose(got.cpu().numpy(), ref, rtol=MARK_RTOL, atol=1e-10 * S0.max(),
+                                       err_msg=f"{kind} tenor {T}")
+
+
+def test_generator_reference_draws_match_golden():
+    """Every stage fed the draws the reference consumed: params from the unit
+    normals, paths from W_main, and each day's marks from that day's W (call, put)."""
+    import torch
+    rb = _rb()
+    g = np.load(os.path.join(GOLD, "rb_generate.npz"))
+    P, n_mc, seed = int(g["num_paths"]), int(g["n_mc"]), int(g["seed"])
+    base = tuple(g["base"])
+    d = orc.ReferenceDraws(seed)
+    unit = np.stack([d.normal(0.0, 1.0, P) for _ in range(5)])
+    Zm = d.complex_normal((P, 256))
+    cfg = rb.make_config(P, seed=seed)
+    params = rb.sample_params(cfg, base, DEV, unit_normals=unit)
+    ref_params = np.stack(orc.perturb_params(base, [s * u for s, u in zip(orc.PERTURB_STD, unit)]))
+    np.testing.assert_array_equal(params.cpu().numpy(), ref_params)
+    paths, vol = rb.simulate_paths(cfg, params, DEV, W=orc.z_to_w(Zm))
+    np.testing.assert_allclose(vol.cpu().numpy(), g["volatilities"], rtol=PATH_RTOL, atol=0)
+    np.testing.assert_allclose(paths.cpu().numpy(), g["paths"], rtol=PATH_RTOL, atol=0)
+    # marks: day j prices at S_{j-1}, K = round(S_{j-1}), xi = v_{j-1} (:404-451)
+    d = orc.ReferenceDraws(seed)
+    T = 252
+    Wc = np.zeros((T, P, n_mc, 32, 2))
+    Wp = np.zeros_like(Wc)
+    for j in range(T):
+        Wc[j] = orc.z_to_w(d.complex_normal((P, n_mc, 32)))
+        Wp[j] = orc.z_to_w(d.complex_normal((P, n_mc, 32)))
+    S = paths[:, :T].T.reshape(-1)          # day-major, as the W arrays
+    v = vol[:, :T].T.reshape(-1)
+    pr = params.cpu().numpy()
+    rep = lambda x: np.tile(x, T)           # noqa: E731
+    for kind, W, key in (("call", Wc, "call_prices_atm"), ("put", Wp, "put_prices_atm")):
+        got = rb.price_rbergomi_option(S, torch.round(S), orc.T_OPTION_TENOR, orc.R, v, rep(pr[2]), rep(pr[3]),
+                                       rep(pr[4]), kind, n_mc, orc.DT, device=DEV, W=W.reshape(T * P, n_mc, 32, 2))
+        got = got.cpu().numpy().reshape(T, P).T
+        np.testing.assert_allclose(got, g[key], rtol=MARK_RTOL, atol=1e-10 * g["paths"].max(), err_msg=key)
+
+
+def test_pricer_edge_inputs_follow_reference():
+    """S0 <= 0, xi < 0 and NaN inputs through the oracle restatement (same draws)."""
+    rb = _rb()
+    rng = np.random.default_rng(4)
+    S0 = np.array([0.0, -5.0, 100.0, np.nan, 1e-9, 50.0])
+    K = np.array([1.0, 1.0, 100.0, 100.0, 0.0, 50.0])
+    xi = np.array([0.04, 0.04, -0.01, 0.04, 0.04, 0.0])
+    H = np.full(6, 0.2)
+    eta = np.full(6, 1.5)
+    rho = np.full(6, -0.5)
+    Z = rng.normal(size=(6, 16, 32)) + 1j * rng.normal(size=(6, 16, 32))
+    for kind in ("call", "put"):
+        ref = orc.price_options(S0, K, 30 / 252, 0.04, xi, H, eta, rho, kind, Z, 1 / 252)
+        got = rb.price_rbergomi_option(S0, K, 30 / 252, 0.04, xi, H, eta, rho, kind, 16, 1 / 252, device=DEV,
+                                       W=orc.z_to_w(Z)).cpu().numpy()
+        np.testing.assert_allclose(got, ref, rtol=MARK_RTOL, atol=1e-12, equal_nan=True, err_msg=kind)
+
+
+@pytest.mark.parametrize("normals", ["f64", "f32"])
+def test_pricer_philox_black_scholes_limit(normals):
+    """eta -> 0 freezes the variance at xi: the Euler step is then exact GBM, so the
+    MC price converges to Black-Scholes.  200k paths: 4 standard errors."""
+    rb = _rb()
+    n_mc = 200000
+    S0 = np.array([100.0, 100.0, 496.48, 80.0])
+    K = np.array([100.0, 105.0, 496.0, 90.0])
+    xi = np.array([0.04, 0.09, 0.029, 0.01])
+    T = 30 / 252
+    for kind, col in (("call", 0), ("put", 1)):
+        got = rb.price_rbergomi_option(S0, K, T, 0.04, xi, np.full(4, 0.3), np.full(4, 1e-9), np.full(4, -0.7),
+                                       kind, n_mc, 1 / 252, device=DEV, normals=normals).cpu().numpy()
+        for i in range(4):
+            want = _bs(S0[i], K[i], T, 0.04, math.sqrt(xi[i]))[col]
+            se = S0[i] * math.sqrt(xi[i] * T) / math.sqrt(n_mc)   # payoff sd <= S sigma sqrt(T)
+            assert abs(got[i] - want) < 4 * se, (kind, i, got[i], want, se)
+
+
+def test_generate_shards_equal_rows_and_is_deterministic():
+    rb = _rb()
+    hist = _history()
+    kw = dict(n_mc=64, device=DEV, seed=9)
+    full = rb.generate_paths_and_options(hist, 8, **kw)
+    part = rb.generate_paths_and_options(hist, 3, path_offset=5, **kw)
+    again = rb.generate_paths_and_options(hist, 8, **kw)
+    for k in ("params", "paths", "volatilities", "call_prices_atm", "put_prices_atm"):
+        a, b = full[k].cpu().numpy(), part[k].cpu().numpy()
+        sub = a[:, 5:8] if k == "params" else a[5:8]
+        np.testing.assert_array_equal(sub, b, err_msg=k)
+        np.testing.assert_array_equal(a, again[k].cpu().numpy(), err_msg=k)
+
+
+def test_generate_properties():
+    import torch
+    rb = _rb()
+    hist = _history()
+    res = rb.generate_paths_and_options(hist, 256, n_mc=512, device=DEV)
+    base = np.array(res["base_params"])
+    np.testing.assert_allclose(base, orc.estimate_base_params(hist), rtol=1e-12)
+    S, v = res["paths"], res["volatilities"]
+    C, Pp = res["call_prices_atm"], res["put_prices_atm"]
+    assert S.shape == (256, 253) and C.shape == (256, 252)
+    for t in (S, v, C, Pp):
+        assert bool(torch.isfinite(t).all())
+    assert bool((S >= 1e-8).all()) and bool((v > 0).all()) and bool((C >= 0).all()) and bool((Pp >= 0).all())
+    pr = res["params"].cpu().numpy()
+    assert (pr[2] >= 0.01).all() and (pr[2] <= 0.49).all() and (pr[4] >= -0.99).all() and (pr[4] <= -0.01).all()
+    np.testing.assert_array_equal(S[:, 0].cpu().numpy(), pr[0])
+    # ATM marks: C - P against S - K e^{-rT}, a loose check (independent MC draws
+    # for C and P, and the reference's scheme is not an exact martingale)
+    Sd = S[:, :252]
+    par = (C - Pp - (Sd - torch.round(Sd) * math.exp(-0.04 * 30 / 252))) / Sd
+    assert abs(float(par.mean())) < 1e-3 and float(par.abs().max()) < 0.05
+    # the perturbed S0 are N(S0 base, 1 %)
+    assert abs(pr[0].mean() / base[0] - 1) < 0.01 * 4 / 16
+
+
+def test_npz_round_trip_into_replay_env(tmp_path):
+    from cantorrl_amd.vec_env import HedgingVecEnv
+    rb = _rb()
+    res = rb.generate_paths_and_options(_history(), 16, n_mc=32, device=DEV)
+    f = tmp_path / "rb.npz"
+    rb.save_npz(str(f), res)
+    z = np.load(f)
+    assert set(z.files) == {"paths", "volatilities", "call_prices_atm", "put_prices_atm"}
+    assert z["paths"].dtype == np.float64 and z["call_prices_atm"].shape == (16, 252)
+    env = HedgingVecEnv(4, str(f), device=DEV, seed=0)
+    obs = env.reset()
+    assert obs.shape == (4, 13)
+    for _ in range(3):
+        obs, rew, done, _info = env.step(np.zeros((4, 2), np.float32))
+    assert np.isfinite(obs).all() and np.isfinite(rew).all()
+    env.close()
