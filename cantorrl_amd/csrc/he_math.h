@@ -182,9 +182,13 @@ HE_HD void box_muller(double u1, double u2, double* z1, double* z2) {
     cp = fma(cp, rr, 0.253669507901048);
     cp = fma(cp, rr, -1.2337005501361697);
     const double cs = fma(cp, rr, 1.0);
+    // quadrant qi: (sin, cos) = (sn, cs), (cs, -sn), (-sn, -cs), (-cs, sn) -- as two
+    // selects and two exact sign flips (a chained ?: on qi lowers to branches)
     const int qi = (int)q & 3;
-    const double sinv = (qi == 0) ? sn : (qi == 1) ? cs : (qi == 2) ? -sn : -cs;
-    const double cosv = (qi == 0) ? cs : (qi == 1) ? -sn : (qi == 2) ? -cs : sn;
+    const bool swp = (qi & 1) != 0;
+    const double s_ = swp ? cs : sn, c_ = swp ? sn : cs;
+    const double sinv = (qi & 2) ? -s_ : s_;
+    const double cosv = ((qi + 1) & 2) ? -c_ : c_;
     *z1 = rad * cosv;
     *z2 = rad * sinv;
 }

@@ -278,8 +278,10 @@ __global__ void __launch_bounds__(kMcThreads, 2) mc_kernel(McArgs a) {
             for (int b = 0; b < MO; ++b) w1[b] = wp[2 * b];
         } else if (NORM == 0) {
 #pragma unroll
-            for (int b = 0; b < MO / 2; ++b)
+            for (int b = 0; b < MO / 2; ++b) {
+                __builtin_amdgcn_sched_barrier(0);
                 normal_pair(rb_ctr((uint32_t)(m * MO + b), kDomMc, sub, gid), a.k0, a.k1, &w1[2 * b], &w1[2 * b + 1]);
+            }
         } else {
 #pragma unroll
             for (int b = 0; b < MO / 4; ++b)
@@ -300,6 +302,9 @@ __global__ void __launch_bounds__(kMcThreads, 2) mc_kernel(McArgs a) {
         double w2q[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
         for (int j = 0; j < MO - 1; ++j) {   // Euler step j + 1 uses X_j, v_j, W_j (:285-295)
+            // one step at a time: interleaving the steps' Philox blocks buys no ILP the
+            // second wave on the SIMD does not already give, and costs registers
+            __builtin_amdgcn_sched_barrier(0);
             if (j < a.n) {
                 double w2;
                 if (NORM == 2) {
