@@ -95,6 +95,10 @@ def parse():
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC traffic pass")
     ap.add_argument("--probe", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--workload", choices=["env", "rbergomi"], default="env",
+                    help="env: the hedging-env step (headline); rbergomi: the rough-Bergomi MC mark generator")
+    ap.add_argument("--rb-paths", type=int, default=2048, help="rbergomi: paths per GPU (x 252 days x call/put)")
+    ap.add_argument("--rb-normals", choices=["f64", "f32"], default="f64")
     return ap.parse_args()
 
 
@@ -406,8 +410,133 @@ def roofline(mode, n, kern_ms, rk, book=False):
                 kernel_us=round(kern_ms * 1e3, 3), bytes_per_launch=int(bytes_launch))
 
 
+# ---------------------------------------------------------------------- rbergomi workload
+RB_MC, RB_DAYS = 5000, 252
+
+
+def rb_cpu_baseline(seconds, base):
+    """The oracle's restatement of price_rbergomi_option_gpu (rbergomi_sim.py:261-306,
+    NumPy FFTs, 1 thread) on batches of 8 options x 5000 MC paths."""
+    from oracle import rbergomi_oracle as orc
+    rng = np.random.default_rng(0)
+    B = 8
+    S0 = np.full(B, base[0])
+    K = np.round(S0)
+    xi, H, eta, rho = (np.full(B, base[k]) for k in (1, 2, 3, 4))
+    n = 0
+    t0 = time.perf_counter()
+    while True:
+        Z = rng.normal(size=(B, RB_MC, 32)) + 1j * rng.normal(size=(B, RB_MC, 32))
+        orc.price_options(S0, K, 30 / 252, 0.04, xi, H, eta, rho, "call", Z, 1 / 252)
+        n += B
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return dict(value=n / el, unit="options/s", cores=1, kind="port",
+                sample=f"oracle/rbergomi_oracle.py price_options (the reference's FFT form), {n} options x "
+                       f"{RB_MC} MC paths in batches of {B} ({el:.1f} s, 1 thread, NumPy)")
+
+
+def rbergomi_main(args):
+    """One step = one rb_price_atm_marks launch: rolling-ATM call and put marks for
+    every (path, day) of args.rb_paths paths x 252 days, 5000 MC paths x 30 Euler
+    steps each (rbergomi_sim.py:404-451, all days at once)."""
+    from cantorrl_amd import rbergomi as rb
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    hist = np.load(os.path.join(REPO, "tests", "golden", "rb_estimate.npz"))["hist__prices"]
+    base = rb.estimate_base_params(hist)
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = rb_cpu_baseline(args.cpu_seconds, base)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    P = args.rb_paths
+    cfg = rb.make_config(P, path_offset=rank * P, normals=args.rb_normals)
+    params = rb.sample_params(cfg, base, dev)
+    paths, vol = rb.simulate_paths(cfg, params, dev)
+    call = torch.empty((P, RB_DAYS), dtype=torch.float64, device=dev)
+    put = torch.empty_like(call)
+    lib = rb.load()
+    stream = torch.cuda.current_stream(dev)
+    sp = ctypes.c_void_p(stream.cuda_stream)
+    ptrs = [ctypes.c_void_p(t.data_ptr()) for t in (params, paths, vol, call, put)]
+
+    def launch():
+        st = lib.rb_price_atm_marks(ctypes.byref(cfg), *ptrs, sp)
+        if st != 0:
+            raise RuntimeError(lib.rb_last_error().decode())
+
+    K, W = max(1, args.steps), max(0, args.warmup)
+    for _ in range(W):
+        launch()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    hev = HipEvents()
+    e0, e1 = hev.create(), hev.create()
+    t0 = time.perf_counter()
+    hev.record(e0, stream)
+    for _ in range(K):
+        launch()
+    hev.record(e1, stream)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    kern_ms = hev.elapsed_ms(e0, e1) / K
+    hev.destroy(e0, e1)
+    t = torch.tensor([wall], dtype=torch.float64, device=dev)
+    if dist is not None:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    wall = float(t.item())
+    n_opt = P * RB_DAYS * 2
+    if rank == 0:
+        line = {
+            "metric": "rolling-ATM MC option marks/sec (rBergomi generator, rbergomi_sim.py)",
+            "value": round(n_opt * world * K / wall, 1),
+            "unit": "options/s",
+            "n_gpus": world,
+            "steps": K,
+            "warmup": W,
+            "ms_per_step": round(wall * 1e3 / K, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64" if args.rb_normals == "f64" else "f64 (f32-precision normals)",
+            "data": "synthetic (rBergomi parameters estimated from data/historical_prices.csv, perturbed per path; "
+                    "Philox4x32-10 normals)",
+            "config": {"workload": f"generate_paths_and_options marks: {P} paths/GPU x {RB_DAYS} days x "
+                                   f"{{call, put}}, {RB_MC} MC paths x 30 Euler steps each",
+                       "paths_per_gpu": P, "n_mc": RB_MC, "normals": args.rb_normals,
+                       "parallelism": f"path-shard x{world}"},
+            "kernel": {"name": "mc_kernel (rb_price_atm_marks)", "ms_per_launch": round(kern_ms, 3),
+                       "options_per_s": round(n_opt / (kern_ms * 1e-3), 1),
+                       "mc_path_steps_per_s": round(n_opt * RB_MC * 30 / (kern_ms * 1e-3), 1),
+                       "bound": "valu (f64 FMA / exp, Philox): no HBM traffic to speak of "
+                                "(5 f64 in, 1 f64 out per option)"},
+            "full_dataset_s": round(100000 * RB_DAYS * 2 / (n_opt * world * K / wall), 2),
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
+    if args.workload == "rbergomi":
+        rbergomi_main(args)
+        return
     if args.envs is None:
         args.envs = CONFIGS[args.config]["envs"]
     if args.mode == "rollout" and (args.rollout_k < 1 or args.rollout_k > M_BLOCK):

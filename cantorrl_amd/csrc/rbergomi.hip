@@ -58,6 +58,7 @@ int fail(int code, const char* fmt, ...) {
 
 constexpr int kDomParams = 1, kDomMain = 2, kDomMc = 3;
 constexpr int kMcThreads = 256;
+constexpr int kXc = 6;   // MC pricer: Euler steps per convolution chunk (divides the 30 of the reference tenor)
 
 HE_HD u32x4 rb_ctr(uint32_t block, int dom, uint32_t sub, uint64_t gid) {
     return u32x4{block, ((uint32_t)dom << 24) | (sub & 0xFFFFFFu), (uint32_t)gid, (uint32_t)(gid >> 32)};
@@ -203,8 +204,10 @@ __device__ __forceinline__ void normal_quad32(u32x4 c, uint32_t k0, uint32_t k1,
 }
 
 // NORM: 0 Philox f64 normals, 1 Philox f32 normals, 2 W from memory (list mode).
-template <int MO, int NORM, bool ATM>
-__global__ void __launch_bounds__(kMcThreads, 2) mc_kernel(McArgs a) {
+// FULL: n == MO - 2 (30 steps on a 32-point grid, the reference's tenor), so the step
+// guards are compile-time; otherwise n is tested per step.
+template <int MO, int NORM, bool ATM, bool FULL>
+__global__ void __launch_bounds__(kMcThreads) mc_kernel(McArgs a) {
     __shared__ double s_lam[MO];
     __shared__ double s_ma[MO];
     __shared__ double s_red[kMcThreads / 64];
@@ -284,51 +287,59 @@ __global__ void __launch_bounds__(kMcThreads, 2) mc_kernel(McArgs a) {
             }
         } else {
 #pragma unroll
-            for (int b = 0; b < MO / 4; ++b)
+            for (int b = 0; b < MO / 4; ++b) {
+                __builtin_amdgcn_sched_barrier(0);
                 normal_quad32(rb_ctr((uint32_t)(m * (MO / 2) + b), kDomMc, sub, gid), a.k0, a.k1, &w1[4 * b]);
+            }
         }
-        // X_j = sum_k lam_k Re W_{(j - k) mod MO}, k outer: lam_k is one LDS broadcast
-        // feeding MO - 1 FMAs
-        double X[MO - 1];
-#pragma unroll
-        for (int j = 0; j < MO - 1; ++j) X[j] = 0.0;
-#pragma unroll
-        for (int k = 0; k < MO; ++k) {
-            const double lk = s_lam[k];
-#pragma unroll
-            for (int j = 0; j < MO - 1; ++j) X[j] = fma(lk, w1[(j - k) & (MO - 1)], X[j]);
-        }
+        // The steps in chunks of kXc: X_j = sum_k lam_k Re W_{(j - k) mod MO} for the
+        // chunk's j, k outer (lam_k one LDS broadcast feeding kXc FMAs), then the chunk's
+        // Euler steps.  Only kXc accumulators live beside Re W: 4 waves per SIMD.
         double L = 0.0;
         double w2q[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-        for (int j = 0; j < MO - 1; ++j) {   // Euler step j + 1 uses X_j, v_j, W_j (:285-295)
-            // one step at a time: interleaving the steps' Philox blocks buys no ILP the
-            // second wave on the SIMD does not already give, and costs registers
-            __builtin_amdgcn_sched_barrier(0);
-            if (j < a.n) {
-                double w2;
-                if (NORM == 2) {
-                    w2 = wp[2 * j + 1];
-                } else if (NORM == 0) {
-                    if ((j & 1) == 0)
-                        normal_pair(rb_ctr((uint32_t)(m * MO + MO / 2 + j / 2), kDomMc, sub, gid), a.k0, a.k1,
-                                    &w2q[0], &w2q[1]);
-                    w2 = w2q[j & 1];
-                } else {
-                    if ((j & 3) == 0)
-                        normal_quad32(rb_ctr((uint32_t)(m * (MO / 2) + MO / 4 + j / 4), kDomMc, sub, gid), a.k0,
-                                      a.k1, w2q);
-                    w2 = w2q[j & 3];
+        for (int j0 = 0; j0 < MO - 1; j0 += kXc) {
+            if (FULL ? (j0 < MO - 2) : (j0 < a.n)) {
+                __asm__ volatile("" ::: "memory");   // re-read lam per chunk (no CSE across chunks)
+                __builtin_amdgcn_sched_barrier(0);   // and no interleaving of chunks: w1 + one chunk live
+                double X[kXc];
+#pragma unroll
+                for (int q = 0; q < kXc; ++q) X[q] = 0.0;
+#pragma unroll
+                for (int k = 0; k < MO; ++k) {
+                    const double lk = s_lam[k];
+#pragma unroll
+                    for (int q = 0; q < kXc; ++q) X[q] = fma(lk, w1[(j0 + q - k) & (MO - 1)], X[q]);
                 }
-                const double Xj = cx * (X[j] * a.inv_sqrt_m);
-                // v = xi e^(X + ma) and sqrt(v) = sqrt(xi) e^((X + ma) / 2): one exp
-                const double e = exp(0.5 * (Xj + s_ma[j]));
-                const double v = xi * (e * e);
-                const double dW = rho * (a.sdt * w1[j]) + rq * (a.sdt * w2);
-                const double drift = (a.r - 0.5 * v) * a.dt;
-                const double diff = (sxi * e) * dW;
-                L = np_max(L + (drift + diff), Lf);
-                if (j == 0 && !s0_pos) L = 0.0;
+#pragma unroll
+                for (int q = 0; q < kXc; ++q) {   // Euler step j + 1 uses X_j, v_j, W_j (:285-295)
+                    const int j = j0 + q;
+                    if (FULL ? (j < MO - 2) : (j < MO - 1 && j < a.n)) {
+                        double w2;
+                        if (NORM == 2) {
+                            w2 = wp[2 * j + 1];
+                        } else if (NORM == 0) {
+                            if ((j & 1) == 0)
+                                normal_pair(rb_ctr((uint32_t)(m * MO + MO / 2 + j / 2), kDomMc, sub, gid), a.k0,
+                                            a.k1, &w2q[0], &w2q[1]);
+                            w2 = w2q[j & 1];
+                        } else {
+                            if ((j & 3) == 0)
+                                normal_quad32(rb_ctr((uint32_t)(m * (MO / 2) + MO / 4 + j / 4), kDomMc, sub, gid),
+                                              a.k0, a.k1, w2q);
+                            w2 = w2q[j & 3];
+                        }
+                        const double Xj = cx * (X[q] * a.inv_sqrt_m);
+                        // v = xi e^(X + ma) and sqrt(v) = sqrt(xi) e^((X + ma) / 2): one exp
+                        const double e = exp(0.5 * (Xj + s_ma[j]));
+                        const double v = xi * (e * e);
+                        const double dW = rho * (a.sdt * w1[j]) + rq * (a.sdt * w2);
+                        const double drift = (a.r - 0.5 * v) * a.dt;
+                        const double diff = (sxi * e) * dW;
+                        L = np_max(L + (drift + diff), Lf);
+                        if (j == 0 && !s0_pos) L = 0.0;
+                    }
+                }
             }
         }
         const double S = Sb * exp(L);
@@ -403,16 +414,23 @@ McArgs mc_args(const rb_config* c, const OptGrid& g) {
     return a;
 }
 
+template <int MO, bool FULL>
+void launch_mc_v(const McArgs& a, int norm, bool atm, dim3 grid, hipStream_t s) {
+    if (atm) {
+        if (norm == RB_NORMALS_F32) hipLaunchKernelGGL((mc_kernel<MO, 1, true, FULL>), grid, dim3(kMcThreads), 0, s, a);
+        else hipLaunchKernelGGL((mc_kernel<MO, 0, true, FULL>), grid, dim3(kMcThreads), 0, s, a);
+    } else {
+        if (a.W) hipLaunchKernelGGL((mc_kernel<MO, 2, false, FULL>), grid, dim3(kMcThreads), 0, s, a);
+        else if (norm == RB_NORMALS_F32)
+            hipLaunchKernelGGL((mc_kernel<MO, 1, false, FULL>), grid, dim3(kMcThreads), 0, s, a);
+        else hipLaunchKernelGGL((mc_kernel<MO, 0, false, FULL>), grid, dim3(kMcThreads), 0, s, a);
+    }
+}
+
 template <int MO>
 int launch_mc_mo(const McArgs& a, int norm, bool atm, dim3 grid, hipStream_t s) {
-    if (atm) {
-        if (norm == RB_NORMALS_F32) hipLaunchKernelGGL((mc_kernel<MO, 1, true>), grid, dim3(kMcThreads), 0, s, a);
-        else hipLaunchKernelGGL((mc_kernel<MO, 0, true>), grid, dim3(kMcThreads), 0, s, a);
-    } else {
-        if (a.W) hipLaunchKernelGGL((mc_kernel<MO, 2, false>), grid, dim3(kMcThreads), 0, s, a);
-        else if (norm == RB_NORMALS_F32) hipLaunchKernelGGL((mc_kernel<MO, 1, false>), grid, dim3(kMcThreads), 0, s, a);
-        else hipLaunchKernelGGL((mc_kernel<MO, 0, false>), grid, dim3(kMcThreads), 0, s, a);
-    }
+    if (MO == 32 && a.n == MO - 2) launch_mc_v<MO, true>(a, norm, atm, grid, s);
+    else launch_mc_v<MO, false>(a, norm, atm, grid, s);
     RB_HIP(hipGetLastError());
     return RB_OK;
 }
