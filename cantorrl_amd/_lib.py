@@ -14,6 +14,7 @@ LIB_PATH = os.path.join(HERE, "lib", "libhedgeenv.so")
 
 HE_ABI_VERSION = 2
 HE_BOOK_MAX = 8
+HE_OBS_DIM = 13
 BOOK_TYPES = {"call": 0, "put": 1, "uo_call": 2}
 HE_OK, HE_EINVAL, HE_ESHAPE, HE_EHIP, HE_ENOMEM, HE_ESTATE = range(6)
 HE_MODE_REPLAY, HE_MODE_GBM, HE_MODE_HESTON = range(3)
@@ -113,8 +114,23 @@ EXPORTS = [
     "he_seed", "he_reset", "he_step", "he_rollout", "he_num_envs", "he_episode_length",
     "he_num_episodes", "he_get_config", "he_state_size", "he_get_state", "he_set_state",
     "he_pcg64_seed_state", "he_host_episode_draws", "he_host_philox", "he_host_div_by", "he_host_div_byf", "he_time_next_step", "he_rollout_policy", "he_host_box_muller",
-    "he_sync_market",
+    "he_sync_market", "he_vecnorm_stats_len", "he_vecnorm_scratch_bytes", "he_vecnorm_init", "he_vecnorm_step",
+    "he_vecnorm_reset",
 ]
+
+
+class HeVecnormParams(ctypes.Structure):
+    _fields_ = [
+        ("obs_dim", ctypes.c_int32),
+        ("training", ctypes.c_int32),
+        ("norm_obs", ctypes.c_int32),
+        ("norm_reward", ctypes.c_int32),
+        ("gamma", ctypes.c_double),
+        ("clip_obs", ctypes.c_double),
+        ("clip_reward", ctypes.c_double),
+        ("epsilon", ctypes.c_double),
+        ("reserved", ctypes.c_int32 * 4),
+    ]
 
 _lib = None
 
@@ -165,6 +181,11 @@ def load(path=LIB_PATH):
         "he_host_box_muller": (i32, [ctypes.c_void_p, ctypes.c_void_p, i64, ctypes.c_void_p, ctypes.c_void_p]),
         "he_time_next_step": (i32, [vp, vp, vp]),
         "he_sync_market": (i32, [vp, vp]),
+        "he_vecnorm_stats_len": (i64, [i32]),
+        "he_vecnorm_scratch_bytes": (i64, [i64, i32]),
+        "he_vecnorm_init": (i32, [vp, i32, vp]),
+        "he_vecnorm_step": (i32, [ctypes.POINTER(HeVecnormParams), i64] + [vp] * 14 + [vp]),
+        "he_vecnorm_reset": (i32, [ctypes.POINTER(HeVecnormParams), i64] + [vp] * 5 + [vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

@@ -30,7 +30,9 @@ FLAGS = [
 RB_SRC = os.path.join(HERE, "csrc", "rbergomi.hip")
 RB_DEPS = [RB_SRC, os.path.join(HERE, "csrc", "he_math.h"), os.path.join(REPO, "include", "rbergomi.h")]
 RB_OUT = os.path.join(HERE, "lib", "librbergomi.so")
-TARGETS = [(SRC, DEPS, OUT), (RB_SRC, RB_DEPS, RB_OUT)]
+VN_SRC = os.path.join(HERE, "csrc", "vecnorm.hip")
+DEPS = DEPS + [VN_SRC]
+TARGETS = [([SRC, VN_SRC], DEPS, OUT), ([RB_SRC], RB_DEPS, RB_OUT)]
 
 
 def needs_build(out=OUT, deps=DEPS):
@@ -42,12 +44,12 @@ def needs_build(out=OUT, deps=DEPS):
 
 def build(force=False, verbose=False):
     """Build every library that is missing or older than its sources; returns the env's."""
-    for src, deps, out in TARGETS:
+    for srcs, deps, out in TARGETS:
         if not force and not needs_build(out, deps):
             continue
         os.makedirs(os.path.dirname(out), exist_ok=True)
         tmp = out + ".tmp"
-        cmd = [HIPCC, *FLAGS, "-o", tmp, src]
+        cmd = [HIPCC, *FLAGS, "-o", tmp, *srcs]
         if verbose:
             print(" ".join(cmd))
         subprocess.run(cmd, check=True)
@@ -58,7 +60,7 @@ def build(force=False, verbose=False):
 def build_variant(out, extra_flags):
     """Diagnostic / A-B builds (e.g. -DHE_TIMING) outside the package directory."""
     os.makedirs(os.path.dirname(os.path.abspath(out)), exist_ok=True)
-    subprocess.run([HIPCC, *FLAGS, *extra_flags, "-o", out, SRC], check=True)
+    subprocess.run([HIPCC, *FLAGS, *extra_flags, "-o", out, SRC, VN_SRC], check=True)
     return out
 
 

@@ -1,0 +1,236 @@
+"""VecNormalize and Monitor statistics on the device, around HedgingVecEnv.
+
+The reference trains behind SB3 2.6.0's `VecNormalize(venv, norm_obs=True,
+norm_reward=True, gamma=...)` (train_ppo_v2.py:204, :305), evaluates with the
+statistics frozen (`training=False, norm_reward=False`, :450-453), and wraps each env in
+`Monitor(info_keywords=...)` (:119).  `DeviceVecNormalize` has VecNormalize's
+constructor, attributes (`obs_rms`, `ret_rms`, `returns`, `training`, `gamma`, ...) and
+VecEnv methods, but keeps the running statistics, the discounted returns and the
+Monitor episode sums in device memory, updated by two kernels per step
+(cantorrl_amd/csrc/vecnorm.hip via he_vecnorm_step).  The obs, rewards and flags never
+leave the GPU on the tensor path (`reset_tensors` / `step_tensors`).
+
+Statistics are saved with `save(path)` as NPZ (no pickle) and restored with
+`DeviceVecNormalize.load(path, venv)`.
+"""
+import ctypes
+import time
+
+import numpy as np
+import torch
+
+from . import _lib
+from .vec_env import InfoView
+
+
+class _RmsView:
+    """RunningMeanStd-shaped host view (mean, var, count) of the device statistics."""
+
+    def __init__(self, mean, var, count):
+        self.mean, self.var, self.count = mean, var, count
+
+
+class DeviceVecNormalize:
+    def __init__(self, venv, training=True, norm_obs=True, norm_reward=True, clip_obs=10.0, clip_reward=10.0,
+                 gamma=0.99, epsilon=1e-8):
+        self.venv = venv
+        self.lib = _lib.load()
+        self.num_envs = venv.num_envs
+        self.observation_space = venv.observation_space
+        self.action_space = venv.action_space
+        self.device = venv.device
+        self.return_numpy = venv.return_numpy
+        self.clip_obs, self.clip_reward, self.gamma, self.epsilon = clip_obs, clip_reward, gamma, epsilon
+        self.training, self.norm_obs, self.norm_reward = training, norm_obs, norm_reward
+        D, n, dev = _lib.HE_OBS_DIM, self.num_envs, self.device
+        self._stats = torch.empty(int(self.lib.he_vecnorm_stats_len(D)), dtype=torch.float64, device=dev)
+        self._scratch = torch.zeros(int(self.lib.he_vecnorm_scratch_bytes(n, D)), dtype=torch.uint8, device=dev)
+        self._returns = torch.zeros(n, dtype=torch.float64, device=dev)
+        self._obs_out = torch.empty((n, D), dtype=torch.float32, device=dev)
+        self._rew_out = torch.empty(n, dtype=torch.float32, device=dev)
+        self._tobs_out = torch.empty((n, D), dtype=torch.float32, device=dev)
+        self._ep_ret = torch.zeros(n, dtype=torch.float64, device=dev)
+        self._ep_len = torch.zeros(n, dtype=torch.int32, device=dev)
+        self._ep_ret_done = torch.zeros(n, dtype=torch.float64, device=dev)
+        self._ep_len_done = torch.zeros(n, dtype=torch.int32, device=dev)
+        self._check(self.lib.he_vecnorm_init(self._p(self._stats), D, self._stream()), "he_vecnorm_init")
+        self._actions_pending = None
+        self._t_start = time.time()
+
+    # ------------------------------------------------------------------ plumbing
+    @staticmethod
+    def _p(t):
+        return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+    def _stream(self):
+        return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def _check(self, st, what):
+        if st != _lib.HE_OK:
+            raise _lib.HedgeEnvError(f"{what} failed with status {st}")
+
+    def _params(self):
+        p = _lib.HeVecnormParams()
+        p.obs_dim = _lib.HE_OBS_DIM
+        p.training, p.norm_obs, p.norm_reward = int(self.training), int(self.norm_obs), int(self.norm_reward)
+        p.gamma, p.clip_obs, p.clip_reward, p.epsilon = (float(self.gamma), float(self.clip_obs),
+                                                           float(self.clip_reward), float(self.epsilon))
+        return p
+
+    # ------------------------------------------------------------------ statistics (SB3 attributes)
+    @property
+    def obs_rms(self):
+        s = self._stats.cpu().numpy()
+        D = _lib.HE_OBS_DIM
+        return _RmsView(s[:D].copy(), s[D:2 * D].copy(), float(s[2 * D]))
+
+    @property
+    def ret_rms(self):
+        s = self._stats.cpu().numpy()
+        D = _lib.HE_OBS_DIM
+        return _RmsView(np.float64(s[2 * D + 1]), np.float64(s[2 * D + 2]), float(s[2 * D + 3]))
+
+    @property
+    def returns(self):
+        return self._returns.cpu().numpy()
+
+    def set_training_mode(self, training):
+        self.training = bool(training)
+
+    def get_state(self):
+        """Running statistics and returns as host arrays (what VecNormalize pickles)."""
+        return dict(stats=self._stats.cpu().numpy(), returns=self._returns.cpu().numpy(),
+                    params=np.array([self.clip_obs, self.clip_reward, self.gamma, self.epsilon]),
+                    flags=np.array([self.training, self.norm_obs, self.norm_reward], np.int64))
+
+    def set_state(self, st):
+        self._stats.copy_(torch.as_tensor(np.asarray(st["stats"], np.float64)))
+        if "returns" in st and len(st["returns"]) == self.num_envs:
+            self._returns.copy_(torch.as_tensor(np.asarray(st["returns"], np.float64)))
+
+    def save(self, path):
+        np.savez(path, **self.get_state())
+
+    @classmethod
+    def load(cls, path, venv):
+        """VecNormalize.load(path, venv) for the NPZ written by save()."""
+        z = np.load(path, allow_pickle=False)
+        clip_obs, clip_reward, gamma, eps = (float(x) for x in z["params"])
+        training, norm_obs, norm_reward = (bool(x) for x in z["flags"])
+        obj = cls(venv, training=training, norm_obs=norm_obs, norm_reward=norm_reward, clip_obs=clip_obs,
+                  clip_reward=clip_reward, gamma=gamma, epsilon=eps)
+        obj.set_state({k: z[k] for k in z.files})
+        return obj
+
+    # ------------------------------------------------------------------ device path
+    def reset_tensors(self):
+        obs = self.venv.reset_tensors()
+        self._check(self.lib.he_vecnorm_reset(ctypes.byref(self._params()), self.num_envs, self._p(obs),
+                                              self._p(self._returns), self._p(self._stats), self._p(self._scratch),
+                                              self._p(self._obs_out), self._stream()), "he_vecnorm_reset")
+        self._ep_ret.zero_()
+        self._ep_len.zero_()
+        return self._obs_out
+
+    def step_tensors(self, actions):
+        """(normalized obs, normalized reward, terminated, truncated) device tensors;
+        the normalized terminal obs of done envs are in `terminal_obs_tensor`."""
+        obs, rew, term, trunc = self.venv.step_tensors(actions)
+        st = self.lib.he_vecnorm_step(ctypes.byref(self._params()), self.num_envs, self._p(obs), self._p(rew),
+                                      self._p(term), self._p(self.venv._tobs), self._p(self._returns),
+                                      self._p(self._stats), self._p(self._scratch), self._p(self._obs_out),
+                                      self._p(self._rew_out), self._p(self._tobs_out), self._p(self._ep_ret),
+                                      self._p(self._ep_len), self._p(self._ep_ret_done), self._p(self._ep_len_done),
+                                      self._stream())
+        self._check(st, "he_vecnorm_step")
+        return self._obs_out, self._rew_out, term, trunc
+
+    @property
+    def terminal_obs_tensor(self):
+        return self._tobs_out
+
+    def get_original_obs(self):
+        return self.venv._obs.cpu().numpy()
+
+    def get_original_reward(self):
+        return self.venv._rew.cpu().numpy()
+
+    # ------------------------------------------------------------------ SB3 VecEnv API
+    def reset(self):
+        obs = self.reset_tensors()
+        return obs.cpu().numpy() if self.return_numpy else obs
+
+    def step_async(self, actions):
+        self._actions_pending = actions
+
+    def step_wait(self):
+        actions, self._actions_pending = self._actions_pending, None
+        obs, rew, term, _ = self.step_tensors(actions)
+        if not self.return_numpy:
+            return obs, rew, term.bool(), InfoView(self.venv, None)
+        done = term.cpu().numpy().astype(bool)
+        infos = _NormInfoView(self, done)
+        if done.any():
+            infos._materialize_done(done)
+        return obs.cpu().numpy(), rew.cpu().numpy(), done, infos
+
+    def step(self, actions):
+        self.step_async(actions)
+        return self.step_wait()
+
+    def normalize_obs(self, obs):
+        """Host normalization with the current statistics (VecNormalize.normalize_obs)."""
+        if not self.norm_obs:
+            return np.array(obs, copy=True)
+        r = self.obs_rms
+        return np.clip((obs - r.mean) / np.sqrt(r.var + self.epsilon), -self.clip_obs, self.clip_obs).astype(np.float32)
+
+    def normalize_reward(self, reward):
+        if not self.norm_reward:
+            return reward
+        return np.clip(reward / np.sqrt(self.ret_rms.var + self.epsilon), -self.clip_reward, self.clip_reward)
+
+    def unnormalize_obs(self, obs):
+        if not self.norm_obs:
+            return np.array(obs, copy=True)
+        r = self.obs_rms
+        return (obs * np.sqrt(r.var + self.epsilon)) + r.mean
+
+    def get_attr(self, attr_name, indices=None):
+        return self.venv.get_attr(attr_name, indices)
+
+    def env_method(self, method_name, *args, indices=None, **kwargs):
+        return self.venv.env_method(method_name, *args, indices=indices, **kwargs)
+
+    def env_is_wrapped(self, wrapper_class, indices=None):
+        return self.venv.env_is_wrapped(wrapper_class, indices)
+
+    def seed(self, seed=None):
+        return self.venv.seed(seed)
+
+    def close(self):
+        self.venv.close()
+
+
+class _NormInfoView(InfoView):
+    """InfoView whose done rows carry the normalized terminal obs and the Monitor
+    episode from the device sums (Monitor.step: r, l, t + info_keywords)."""
+
+    def __init__(self, wrapper, done):
+        super().__init__(wrapper.venv, done)
+        self._w = wrapper
+
+    def _materialize_done(self, done):
+        w, v = self._w, self._w.venv
+        tobs = w._tobs_out.cpu().numpy()
+        er = w._ep_ret_done.cpu().numpy()
+        el = w._ep_len_done.cpu().numpy()
+        h = self._host_info()
+        for i in np.nonzero(done)[0]:
+            d = self[i]
+            d["terminal_observation"] = tobs[i].copy()
+            if v.monitor_keywords is not None:
+                ep = {"r": round(float(er[i]), 6), "l": int(el[i]), "t": round(time.time() - w._t_start, 6)}
+                for k in v.monitor_keywords:
+                    ep[k] = h[k][i].item() if k in h else None
+                d["episode"] = ep

@@ -291,6 +291,53 @@ he_status he_host_box_muller(const double* u1, const double* u2, int64_t count, 
 /* f32 twin for the obs quotients by per-handle constants (must equal IEEE a[k] / b). */
 he_status he_host_div_byf(const float* a, int64_t count, float b, float* out);
 
+/* ---- VecNormalize and Monitor on the device ---------------------------------------
+ * SB3 2.6.0 VecNormalize (+ RunningMeanStd) as wrapped around the env at
+ * train_ppo_v2.py:204,305,450, and Monitor's per-episode return / length (:119),
+ * restated from SB3's published algorithm (SB3 is not in this image: parity with
+ * it is unpinned; oracle/vecnorm_oracle.py restates it in NumPy).
+ *
+ * stats: device f64 [2 D + 4] = obs_mean[D], obs_var[D], obs_count, ret_mean, ret_var,
+ * ret_count (RunningMeanStd(shape=(D,)) and RunningMeanStd(shape=())).  The batch
+ * moments are exact two-pass f64 per block, merged in block order (deterministic). */
+typedef struct he_vecnorm_params {
+    int32_t obs_dim;        /* D; 13 (HE_OBS_DIM) is the one supported */
+    int32_t training;       /* update obs_rms / ret_rms / returns */
+    int32_t norm_obs;
+    int32_t norm_reward;
+    double gamma;           /* discount of the running return */
+    double clip_obs;        /* 10.0 */
+    double clip_reward;     /* 10.0 */
+    double epsilon;         /* 1e-8 */
+    int32_t reserved[4];
+} he_vecnorm_params;
+
+/* Sizes of the device buffers the caller owns. */
+int64_t he_vecnorm_stats_len(int32_t obs_dim);                 /* doubles: 2 D + 4 */
+int64_t he_vecnorm_scratch_bytes(int64_t n, int32_t obs_dim);
+
+/* RunningMeanStd init: means 0, variances 1, counts 1e-4. */
+he_status he_vecnorm_init(double* stats, int32_t obs_dim, void* stream);
+
+/* VecNormalize.step_wait on one batch of n envs (obs [n][D], reward [n] f32, done [n]):
+ * obs_rms.update(obs) (training && norm_obs); returns = returns * gamma + reward and
+ * ret_rms.update(returns) (training); obs_out = clip((obs - mean) / sqrt(var + eps));
+ * reward_out = clip(reward / sqrt(ret_var + eps)) (norm_reward, else a copy);
+ * terminal_obs_out[i] normalized for done rows (when both pointers are given);
+ * returns[done] = 0.  Monitor (ep_return / ep_length non-NULL): the raw rewards are
+ * summed per env, and a done row copies its episode's sum / length to
+ * ep_return_done / ep_length_done and restarts from 0. */
+he_status he_vecnorm_step(const he_vecnorm_params* p, int64_t n, const float* obs, const float* reward,
+                          const uint8_t* done, const float* terminal_obs, double* returns, double* stats,
+                          void* scratch, float* obs_out, float* reward_out, float* terminal_obs_out,
+                          double* ep_return, int32_t* ep_length, double* ep_return_done,
+                          int32_t* ep_length_done, void* stream);
+
+/* VecNormalize.reset: returns = 0; obs_rms.update(obs) (training && norm_obs);
+ * obs_out normalized (norm_obs, else a copy). */
+he_status he_vecnorm_reset(const he_vecnorm_params* p, int64_t n, const float* obs, double* returns,
+                           double* stats, void* scratch, float* obs_out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,100 @@
+"""DeviceVecNormalize (he_vecnorm_step / he_vecnorm_reset) against the SB3 2.6.0
+restatement, on raw obs / rewards / dones produced by the env on the GPU."""
+import numpy as np
+import pytest
+import torch
+
+from oracle.vecnorm_oracle import VecNormalizeOracle
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+KW = dict(loss_type="abs", pnl_penalty_weight=0.001, lambda_cost=0.0001, theta_weight=0.0002, slippage_bps=1.0)
+GEN = dict(s0=496.48001098632812, variance=0.029028, mu=0.04, dt=1 / 252, episode_length=12)
+
+
+def _env(n):
+    from cantorrl_amd.vec_env import HedgingVecEnv
+    return HedgingVecEnv(n, mode="gbm", generate=GEN, seed=7, device=DEV, return_numpy=False, info_keys=(), **KW)
+
+
+def _run(n, steps, training=True, norm_reward=True, gamma=0.95):
+    from cantorrl_amd.vec_normalize import DeviceVecNormalize
+    env = _env(n)
+    vn = DeviceVecNormalize(env, training=training, norm_reward=norm_reward, gamma=gamma)
+    ref = VecNormalizeOracle(n, training=training, norm_reward=norm_reward, gamma=gamma, moments="f64")
+    sb3 = VecNormalizeOracle(n, training=training, norm_reward=norm_reward, gamma=gamma, moments="sb3")
+    obs = vn.reset_tensors()
+    raw = env._obs.cpu().numpy()
+    np.testing.assert_allclose(obs.cpu().numpy(), ref.reset(raw), rtol=0, atol=2e-6)
+    sb3.reset(raw)
+    rng = np.random.default_rng(0)
+    for k in range(steps):
+        a = torch.as_tensor(rng.uniform(-1, 1, size=(n, 2)).astype(np.float32), device=DEV)
+        o, r, term, _ = vn.step_tensors(a)
+        raw_o, raw_r = env._obs.cpu().numpy(), env._rew.cpu().numpy()
+        done = term.cpu().numpy().astype(bool)
+        tobs = env._tobs.cpu().numpy()
+        eo, er, et, eps = ref.step(raw_o, raw_r, done, tobs)
+        so, sr, _, _ = sb3.step(raw_o, raw_r, done, tobs)
+        np.testing.assert_allclose(o.cpu().numpy(), eo, rtol=0, atol=2e-6, err_msg=f"obs step {k}")
+        np.testing.assert_allclose(r.cpu().numpy(), er.astype(np.float32), rtol=1e-6, atol=1e-7)
+        # SB3's literal calls take the batch mean / var of the f32 obs in f32 (NumPy
+        # reduces axis 0 row by row): that alone moves normalized values by up to ~1e-3
+        # at n = 1000 (measured 6.3e-4) and by 0.17 at n = 70,000 -- SB3's own rounding,
+        # which the f64 moments here do not have.  Compared at small n only; the f64
+        # restatement above is the tight check.
+        if n <= 4096:
+            np.testing.assert_allclose(o.cpu().numpy(), so, rtol=0, atol=2e-3)
+            np.testing.assert_allclose(r.cpu().numpy(), sr.astype(np.float32), rtol=1e-4, atol=1e-6)
+        if done.any():
+            to = vn.terminal_obs_tensor.cpu().numpy()
+            erd, eld = vn._ep_ret_done.cpu().numpy(), vn._ep_len_done.cpu().numpy()
+            for i, t in et.items():
+                np.testing.assert_allclose(to[i], t, rtol=0, atol=2e-6)
+                assert erd[i] == eps[i][0] and eld[i] == eps[i][1]
+    rms, ret = vn.obs_rms, vn.ret_rms
+    np.testing.assert_allclose(rms.mean, ref.obs_rms.mean, rtol=1e-10, atol=1e-12)
+    np.testing.assert_allclose(rms.var, ref.obs_rms.var, rtol=1e-8, atol=1e-14)
+    assert abs(rms.count - ref.obs_rms.count) < 1e-6
+    np.testing.assert_allclose(ret.var, ref.ret_rms.var, rtol=1e-9)
+    np.testing.assert_allclose(vn.returns, ref.returns, rtol=1e-12, atol=1e-15)
+    return vn
+
+
+@pytest.mark.parametrize("n", [1000, 70000])
+def test_device_vecnormalize_matches_restatement(n):
+    _run(n, 30)
+
+
+def test_device_vecnormalize_eval_mode_freezes_stats():
+    vn = _run(512, 14, training=False, norm_reward=False)
+    r = vn.obs_rms
+    np.testing.assert_array_equal(r.mean, np.zeros(13))
+    np.testing.assert_array_equal(r.var, np.ones(13))
+
+
+def test_sb3_api_and_save_load(tmp_path):
+    from cantorrl_amd.vec_env import HedgingVecEnv
+    from cantorrl_amd.vec_normalize import DeviceVecNormalize
+    env = HedgingVecEnv(64, mode="gbm", generate=GEN, seed=3, device=DEV,
+                        monitor_keywords=("per_share_step_pnl",), **KW)
+    vn = DeviceVecNormalize(env, gamma=0.9)
+    obs = vn.reset()
+    assert obs.shape == (64, 13) and obs.dtype == np.float32
+    seen = 0
+    for _ in range(13):
+        obs, rew, done, infos = vn.step(np.zeros((64, 2), np.float32))
+        for i in np.nonzero(done)[0]:
+            ep = infos[i]["episode"]
+            assert ep["l"] == 12 and "per_share_step_pnl" in ep
+            assert infos[i]["terminal_observation"].shape == (13,)
+            seen += 1
+    assert seen == 64
+    vn.save(str(tmp_path / "vn.npz"))
+    vn2 = DeviceVecNormalize.load(str(tmp_path / "vn.npz"), env)
+    np.testing.assert_array_equal(vn2.obs_rms.mean, vn.obs_rms.mean)
+    np.testing.assert_array_equal(vn2.ret_rms.var, vn.ret_rms.var)
+    o = vn.get_original_obs()
+    np.testing.assert_allclose(vn.normalize_obs(o), np.clip((o - vn.obs_rms.mean) / np.sqrt(vn.obs_rms.var + 1e-8),
+                                                            -10, 10).astype(np.float32))
+    vn.close()
