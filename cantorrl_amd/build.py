@@ -31,8 +31,9 @@ RB_SRC = os.path.join(HERE, "csrc", "rbergomi.hip")
 RB_DEPS = [RB_SRC, os.path.join(HERE, "csrc", "he_math.h"), os.path.join(REPO, "include", "rbergomi.h")]
 RB_OUT = os.path.join(HERE, "lib", "librbergomi.so")
 VN_SRC = os.path.join(HERE, "csrc", "vecnorm.hip")
-DEPS = DEPS + [VN_SRC]
-TARGETS = [([SRC, VN_SRC], DEPS, OUT), ([RB_SRC], RB_DEPS, RB_OUT)]
+AN_SRC = os.path.join(HERE, "csrc", "analytics.hip")
+DEPS = DEPS + [VN_SRC, AN_SRC]
+TARGETS = [([SRC, VN_SRC, AN_SRC], DEPS, OUT), ([RB_SRC], RB_DEPS, RB_OUT)]
 
 
 def needs_build(out=OUT, deps=DEPS):
@@ -60,7 +61,7 @@ def build(force=False, verbose=False):
 def build_variant(out, extra_flags):
     """Diagnostic / A-B builds (e.g. -DHE_TIMING) outside the package directory."""
     os.makedirs(os.path.dirname(os.path.abspath(out)), exist_ok=True)
-    subprocess.run([HIPCC, *FLAGS, *extra_flags, "-o", out, SRC, VN_SRC], check=True)
+    subprocess.run([HIPCC, *FLAGS, *extra_flags, "-o", out, SRC, VN_SRC, AN_SRC], check=True)
     return out
 
 

@@ -338,6 +338,25 @@ he_status he_vecnorm_step(const he_vecnorm_params* p, int64_t n, const float* ob
 he_status he_vecnorm_reset(const he_vecnorm_params* p, int64_t n, const float* obs, double* returns,
                            double* stats, void* scratch, float* obs_out, void* stream);
 
+/* ---- Offline analytics over price paths -------------------------------------------
+ * paths: device f64 [n_paths][n_cols] (row-major, the NPZ / .npy layout).
+ * One thread per path scans the columns once: the expanding-window realized
+ * volatility is a running (Welford) mean / M2 of the log returns, so the reference's
+ * O(n_cols^2) per path becomes O(n_cols). */
+
+/* src/sim/option_price_assignment.py:10-52: vols[:, t] = std(log returns of
+ * paths[:, :t+1], ddof=1) * sqrt(252) (0 at t = 0, NaN at t = 1 as NumPy gives), and
+ * the fixed-strike European Black-Scholes marks with K = rint(paths[:, 0]),
+ * T = max(1 - t/252, 0), rate r.  vols may be NULL. */
+he_status he_fixed_european_marks(const double* paths, int64_t n_paths, int32_t n_cols, double r, double* vols,
+                                  double* calls, double* puts, void* stream);
+
+/* src/tools/bs_delta.py:36-55: a daily Black-Scholes delta hedge of a call struck at
+ * paths[:, 0] expiring at n_cols * dt, with the realized volatility of the path so far;
+ * pnl[:, t] = cash + delta * S - call after the rebalance at t. */
+he_status he_bs_delta_hedge(const double* paths, int64_t n_paths, int32_t n_cols, double r, double dt, double* pnl,
+                            void* stream);
+
 #ifdef __cplusplus
 }
 #endif
