@@ -26,7 +26,7 @@ namespace {
 
 constexpr int kD = HE_OBS_DIM;
 constexpr int kVnThreads = 256;
-constexpr int kVnMaxBlocks = 512;
+constexpr int kVnMaxBlocks = 64;    // the last block stages all partials in LDS and merges them serially
 
 // scratch layout: [blocks][kPart] doubles, then one u32 ticket
 constexpr int kPart = 2 * kD + 3;   // count, mean[D], M2[D], ret_mean, ret_M2
@@ -55,17 +55,27 @@ struct VnArgs {
     int reset;   // he_vecnorm_reset: returns = 0 instead of the discounted update
 };
 
-__device__ __forceinline__ double block_sum(double v, double* sh) {
+// Sum of s[0..kD] over the block into out[0..kD] (LDS): a wave-level butterfly per
+// column, then one barrier and a 4-way sum -- two barriers for all 14 columns.
+__device__ __forceinline__ void block_sum_cols(double* s, double (*sh)[kD + 1], double* out) {
 #pragma unroll
-    for (int s = 32; s >= 1; s >>= 1) v += __shfl_xor(v, s, 64);
+    for (int c = 0; c <= kD; ++c) {
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) s[c] += __shfl_xor(s[c], m, 64);
+    }
     const int w = threadIdx.x >> 6;
-    __syncthreads();
-    if ((threadIdx.x & 63) == 0) sh[w] = v;
-    __syncthreads();
-    double t = 0.0;
+    if ((threadIdx.x & 63) == 0) {
 #pragma unroll
-    for (int i = 0; i < kVnThreads / 64; ++i) t += sh[i];
-    return t;
+        for (int c = 0; c <= kD; ++c) sh[w][c] = s[c];
+    }
+    __syncthreads();
+    if (threadIdx.x <= kD) {
+        double t = 0.0;
+#pragma unroll
+        for (int i = 0; i < kVnThreads / 64; ++i) t += sh[i][threadIdx.x];
+        out[threadIdx.x] = t;
+    }
+    __syncthreads();
 }
 
 // RunningMeanStd.update_from_moments (SB3 common/running_mean_std.py), f64
@@ -83,8 +93,9 @@ __device__ __forceinline__ void rms_update(double* mean, double* var, double* co
 }
 
 __global__ void __launch_bounds__(kVnThreads) moments_kernel(VnArgs a) {
-    __shared__ double sh[kVnThreads / 64];
+    __shared__ double sh[kVnThreads / 64][kD + 1];
     __shared__ double smean[kD + 1];
+    __shared__ double sm2[kD + 1];
     __shared__ bool last;
     const int b = blockIdx.x;
     const int64_t r0 = (int64_t)b * a.rows_per_block;
@@ -105,11 +116,8 @@ __global__ void __launch_bounds__(kVnThreads) moments_kernel(VnArgs a) {
             s[kD] += ret;
         }
     }
-#pragma unroll
-    for (int c = 0; c <= kD; ++c) {
-        const double t = block_sum(s[c], sh);
-        if (threadIdx.x == 0) smean[c] = (cnt > 0.0) ? t / cnt : 0.0;
-    }
+    block_sum_cols(s, sh, smean);
+    if (threadIdx.x <= kD) smean[threadIdx.x] = (cnt > 0.0) ? smean[threadIdx.x] / cnt : 0.0;
     __syncthreads();
     // pass 2: sums of squared deviations from the block means
 #pragma unroll
@@ -127,20 +135,14 @@ __global__ void __launch_bounds__(kVnThreads) moments_kernel(VnArgs a) {
             s[kD] += d * d;
         }
     }
+    block_sum_cols(s, sh, sm2);
     double* part = a.part + (int64_t)b * kPart;
-#pragma unroll
-    for (int c = 0; c <= kD; ++c) {
-        const double t = block_sum(s[c], sh);
-        if (threadIdx.x == 0) {
-            if (c < kD) {
-                part[1 + c] = smean[c];
-                part[1 + kD + c] = t;
-            } else {
-                part[1 + 2 * kD] = smean[kD];
-                part[2 + 2 * kD] = t;
-            }
-        }
+    if (threadIdx.x <= kD) {
+        const int c = threadIdx.x;
+        part[(c < kD) ? 1 + c : 1 + 2 * kD] = smean[c];
+        part[(c < kD) ? 1 + kD + c : 2 + 2 * kD] = sm2[c];
     }
+    __syncthreads();
     if (threadIdx.x == 0) {
         part[0] = cnt;
         __threadfence();
@@ -148,27 +150,55 @@ __global__ void __launch_bounds__(kVnThreads) moments_kernel(VnArgs a) {
     }
     __syncthreads();
     if (!last) return;
-    // the last block: merge the partials in block order, one thread per column; the
-    // D obs columns share one count, read before anyone writes it
+    // the last block: stage every block's partials in LDS (parallel loads), then merge
+    // them in block order, one thread per column; the D obs columns share one count,
+    // read before anyone writes it
     __threadfence();
+    __shared__ double sp[kVnMaxBlocks * kPart];
+    {
+        const volatile double* P = a.part;
+        for (int k = threadIdx.x; k < a.blocks * kPart; k += kVnThreads) sp[k] = P[k];
+    }
     const double obs_count0 = a.stats[2 * kD];
     __syncthreads();
     const int c = threadIdx.x;
     if (c <= kD) {
-        const volatile double* P = a.part;
-        double n_a = 0.0, mean_a = 0.0, m2_a = 0.0;
+        // exact merge, two passes over the staged partials in block order: the batch
+        // mean from the block sums, then M2 = sum_b M2_b + n_b (mean_b - mean)^2
         const int mi = (c < kD) ? 1 + c : 1 + 2 * kD;
         const int qi = (c < kD) ? 1 + kD + c : 2 + 2 * kD;
-        for (int k = 0; k < a.blocks; ++k) {
-            const double n_b = P[(int64_t)k * kPart];
-            if (n_b == 0.0) continue;
-            const double mean_b = P[(int64_t)k * kPart + mi], m2_b = P[(int64_t)k * kPart + qi];
-            const double n_ab = n_a + n_b;
-            const double delta = mean_b - mean_a;
-            mean_a = mean_a + delta * (n_b / n_ab);
-            m2_a = m2_a + m2_b + delta * delta * (n_a * n_b / n_ab);
-            n_a = n_ab;
+        // four interleaved accumulators (k mod 4), combined in a fixed order: the LDS
+        // reads of a chain are independent, so the loop is not latency-bound
+        double n4[4] = {0.0, 0.0, 0.0, 0.0}, s4[4] = {0.0, 0.0, 0.0, 0.0};
+        int k = 0;
+        for (; k + 4 <= a.blocks; k += 4) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const double n_b = sp[(k + u) * kPart];
+                n4[u] += n_b;
+                s4[u] = fma(n_b, sp[(k + u) * kPart + mi], s4[u]);
+            }
         }
+        for (; k < a.blocks; ++k) {
+            const double n_b = sp[k * kPart];
+            n4[0] += n_b;
+            s4[0] = fma(n_b, sp[k * kPart + mi], s4[0]);
+        }
+        const double n_a = (n4[0] + n4[1]) + (n4[2] + n4[3]);
+        const double mean_a = ((s4[0] + s4[1]) + (s4[2] + s4[3])) / n_a;
+        double q4[4] = {0.0, 0.0, 0.0, 0.0};
+        for (k = 0; k + 4 <= a.blocks; k += 4) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const double d = sp[(k + u) * kPart + mi] - mean_a;
+                q4[u] += sp[(k + u) * kPart + qi] + sp[(k + u) * kPart] * (d * d);
+            }
+        }
+        for (; k < a.blocks; ++k) {
+            const double d = sp[k * kPart + mi] - mean_a;
+            q4[0] += sp[k * kPart + qi] + sp[k * kPart] * (d * d);
+        }
+        const double m2_a = (q4[0] + q4[1]) + (q4[2] + q4[3]);
         // np.mean / np.var(ddof=0) of the batch, then update_from_moments (:update)
         if (c < kD) {
             if (a.upd_obs) {
@@ -234,7 +264,7 @@ __global__ void __launch_bounds__(kVnThreads) apply_kernel(VnArgs a) {
 }
 
 int blocks_for(int64_t n) {
-    int64_t b = (n + kVnThreads - 1) / kVnThreads;
+    int64_t b = (n + 4 * kVnThreads - 1) / (4 * kVnThreads);   // >= 4 rows per thread
     if (b > kVnMaxBlocks) b = kVnMaxBlocks;
     return (int)(b < 1 ? 1 : b);
 }

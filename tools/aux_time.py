@@ -1,0 +1,77 @@
+"""Device time of the auxiliary kernels: DeviceVecNormalize per step at 65,536 envs
+(he_vecnorm_step: moments + apply) and the path analytics at 1M paths x 253 columns."""
+import ctypes
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from cantorrl_amd import _lib, analytics as an  # noqa: E402
+from cantorrl_amd.vec_env import HedgingVecEnv  # noqa: E402
+from cantorrl_amd.vec_normalize import DeviceVecNormalize  # noqa: E402
+
+dev = "cuda:0"
+KW = dict(loss_type="abs", pnl_penalty_weight=0.001, lambda_cost=0.0001, theta_weight=0.0002, slippage_bps=1.0)
+GEN = dict(s0=496.48001098632812, variance=0.029028, mu=0.04, dt=1 / 252, episode_length=252)
+
+
+def ev():
+    return torch.cuda.Event(enable_timing=True)
+
+
+n = 65536
+env = HedgingVecEnv(n, mode="gbm", generate=GEN, seed=1, device=dev, return_numpy=False, info_keys=(), **KW)
+vn = DeviceVecNormalize(env)
+vn.reset_tensors()
+acts = torch.rand((64, n, 2), device=dev) * 2 - 1
+for k in range(16):
+    vn.step_tensors(acts[k])
+torch.cuda.synchronize()
+lib = env.lib
+p = vn._params()
+P = vn._p
+args = [ctypes.byref(p), n, P(env._obs), P(env._rew), P(env._term), P(env._tobs), P(vn._returns), P(vn._stats),
+        P(vn._scratch), P(vn._obs_out), P(vn._rew_out), P(vn._tobs_out), P(vn._ep_ret), P(vn._ep_len),
+        P(vn._ep_ret_done), P(vn._ep_len_done), vn._stream()]
+e0, e1 = ev(), ev()
+e0.record()
+R = 200
+for _ in range(R):
+    lib.he_vecnorm_step(*args)
+e1.record()
+torch.cuda.synchronize()
+us = e0.elapsed_time(e1) * 1e3 / R
+print(f"he_vecnorm_step n={n}: {us:.2f} us/step (moments + apply), {n * 68 / (us * 1e-6) / 1e9:.1f} GB/s of obs+reward "
+      f"in/out", flush=True)
+# env step + vecnorm, one launch each
+e0.record()
+for k in range(64):
+    vn.step_tensors(acts[k])
+e1.record()
+torch.cuda.synchronize()
+print(f"env he_step + vecnorm, eager: {e0.elapsed_time(e1) * 1e3 / 64:.2f} us/step", flush=True)
+env.close()
+
+g = torch.Generator(device=dev).manual_seed(0)
+N, T1 = 1 << 20, 253
+inc = torch.randn((N, T1), generator=g, device=dev, dtype=torch.float64) * 0.01
+inc[:, 0] = 0
+paths = 100 * torch.exp(torch.cumsum(inc, dim=1))
+del inc
+an.fixed_european_marks(paths, device=dev)
+an.bs_delta_hedge(paths, device=dev)
+torch.cuda.synchronize()
+for name, fn in (("he_fixed_european_marks", lambda: an.fixed_european_marks(paths, device=dev)),
+                 ("he_bs_delta_hedge", lambda: an.bs_delta_hedge(paths, device=dev))):
+    e0.record()
+    for _ in range(3):
+        out = fn()
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / 3
+    el = N * T1
+    print(f"{name} {N} paths x {T1}: {ms:.2f} ms  {el / (ms * 1e-3):.3g} path-columns/s", flush=True)
+    del out
