@@ -77,6 +77,7 @@ constexpr int64_t kPrefetchMinEnvs = 131072;  // auto prefetch for single steps 
 struct BookOpt {
     int32_t type, expiry;
     double K, H, q100;
+    double lnK, lnH, lnH2K;   // log K, log H, 2 log H - log K (host)
 };
 
 struct Params {
@@ -126,6 +127,7 @@ struct Params {
     // liability book (generate modes)
     int32_t book_n;
     const BookOpt* book;    // device copy [book_n], read through the scalar cache
+    const double* book_tab; // [m][3] = {sqrt(m dt), 1 / sqrt(m dt), exp(-r m dt)}, m = 0..max expiry
     double book_rst;        // book value of the reset market (t = 0, S0, v0)
     double* tileC;          // [M+1][N] f64 book value of every slot
 #ifdef HE_TIMING
@@ -382,21 +384,42 @@ __device__ __forceinline__ void marks(const Params& p, double S64, double var64,
 // (option_calculator.py:11-27, intrinsic when tau <= 0 or sig <= 0).  Up-and-out call
 // (q = 0, Hull, "Options, Futures and Other Derivatives", barrier options):
 // c_uo = c - c_ui, worthless once S touched H at a step date or when H <= K.
-__device__ __forceinline__ double book_option(const BookOpt& o, double S, double sig, double tau, double r,
+// tab[m] = {sqrt(m dt), 1 / sqrt(m dt), exp(-r m dt)} (tau = m dt as in book_option)
+__global__ void book_tab_kernel(double* tab, int32_t n, double dt, double r) {
+    const int m = blockIdx.x * blockDim.x + threadIdx.x;
+    if (m >= n) return;
+    const double tau = (double)m * dt;
+    const double sq = sqrt(tau);
+    tab[3 * m] = sq;
+    tab[3 * m + 1] = 1.0 / sq;
+    tab[3 * m + 2] = exp(-r * tau);
+}
+
+// Per env-step constants shared by the book's options: log S once (log(S/K) =
+// log S - log K), 1/sigma, and lam of the barrier formula; per option the
+// tau-dependent sqrt(tau), 1/sqrt(tau) and exp(-r tau) come from a table indexed by
+// the remaining steps m = expiry - t (tau = m dt, the same f64 product as before).
+struct BookEnv {
+    double S, lnS, sig, isig, s2, lam;
+};
+
+__device__ __forceinline__ double book_option(const Params& p, const BookOpt& o, const BookEnv& b, int32_t m,
                                               double runmax) {
     if (o.type == HE_BOOK_UO_CALL && runmax >= o.H) return 0.0;
-    const double K = o.K;
-    if (tau <= 0.0 || sig <= 0.0) {
+    const double K = o.K, S = b.S, r = p.r_d;
+    if (m <= 0 || b.sig <= 0.0) {   // tau = m dt <= 0
         const double ic = S - K, ip = K - S;
         if (o.type == HE_BOOK_PUT) return (ip < 0.0) ? 0.0 : ip;
         return (ic < 0.0) ? 0.0 : ic;
     }
     if (o.type == HE_BOOK_UO_CALL && o.H <= K) return 0.0;
-    const double s2 = sig * sig;
-    const double sst = sig * sqrt(tau);
-    const double d1 = (log(S / K) + (r + 0.5 * s2) * tau) / sst;
+    const double tau = (double)m * p.dt;
+    const double* e = p.book_tab + 3 * m;
+    const double sst = b.sig * e[0];
+    const double isst = b.isig * e[1];
+    const double d1 = ((b.lnS - o.lnK) + (r + 0.5 * b.s2) * tau) * isst;
     const double d2 = d1 - sst;
-    const double Kd = K * exp(-r * tau);
+    const double Kd = K * e[2];
     double n1, m1, n2, m2;
     ndtr_pair(d1, &n1, &m1);
     ndtr_pair(d2, &n2, &m2);
@@ -406,15 +429,13 @@ __device__ __forceinline__ double book_option(const BookOpt& o, double S, double
     } else {
         v = S * n1 - Kd * n2;
         if (o.type == HE_BOOK_UO_CALL) {
-            const double H = o.H;
-            const double lam = (r + 0.5 * s2) / s2;
-            const double ls = lam * sst;
-            const double lhs = log(H / S);
-            const double x1 = log(S / H) / sst + ls;
-            const double y = log((H * H) / (S * K)) / sst + ls;
-            const double y1 = lhs / sst + ls;
-            const double p2l = exp((2.0 * lam) * lhs);          // (H/S)^(2 lam)
-            const double p2l2 = exp((2.0 * lam - 2.0) * lhs);   // (H/S)^(2 lam - 2)
+            const double ls = b.lam * sst;
+            const double lhs = o.lnH - b.lnS;                    // log(H / S)
+            const double x1 = -lhs * isst + ls;                  // log(S / H) / sst + lam sst
+            const double y = (o.lnH2K - b.lnS) * isst + ls;      // log(H^2 / (S K)) / sst + lam sst
+            const double y1 = lhs * isst + ls;
+            const double p2l = exp((2.0 * b.lam) * lhs);          // (H/S)^(2 lam)
+            const double p2l2 = exp((2.0 * b.lam - 2.0) * lhs);   // (H/S)^(2 lam - 2)
             const double cui = S * ndtr(x1) - Kd * ndtr(x1 - sst) - S * p2l * (ndtr(-y) - ndtr(-y1)) +
                                Kd * p2l2 * (ndtr(-y + sst) - ndtr(-y1 + sst));
             v = v - cui;
@@ -426,12 +447,17 @@ __device__ __forceinline__ double book_option(const BookOpt& o, double S, double
 // sum_k q_k * 100 * V_k after step t of the episode (variance var: GBM constant,
 // Heston the env's v_t).
 __device__ __forceinline__ double book_value(const Params& p, double S, double var, int32_t t, double runmax) {
-    const double sig = sqrt(var < 0.0 ? 0.0 : var);
+    BookEnv b;
+    b.S = S;
+    b.lnS = log(S);
+    b.sig = sqrt(var < 0.0 ? 0.0 : var);
+    b.isig = 1.0 / b.sig;
+    b.s2 = b.sig * b.sig;
+    b.lam = (p.r_d + 0.5 * b.s2) / b.s2;
     double B = 0.0;
     for (int k = 0; k < p.book_n; ++k) {
         const BookOpt o = p.book[k];
-        const double tau = (double)(o.expiry - t) * p.dt;
-        B = B + o.q100 * book_option(o, S, sig, tau, p.r_d, runmax);
+        B = B + o.q100 * book_option(p, o, b, o.expiry - t, runmax);
     }
     return B;
 }
@@ -1399,6 +1425,7 @@ struct he_env {
     float* rst = nullptr;     // reset market + obs (generate)
     Params* dparams = nullptr;  // device copies of tile_params(env, 0 / 1) for step1_kernel
     BookOpt* dbook = nullptr;   // liability book, device copy (generate modes)
+    double* dbook_tab = nullptr;  // book tau table (book_option)
     unsigned long long* scratch_count = nullptr;  // he_rollout_policy without records
     double book_rst = 0.0;      // book value of the reset market (host copy)
     int64_t n_paths = 0;
@@ -1532,6 +1559,7 @@ static void fill_params(he_env* env) {
     p.recg = env->recg;
     p.book_n = is_generate(env) ? c.book_size : 0;
     p.book = env->dbook;
+    p.book_tab = env->dbook_tab;
     p.book_rst = env->book_rst;
     p.tileC = nullptr;
 #ifdef HE_TIMING
@@ -1946,9 +1974,19 @@ he_status he_create(const he_config* cfg, he_env** out) {
             hb[k].K = c.book[k].strike;
             hb[k].H = c.book[k].barrier;
             hb[k].q100 = c.book[k].quantity * 100.0;
+            hb[k].lnK = log(hb[k].K);
+            hb[k].lnH = log(hb[k].H);
+            hb[k].lnH2K = 2.0 * hb[k].lnH - hb[k].lnK;
         }
         HE_HIP(env, hipMalloc(&env->dbook, HE_BOOK_MAX * sizeof(BookOpt)));
         HE_HIP(env, hipMemcpy(env->dbook, hb, c.book_size * sizeof(BookOpt), hipMemcpyHostToDevice));
+        int32_t max_exp = 1;
+        for (int k = 0; k < c.book_size; ++k) max_exp = (c.book[k].expiry > max_exp) ? c.book[k].expiry : max_exp;
+        HE_HIP(env, hipMalloc(&env->dbook_tab, (size_t)3 * (size_t)(max_exp + 1) * sizeof(double)));
+        hipLaunchKernelGGL(book_tab_kernel, dim3((unsigned)((max_exp + 256) / 256)), dim3(256), 0, 0, env->dbook_tab,
+                           max_exp + 1, c.dt, c.risk_free_rate);
+        HE_HIP(env, hipGetLastError());
+        HE_HIP(env, hipDeviceSynchronize());
     }
     he_status st = upload_tables(env);
     if (st != HE_OK) return st;
@@ -1973,6 +2011,7 @@ he_status he_destroy(he_env* env) {
         if (env->rst) (void)hipFree(env->rst);
         if (env->dparams) (void)hipFree(env->dparams);
         if (env->dbook) (void)hipFree(env->dbook);
+        if (env->dbook_tab) (void)hipFree(env->dbook_tab);
         if (env->scratch_count) (void)hipFree(env->scratch_count);
         if (env->xs) {
             (void)hipStreamSynchronize(env->xs);
