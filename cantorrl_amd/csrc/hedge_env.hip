@@ -403,6 +403,23 @@ struct BookEnv {
     double S, lnS, sig, isig, s2, lam;
 };
 
+// (N(a), N(-a)) from one erfc(|a|/sqrt2) on every lane.  ndtr_pair's erf branch for
+// |a| < 1 would make a wave of mixed d's run both branches; the book (an extension
+// without a reference, checked against oracle/hedging_oracle.py through the P&L in
+// tests/test_gpu_parity.py) takes the erfc form throughout: the same values to
+// ~1e-16 absolute.
+__device__ __forceinline__ void ncdf_pair(double a, double* pos, double* neg) {
+    const double y = 0.5 * erfc(fabs(a) * 0.70710678118654752440);
+    const bool p = a > 0.0;
+    *pos = p ? 1.0 - y : y;
+    *neg = p ? y : 1.0 - y;
+}
+
+__device__ __forceinline__ double ncdf(double a) {
+    const double y = 0.5 * erfc(fabs(a) * 0.70710678118654752440);
+    return (a > 0.0) ? 1.0 - y : y;
+}
+
 __device__ __forceinline__ double book_option(const Params& p, const BookOpt& o, const BookEnv& b, int32_t m,
                                               double runmax) {
     if (o.type == HE_BOOK_UO_CALL && runmax >= o.H) return 0.0;
@@ -421,8 +438,8 @@ __device__ __forceinline__ double book_option(const Params& p, const BookOpt& o,
     const double d2 = d1 - sst;
     const double Kd = K * e[2];
     double n1, m1, n2, m2;
-    ndtr_pair(d1, &n1, &m1);
-    ndtr_pair(d2, &n2, &m2);
+    ncdf_pair(d1, &n1, &m1);
+    ncdf_pair(d2, &n2, &m2);
     double v;
     if (o.type == HE_BOOK_PUT) {
         v = Kd * m2 - S * m1;
@@ -436,8 +453,8 @@ __device__ __forceinline__ double book_option(const Params& p, const BookOpt& o,
             const double y1 = lhs * isst + ls;
             const double p2l = exp((2.0 * b.lam) * lhs);          // (H/S)^(2 lam)
             const double p2l2 = exp((2.0 * b.lam - 2.0) * lhs);   // (H/S)^(2 lam - 2)
-            const double cui = S * ndtr(x1) - Kd * ndtr(x1 - sst) - S * p2l * (ndtr(-y) - ndtr(-y1)) +
-                               Kd * p2l2 * (ndtr(-y + sst) - ndtr(-y1 + sst));
+            const double cui = S * ncdf(x1) - Kd * ncdf(x1 - sst) - S * p2l * (ncdf(-y) - ncdf(-y1)) +
+                               Kd * p2l2 * (ncdf(-y + sst) - ncdf(-y1 + sst));
             v = v - cui;
         }
     }
