@@ -190,3 +190,28 @@ def test_npz_round_trip_into_replay_env(tmp_path):
         obs, rew, done, _info = env.step(np.zeros((4, 2), np.float32))
     assert np.isfinite(obs).all() and np.isfinite(rew).all()
     env.close()
+
+
+def test_inf_on_generated_dataset(tmp_path):
+    """src/agents/test_inf.py on our own rBergomi data: the v1 env with its parameters
+    (tcpc 0.05, lambda 1.0, 10,000 shares, 200 contracts) replays the generated NPZ
+    under random actions; every reward and obs stays finite (here 2,048 envs x 600
+    steps = 1.2M env-steps instead of 10k)."""
+    import torch
+    from cantorrl_amd.vec_env import HedgingVecEnv
+    rb = _rb()
+    res = rb.generate_paths_and_options(_history(), 64, n_mc=256, device=DEV, seed=5)
+    f = tmp_path / "paths_rbergomi_options.npz"
+    rb.save_npz(str(f), res)
+    env = HedgingVecEnv(2048, str(f), variant=1, device=DEV, seed=0, return_numpy=False, info_keys=(),
+                        transaction_cost_per_contract=0.05, lambda_cost=1.0, shares_to_hedge=10_000,
+                        max_contracts_held_per_type=200)
+    env.reset_tensors()
+    g = torch.Generator(device=DEV).manual_seed(1)
+    bad = 0
+    for _ in range(600):
+        a = torch.rand((2048, 2), generator=g, device=DEV) * 2 - 1
+        obs, rew, term, _ = env.step_tensors(a)
+        bad += int((~torch.isfinite(rew)).sum()) + int((~torch.isfinite(obs)).sum())
+    env.close()
+    assert bad == 0
