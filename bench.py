@@ -414,15 +414,17 @@ def roofline(mode, n, kern_ms, rk, book=False):
 RB_MC, RB_DAYS = 5000, 252
 
 
-def rb_cpu_baseline(seconds, base):
-    """The oracle's restatement of price_rbergomi_option_gpu (rbergomi_sim.py:261-306,
-    NumPy FFTs, 1 thread) on batches of 8 options x 5000 MC paths."""
+def _rb_cpu_sample(seconds, base, seed=0, barrier=None):
+    """One host core: the oracle's restatement of price_rbergomi_option_gpu
+    (rbergomi_sim.py:261-306, NumPy FFTs) on batches of 8 options x 5000 MC paths."""
     from oracle import rbergomi_oracle as orc
-    rng = np.random.default_rng(0)
+    rng = np.random.default_rng(seed)
     B = 8
     S0 = np.full(B, base[0])
     K = np.round(S0)
     xi, H, eta, rho = (np.full(B, base[k]) for k in (1, 2, 3, 4))
+    if barrier is not None:
+        barrier.wait()
     n = 0
     t0 = time.perf_counter()
     while True:
@@ -432,9 +434,31 @@ def rb_cpu_baseline(seconds, base):
         el = time.perf_counter() - t0
         if el >= seconds:
             break
-    return dict(value=n / el, unit="options/s", cores=1, kind="port",
-                sample=f"oracle/rbergomi_oracle.py price_options (the reference's FFT form), {n} options x "
-                       f"{RB_MC} MC paths in batches of {B} ({el:.1f} s, 1 thread, NumPy)")
+    return n, el
+
+
+def _rb_pool_task(a):
+    return _rb_cpu_sample(a[0], a[1], a[2], _BARRIER)
+
+
+def rb_cpu_baseline(seconds, base):
+    """1 thread and one process per granted host core (forked before GPU init)."""
+    import multiprocessing as mp
+    n1, el1 = _rb_cpu_sample(seconds, base)
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count() or 1
+    procs = max(1, min(avail, 16))
+    ctx = mp.get_context("fork")
+    b = ctx.Barrier(procs)
+    with ctx.Pool(procs, initializer=_pool_init, initargs=(b,)) as pool:
+        res = pool.map(_rb_pool_task, [(seconds, tuple(base), i + 1) for i in range(procs)])
+    return dict(value=sum(n / e for n, e in res), unit="options/s", cores=procs, kind="port",
+                sample=f"oracle/rbergomi_oracle.py price_options (the reference's FFT form), batches of 8 options x "
+                       f"{RB_MC} MC paths, {procs} processes x {seconds:.0f} s (NumPy, 1 thread each)",
+                single_core_value=n1 / el1,
+                single_core_sample=f"{n1} options in {el1:.1f} s, 1 thread")
 
 
 def rbergomi_main(args):
