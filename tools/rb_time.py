@@ -1,12 +1,13 @@
 """Time the rBergomi MC marks kernel (rb_price_atm_marks) on one GPU: options/s for
 f64 and f32 normals at a bounded number of paths."""
+import os
 import sys
 import time
 
 import numpy as np
 import torch
 
-sys.path.insert(0, ".")
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from cantorrl_amd import rbergomi as rb  # noqa: E402
 
 P = int(sys.argv[1]) if len(sys.argv) > 1 else 512
@@ -14,7 +15,7 @@ if len(sys.argv) > 2:          # A/B: an alternative build of librbergomi
     rb.load(sys.argv[2])
     print("lib", sys.argv[2])
 dev = "cuda:0"
-hist = np.load("tests/golden/rb_estimate.npz")["hist__prices"]
+hist = np.load(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "golden", "rb_estimate.npz"))["hist__prices"]
 base = rb.estimate_base_params(hist)
 for normals in ("f32", "f64"):
     cfg = rb.make_config(P, normals=normals)
