@@ -153,3 +153,15 @@ def test_host_normals_are_the_env_box_muller():
     other = np.zeros(1000)
     lib.rb_host_normals(42, 3, 5, 8, 0, other.size, other.ctypes.data)
     assert not np.array_equal(other, again)
+
+
+def test_library_exports_every_header_symbol():
+    import re
+    txt = open(os.path.join(os.path.dirname(os.path.dirname(__file__)), "include", "rbergomi.h")).read()
+    syms = sorted(set(re.findall(r"^\S[^;(]*?\b(rb_\w+)\s*\(", txt, flags=re.M)))
+    rb = _rb()
+    lib = rb.load()
+    assert len(syms) >= 10, syms
+    for s in syms:
+        assert hasattr(lib, s), f"librbergomi does not export {s}"
+    assert set(syms) == set(rb.EXPORTS)
