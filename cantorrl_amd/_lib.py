@@ -115,7 +115,7 @@ EXPORTS = [
     "he_num_episodes", "he_get_config", "he_state_size", "he_get_state", "he_set_state",
     "he_pcg64_seed_state", "he_host_episode_draws", "he_host_philox", "he_host_div_by", "he_host_div_byf", "he_time_next_step", "he_rollout_policy", "he_host_box_muller",
     "he_sync_market", "he_vecnorm_stats_len", "he_vecnorm_scratch_bytes", "he_vecnorm_init", "he_vecnorm_step",
-    "he_vecnorm_reset", "he_fixed_european_marks", "he_bs_delta_hedge",
+    "he_vecnorm_reset", "he_fixed_european_marks", "he_bs_delta_hedge", "he_count_nonfinite",
 ]
 
 
@@ -188,6 +188,7 @@ def load(path=LIB_PATH):
         "he_vecnorm_reset": (i32, [ctypes.POINTER(HeVecnormParams), i64] + [vp] * 5 + [vp]),
         "he_fixed_european_marks": (i32, [vp, i64, i32, ctypes.c_double, vp, vp, vp, vp]),
         "he_bs_delta_hedge": (i32, [vp, i64, i32, ctypes.c_double, ctypes.c_double, vp, vp]),
+        "he_count_nonfinite": (i32, [vp, i64, vp, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

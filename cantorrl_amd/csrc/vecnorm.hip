@@ -316,9 +316,29 @@ VnArgs base_args(const he_vecnorm_params* p, int64_t n) {
     return a;
 }
 
+__global__ void __launch_bounds__(kVnThreads) nonfinite_kernel(const float* __restrict__ a, int64_t n,
+                                                               unsigned long long* count) {
+    unsigned long long c = 0;
+    for (int64_t i = (int64_t)blockIdx.x * kVnThreads + threadIdx.x; i < n; i += (int64_t)gridDim.x * kVnThreads)
+        c += isfinite(a[i]) ? 0ull : 1ull;
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) c += __shfl_xor(c, m, 64);
+    if ((threadIdx.x & 63) == 0 && c) atomicAdd(count, c);
+}
+
 }  // namespace
 
 extern "C" {
+
+he_status he_count_nonfinite(const float* a, int64_t n, unsigned long long* count, void* stream) {
+    if (n < 0 || !count || (n > 0 && !a)) return HE_EINVAL;
+    if (n == 0) return HE_OK;
+    int64_t blocks = (n + kVnThreads - 1) / kVnThreads;
+    if (blocks > 2048) blocks = 2048;
+    hipLaunchKernelGGL(nonfinite_kernel, dim3((unsigned)blocks), dim3(kVnThreads), 0, (hipStream_t)stream, a, n, count);
+    return hipGetLastError() == hipSuccess ? HE_OK : HE_EHIP;
+}
+
 
 int64_t he_vecnorm_stats_len(int32_t obs_dim) { return 2 * (int64_t)obs_dim + 4; }
 

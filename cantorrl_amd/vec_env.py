@@ -75,7 +75,7 @@ class HedgingVecEnv:
     def __init__(self, n_envs, data_file_path=None, *, tables=None, variant=2, mode=None,
                  generate=None, device=None, seed=None, global_env_offset=0, autoreset=True,
                  return_numpy=True, info_keys=MONITOR_KEYWORDS, monitor_keywords=None,
-                 market_block=64, market_prefetch="auto", **env_kwargs):
+                 market_block=64, market_prefetch="auto", check_finite=False, **env_kwargs):
         self.lib = _lib.load()
         self.num_envs = int(n_envs)
         self.variant = int(variant)
@@ -193,6 +193,10 @@ class HedgingVecEnv:
         self._actions_pending = None
         self._ep_ret = np.zeros(n, np.float64)
         self._ep_len = np.zeros(n, np.int64)
+        # failure detection: device count of non-finite obs / reward values since
+        # construction (he_count_nonfinite after every step when check_finite)
+        self.check_finite = bool(check_finite)
+        self._nonfinite = torch.zeros(1, dtype=torch.int64, device=dev)
         self._t_start = time.time()
 
         self.action_space = Box(-1.0, 1.0, (2,), np.float32)
@@ -284,7 +288,16 @@ class HedgingVecEnv:
                               _lib.ctypes.byref(self._info) if (info and self._info_t) else None,
                               self.stream)
         _lib.check(self.lib, self._h, st, "he_step")
+        if self.check_finite:
+            for t in (self._obs, self._rew):
+                _lib.check(self.lib, self._h, self.lib.he_count_nonfinite(t.data_ptr(), t.numel(),
+                                                                          self._nonfinite.data_ptr(), self.stream),
+                           "he_count_nonfinite")
         return self._obs, self._rew, self._term, self._trunc
+
+    def nonfinite_count(self):
+        """Non-finite obs / reward values produced so far (check_finite=True); syncs."""
+        return int(self._nonfinite.item())
 
     def step_async(self, actions):
         self._actions_pending = actions

@@ -357,6 +357,12 @@ he_status he_fixed_european_marks(const double* paths, int64_t n_paths, int32_t 
 he_status he_bs_delta_hedge(const double* paths, int64_t n_paths, int32_t n_cols, double r, double dt, double* pnl,
                             void* stream);
 
+/* Failure detection (the reference's src/agents/test_inf.py checks rewards
+ * for infinities by hand): *count += number of non-finite values among n f32 values
+ * of a (obs rows, rewards, ...), one wave-level reduction and one atomic per wave.
+ * Stream-ordered; read *count when convenient. */
+he_status he_count_nonfinite(const float* a, int64_t n, unsigned long long* count, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

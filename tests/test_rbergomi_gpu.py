@@ -203,7 +203,7 @@ def test_inf_on_generated_dataset(tmp_path):
     res = rb.generate_paths_and_options(_history(), 64, n_mc=256, device=DEV, seed=5)
     f = tmp_path / "paths_rbergomi_options.npz"
     rb.save_npz(str(f), res)
-    env = HedgingVecEnv(2048, str(f), variant=1, device=DEV, seed=0, return_numpy=False, info_keys=(),
+    env = HedgingVecEnv(2048, str(f), variant=1, device=DEV, seed=0, return_numpy=False, info_keys=(), check_finite=True,
                         transaction_cost_per_contract=0.05, lambda_cost=1.0, shares_to_hedge=10_000,
                         max_contracts_held_per_type=200)
     env.reset_tensors()
@@ -213,5 +213,6 @@ def test_inf_on_generated_dataset(tmp_path):
         a = torch.rand((2048, 2), generator=g, device=DEV) * 2 - 1
         obs, rew, term, _ = env.step_tensors(a)
         bad += int((~torch.isfinite(rew)).sum()) + int((~torch.isfinite(obs)).sum())
+    assert env.nonfinite_count() == 0      # the device-side counter agrees
     env.close()
     assert bad == 0

@@ -98,3 +98,30 @@ def test_sb3_api_and_save_load(tmp_path):
     np.testing.assert_allclose(vn.normalize_obs(o), np.clip((o - vn.obs_rms.mean) / np.sqrt(vn.obs_rms.var + 1e-8),
                                                             -10, 10).astype(np.float32))
     vn.close()
+
+
+def test_nonfinite_counter():
+    """check_finite: he_count_nonfinite after each step counts non-finite obs/reward
+    values on the device.  Replay tables with a NaN mark column (as the shipped
+    paths_options.npz has at t = 1) produce them; clean tables do not."""
+    from cantorrl_amd.vec_env import HedgingVecEnv
+    rng = np.random.default_rng(0)
+    P_, T1 = 8, 21
+    S = 100 * np.exp(np.cumsum(rng.normal(0, 0.01, size=(P_, T1)), axis=1))
+    v = np.full((P_, T1), 0.04)
+    C = np.full((P_, T1 - 1), 2.0)
+    Pu = np.full((P_, T1 - 1), 1.5)
+    clean = HedgingVecEnv(16, tables=(S, v, C, Pu), device=DEV, seed=0, return_numpy=False, info_keys=(),
+                          check_finite=True)
+    C2 = C.copy()
+    C2[:, 1] = np.nan
+    dirty = HedgingVecEnv(16, tables=(S, v, C2, Pu), device=DEV, seed=0, return_numpy=False, info_keys=(),
+                          check_finite=True)
+    for e in (clean, dirty):
+        e.reset_tensors()
+        for _ in range(25):
+            e.step_tensors(torch.zeros((16, 2), device=DEV))
+    assert clean.nonfinite_count() == 0
+    assert dirty.nonfinite_count() > 0
+    clean.close()
+    dirty.close()
