@@ -58,6 +58,7 @@ int fail(int code, const char* fmt, ...) {
 
 constexpr int kDomParams = 1, kDomMain = 2, kDomMc = 3;
 constexpr int kMcThreads = 256;
+constexpr int64_t kAtmChunk = 8192;   // rb_price_atm_marks: paths per launch
 constexpr int kXc = 6;   // MC pricer: Euler steps per convolution chunk (divides the 30 of the reference tenor)
 
 HE_HD u32x4 rb_ctr(uint32_t block, int dom, uint32_t sub, uint64_t gid) {
@@ -171,6 +172,7 @@ __global__ void __launch_bounds__(1024) paths_kernel(PathArgs a) {
 // ------------------------------------------------------------------ MC option pricer
 struct McArgs {
     int64_t n_opt;       // options (list) or paths (ATM)
+    int64_t o_base;      // ATM: option index of blockIdx.x = 0 (chunked launches)
     uint64_t off;
     uint32_t k0, k1;
     int T;               // ATM: days per path
@@ -212,13 +214,13 @@ __global__ void __launch_bounds__(kMcThreads) mc_kernel(McArgs a) {
     __shared__ double s_ma[MO];
     __shared__ double s_red[kMcThreads / 64];
     const int tid = threadIdx.x;
-    const int64_t o = blockIdx.x;
+    const int64_t o = (ATM ? a.o_base : 0) + (int64_t)blockIdx.x;
     const int type = ATM ? (int)blockIdx.y : a.type;
     double S0, K, xi, H, eta, rho;
     uint64_t gid;
     uint32_t sub;
     if (ATM) {
-        const int64_t p = (int64_t)((uint32_t)o / (uint32_t)a.T);   // o < 2^31 (host-checked)
+        const int64_t p = o / a.T;
         const int d = (int)(o - p * a.T);
         S0 = a.paths[p * (a.T + 1) + d];
         xi = a.vol[p * (a.T + 1) + d];
@@ -738,9 +740,15 @@ int32_t rb_price_atm_marks(const rb_config* c, const double* params, const doubl
     a.vol = vol;
     a.call = call;
     a.put = put;
-    const int64_t n_o = c->n_paths * (int64_t)c->n_steps;
-    if (n_o > 0x7FFFFFFF) return fail(RB_EINVAL, "n_paths * n_steps > 2^31 - 1 in one call: shard the paths");
-    return launch_mc(a, g.M, c->normals, true, dim3((unsigned)n_o, 2), (hipStream_t)stream);
+    // launches of kAtmChunk paths (x n_steps days x {call, put}): a few seconds each
+    // at 5000 MC paths, and grids far below the 2^31 workgroup limit at any n_paths
+    for (int64_t p0 = 0; p0 < c->n_paths; p0 += kAtmChunk) {
+        const int64_t np = (c->n_paths - p0 < kAtmChunk) ? c->n_paths - p0 : kAtmChunk;
+        a.o_base = p0 * (int64_t)c->n_steps;
+        if (int e = launch_mc(a, g.M, c->normals, true, dim3((unsigned)(np * c->n_steps), 2), (hipStream_t)stream))
+            return e;
+    }
+    return RB_OK;
 }
 
 int32_t rb_generate(const rb_config* c, const rb_base_params* b, double* params, double* paths, double* vol,

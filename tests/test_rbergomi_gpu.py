@@ -216,3 +216,14 @@ def test_inf_on_generated_dataset(tmp_path):
     assert env.nonfinite_count() == 0      # the device-side counter agrees
     env.close()
     assert bad == 0
+
+
+def test_chunked_mark_launches_equal_a_shard():
+    """rb_price_atm_marks launches 8,192 paths at a time: rows on both sides of the
+    chunk boundary equal the same rows generated as a small shard."""
+    rb = _rb()
+    kw = dict(n_mc=2, device=DEV, seed=13)
+    big = rb.generate_paths_and_options(_history(), 8200, **kw)
+    part = rb.generate_paths_and_options(_history(), 12, path_offset=8186, **kw)
+    for k in ("call_prices_atm", "put_prices_atm", "paths"):
+        np.testing.assert_array_equal(big[k][8186:8198].cpu().numpy(), part[k].cpu().numpy(), err_msg=k)
