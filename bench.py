@@ -35,19 +35,21 @@ import torch
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
-# Algorithmic HBM bytes per env-step:
+# Algorithmic HBM bytes per env-step.  Market tile records are
+# 12 B in GBM mode ({S, C, P} and {greeks}: v is a constant, the lag return is
+# recomputed by the step kernel) and 16 B under Heston ({S, v, C, P}, {greeks, lag}).
 # he_step (step1_kernel, one launch per step):
 #   reads : state (t 4, pos 4, cash 8) 16 + action 8 + market tile slots
-#           (pre {S,v,C,P} 16, post {S,v,C,P} 16, post greeks+lag 16) 48            = 72
-#   writes: state 16 + obs 52 + reward 4 + terminated 1 + truncated 1             = 74
-STEP_BYTES_PER_ENV = 146
+#           (pre A, post A, post B) 3 x 12 (GBM) | 3 x 16 (Heston)     = 60 | 72
+#   writes: state 16 + obs 52 + reward 4 + terminated 1 + truncated 1 = 74
+STEP_BYTES_PER_ENV = {"gbm": 134, "heston": 146}
 # he_rollout (step_kernel, K steps per launch, state in registers):
-#   per step: action 8 + tile post slots 32 (read) + obs 52 + reward 4 + terminated 1 = 97
-#   per launch: state 16 read + 16 written + pre slot 16 read                         = 48
-ROLLOUT_BYTES_PER_ENV = 97
-ROLLOUT_STATE_BYTES = 48
-# market_kernel per env-step: tile {S,v,C,P} + {greeks, lag} written (32)
-MARKET_BYTES_PER_ENV = 32
+#   per step: action 8 + tile post slots 24 | 32 (read) + obs 52 + reward 4 + terminated 1 = 89 | 97
+#   per launch: state 16 read + 16 written + pre slot 12 | 16 read                         = 44 | 48
+ROLLOUT_BYTES_PER_ENV = {"gbm": 89, "heston": 97}
+ROLLOUT_STATE_BYTES = {"gbm": 44, "heston": 48}
+# market_kernel per env-step: tile A + B written
+MARKET_BYTES_PER_ENV = {"gbm": 24, "heston": 32}
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
 M_BLOCK = 64           # market block (he_config.market_block)
 
@@ -396,13 +398,14 @@ def timed(runner, K, W, dist):
     return float(t.item()), ev0.elapsed_time(ev1)
 
 
-def roofline(mode, n, kern_ms, rk, book=False):
-    """book: + the f64 book slot per env-step (post; he_step also reads the pre slot)."""
+def roofline(mode, n, kern_ms, rk, book=False, market="gbm"):
+    """book: + the f64 book slot per env-step (post; he_step also reads the pre slot).
+    market: "gbm" | "heston" (tile record size)."""
     if mode == "rollout":
-        bytes_launch = n * rk * (ROLLOUT_BYTES_PER_ENV + (8 if book else 0) + ROLLOUT_STATE_BYTES / rk)
+        bytes_launch = n * rk * (ROLLOUT_BYTES_PER_ENV[market] + (8 if book else 0) + ROLLOUT_STATE_BYTES[market] / rk)
         kname = "step_kernel (he_rollout, K=%d fused steps)" % rk
     else:
-        bytes_launch = n * (STEP_BYTES_PER_ENV + (16 if book else 0))
+        bytes_launch = n * (STEP_BYTES_PER_ENV[market] + (16 if book else 0))
         kname = "step1_kernel (he_step, K=1)"
     achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
     return dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
@@ -604,7 +607,7 @@ def main():
     env.close()
 
     has_book = bool(cfg["gen"].get("book"))
-    roof = roofline(args.mode, n, kern_ms, args.rollout_k, has_book)
+    roof = roofline(args.mode, n, kern_ms, args.rollout_k, has_book, cfg["mode"])
     mkt_ms = market_time_ms(hev, args, dev, acts, stream)
     roof["market_kernel_us_per_64_steps"] = round(mkt_ms * 1e3, 3)
     roof["market_kernel_us_per_step"] = round(mkt_ms * 1e3 / M_BLOCK, 3)
@@ -623,7 +626,7 @@ def main():
         wall_g, _ = timed(rg, Kg, M_BLOCK * 4, None)
         kg = kernel_time_ms(hev, rg, 256)
         env_g.close()
-        rf = roofline("graph", n, kg, 1, has_book)
+        rf = roofline("graph", n, kg, 1, has_book, cfg["mode"])
         step_api = dict(mode="graph (he_step, one launch per step)", value=round(n * Kg / wall_g, 1),
                         ms_per_step=round(wall_g * 1e3 / Kg, 6), kernel=rf["kernel"], kernel_us=rf["kernel_us"],
                         achieved_gbs=rf["achieved"], frac=rf["frac"], bytes_per_launch=rf["bytes_per_launch"])

@@ -52,6 +52,28 @@ __device__ __forceinline__ float2 ld2(const GLOBAL v2f* p, int64_t k) {
     v2f x = p[k];
     return make_float2(x.x, x.y);
 }
+// GBM market tiles hold 12-B records (one dwordx3 per lane): tileA {S, C, P} (v is
+// the handle's constant variance) and tileB {call_delta, gamma, put_delta}; the lag
+// return is recomputed by the step kernel from S and the previous S (same f32
+// quotient the market kernel would have stored).  Heston keeps 16-B {S, v, C, P} and
+// {greeks, lag} records.
+struct __attribute__((packed, aligned(4))) f3 {
+    float x, y, z;
+};
+__device__ __forceinline__ float4 ld3A(const GLOBAL v4f* p, int64_t k, float v) {
+    const GLOBAL f3* r = (const GLOBAL f3*)p + k;
+    return make_float4(r->x, v, r->y, r->z);
+}
+__device__ __forceinline__ float4 ld3B(const GLOBAL v4f* p, int64_t k) {
+    const GLOBAL f3* r = (const GLOBAL f3*)p + k;
+    return make_float4(r->x, r->y, r->z, 0.0f);
+}
+__device__ __forceinline__ void st3(float4* p, int64_t k, float x, float y, float z) {
+    GLOBAL f3* r = (GLOBAL f3*)p + k;
+    r->x = x;
+    r->y = y;
+    r->z = z;
+}
 
 constexpr int kBlock = 256;      // step kernel: threads per workgroup (4 waves)
 #ifndef HE_STEP_EPW
@@ -117,8 +139,8 @@ struct Params {
     int32_t den_const;      // generate: reward denominator of the shared S0 (all envs)
     double den, inv_den;
     int32_t M;              // market block length
-    float4* tileA;          // [M+1][N] {S, v, C, P}
-    float4* tileB;          // [M+1][N] {call_delta, gamma, put_delta, 0}
+    float4* tileA;          // [M+1][N] {S, v, C, P}; GBM: 12-B {S, C, P} records (ld3A)
+    float4* tileB;          // [M+1][N] {call_delta, gamma, put_delta, lag}; GBM: 12-B {greeks} (ld3B)
     float rstv[4 + kObs];   // reset market + obs (generate): {S0, v0, C0, P0, obs0[13]}, by value
     // replay
     const float4* rec;      // [n_paths][T+1] {S, v, C, P}; C/P at T hold row T-1
@@ -648,25 +670,37 @@ __global__ __launch_bounds__(kMktEnvs * kMktLanes, HE_MKT_WAVES) void market_ker
         if (advance_only) continue;
         float S32 = (float)S64;
         float v32 = HESTON ? (float)v64 : p.var_f;
-        p.tileA[(int64_t)j * N + i] = make_float4(S32, v32, C, P);
+        if (HESTON) p.tileA[(int64_t)j * N + i] = make_float4(S32, v32, C, P);
+        else st3(p.tileA, (int64_t)j * N + i, S32, C, P);
 #if defined(HE_MKT_SKIP) && (HE_MKT_SKIP & 1)
         float4 g = make_float4(S32, v32, 0.f, 0.f);  // diagnostic build: no greeks
 #else
         float4 g = p.record_metrics ? greeks_fast<!HESTON>(p, S32, v32) : make_float4(0.f, 0.f, 0.f, 0.f);
 #endif
-        // the step into slot j starts from the reset market (first step of an
-        // episode) or from slot j-1
-        const float Sp32 = (tj == 1u) ? p.rstv[0] : (float)shS[lane][j - 1];
-        g.w = lag_return(S32, Sp32);
-        p.tileB[(int64_t)j * N + i] = g;
+        if (HESTON) {
+            // the step into slot j starts from the reset market (first step of an
+            // episode) or from slot j-1
+            const float Sp32 = (tj == 1u) ? p.rstv[0] : (float)shS[lane][j - 1];
+            g.w = lag_return(S32, Sp32);
+            p.tileB[(int64_t)j * N + i] = g;
+        } else {
+            st3(p.tileB, (int64_t)j * N + i, g.x, g.y, g.z);
+        }
         if (BOOK) p.tileC[(int64_t)j * N + i] = book_value(p, S64, v64, (int32_t)tj, shM[lane][j]);
     }
     if (!advance_only && sub == 0 && live) {
         float v32 = HESTON ? (float)v0v : p.var_f;
-        p.tileA[i] = make_float4((float)S0v, v32, C0v, P0v);
         // greeks of the block start (the obs policy rollouts resume from); equal to
         // the previous block's last slot, same function of the same (S, v)
-        p.tileB[i] = p.record_metrics ? greeks_fast<!HESTON>(p, (float)S0v, v32) : make_float4(0.f, 0.f, 0.f, 0.f);
+        const float4 g0 =
+            p.record_metrics ? greeks_fast<!HESTON>(p, (float)S0v, v32) : make_float4(0.f, 0.f, 0.f, 0.f);
+        if (HESTON) {
+            p.tileA[i] = make_float4((float)S0v, v32, C0v, P0v);
+            p.tileB[i] = g0;
+        } else {
+            st3(p.tileA, i, (float)S0v, C0v, P0v);
+            st3(p.tileB, i, g0.x, g0.y, g0.z);
+        }
         // slot 0 = the block start; at t0 in {0, T} the next step starts from the reset
         // market and reads book_rst instead
         if (BOOK)
@@ -977,6 +1011,7 @@ template <int MODE, bool INFO, bool SINGLE, bool BOOK, bool FAST, bool POL>
 __device__ __forceinline__ void step_body(const Params& pk, int64_t n_envs, const float4* tA, const float4* tB,
                                           const double* tC, State s, Io io, int k_steps_arg, int slot0) {
     constexpr bool REPLAY = (MODE == HE_MODE_REPLAY);
+    constexpr bool CT = (MODE == HE_MODE_GBM);  // 12-B tile records (see ld3A)
     const int k_steps = SINGLE ? 1 : k_steps_arg;
     Params p = pk;
     HE_TIM(0);
@@ -1011,6 +1046,9 @@ __device__ __forceinline__ void step_body(const Params& pk, int64_t n_envs, cons
     asm volatile("" : "+s"(s_t), "+s"(s_pos), "+s"(s_cash), "+s"(gact), "+s"(mA), "+s"(mB), "+s"(hot_i));
     if (BOOK) asm volatile("" : "+s"(mC));
     if (REPLAY) asm volatile("" : "+s"(s_path), "+s"(s_s0));
+    const float var_f = p.var_f;
+    auto ldA = [=](int64_t r) { return CT ? ld3A(mA, r, var_f) : ld4(mA, r); };
+    auto ldB = [=](int64_t r) { return CT ? ld3B(mB, r) : ld4(mB, r); };
     HE_TIM(1);
     Env e;
     Mkt pre;
@@ -1036,9 +1074,9 @@ __device__ __forceinline__ void step_body(const Params& pk, int64_t n_envs, cons
             e.s0_small = (s0 == -1.0f);
             e.s0 = e.s0_small ? 1.0f : s0;
         } else {
-            float4 preA = ld4(mA, (int64_t)hot_i * N + i);
-            postA = ld4(mA, (int64_t)(hot_i + 1) * N + i);
-            postB = ld4(mB, (int64_t)(hot_i + 1) * N + i);
+            float4 preA = ldA((int64_t)hot_i * N + i);
+            postA = ldA((int64_t)(hot_i + 1) * N + i);
+            postB = ldB((int64_t)(hot_i + 1) * N + i);
             double preC = 0.0;
             if (BOOK) {
                 preC = mC[(int64_t)hot_i * N + i];
@@ -1076,7 +1114,7 @@ __device__ __forceinline__ void step_body(const Params& pk, int64_t n_envs, cons
             const uint32_t tt = e.t > (uint32_t)p.T ? (uint32_t)p.T : e.t;
             gpre = tB[(int64_t)e.path * (p.T + 1) + tt];
         } else {
-            gpre = (e.t == 0) ? make_float4(p.rstv[4 + 7], 0.0f, p.rstv[4 + 9], 0.0f) : tB[(int64_t)slot0 * N + i];
+            gpre = (e.t == 0) ? make_float4(p.rstv[4 + 7], 0.0f, p.rstv[4 + 9], 0.0f) : ldB((int64_t)slot0 * N + i);
         }
         const bool met = p.record_metrics != 0;
         pol_cd = met ? gpre.x : 0.0f;
@@ -1091,10 +1129,15 @@ __device__ __forceinline__ void step_body(const Params& pk, int64_t n_envs, cons
     float* const orow = tile + (wave * kEpw + (lane < kEpw ? lane : 0)) * kObs;
     // step k of every env from market `post` (greeks + lag return `g`) with action ak:
     // state update, reward/done stores, the obs row into the wave's LDS tile, auto-reset
-    auto step_part = [&](int k, const Mkt post, const float4 g, float2 ak) {
+    auto step_part = [&](int k, const Mkt post, float4 g, float2 ak) {
         const int64_t koff = (int64_t)k * N;
         bool term = false;
         if (live) {
+            // compact tiles: the lag return of the market kernel's slot.  The step from
+            // t in {0, T} starts from the reset market; at t == 0 pre is rst already
+            // (and spelling out both tests trips an illegal VGPR-to-SGPR copy in the
+            // ROCm 7.2 backend)
+            if constexpr (CT) g.w = lag_return(post.S, (e.t >= (uint32_t)p.T) ? rst.S : pre.S);
             if (POL) {
                 ak = policy_action(p, io.pol.policy, e.call, e.put, pol_o3, pol_o4, pol_cd, pol_pd);
                 if (io.pol.act_out) {
@@ -1206,8 +1249,8 @@ __device__ __forceinline__ void step_body(const Params& pk, int64_t n_envs, cons
             kk = kk < k_steps ? kk : k_steps - 1;
             const int64_t r = (int64_t)(slot0 + kk + 1) * N + ic;
             if (!POL) ra[d] = ld2(gact, (int64_t)kk * N + ic);
-            rA[d] = ld4(mA, r);
-            rB[d] = ld4(mB, r);
+            rA[d] = ldA(r);
+            rB[d] = ldB(r);
             if (BOOK) rC[d] = mC[r];
         };
 #pragma unroll
