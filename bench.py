@@ -35,21 +35,35 @@ import torch
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
-# Algorithmic HBM bytes per env-step.  Market tile records are
-# 12 B in GBM mode ({S, C, P} and {greeks}: v is a constant, the lag return is
-# recomputed by the step kernel) and 16 B under Heston ({S, v, C, P}, {greeks, lag}).
+# Algorithmic HBM bytes per env-step.  Market tile records:
+#   "gbm"        12-B {S, C, P} + 12-B {greeks}   (GBM below GREEKS_IN_STEP_MIN_ENVS envs)
+#   "gbm_step"   12-B {S, C, P} only              (GBM from there: the step kernel
+#                                                  evaluates the f32 obs greeks itself)
+#   "heston"     16-B {S, v, C, P} + 16-B {greeks, lag}
+# In GBM mode v is a constant and the step kernel recomputes the lag return.
 # he_step (step1_kernel, one launch per step):
 #   reads : state (t 4, pos 4, cash 8) 16 + action 8 + market tile slots
-#           (pre A, post A, post B) 3 x 12 (GBM) | 3 x 16 (Heston)     = 60 | 72
-#   writes: state 16 + obs 52 + reward 4 + terminated 1 + truncated 1 = 74
-STEP_BYTES_PER_ENV = {"gbm": 134, "heston": 146}
+#           (pre A, post A, post B) 36 | (pre A, post A) 24 | 48              = 60 | 48 | 72
+#   writes: state 16 + obs 52 + reward 4 + terminated 1 + truncated 1           = 74
 # he_rollout (step_kernel, K steps per launch, state in registers):
-#   per step: action 8 + tile post slots 24 | 32 (read) + obs 52 + reward 4 + terminated 1 = 89 | 97
-#   per launch: state 16 read + 16 written + pre slot 12 | 16 read                         = 44 | 48
-ROLLOUT_BYTES_PER_ENV = {"gbm": 89, "heston": 97}
-ROLLOUT_STATE_BYTES = {"gbm": 44, "heston": 48}
-# market_kernel per env-step: tile A + B written
-MARKET_BYTES_PER_ENV = {"gbm": 24, "heston": 32}
+#   per step: action 8 + tile post slots 24 | 12 | 32 (read) + obs 52 + reward 4
+#             + terminated 1                                                   = 89 | 77 | 97
+#   per launch: state 16 read + 16 written + pre slot 12 | 12 | 16 read        = 44 | 44 | 48
+GREEKS_IN_STEP_MIN_ENVS = 262144  # hedge_env.hip kGreeksInStepMinEnvs
+STEP_BYTES_PER_ENV = {"gbm": 134, "gbm_step": 122, "heston": 146}
+ROLLOUT_BYTES_PER_ENV = {"gbm": 89, "gbm_step": 77, "heston": 97}
+ROLLOUT_STATE_BYTES = {"gbm": 44, "gbm_step": 44, "heston": 48}
+# market_kernel per env-step: tile records written
+MARKET_BYTES_PER_ENV = {"gbm": 24, "gbm_step": 12, "heston": 32}
+
+
+def tile_layout(mode, n):
+    if mode == "heston":
+        return "heston"
+    thr = int(os.environ.get("HE_GREEKS_IN_STEP_MIN_ENVS") or GREEKS_IN_STEP_MIN_ENVS)
+    return "gbm_step" if n >= thr else "gbm"
+
+
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
 M_BLOCK = 64           # market block (he_config.market_block)
 
@@ -400,7 +414,7 @@ def timed(runner, K, W, dist):
 
 def roofline(mode, n, kern_ms, rk, book=False, market="gbm"):
     """book: + the f64 book slot per env-step (post; he_step also reads the pre slot).
-    market: "gbm" | "heston" (tile record size)."""
+    market: tile layout, see tile_layout()."""
     if mode == "rollout":
         bytes_launch = n * rk * (ROLLOUT_BYTES_PER_ENV[market] + (8 if book else 0) + ROLLOUT_STATE_BYTES[market] / rk)
         kname = "step_kernel (he_rollout, K=%d fused steps)" % rk
@@ -607,7 +621,8 @@ def main():
     env.close()
 
     has_book = bool(cfg["gen"].get("book"))
-    roof = roofline(args.mode, n, kern_ms, args.rollout_k, has_book, cfg["mode"])
+    roof = roofline(args.mode, n, kern_ms, args.rollout_k, has_book, tile_layout(cfg["mode"], n))
+    roof["tile_layout"] = tile_layout(cfg["mode"], n)
     mkt_ms = market_time_ms(hev, args, dev, acts, stream)
     roof["market_kernel_us_per_64_steps"] = round(mkt_ms * 1e3, 3)
     roof["market_kernel_us_per_step"] = round(mkt_ms * 1e3 / M_BLOCK, 3)
@@ -626,7 +641,7 @@ def main():
         wall_g, _ = timed(rg, Kg, M_BLOCK * 4, None)
         kg = kernel_time_ms(hev, rg, 256)
         env_g.close()
-        rf = roofline("graph", n, kg, 1, has_book, cfg["mode"])
+        rf = roofline("graph", n, kg, 1, has_book, tile_layout(cfg["mode"], n))
         step_api = dict(mode="graph (he_step, one launch per step)", value=round(n * Kg / wall_g, 1),
                         ms_per_step=round(wall_g * 1e3 / Kg, 6), kernel=rf["kernel"], kernel_us=rf["kernel_us"],
                         achieved_gbs=rf["achieved"], frac=rf["frac"], bytes_per_launch=rf["bytes_per_launch"])

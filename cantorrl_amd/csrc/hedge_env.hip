@@ -53,9 +53,11 @@ __device__ __forceinline__ float2 ld2(const GLOBAL v2f* p, int64_t k) {
     return make_float2(x.x, x.y);
 }
 // GBM market tiles hold 12-B records (one dwordx3 per lane): tileA {S, C, P} (v is
-// the handle's constant variance) and tileB {call_delta, gamma, put_delta}; the lag
-// return is recomputed by the step kernel from S and the previous S (same f32
-// quotient the market kernel would have stored).  Heston keeps 16-B {S, v, C, P} and
+// the handle's constant variance) and, below kGreeksInStepMinEnvs envs, tileB
+// {call_delta, gamma, put_delta}.  The step kernel recomputes the lag return from S
+// and the previous S, and from kGreeksInStepMinEnvs envs also the f32 obs greeks
+// (greeks_fast, a function of S alone at constant v): the same f32 code the market
+// kernel would run, so the same values.  Heston keeps 16-B {S, v, C, P} and
 // {greeks, lag} records.
 struct __attribute__((packed, aligned(4))) f3 {
     float x, y, z;
@@ -93,6 +95,14 @@ constexpr int kRolloutPrefetch = HE_ROLLOUT_PREFETCH;  // rollout: steps of inpu
 #define HE_MKT_WAVES 2  // market_kernel: min waves per SIMD (3 is faster alone, slower beside rollouts)
 #endif
 constexpr int64_t kPrefetchMinEnvs = 131072;  // auto prefetch for single steps from here
+// GBM: obs greeks evaluated by the step kernel (no tileB) from this many envs.  A
+// rollout wave at 65,536 envs (one wave per SIMD) pays the f32 greeks' dependent
+// VALU latency in full (3.19e10 -> 2.88e10 env-steps/s), while at 1,048,576 envs the
+// 12 bytes per env-step saved win (2.95e10 -> 3.68e10; MI355X, he_rollout K=64).
+#ifndef HE_GREEKS_IN_STEP_MIN_ENVS
+#define HE_GREEKS_IN_STEP_MIN_ENVS 262144
+#endif
+constexpr int64_t kGreeksInStepMinEnvs = HE_GREEKS_IN_STEP_MIN_ENVS;
 
 // ------------------------------------------------------------------ parameters
 // One option of the liability book (he_book_option), device copy: q100 = quantity*100.
@@ -107,6 +117,7 @@ struct Params {
     int64_t goff;
     int32_t T;
     int32_t variant, loss, record_metrics, autoreset, mode;
+    int32_t tile_greeks;    // GBM: the market kernel writes tileB {greeks} (else the step kernel evaluates them)
     int32_t mt, maxh;
     float mt_f, maxh_f, T_f;
     float inv_maxh_f, inv_T_f;  // RN_f32(1/x) for div_byf
@@ -140,7 +151,7 @@ struct Params {
     double den, inv_den;
     int32_t M;              // market block length
     float4* tileA;          // [M+1][N] {S, v, C, P}; GBM: 12-B {S, C, P} records (ld3A)
-    float4* tileB;          // [M+1][N] {call_delta, gamma, put_delta, lag}; GBM: 12-B {greeks} (ld3B)
+    float4* tileB;          // [M+1][N] {call_delta, gamma, put_delta, lag}; GBM: 12-B {greeks} if tile_greeks
     float rstv[4 + kObs];   // reset market + obs (generate): {S0, v0, C0, P0, obs0[13]}, by value
     // replay
     const float4* rec;      // [n_paths][T+1] {S, v, C, P}; C/P at T hold row T-1
@@ -672,34 +683,36 @@ __global__ __launch_bounds__(kMktEnvs * kMktLanes, HE_MKT_WAVES) void market_ker
         float v32 = HESTON ? (float)v64 : p.var_f;
         if (HESTON) p.tileA[(int64_t)j * N + i] = make_float4(S32, v32, C, P);
         else st3(p.tileA, (int64_t)j * N + i, S32, C, P);
-#if defined(HE_MKT_SKIP) && (HE_MKT_SKIP & 1)
-        float4 g = make_float4(S32, v32, 0.f, 0.f);  // diagnostic build: no greeks
-#else
-        float4 g = p.record_metrics ? greeks_fast<!HESTON>(p, S32, v32) : make_float4(0.f, 0.f, 0.f, 0.f);
-#endif
         if (HESTON) {
+#if defined(HE_MKT_SKIP) && (HE_MKT_SKIP & 1)
+            float4 g = make_float4(S32, v32, 0.f, 0.f);  // diagnostic build: no greeks
+#else
+            float4 g = p.record_metrics ? greeks_fast<false>(p, S32, v32) : make_float4(0.f, 0.f, 0.f, 0.f);
+#endif
             // the step into slot j starts from the reset market (first step of an
             // episode) or from slot j-1
             const float Sp32 = (tj == 1u) ? p.rstv[0] : (float)shS[lane][j - 1];
             g.w = lag_return(S32, Sp32);
             p.tileB[(int64_t)j * N + i] = g;
-        } else {
+        } else if (p.tile_greeks) {
+            const float4 g = p.record_metrics ? greeks_fast<true>(p, S32, v32) : make_float4(0.f, 0.f, 0.f, 0.f);
             st3(p.tileB, (int64_t)j * N + i, g.x, g.y, g.z);
         }
         if (BOOK) p.tileC[(int64_t)j * N + i] = book_value(p, S64, v64, (int32_t)tj, shM[lane][j]);
     }
     if (!advance_only && sub == 0 && live) {
         float v32 = HESTON ? (float)v0v : p.var_f;
-        // greeks of the block start (the obs policy rollouts resume from); equal to
-        // the previous block's last slot, same function of the same (S, v)
-        const float4 g0 =
-            p.record_metrics ? greeks_fast<!HESTON>(p, (float)S0v, v32) : make_float4(0.f, 0.f, 0.f, 0.f);
         if (HESTON) {
             p.tileA[i] = make_float4((float)S0v, v32, C0v, P0v);
-            p.tileB[i] = g0;
+            // greeks of the block start (the obs policy rollouts resume from); equal to
+            // the previous block's last slot, same function of the same (S, v)
+            p.tileB[i] = p.record_metrics ? greeks_fast<false>(p, (float)S0v, v32) : make_float4(0.f, 0.f, 0.f, 0.f);
         } else {
             st3(p.tileA, i, (float)S0v, C0v, P0v);
-            st3(p.tileB, i, g0.x, g0.y, g0.z);
+            if (p.tile_greeks) {
+                const float4 g = p.record_metrics ? greeks_fast<true>(p, (float)S0v, v32) : make_float4(0.f, 0.f, 0.f, 0.f);
+                st3(p.tileB, i, g.x, g.y, g.z);
+            }
         }
         // slot 0 = the block start; at t0 in {0, T} the next step starts from the reset
         // market and reads book_rst instead
@@ -1007,7 +1020,7 @@ __device__ __forceinline__ void env_reset_common(const Params& p, Env& e) {
 // SINGLE: the he_step instance (k_steps == 1 at compile time, straight-line code).
 // tA/tB: the market source, tile buffer {S,v,C,P} / greeks (generate) or the
 // replay table rec / recg.
-template <int MODE, bool INFO, bool SINGLE, bool BOOK, bool FAST, bool POL>
+template <int MODE, bool INFO, bool SINGLE, bool BOOK, bool FAST, bool POL, bool GS>
 __device__ __forceinline__ void step_body(const Params& pk, int64_t n_envs, const float4* tA, const float4* tB,
                                           const double* tC, State s, Io io, int k_steps_arg, int slot0) {
     constexpr bool REPLAY = (MODE == HE_MODE_REPLAY);
@@ -1048,7 +1061,14 @@ __device__ __forceinline__ void step_body(const Params& pk, int64_t n_envs, cons
     if (REPLAY) asm volatile("" : "+s"(s_path), "+s"(s_s0));
     const float var_f = p.var_f;
     auto ldA = [=](int64_t r) { return CT ? ld3A(mA, r, var_f) : ld4(mA, r); };
-    auto ldB = [=](int64_t r) { return CT ? ld3B(mB, r) : ld4(mB, r); };
+    constexpr bool tg = !(CT && GS);  // greeks from the tile (GS: gbm_greeks in this kernel)
+    auto ldB = [=](int64_t r) {
+        return CT ? (tg ? ld3B(mB, r) : make_float4(0.f, 0.f, 0.f, 0.f)) : ld4(mB, r);
+    };
+    // GBM: the obs greeks of market price S (the market kernel's Heston slot values)
+    auto gbm_greeks = [&](float S) {
+        return (FAST || p.record_metrics) ? greeks_fast<true>(p, S, var_f) : make_float4(0.f, 0.f, 0.f, 0.f);
+    };
     HE_TIM(1);
     Env e;
     Mkt pre;
@@ -1114,7 +1134,8 @@ __device__ __forceinline__ void step_body(const Params& pk, int64_t n_envs, cons
             const uint32_t tt = e.t > (uint32_t)p.T ? (uint32_t)p.T : e.t;
             gpre = tB[(int64_t)e.path * (p.T + 1) + tt];
         } else {
-            gpre = (e.t == 0) ? make_float4(p.rstv[4 + 7], 0.0f, p.rstv[4 + 9], 0.0f) : ldB((int64_t)slot0 * N + i);
+            if (e.t == 0) gpre = make_float4(p.rstv[4 + 7], 0.0f, p.rstv[4 + 9], 0.0f);
+            else gpre = tg ? ldB((int64_t)slot0 * N + i) : gbm_greeks(pre.S);
         }
         const bool met = p.record_metrics != 0;
         pol_cd = met ? gpre.x : 0.0f;
@@ -1133,11 +1154,14 @@ __device__ __forceinline__ void step_body(const Params& pk, int64_t n_envs, cons
         const int64_t koff = (int64_t)k * N;
         bool term = false;
         if (live) {
-            // compact tiles: the lag return of the market kernel's slot.  The step from
-            // t in {0, T} starts from the reset market; at t == 0 pre is rst already
-            // (and spelling out both tests trips an illegal VGPR-to-SGPR copy in the
-            // ROCm 7.2 backend)
-            if constexpr (CT) g.w = lag_return(post.S, (e.t >= (uint32_t)p.T) ? rst.S : pre.S);
+            // GBM: the lag return (and without tile_greeks the greeks) of the market
+            // slot (see ld3A).  The step from t in {0, T} starts from the reset market;
+            // at t == 0 pre is rst already (and spelling out both tests trips an
+            // illegal VGPR-to-SGPR copy in the ROCm 7.2 backend)
+            if constexpr (CT) {
+                if (!tg) g = gbm_greeks(post.S);
+                g.w = lag_return(post.S, (e.t >= (uint32_t)p.T) ? rst.S : pre.S);
+            }
             if (POL) {
                 ak = policy_action(p, io.pol.policy, e.call, e.put, pol_o3, pol_o4, pol_cd, pol_pd);
                 if (io.pol.act_out) {
@@ -1303,10 +1327,12 @@ __device__ __forceinline__ void step_body(const Params& pk, int64_t n_envs, cons
 }
 
 // Every step path: Params by value in the kernel arguments.
-template <int MODE, bool INFO, bool SINGLE, bool BOOK, bool FAST, bool POL = false>
+// GS (GBM only): the obs greeks are evaluated here instead of read from tileB
+// (Params::tile_greeks == 0).
+template <int MODE, bool INFO, bool SINGLE, bool BOOK, bool FAST, bool POL = false, bool GS = false>
 __global__ __launch_bounds__(kBlock) void step_kernel(Params pk, State s, Io io, int k_steps, int slot0) {
     constexpr bool REPLAY = (MODE == HE_MODE_REPLAY);
-    step_body<MODE, INFO, SINGLE, BOOK, FAST, POL>(pk, pk.n, REPLAY ? pk.rec : pk.tileA,
+    step_body<MODE, INFO, SINGLE, BOOK, FAST, POL, GS>(pk, pk.n, REPLAY ? pk.rec : pk.tileA,
                                                    REPLAY ? pk.recg : pk.tileB, pk.tileC, s, io, k_steps, slot0);
 }
 
@@ -1320,7 +1346,7 @@ struct StepIo {
     uint8_t* trunc;
     float* tobs;
 };
-template <int MODE, bool BOOK, bool FAST>
+template <int MODE, bool BOOK, bool FAST, bool GS>
 __global__ __launch_bounds__(kBlock) void step1_kernel(const Params* __restrict__ pc, int64_t n, const float4* tA,
                                                        const float4* tB, const double* tC, State s, StepIo sio,
                                                        int slot0) {
@@ -1332,7 +1358,7 @@ __global__ __launch_bounds__(kBlock) void step1_kernel(const Params* __restrict_
     io.trunc = sio.trunc;
     io.tobs = sio.tobs;
     io.info = he_info{};
-    step_body<MODE, false, true, BOOK, FAST, false>(*pc, n, tA, tB, tC, s, io, 1, slot0);
+    step_body<MODE, false, true, BOOK, FAST, false, GS>(*pc, n, tA, tB, tC, s, io, 1, slot0);
 }
 
 // Explicit reset of envs `ids` (NULL: all).  Generate: the market position of a
@@ -1533,6 +1559,11 @@ static void fill_params(he_env* env) {
     p.variant = c.variant;
     p.loss = c.loss_type;
     p.record_metrics = c.record_metrics ? 1 : 0;
+    {   // HE_GREEKS_IN_STEP_MIN_ENVS in the environment overrides the threshold (tests, A/B)
+        const char* ev = getenv("HE_GREEKS_IN_STEP_MIN_ENVS");
+        const int64_t thr = (ev && *ev) ? (int64_t)atoll(ev) : kGreeksInStepMinEnvs;
+        p.tile_greeks = (c.mode == HE_MODE_HESTON || c.n_envs < thr) ? 1 : 0;
+    }
     p.autoreset = c.autoreset ? 1 : 0;
     p.mode = c.mode;
     p.mt = c.max_trade_per_step;
@@ -1755,12 +1786,12 @@ static void launch_reset(he_env* env, const int64_t* ids, int64_t count, float* 
                        env->cur, ids, count, obs, inf);
 }
 
-template <int MODE, bool BOOK, bool FAST>
-static void launch_step(he_env* env, const Params& p, const Io& io, bool info, int k, int slot0,
-                        hipStream_t st) {
+template <int MODE, bool BOOK, bool FAST, bool GS>
+static void launch_step_gs(he_env* env, const Params& p, const Io& io, bool info, int k, int slot0,
+                           hipStream_t st) {
     int64_t blocks = (env->cfg.n_envs + kEpb - 1) / kEpb;
     if (io.pol_on) {  // policy rollouts (any k)
-        void (*pk)(Params, State, Io, int, int) = step_kernel<MODE, false, false, BOOK, FAST, true>;
+        void (*pk)(Params, State, Io, int, int) = step_kernel<MODE, false, false, BOOK, FAST, true, GS>;
         hipLaunchKernelGGL(pk, dim3((unsigned)blocks), dim3(kBlock), 0, st, p, env->s, io, k, slot0);
         return;
     }
@@ -1773,17 +1804,21 @@ static void launch_step(he_env* env, const Params& p, const Io& io, bool info, i
         if (env->ev_start) {
             hipEvent_t a = (hipEvent_t)env->ev_start, b = (hipEvent_t)env->ev_stop;
             env->ev_start = env->ev_stop = nullptr;
-            hipExtLaunchKernelGGL((step1_kernel<MODE, BOOK, FAST>), dim3((unsigned)blocks), dim3(kBlock), 0, st, a, b, 0,
+            hipExtLaunchKernelGGL((step1_kernel<MODE, BOOK, FAST, GS>), dim3((unsigned)blocks), dim3(kBlock), 0, st, a, b, 0,
                                   pc, p.n, tA, tB, (const double*)p.tileC, env->s, sio, slot0);
             return;
         }
-        hipLaunchKernelGGL((step1_kernel<MODE, BOOK, FAST>), dim3((unsigned)blocks), dim3(kBlock), 0, st, pc, p.n, tA, tB,
+        hipLaunchKernelGGL((step1_kernel<MODE, BOOK, FAST, GS>), dim3((unsigned)blocks), dim3(kBlock), 0, st, pc, p.n, tA, tB,
                            (const double*)p.tileC, env->s, sio, slot0);
         return;
     }
     void (*kern)(Params, State, Io, int, int);
-    if (k == 1) kern = info ? step_kernel<MODE, true, true, BOOK, false> : step_kernel<MODE, false, true, BOOK, FAST>;
-    else kern = info ? step_kernel<MODE, true, false, BOOK, false> : step_kernel<MODE, false, false, BOOK, FAST>;
+    if (k == 1)
+        kern = info ? step_kernel<MODE, true, true, BOOK, false, false, GS>
+                    : step_kernel<MODE, false, true, BOOK, FAST, false, GS>;
+    else
+        kern = info ? step_kernel<MODE, true, false, BOOK, false, false, GS>
+                    : step_kernel<MODE, false, false, BOOK, FAST, false, GS>;
     if (env->ev_start) {  // one-shot: bracket exactly this dispatch (hipExtLaunchKernelGGL)
         hipEvent_t a = (hipEvent_t)env->ev_start, b = (hipEvent_t)env->ev_stop;
         env->ev_start = env->ev_stop = nullptr;
@@ -1791,6 +1826,18 @@ static void launch_step(he_env* env, const Params& p, const Io& io, bool info, i
         return;
     }
     hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kBlock), 0, st, p, env->s, io, k, slot0);
+}
+
+template <int MODE, bool BOOK, bool FAST>
+static void launch_step(he_env* env, const Params& p, const Io& io, bool info, int k, int slot0,
+                        hipStream_t st) {
+    if constexpr (MODE == HE_MODE_GBM) {
+        if (!p.tile_greeks) {
+            launch_step_gs<MODE, BOOK, FAST, true>(env, p, io, info, k, slot0, st);
+            return;
+        }
+    }
+    launch_step_gs<MODE, BOOK, FAST, false>(env, p, io, info, k, slot0, st);
 }
 
 // Start the next block: make its market tile current (generated ahead on the side
