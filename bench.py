@@ -55,6 +55,17 @@ ROLLOUT_BYTES_PER_ENV = {"gbm": 89, "gbm_step": 77, "heston": 97}
 ROLLOUT_STATE_BYTES = {"gbm": 44, "gbm_step": 44, "heston": 48}
 # market_kernel per env-step: tile records written
 MARKET_BYTES_PER_ENV = {"gbm": 24, "gbm_step": 12, "heston": 32}
+# market_kernel per env and block: block-start state read (ep 4, t 4, S 8, C 4, P 4),
+# written back to `cur` and to the rewind copy `bak` (3 x 24), + v (Heston) and the
+# running max (book) at 8 B each, 3 times
+MARKET_STATE_BYTES = 72
+# he_rollout in rollout mode runs step_market_kernel: the step workgroups of block b
+# and the market workgroups of block b+1 in one grid (HE_FUSED_MARKET=0, or with a
+# liability book: the market on a side stream, step_kernel alone)
+
+
+def fused_market():
+    return os.environ.get("HE_FUSED_MARKET", "1") != "0"
 
 
 def tile_layout(mode, n):
@@ -302,7 +313,7 @@ def pmc_traffic(args):
             for f in glob.glob(os.path.join(td, "**", "*counter_collection.csv"), recursive=True):
                 with open(f) as fh:
                     for r in csv.DictReader(fh):
-                        if re.search(r"step1?_kernel", r.get("Kernel_Name", "")) and r.get("Counter_Name") == ctr:
+                        if re.search(r"step1?_kernel|step_market_kernel", r.get("Kernel_Name", "")) and r.get("Counter_Name") == ctr:
                             rows.append(float(r["Counter_Value"]))
             if not rows:
                 return None, f"no {ctr} rows for the step kernel"
@@ -418,6 +429,11 @@ def roofline(mode, n, kern_ms, rk, book=False, market="gbm"):
     if mode == "rollout":
         bytes_launch = n * rk * (ROLLOUT_BYTES_PER_ENV[market] + (8 if book else 0) + ROLLOUT_STATE_BYTES[market] / rk)
         kname = "step_kernel (he_rollout, K=%d fused steps)" % rk
+        if fused_market() and not book:
+            mstate = MARKET_STATE_BYTES + (24 if market == "heston" else 0) + (24 if book else 0)
+            bytes_launch += n * (rk * (MARKET_BYTES_PER_ENV[market] + (8 if book else 0)) + mstate)
+            kname = ("step_market_kernel (he_rollout, K=%d fused steps + the next block's market "
+                     "in the same grid)" % rk)
     else:
         bytes_launch = n * (STEP_BYTES_PER_ENV[market] + (16 if book else 0))
         kname = "step1_kernel (he_step, K=1)"

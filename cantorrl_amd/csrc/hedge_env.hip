@@ -526,15 +526,14 @@ __device__ __forceinline__ void normals(const Params& p, int64_t gid, uint64_t n
 // from S0 when t in {0, T} (autoreset), so every slot is a pure function of the
 // block-start state.
 template <int MODE, bool BOOK>
-__global__ __launch_bounds__(kMktEnvs * kMktLanes, HE_MKT_WAVES) void market_kernel(Params p, Market cur, Market bak,
-                                                                       int32_t advance_only) {
+__device__ __forceinline__ void market_body(Params p, Market cur, Market bak, int32_t advance_only, int64_t bid) {
     constexpr bool HESTON = (MODE == HE_MODE_HESTON);
     __shared__ double shS[kMktEnvs][kMaxBlock + 1];
     __shared__ double shV[HESTON ? kMktEnvs : 1][HESTON ? kMaxBlock + 1 : 1];
     __shared__ double shM[BOOK ? kMktEnvs : 1][BOOK ? kMaxBlock + 1 : 1];  // running max of S
     const int lane = threadIdx.x & (kMktEnvs - 1);
     const int sub = threadIdx.x / kMktEnvs;
-    const int64_t i = (int64_t)blockIdx.x * kMktEnvs + lane;
+    const int64_t i = bid * kMktEnvs + lane;
     const bool live = i < p.n;
     const int M = p.M;
     const uint32_t T = (uint32_t)p.T;
@@ -720,6 +719,12 @@ __global__ __launch_bounds__(kMktEnvs * kMktLanes, HE_MKT_WAVES) void market_ker
             p.tileC[i] = (t0 == 0u || t0 >= T) ? p.book_rst
                                                 : book_value(p, S0v, HESTON ? v0v : p.var, (int32_t)t0, M0v);
     }
+}
+
+template <int MODE, bool BOOK>
+__global__ __launch_bounds__(kMktEnvs * kMktLanes, HE_MKT_WAVES) void market_kernel(Params p, Market cur, Market bak,
+                                                                                     int32_t advance_only) {
+    market_body<MODE, BOOK>(p, cur, bak, advance_only, blockIdx.x);
 }
 
 // Reset market constants + reset obs row (generate): rst = {S0, v0, C0, P0, obs0[13]}.
@@ -1022,7 +1027,8 @@ __device__ __forceinline__ void env_reset_common(const Params& p, Env& e) {
 // replay table rec / recg.
 template <int MODE, bool INFO, bool SINGLE, bool BOOK, bool FAST, bool POL, bool GS>
 __device__ __forceinline__ void step_body(const Params& pk, int64_t n_envs, const float4* tA, const float4* tB,
-                                          const double* tC, State s, Io io, int k_steps_arg, int slot0) {
+                                          const double* tC, State s, Io io, int k_steps_arg, int slot0,
+                                          int64_t bid) {
     constexpr bool REPLAY = (MODE == HE_MODE_REPLAY);
     constexpr bool CT = (MODE == HE_MODE_GBM);  // 12-B tile records (see ld3A)
     const int k_steps = SINGLE ? 1 : k_steps_arg;
@@ -1033,7 +1039,7 @@ __device__ __forceinline__ void step_body(const Params& pk, int64_t n_envs, cons
     __builtin_amdgcn_s_setprio(3);
     __shared__ __attribute__((aligned(16))) float tile[kEpb * kObs];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int64_t wrow0 = (int64_t)blockIdx.x * kEpb + wave * kEpw;  // first env of this wave
+    const int64_t wrow0 = bid * kEpb + wave * kEpw;  // first env of this wave
     const int64_t i = wrow0 + lane;
     const int64_t N = n_envs;
     const bool live = lane < kEpw && i < N;
@@ -1333,7 +1339,8 @@ template <int MODE, bool INFO, bool SINGLE, bool BOOK, bool FAST, bool POL = fal
 __global__ __launch_bounds__(kBlock) void step_kernel(Params pk, State s, Io io, int k_steps, int slot0) {
     constexpr bool REPLAY = (MODE == HE_MODE_REPLAY);
     step_body<MODE, INFO, SINGLE, BOOK, FAST, POL, GS>(pk, pk.n, REPLAY ? pk.rec : pk.tileA,
-                                                   REPLAY ? pk.recg : pk.tileB, pk.tileC, s, io, k_steps, slot0);
+                                                   REPLAY ? pk.recg : pk.tileB, pk.tileC, s, io, k_steps, slot0,
+                                                       blockIdx.x);
 }
 
 // he_step without info: Params from a device-resident copy; the kernel arguments carry
@@ -1358,7 +1365,26 @@ __global__ __launch_bounds__(kBlock) void step1_kernel(const Params* __restrict_
     io.trunc = sio.trunc;
     io.tobs = sio.tobs;
     io.info = he_info{};
-    step_body<MODE, false, true, BOOK, FAST, false, GS>(*pc, n, tA, tB, tC, s, io, 1, slot0);
+    step_body<MODE, false, true, BOOK, FAST, false, GS>(*pc, n, tA, tB, tC, s, io, 1, slot0, blockIdx.x);
+}
+
+// Rollout block with the next block's market in the same grid: workgroups
+// [0, step_blocks) step block b from tile pk (as step_kernel), the rest generate block
+// b+1 into tile pm (as market_kernel, workgroup bid - step_blocks).  One dispatch per
+// block on the caller's stream: block b+1's steps are ordered after its market by the
+// stream alone, with no cross-queue event between them (measured 25 us between the
+// side-stream market's end and the next step dispatch at 65,536 envs).  The step
+// workgroups come first in dispatch order and keep s_setprio 3.
+template <int MODE, bool BOOK, bool FAST, bool GS>
+__global__ __launch_bounds__(kBlock, HE_MKT_WAVES) void step_market_kernel(Params pk, State s, Io io, int k_steps,
+                                                                           int slot0, Params pm, Market cur,
+                                                                           Market bak, int32_t step_blocks) {
+    static_assert(kBlock == kMktEnvs * kMktLanes, "one workgroup shape for both roles");
+    if ((int32_t)blockIdx.x < step_blocks)
+        step_body<MODE, false, false, BOOK, FAST, false, GS>(pk, pk.n, pk.tileA, pk.tileB, pk.tileC, s, io, k_steps,
+                                                              slot0, blockIdx.x);
+    else
+        market_body<MODE, BOOK>(pm, cur, bak, 0, (int64_t)blockIdx.x - step_blocks);
 }
 
 // Explicit reset of envs `ids` (NULL: all).  Generate: the market position of a
@@ -1518,6 +1544,7 @@ struct he_env {
     int32_t block_pos = 0;    // generate: next slot to consume; M = tile exhausted/invalid
     int32_t cur_buf = 0;      // tile buffer of the block being consumed
     int32_t next_state = 0;   // next block: 0 none, 1 generating on `xs` (ev_next), 2 ready
+    bool fuse_market = true;  // rollouts: next block's market in the step grid (HE_FUSED_MARKET=0: side stream)
     int32_t prefetch_mode = 0; // 0 auto, 1 never, 2 always: market_kernel(b+1) on `xs` during block b
     hipStream_t xs = nullptr; // library side stream for market prefetch
     hipEvent_t ev_fork = nullptr, ev_next = nullptr;
@@ -1840,6 +1867,37 @@ static void launch_step(he_env* env, const Params& p, const Io& io, bool info, i
     launch_step_gs<MODE, BOOK, FAST, false>(env, p, io, info, k, slot0, st);
 }
 
+template <int MODE, bool BOOK, bool FAST, bool GS>
+static void launch_fused_gs(he_env* env, const Params& p, const Io& io, int k, int slot0, hipStream_t st) {
+    const int64_t sblocks = (env->cfg.n_envs + kEpb - 1) / kEpb;
+    const int64_t mblocks = (env->cfg.n_envs + kMktEnvs - 1) / kMktEnvs;
+    const int nb = env->cur_buf ^ 1;
+    const Params pm = tile_params(env, nb);
+    const dim3 grid((unsigned)(sblocks + mblocks));
+    if (env->ev_start) {  // one-shot: bracket exactly this dispatch (hipExtLaunchKernelGGL)
+        hipEvent_t a = (hipEvent_t)env->ev_start, b = (hipEvent_t)env->ev_stop;
+        env->ev_start = env->ev_stop = nullptr;
+        hipExtLaunchKernelGGL((step_market_kernel<MODE, BOOK, FAST, GS>), grid, dim3(kBlock), 0, st, a, b, 0, p,
+                              env->s, io, k, slot0, pm, env->cur, env->bak[nb], (int32_t)sblocks);
+        return;
+    }
+    hipLaunchKernelGGL((step_market_kernel<MODE, BOOK, FAST, GS>), grid, dim3(kBlock), 0, st, p, env->s, io, k, slot0,
+                       pm, env->cur, env->bak[nb], (int32_t)sblocks);
+}
+
+// step the current block (k steps from slot0) and generate the next block into the
+// other tile buffer, one dispatch (step_market_kernel)
+template <int MODE, bool BOOK, bool FAST>
+static void launch_fused(he_env* env, const Params& p, const Io& io, int k, int slot0, hipStream_t st) {
+    if constexpr (MODE == HE_MODE_GBM) {
+        if (!p.tile_greeks) {
+            launch_fused_gs<MODE, BOOK, FAST, true>(env, p, io, k, slot0, st);
+            return;
+        }
+    }
+    launch_fused_gs<MODE, BOOK, FAST, false>(env, p, io, k, slot0, st);
+}
+
 // Start the next block: make its market tile current (generated ahead on the side
 // stream, or now on `st`), then prefetch the block after it on the side stream so
 // that market_kernel(b+1) runs concurrently with the step kernels of block b.
@@ -1890,6 +1948,7 @@ static he_status launch_steps(he_env* env, Io io, bool info, int k_total, void* 
     const int64_t N = c.n_envs;
     int done = 0;
     while (done < k_total) {
+        bool fuse = false;
         if (env->block_pos >= M) {
             // auto policy (MI355X, graph-mode he_step, GBM): at 65,536 envs the
             // background market waves slow the latency-bound step_kernel more than
@@ -1897,7 +1956,12 @@ static he_status launch_steps(he_env* env, Io io, bool info, int k_total, void* 
             // bandwidth-bound and overlap wins (+5% at 262k, +14% at 524k, +19% at 1M)
             bool want = env->prefetch_mode == 2 ||
                         (env->prefetch_mode == 0 && (k_total > 1 || c.n_envs >= kPrefetchMinEnvs));
-            he_status s = advance_block(env, st, want);
+            // rollouts: the next block's market rides in the step grid (stream-ordered,
+            // no side-stream join).  Not with a liability book: its market is 3x the
+            // step work and VALU-bound, the side stream's overlap measures the same
+            // (configs 4/5: 1.25e10 / 1.12e10 env-steps/s either way)
+            fuse = want && env->fuse_market && k_total > 1 && !info && !io.pol_on && c.book_size == 0;
+            he_status s = advance_block(env, st, want && !fuse);
             if (s != HE_OK) return s;
         }
         int k = k_total - done;
@@ -1911,7 +1975,26 @@ static he_status launch_steps(he_env* env, Io io, bool info, int k_total, void* 
         Params p = tile_params(env, env->cur_buf);
         const bool book = c.book_size > 0;
         const bool fast = fast_config(env);
-        if (c.mode == HE_MODE_GBM) {
+        if (fuse) {
+            if (c.mode == HE_MODE_GBM) {
+                if (book) {
+                    if (fast) launch_fused<HE_MODE_GBM, true, true>(env, p, sub, k, env->block_pos, st);
+                    else launch_fused<HE_MODE_GBM, true, false>(env, p, sub, k, env->block_pos, st);
+                } else {
+                    if (fast) launch_fused<HE_MODE_GBM, false, true>(env, p, sub, k, env->block_pos, st);
+                    else launch_fused<HE_MODE_GBM, false, false>(env, p, sub, k, env->block_pos, st);
+                }
+            } else {
+                if (book) {
+                    if (fast) launch_fused<HE_MODE_HESTON, true, true>(env, p, sub, k, env->block_pos, st);
+                    else launch_fused<HE_MODE_HESTON, true, false>(env, p, sub, k, env->block_pos, st);
+                } else {
+                    if (fast) launch_fused<HE_MODE_HESTON, false, true>(env, p, sub, k, env->block_pos, st);
+                    else launch_fused<HE_MODE_HESTON, false, false>(env, p, sub, k, env->block_pos, st);
+                }
+            }
+            env->next_state = 2;  // ordered on st before the next block's steps
+        } else if (c.mode == HE_MODE_GBM) {
             if (book) {
                 if (fast) launch_step<HE_MODE_GBM, true, true>(env, p, sub, info, k, env->block_pos, st);
                 else launch_step<HE_MODE_GBM, true, false>(env, p, sub, info, k, env->block_pos, st);
@@ -2068,6 +2151,10 @@ he_status he_create(const he_config* cfg, he_env** out) {
         HE_HIP(env, hipMalloc(&env->rst, 32 * sizeof(float)));
         env->block_pos = c.market_block;
         env->prefetch_mode = c.market_prefetch;  // 0 auto, 1 never, 2 always
+        {
+            const char* ev = getenv("HE_FUSED_MARKET");
+            env->fuse_market = !(ev && ev[0] == '0');
+        }
         HE_HIP(env, hipStreamCreateWithFlags(&env->xs, hipStreamNonBlocking));
         HE_HIP(env, hipEventCreateWithFlags(&env->ev_fork, hipEventDisableTiming));
         HE_HIP(env, hipEventCreateWithFlags(&env->ev_next, hipEventDisableTiming));

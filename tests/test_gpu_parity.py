@@ -408,18 +408,23 @@ def test_policy_rollout_generate_equals_host_policy_steps(policy, greeks_site):
 
 def test_greeks_site_bit_identical(monkeypatch):
     """The step kernel's GBM greeks are the market kernel's values bit for bit (same f32
-    code on the same S): rollouts with either site agree exactly, policies included."""
+    code on the same S), and the fused step+market grid equals the side-stream market:
+    rollouts agree exactly in all four combinations."""
     from cantorrl_amd.vec_env import HedgingVecEnv
     n, K = 3000, 150
     gen = dict(episode_length=40)
     acts = torch.rand((K, n, 2), device="cuda") * 2.2 - 1.1
     out = []
-    for thr in (str(1 << 62), "0"):
+    # greeks site x where the next block's market runs (in the rollout grid, or on the
+    # side stream beside step_kernel)
+    for thr, fused in ((str(1 << 62), "1"), ("0", "1"), (str(1 << 62), "0"), ("0", "0")):
         monkeypatch.setenv("HE_GREEKS_IN_STEP_MIN_ENVS", thr)
+        monkeypatch.setenv("HE_FUSED_MARKET", fused)
         env = HedgingVecEnv(n, mode="gbm", generate=gen, seed=11, return_numpy=False, info_keys=())
         obs0 = env.reset_tensors().clone()
         res = env.rollout(acts)
         out.append((obs0, *[r.clone() for r in res]))
         env.close()
-    for a, b in zip(out[0], out[1]):
-        assert torch.equal(a, b)
+    for o in out[1:]:
+        for a, b in zip(out[0], o):
+            assert torch.equal(a, b)
