@@ -1375,6 +1375,27 @@ __global__ __launch_bounds__(kBlock) void step1_kernel(const Params* __restrict_
 // stream alone, with no cross-queue event between them (measured 25 us between the
 // side-stream market's end and the next step dispatch at 65,536 envs).  The step
 // workgroups come first in dispatch order and keep s_setprio 3.
+#ifndef HE_FUSED_DPARAMS
+#define HE_FUSED_DPARAMS 1
+#endif
+#if HE_FUSED_DPARAMS
+// Params of both tile buffers from the device copies (pc[buf] steps, pc[buf ^ 1] is the
+// market's): a 0.2 KB kernarg segment instead of 2 x Params by value.
+template <int MODE, bool BOOK, bool FAST, bool GS>
+__global__ __launch_bounds__(kBlock, HE_MKT_WAVES) void step_market_kernel(const Params* __restrict__ pc, int32_t buf,
+                                                                           State s, Io io, int k_steps, int slot0,
+                                                                           Market cur, Market bak,
+                                                                           int32_t step_blocks) {
+    static_assert(kBlock == kMktEnvs * kMktLanes, "one workgroup shape for both roles");
+    if ((int32_t)blockIdx.x < step_blocks) {
+        const Params& pk = pc[buf];
+        step_body<MODE, false, false, BOOK, FAST, false, GS>(pk, pk.n, pk.tileA, pk.tileB, pk.tileC, s, io, k_steps,
+                                                              slot0, blockIdx.x);
+    } else {
+        market_body<MODE, BOOK>(pc[buf ^ 1], cur, bak, 0, (int64_t)blockIdx.x - step_blocks);
+    }
+}
+#else
 template <int MODE, bool BOOK, bool FAST, bool GS>
 __global__ __launch_bounds__(kBlock, HE_MKT_WAVES) void step_market_kernel(Params pk, State s, Io io, int k_steps,
                                                                            int slot0, Params pm, Market cur,
@@ -1386,6 +1407,7 @@ __global__ __launch_bounds__(kBlock, HE_MKT_WAVES) void step_market_kernel(Param
     else
         market_body<MODE, BOOK>(pm, cur, bak, 0, (int64_t)blockIdx.x - step_blocks);
 }
+#endif
 
 // Explicit reset of envs `ids` (NULL: all).  Generate: the market position of a
 // reset env moves to the start of its next episode.
@@ -1872,17 +1894,32 @@ static void launch_fused_gs(he_env* env, const Params& p, const Io& io, int k, i
     const int64_t sblocks = (env->cfg.n_envs + kEpb - 1) / kEpb;
     const int64_t mblocks = (env->cfg.n_envs + kMktEnvs - 1) / kMktEnvs;
     const int nb = env->cur_buf ^ 1;
-    const Params pm = tile_params(env, nb);
     const dim3 grid((unsigned)(sblocks + mblocks));
+    hipEvent_t a = nullptr, b = nullptr;
     if (env->ev_start) {  // one-shot: bracket exactly this dispatch (hipExtLaunchKernelGGL)
-        hipEvent_t a = (hipEvent_t)env->ev_start, b = (hipEvent_t)env->ev_stop;
+        a = (hipEvent_t)env->ev_start;
+        b = (hipEvent_t)env->ev_stop;
         env->ev_start = env->ev_stop = nullptr;
+    }
+#if HE_FUSED_DPARAMS
+    (void)p;
+    const Params* pc = env->dparams;
+    const int32_t buf = env->cur_buf;
+    if (a)
+        hipExtLaunchKernelGGL((step_market_kernel<MODE, BOOK, FAST, GS>), grid, dim3(kBlock), 0, st, a, b, 0, pc, buf,
+                              env->s, io, k, slot0, env->cur, env->bak[nb], (int32_t)sblocks);
+    else
+        hipLaunchKernelGGL((step_market_kernel<MODE, BOOK, FAST, GS>), grid, dim3(kBlock), 0, st, pc, buf, env->s, io,
+                           k, slot0, env->cur, env->bak[nb], (int32_t)sblocks);
+#else
+    const Params pm = tile_params(env, nb);
+    if (a)
         hipExtLaunchKernelGGL((step_market_kernel<MODE, BOOK, FAST, GS>), grid, dim3(kBlock), 0, st, a, b, 0, p,
                               env->s, io, k, slot0, pm, env->cur, env->bak[nb], (int32_t)sblocks);
-        return;
-    }
-    hipLaunchKernelGGL((step_market_kernel<MODE, BOOK, FAST, GS>), grid, dim3(kBlock), 0, st, p, env->s, io, k, slot0,
-                       pm, env->cur, env->bak[nb], (int32_t)sblocks);
+    else
+        hipLaunchKernelGGL((step_market_kernel<MODE, BOOK, FAST, GS>), grid, dim3(kBlock), 0, st, p, env->s, io, k,
+                           slot0, pm, env->cur, env->bak[nb], (int32_t)sblocks);
+#endif
 }
 
 // step the current block (k steps from slot0) and generate the next block into the
