@@ -428,3 +428,45 @@ def test_greeks_site_bit_identical(monkeypatch):
     for o in out[1:]:
         for a, b in zip(out[0], o):
             assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("mode", ["gbm", "heston"])
+def test_fused_rollouts_mixed_with_steps_resets_and_checkpoints(mode, monkeypatch):
+    """The fused step+market grid leaves the next block generated on the stream
+    (next_state 2).  Interleaving rollouts of ragged lengths with he_step calls, a
+    partial reset mid-block and a checkpoint gives exactly what the side-stream market
+    gives on the same sequence."""
+    from cantorrl_amd.vec_env import HedgingVecEnv
+    n = 700
+    gen = dict(episode_length=50)
+    acts = torch.rand((400, n, 2), device="cuda") * 2.2 - 1.1
+    outs = []
+    for fused in ("1", "0"):
+        monkeypatch.setenv("HE_FUSED_MARKET", fused)
+        env = HedgingVecEnv(n, mode=mode, generate=gen, seed=21, return_numpy=False, info_keys=())
+        env.reset_tensors()
+        got = []
+        a0 = 0
+        for kind, k in (("r", 64), ("r", 30), ("s", 5), ("r", 93), ("reset", 0), ("r", 17), ("ckpt", 0),
+                        ("r", 64), ("s", 2), ("r", 70)):
+            if kind == "r":
+                o, r, t = env.rollout(acts[a0:a0 + k].contiguous())
+                got += [o.clone(), r.clone(), t.clone()]
+                a0 += k
+            elif kind == "s":
+                for _ in range(k):
+                    o, r, t, _ = env.step_tensors(acts[a0], terminal_obs=False)
+                    got += [o.clone(), r.clone(), t.clone()]
+                    a0 += 1
+            elif kind == "reset":
+                got.append(env.reset_tensors(env_ids=[0, 5, 350, 699]).clone())
+            else:
+                blob = env.get_state()
+                env.close()
+                env = HedgingVecEnv(n, mode=mode, generate=gen, seed=21, return_numpy=False, info_keys=())
+                env.set_state(blob)
+        env.close()
+        outs.append(got)
+    assert len(outs[0]) == len(outs[1])
+    for i, (a, b) in enumerate(zip(*outs)):
+        assert torch.equal(a, b), i
