@@ -1378,11 +1378,17 @@ __global__ __launch_bounds__(kBlock) void step1_kernel(const Params* __restrict_
 #ifndef HE_FUSED_DPARAMS
 #define HE_FUSED_DPARAMS 1
 #endif
+// min waves per SIMD of step_market_kernel.  4 (VGPR cap 128: one step + three market
+// workgroups per CU) measured +3.8% at 1,048,576 envs and +0% at 65,536, but spills
+// ~100 B per lane to scratch; kept at the market kernel's 2 (167 VGPRs, 3 per CU)
+#ifndef HE_FUSED_WAVES
+#define HE_FUSED_WAVES HE_MKT_WAVES
+#endif
 #if HE_FUSED_DPARAMS
 // Params of both tile buffers from the device copies (pc[buf] steps, pc[buf ^ 1] is the
 // market's): a 0.2 KB kernarg segment instead of 2 x Params by value.
 template <int MODE, bool BOOK, bool FAST, bool GS>
-__global__ __launch_bounds__(kBlock, HE_MKT_WAVES) void step_market_kernel(const Params* __restrict__ pc, int32_t buf,
+__global__ __launch_bounds__(kBlock, HE_FUSED_WAVES) void step_market_kernel(const Params* __restrict__ pc, int32_t buf,
                                                                            State s, Io io, int k_steps, int slot0,
                                                                            Market cur, Market bak,
                                                                            int32_t step_blocks) {
@@ -1397,7 +1403,7 @@ __global__ __launch_bounds__(kBlock, HE_MKT_WAVES) void step_market_kernel(const
 }
 #else
 template <int MODE, bool BOOK, bool FAST, bool GS>
-__global__ __launch_bounds__(kBlock, HE_MKT_WAVES) void step_market_kernel(Params pk, State s, Io io, int k_steps,
+__global__ __launch_bounds__(kBlock, HE_FUSED_WAVES) void step_market_kernel(Params pk, State s, Io io, int k_steps,
                                                                            int slot0, Params pm, Market cur,
                                                                            Market bak, int32_t step_blocks) {
     static_assert(kBlock == kMktEnvs * kMktLanes, "one workgroup shape for both roles");
@@ -1895,6 +1901,18 @@ static void launch_fused_gs(he_env* env, const Params& p, const Io& io, int k, i
     const int64_t mblocks = (env->cfg.n_envs + kMktEnvs - 1) / kMktEnvs;
     const int nb = env->cur_buf ^ 1;
     const dim3 grid((unsigned)(sblocks + mblocks));
+    size_t pad = 0;
+#if defined(HE_FUSED_WG_PER_CU) && HE_FUSED_WG_PER_CU > 0
+    {   // diagnostic: cap the grid's workgroups per CU through dynamic LDS
+        static size_t stat = [] {
+            hipFuncAttributes fa{};
+            (void)hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(step_market_kernel<MODE, BOOK, FAST, GS>));
+            return (size_t)fa.sharedSizeBytes;
+        }();
+        const size_t per = kCuLds / (HE_FUSED_WG_PER_CU + 1) + 1024;
+        pad = per > stat ? per - stat : 0;
+    }
+#endif
     hipEvent_t a = nullptr, b = nullptr;
     if (env->ev_start) {  // one-shot: bracket exactly this dispatch (hipExtLaunchKernelGGL)
         a = (hipEvent_t)env->ev_start;
@@ -1906,18 +1924,18 @@ static void launch_fused_gs(he_env* env, const Params& p, const Io& io, int k, i
     const Params* pc = env->dparams;
     const int32_t buf = env->cur_buf;
     if (a)
-        hipExtLaunchKernelGGL((step_market_kernel<MODE, BOOK, FAST, GS>), grid, dim3(kBlock), 0, st, a, b, 0, pc, buf,
+        hipExtLaunchKernelGGL((step_market_kernel<MODE, BOOK, FAST, GS>), grid, dim3(kBlock), pad, st, a, b, 0, pc, buf,
                               env->s, io, k, slot0, env->cur, env->bak[nb], (int32_t)sblocks);
     else
-        hipLaunchKernelGGL((step_market_kernel<MODE, BOOK, FAST, GS>), grid, dim3(kBlock), 0, st, pc, buf, env->s, io,
+        hipLaunchKernelGGL((step_market_kernel<MODE, BOOK, FAST, GS>), grid, dim3(kBlock), pad, st, pc, buf, env->s, io,
                            k, slot0, env->cur, env->bak[nb], (int32_t)sblocks);
 #else
     const Params pm = tile_params(env, nb);
     if (a)
-        hipExtLaunchKernelGGL((step_market_kernel<MODE, BOOK, FAST, GS>), grid, dim3(kBlock), 0, st, a, b, 0, p,
+        hipExtLaunchKernelGGL((step_market_kernel<MODE, BOOK, FAST, GS>), grid, dim3(kBlock), pad, st, a, b, 0, p,
                               env->s, io, k, slot0, pm, env->cur, env->bak[nb], (int32_t)sblocks);
     else
-        hipLaunchKernelGGL((step_market_kernel<MODE, BOOK, FAST, GS>), grid, dim3(kBlock), 0, st, p, env->s, io, k,
+        hipLaunchKernelGGL((step_market_kernel<MODE, BOOK, FAST, GS>), grid, dim3(kBlock), pad, st, p, env->s, io, k,
                            slot0, pm, env->cur, env->bak[nb], (int32_t)sblocks);
 #endif
 }
