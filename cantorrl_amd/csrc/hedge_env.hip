@@ -2030,23 +2030,13 @@ static he_status launch_steps(he_env* env, Io io, bool info, int k_total, void* 
         Params p = tile_params(env, env->cur_buf);
         const bool book = c.book_size > 0;
         const bool fast = fast_config(env);
-        if (fuse) {
+        if (fuse) {  // never with a book (see above)
             if (c.mode == HE_MODE_GBM) {
-                if (book) {
-                    if (fast) launch_fused<HE_MODE_GBM, true, true>(env, p, sub, k, env->block_pos, st);
-                    else launch_fused<HE_MODE_GBM, true, false>(env, p, sub, k, env->block_pos, st);
-                } else {
-                    if (fast) launch_fused<HE_MODE_GBM, false, true>(env, p, sub, k, env->block_pos, st);
-                    else launch_fused<HE_MODE_GBM, false, false>(env, p, sub, k, env->block_pos, st);
-                }
+                if (fast) launch_fused<HE_MODE_GBM, false, true>(env, p, sub, k, env->block_pos, st);
+                else launch_fused<HE_MODE_GBM, false, false>(env, p, sub, k, env->block_pos, st);
             } else {
-                if (book) {
-                    if (fast) launch_fused<HE_MODE_HESTON, true, true>(env, p, sub, k, env->block_pos, st);
-                    else launch_fused<HE_MODE_HESTON, true, false>(env, p, sub, k, env->block_pos, st);
-                } else {
-                    if (fast) launch_fused<HE_MODE_HESTON, false, true>(env, p, sub, k, env->block_pos, st);
-                    else launch_fused<HE_MODE_HESTON, false, false>(env, p, sub, k, env->block_pos, st);
-                }
+                if (fast) launch_fused<HE_MODE_HESTON, false, true>(env, p, sub, k, env->block_pos, st);
+                else launch_fused<HE_MODE_HESTON, false, false>(env, p, sub, k, env->block_pos, st);
             }
             env->next_state = 2;  // ordered on st before the next block's steps
         } else if (c.mode == HE_MODE_GBM) {
