@@ -128,9 +128,11 @@ typedef struct he_config {
     double heston_rho;
     int32_t market_block;       /* generate modes: steps of market data generated per
                                    market_kernel launch (1..64, default 64)          */
-    int32_t market_prefetch;    /* market_kernel(b+1) on the side stream: 0 auto (fused
+    int32_t market_prefetch;    /* market of block b+1 generated ahead: 0 auto (fused
                                    rollouts, or he_step from 131,072 envs), 1 never,
-                                   2 always                                          */
+                                   2 always.  he_rollout without a book generates it in
+                                   the step grid on `stream` (step_market_kernel), the
+                                   other paths on the side stream                    */
     int32_t book_size;          /* generate modes: options in the liability book (0..8) */
     int32_t reserved_i;
     he_book_option book[HE_BOOK_MAX];
@@ -252,9 +254,11 @@ he_status he_rollout_policy(he_env* env, int32_t k_steps, int32_t policy, float*
                             int64_t record_capacity, unsigned long long* record_count, void* stream);
 
 /* Generate modes run market_kernel for block b+1 on a library-owned side stream
- * while the step kernels of block b run on `stream`.  he_sync_market makes `stream`
- * wait for that prefetch (a join): call it before ending a hipGraph capture that
- * contains he_step/he_rollout calls.  No-op in replay mode. */
+ * while the step kernels of block b run on `stream` (he_step, policy rollouts, books;
+ * he_rollout otherwise generates it inside its own grid on `stream`, which needs no
+ * join).  he_sync_market makes `stream` wait for a side-stream prefetch: call it
+ * before ending a hipGraph capture that contains he_step/he_rollout calls.  No-op in
+ * replay mode and when nothing is pending. */
 he_status he_sync_market(he_env* env, void* stream);
 
 /* Measurement: the next step_kernel dispatch (he_step / he_rollout) records
