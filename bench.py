@@ -35,33 +35,42 @@ import torch
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
-# Algorithmic HBM bytes per env-step.  Market tile records:
+# Algorithmic HBM bytes, SURVEY.md 8(d) -- the figure roofline.achieved is priced on:
+#   he_rollout (fused K-step rollout): 66 B per env-step (action 8 + obs 52 + reward 4 +
+#       terminated/truncated 2) + 120 B per env per launch (state read + written, 2 x 60)
+#   he_step (Gym API, one launch per step): 186 B per env-step
+SURVEY_ROLLOUT_B, SURVEY_ROLLOUT_STATE_B, SURVEY_STEP_B = 66, 120, 186
+# What the kernels themselves must move:
+#   lds_rollout_kernel (he_rollout, GBM, no book; the market is made in LDS): per env-step
+#       action 8 + obs 52 + reward 4 + terminated 1 = 65; per env per launch the step
+#       state (t 4, pos 4, cash 8) read + written 32 and the market position (ep 4, t 4,
+#       S 8, C 4, P 4) read + written 48 = 80
+LDS_STEP_B, LDS_STATE_B = 65, 80
+# Tile kernels (he_step; he_rollout with a liability book or HE_LDS_ROLLOUT=0): the market
+# is written to an HBM tile [M+1][N] by market_kernel and read back by the step kernel.
+# Tile records per env-step:
 #   "gbm"        12-B {S, C, P} + 12-B {greeks}   (GBM below GREEKS_IN_STEP_MIN_ENVS envs)
 #   "gbm_step"   12-B {S, C, P} only              (GBM from there: the step kernel
 #                                                  evaluates the f32 obs greeks itself)
 #   "heston"     16-B {S, v, C, P} + 16-B {greeks, lag}
-# In GBM mode v is a constant and the step kernel recomputes the lag return.
-# he_step (step1_kernel, one launch per step):
-#   reads : state (t 4, pos 4, cash 8) 16 + action 8 + market tile slots
-#           (pre A, post A, post B) 36 | (pre A, post A) 24 | 48              = 60 | 48 | 72
-#   writes: state 16 + obs 52 + reward 4 + terminated 1 + truncated 1           = 74
-# he_rollout (step_kernel, K steps per launch, state in registers):
-#   per step: action 8 + tile post slots 24 | 12 | 32 (read) + obs 52 + reward 4
-#             + terminated 1                                                   = 89 | 77 | 97
-#   per launch: state 16 read + 16 written + pre slot 12 | 12 | 16 read        = 44 | 44 | 48
+# he_step (step1_kernel): reads state 16 + action 8 + tile slots (pre A, post A, post B)
+#   36 | 24 | 48; writes state 16 + obs 52 + reward 4 + terminated 1 + truncated 1
+# he_rollout step_kernel (K steps): per step action 8 + tile post slots 24 | 12 | 32 + obs
+#   52 + reward 4 + terminated 1; per launch state 32 + pre slot 12 | 12 | 16
 GREEKS_IN_STEP_MIN_ENVS = 262144  # hedge_env.hip kGreeksInStepMinEnvs
 STEP_BYTES_PER_ENV = {"gbm": 134, "gbm_step": 122, "heston": 146}
 ROLLOUT_BYTES_PER_ENV = {"gbm": 89, "gbm_step": 77, "heston": 97}
 ROLLOUT_STATE_BYTES = {"gbm": 44, "gbm_step": 44, "heston": 48}
-# market_kernel per env-step: tile records written
+# market_kernel per env-step: tile records written; per env and block: the block-start
+# state read (ep 4, t 4, S 8, C 4, P 4), written back to `cur` and to the rewind copy
+# `bak` (3 x 24), + v (Heston) and the running max (book) at 8 B each, 3 times
 MARKET_BYTES_PER_ENV = {"gbm": 24, "gbm_step": 12, "heston": 32}
-# market_kernel per env and block: block-start state read (ep 4, t 4, S 8, C 4, P 4),
-# written back to `cur` and to the rewind copy `bak` (3 x 24), + v (Heston) and the
-# running max (book) at 8 B each, 3 times
 MARKET_STATE_BYTES = 72
-# he_rollout in rollout mode runs step_market_kernel: the step workgroups of block b
-# and the market workgroups of block b+1 in one grid (HE_FUSED_MARKET=0, or with a
-# liability book: the market on a side stream, step_kernel alone)
+
+
+def lds_rollout(cfg):
+    """he_rollout runs lds_rollout_kernel (GBM without a book, unless HE_LDS_ROLLOUT=0)."""
+    return cfg["mode"] == "gbm" and not cfg["gen"].get("book") and os.environ.get("HE_LDS_ROLLOUT", "1") != "0"
 
 
 def fused_market():
@@ -76,6 +85,7 @@ def tile_layout(mode, n):
 
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
+MIN_TIMED_STEPS = 512  # >= 2 episodes of 252 steps
 M_BLOCK = 64           # market block (he_config.market_block)
 
 TRAIN_KW = dict(loss_type="abs", pnl_penalty_weight=0.001, lambda_cost=0.0001, theta_weight=0.0002,
@@ -115,7 +125,9 @@ def parse():
     ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS), help="BASELINE.json config")
     ap.add_argument("--envs", type=int, default=None, help="envs per GPU (default: the config's)")
     ap.add_argument("--mode", choices=["rollout", "graph", "eager"], default="rollout")
-    ap.add_argument("--rollout-k", type=int, default=64)
+    ap.add_argument("--rollout-k", type=int, default=None,
+                    help="steps per he_rollout call (default: 256, the n_steps rollout-buffer boundary of "
+                         "train_ppo_v2.py:48, on the LDS path; 64 on the tile path)")
     ap.add_argument("--no-step-api", action="store_true", help="skip the secondary graph-mode he_step run")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -313,7 +325,7 @@ def pmc_traffic(args):
             for f in glob.glob(os.path.join(td, "**", "*counter_collection.csv"), recursive=True):
                 with open(f) as fh:
                     for r in csv.DictReader(fh):
-                        if re.search(r"step1?_kernel|step_market_kernel", r.get("Kernel_Name", "")) and r.get("Counter_Name") == ctr:
+                        if re.search(r"step1?_kernel|step_market_kernel|lds_rollout_kernel", r.get("Kernel_Name", "")) and r.get("Counter_Name") == ctr:
                             rows.append(float(r["Counter_Value"]))
             if not rows:
                 return None, f"no {ctr} rows for the step kernel"
@@ -423,24 +435,37 @@ def timed(runner, K, W, dist):
     return float(t.item()), ev0.elapsed_time(ev1)
 
 
-def roofline(mode, n, kern_ms, rk, book=False, market="gbm"):
-    """book: + the f64 book slot per env-step (post; he_step also reads the pre slot).
-    market: tile layout, see tile_layout()."""
+def roofline(mode, n, kern_ms, rk, book=False, market="gbm", lds=False):
+    """The dominant kernel's roofline.  `achieved` = SURVEY 8(d)'s algorithmic bytes per
+    launch / the kernel's average duration.  `kernel_bytes_per_launch` is what this
+    kernel itself must move (the 8(d) I/O plus the market position; the tile kernels add
+    their HBM market tile, reported apart as `overhead_bytes_per_launch`)."""
+    overhead = 0
     if mode == "rollout":
-        bytes_launch = n * rk * (ROLLOUT_BYTES_PER_ENV[market] + (8 if book else 0) + ROLLOUT_STATE_BYTES[market] / rk)
-        kname = "step_kernel (he_rollout, K=%d fused steps)" % rk
-        if fused_market() and not book:
-            mstate = MARKET_STATE_BYTES + (24 if market == "heston" else 0) + (24 if book else 0)
-            bytes_launch += n * (rk * (MARKET_BYTES_PER_ENV[market] + (8 if book else 0)) + mstate)
-            kname = ("step_market_kernel (he_rollout, K=%d fused steps + the next block's market "
-                     "in the same grid)" % rk)
+        survey = n * (rk * SURVEY_ROLLOUT_B + SURVEY_ROLLOUT_STATE_B)
+        if lds:
+            own = n * (rk * LDS_STEP_B + LDS_STATE_B)
+            kname = ("lds_rollout_kernel (he_rollout, K=%d fused steps; the market made in LDS by "
+                     "producer waves, never written to HBM)" % rk)
+        else:
+            own = n * (rk * (65 + (8 if book else 0)) + 32)
+            overhead = n * rk * (ROLLOUT_BYTES_PER_ENV[market] - 65) + n * (ROLLOUT_STATE_BYTES[market] - 32)
+            kname = "step_kernel (he_rollout, K=%d fused steps, market tile in HBM)" % rk
+            if fused_market() and not book:
+                mstate = MARKET_STATE_BYTES + (24 if market == "heston" else 0)
+                overhead += n * (rk * MARKET_BYTES_PER_ENV[market] + mstate)
+                kname = ("step_market_kernel (he_rollout, K=%d fused steps + the next block's market "
+                         "tile in the same grid)" % rk)
     else:
-        bytes_launch = n * (STEP_BYTES_PER_ENV[market] + (16 if book else 0))
+        survey = n * SURVEY_STEP_B
+        own = n * (STEP_BYTES_PER_ENV[market] + (16 if book else 0))
         kname = "step1_kernel (he_step, K=1)"
-    achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
+    achieved = survey / (kern_ms * 1e-3) / 1e9
     return dict(bound="hbm", achieved=round(achieved, 1), peak=HBM_PEAK_GBS, unit="GB/s",
                 frac=round(achieved / HBM_PEAK_GBS, 4), traffic=None, kernel=kname,
-                kernel_us=round(kern_ms * 1e3, 3), bytes_per_launch=int(bytes_launch))
+                kernel_us=round(kern_ms * 1e3, 3), bytes_model="SURVEY.md 8(d)", bytes_per_launch=int(survey),
+                kernel_bytes_per_launch=int(own), overhead_bytes_per_launch=int(overhead),
+                kernel_gbs=round(own / (kern_ms * 1e-3) / 1e9, 1))
 
 
 # ---------------------------------------------------------------------- rbergomi workload
@@ -596,8 +621,11 @@ def main():
         return
     if args.envs is None:
         args.envs = CONFIGS[args.config]["envs"]
-    if args.mode == "rollout" and (args.rollout_k < 1 or args.rollout_k > M_BLOCK):
-        raise SystemExit("--rollout-k must be in [1, 64]")
+    lds = args.mode == "rollout" and lds_rollout(CONFIGS[args.config])
+    if args.rollout_k is None:
+        args.rollout_k = 256 if lds else M_BLOCK
+    if args.mode == "rollout" and (args.rollout_k < 1 or (not lds and args.rollout_k > M_BLOCK)):
+        raise SystemExit("--rollout-k must be >= 1 (<= 64 on the tile path: one dispatch per call is timed)")
     if args.probe:
         probe(args)
         return
@@ -629,7 +657,8 @@ def main():
 
     env = make_env(args, dev, rank)
     runner = Runner(args, env, args.mode, acts, stream, dist, gathered)
-    K = -(-args.steps // runner.chunk) * runner.chunk
+    # at least two full episodes (504 steps) in the timed window
+    K = -(-max(args.steps, MIN_TIMED_STEPS) // runner.chunk) * runner.chunk
     W = -(-args.warmup // runner.chunk) * runner.chunk
     wall, dev_ms = timed(runner, K, W, dist)
     hev = HipEvents()
@@ -637,13 +666,15 @@ def main():
     env.close()
 
     has_book = bool(cfg["gen"].get("book"))
-    roof = roofline(args.mode, n, kern_ms, args.rollout_k, has_book, tile_layout(cfg["mode"], n))
-    roof["tile_layout"] = tile_layout(cfg["mode"], n)
-    mkt_ms = market_time_ms(hev, args, dev, acts, stream)
-    roof["market_kernel_us_per_64_steps"] = round(mkt_ms * 1e3, 3)
-    roof["market_kernel_us_per_step"] = round(mkt_ms * 1e3 / M_BLOCK, 3)
+    roof = roofline(args.mode, n, kern_ms, args.rollout_k, has_book, tile_layout(cfg["mode"], n), lds)
+    if not lds:  # the tile path: market_kernel makes the HBM market tile
+        roof["tile_layout"] = tile_layout(cfg["mode"], n)
+        mkt_ms = market_time_ms(hev, args, dev, acts, stream)
+        roof["market_kernel_us_per_64_steps"] = round(mkt_ms * 1e3, 3)
+        roof["market_kernel_us_per_step"] = round(mkt_ms * 1e3 / M_BLOCK, 3)
     if pmc[0] is not None:
         roof["traffic"] = int(pmc[0])
+        roof["traffic_over_bytes"] = round(pmc[0] / roof["bytes_per_launch"], 4)
         roof["traffic_counters_kb"] = {k: round(v, 1) for k, v in pmc[1].items()}
     else:
         roof["traffic_note"] = pmc[1]

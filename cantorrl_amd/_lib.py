@@ -10,7 +10,8 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libhedgeenv.so")
+# CANTORRL_HEDGEENV_LIB: an alternative build (diagnostic / A-B builds under tools/ab/)
+LIB_PATH = os.environ.get("CANTORRL_HEDGEENV_LIB") or os.path.join(HERE, "lib", "libhedgeenv.so")
 
 HE_ABI_VERSION = 2
 HE_BOOK_MAX = 8

@@ -25,6 +25,11 @@ FLAGS = [
     "-ffp-contract=off", "-fhip-fp32-correctly-rounded-divide-sqrt",
     "-fno-gpu-flush-denormals-to-zero", "-Wall", "-Wno-unused-function",
 ]
+# hedge_env.hip only: MachineLICM hoists every f64 polynomial constant of the market
+# code (Box-Muller, exp, marks, greeks) out of the block loops into VGPR pairs, which
+# then spill (lds_rollout_kernel: 168 VGPRs + 236 B/lane of scratch; without it 80
+# VGPRs, no scratch).  Rematerialising them at the use is cheaper than scratch.
+ENV_FLAGS = ["-mllvm", "-disable-machine-licm"]
 
 
 RB_SRC = os.path.join(HERE, "csrc", "rbergomi.hip")
@@ -33,7 +38,7 @@ RB_OUT = os.path.join(HERE, "lib", "librbergomi.so")
 VN_SRC = os.path.join(HERE, "csrc", "vecnorm.hip")
 AN_SRC = os.path.join(HERE, "csrc", "analytics.hip")
 DEPS = DEPS + [VN_SRC, AN_SRC]
-TARGETS = [([SRC, VN_SRC, AN_SRC], DEPS, OUT), ([RB_SRC], RB_DEPS, RB_OUT)]
+TARGETS = [([SRC, VN_SRC, AN_SRC], DEPS, OUT, ENV_FLAGS), ([RB_SRC], RB_DEPS, RB_OUT, [])]
 
 
 def needs_build(out=OUT, deps=DEPS):
@@ -45,12 +50,12 @@ def needs_build(out=OUT, deps=DEPS):
 
 def build(force=False, verbose=False):
     """Build every library that is missing or older than its sources; returns the env's."""
-    for srcs, deps, out in TARGETS:
+    for srcs, deps, out, extra in TARGETS:
         if not force and not needs_build(out, deps):
             continue
         os.makedirs(os.path.dirname(out), exist_ok=True)
         tmp = out + ".tmp"
-        cmd = [HIPCC, *FLAGS, "-o", tmp, *srcs]
+        cmd = [HIPCC, *FLAGS, *extra, "-o", tmp, *srcs]
         if verbose:
             print(" ".join(cmd))
         subprocess.run(cmd, check=True)
@@ -61,7 +66,7 @@ def build(force=False, verbose=False):
 def build_variant(out, extra_flags):
     """Diagnostic / A-B builds (e.g. -DHE_TIMING) outside the package directory."""
     os.makedirs(os.path.dirname(os.path.abspath(out)), exist_ok=True)
-    subprocess.run([HIPCC, *FLAGS, *extra_flags, "-o", out, SRC, VN_SRC, AN_SRC], check=True)
+    subprocess.run([HIPCC, *FLAGS, *ENV_FLAGS, *extra_flags, "-o", out, SRC, VN_SRC, AN_SRC], check=True)
     return out
 
 

@@ -15,6 +15,66 @@
 
 namespace he {
 
+// ---------------------------------------------------------------- constant FMAs
+// a * b + c for a constant c (polynomial coefficients), bit-identical to fma(a, b, c).
+// Left to itself the compiler emits v_fmac_f64 -- whose addend is its destination
+// register, overwritten -- plus two v_mov per Horner step to re-materialise c: three
+// VALU instructions.  The VOP3 v_fma_f64 reads c from an SGPR pair (s_mov, scalar
+// unit, shared by every use in the block): one VALU instruction.
+HE_HD double fma_k(double a, double b, double c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    double r;
+    asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(c));
+    return r;
+#else
+    return fma(a, b, c);
+#endif
+}
+
+// a * k + c for a constant multiplicand k (an SGPR pair), bit-identical to fma(a, k, c).
+HE_HD double fma_kb(double a, double k, double c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    double r;
+    asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "s"(k), "v"(c));
+    return r;
+#else
+    return fma(a, k, c);
+#endif
+}
+
+// exp(x), f64, for the price advance exp((r - v/2) dt + sqrt(v) dW) (rbergomi_sim.py:459-463):
+// x = k ln2 + r with k = rint(x / ln2), r by a two-constant Cody-Waite step (k ln2_hi exact
+// for |k| < 2^21), e^r = (1 + r) + r^2 q(r) with q the Taylor series of (e^r - 1 - r) / r^2
+// to r^15 (truncation < 2^-70 on |r| <= ln2 / 2) and the rounding error of 1 + r carried
+// (Fast2Sum), then 2^k by v_ldexp.  Within 1 ulp of the correctly rounded value
+// (tests/test_lib_cpu.py samples it against numpy); every constant an SGPR operand.  |x| >= 700 (over/underflow range) takes the library exp.
+HE_HD double exp_k(double x) {
+    if (!(fabs(x) < 700.0)) return exp(x);
+    const double k = rint(x * 1.4426950408889634074);
+    const double rh = fma_kb(-k, 6.93147180369123816490e-01, x);   // exact
+    const double r = fma_kb(-k, 1.90821492927058770002e-10, rh);
+    double q = 1.0 / 355687428096000.0;           // 1/17!, the r^15 coefficient of q
+    q = fma_k(q, r, 1.0 / 20922789888000.0);      // 1/16!
+    q = fma_k(q, r, 1.0 / 1307674368000.0);       // 1/15!
+    q = fma_k(q, r, 1.0 / 87178291200.0);         // 1/14!
+    q = fma_k(q, r, 1.0 / 6227020800.0);          // 1/13!
+    q = fma_k(q, r, 1.0 / 479001600.0);           // 1/12!
+    q = fma_k(q, r, 1.0 / 39916800.0);            // 1/11!
+    q = fma_k(q, r, 1.0 / 3628800.0);             // 1/10!
+    q = fma_k(q, r, 1.0 / 362880.0);
+    q = fma_k(q, r, 1.0 / 40320.0);
+    q = fma_k(q, r, 1.0 / 5040.0);
+    q = fma_k(q, r, 1.0 / 720.0);
+    q = fma_k(q, r, 1.0 / 120.0);
+    q = fma_k(q, r, 1.0 / 24.0);
+    q = fma_k(q, r, 1.0 / 6.0);
+    q = fma_k(q, r, 0.5);
+    // 1 + r + r^2 q with the rounding error of 1 + r kept (Fast2Sum: |1| >= |r|)
+    const double s1 = 1.0 + r;
+    const double e1 = (1.0 - s1) + r;              // exact
+    return ldexp(s1 + fma(r * r, q, e1), (int)k);
+}
+
 // ---------------------------------------------------------------- numpy helpers
 // np.maximum / np.minimum: NaN in either operand propagates.
 HE_HD float np_maxf(float a, float b) { return (a != a) ? a : ((b != b) ? b : (a > b ? a : b)); }
@@ -49,6 +109,16 @@ HE_HD float div_byf(float a, float b, float y) {
     return fmaf(r, y, q);
 }
 
+// div_by without its guard, for dividends that are 0 or normal with |a| < 2^900 and
+// quotients clear of the subnormals (every FAST-configuration P&L and reward term: a
+// difference of portfolio values is 0 or a multiple of ulp(pv), see fast_config):
+// there q, r = a - b q (exact by FMA) and RN(q + r y) equal the guarded path bit for
+// bit, a = +0 included.  Branch-free.
+HE_HD double div_by_nb(double a, double b, double y) {
+    const double q = a * y;
+    return fma(fma(-q, b, a), y, q);
+}
+
 // Integer-valued a (|a| <= 2^24) by a constant 1 <= b <= 2^30: the Markstein step with
 // no guard -- q = a*y can neither overflow nor fall near the subnormals, and a = 0
 // gives +0 like +0 / b.  f32 (obs positions / max held, (T - t) / T) and f64 ((T - t)
@@ -77,12 +147,14 @@ HE_HD float div_f32_by(float a, double b, double y64) {
 
 // np.rint(f32).astype(int64) then np.clip(., -mt, mt)  (hedging_env_v2.py:184-188).
 // x86 cvttss2si maps NaN and |x| >= 2^63 to INT64_MIN, which the clip sends to -mt.
+// Branch-free (selects only): the step kernels keep whole steps in one basic block.
 HE_HD int32_t trade_round(float f, int32_t mt) {
-    float r = rintf(f);
-    if (!(fabsf(r) < 9.2233720368547758e18f)) return -mt;
-    float lo = -(float)mt, hi = (float)mt;
-    r = r < lo ? lo : (r > hi ? hi : r);
-    return (int32_t)r;
+    const float r = rintf(f);
+    const bool ok = fabsf(r) < 9.2233720368547758e18f;  // false for NaN and |x| >= 2^63
+    const float lo = -(float)mt, hi = (float)mt;
+    const float c = r < lo ? lo : (r > hi ? hi : r);
+    const int32_t v = ok ? (int32_t)c : 0;
+    return ok ? v : -mt;
 }
 
 // ---------------------------------------------------------------- Philox4x32-10
@@ -146,14 +218,14 @@ HE_HD void box_muller(double u1, double u2, double* z1, double* z2) {
     const double s = (m - 1.0) / (m + 1.0);
     const double s2 = s * s;
     double p = 1.0 / 19.0;
-    p = fma(p, s2, 1.0 / 17.0);
-    p = fma(p, s2, 1.0 / 15.0);
-    p = fma(p, s2, 1.0 / 13.0);
-    p = fma(p, s2, 1.0 / 11.0);
-    p = fma(p, s2, 1.0 / 9.0);
-    p = fma(p, s2, 1.0 / 7.0);
-    p = fma(p, s2, 1.0 / 5.0);
-    p = fma(p, s2, 1.0 / 3.0);
+    p = fma_k(p, s2, 1.0 / 17.0);
+    p = fma_k(p, s2, 1.0 / 15.0);
+    p = fma_k(p, s2, 1.0 / 13.0);
+    p = fma_k(p, s2, 1.0 / 11.0);
+    p = fma_k(p, s2, 1.0 / 9.0);
+    p = fma_k(p, s2, 1.0 / 7.0);
+    p = fma_k(p, s2, 1.0 / 5.0);
+    p = fma_k(p, s2, 1.0 / 3.0);
     const double lm = (2.0 * s) + (2.0 * s) * (s2 * p);   // 2 atanh(s)
     const double ed = (double)e;
     const double lg = fma(ed, 6.93147180369123816490e-01, fma(ed, 1.90821492927058770002e-10, lm));
@@ -164,24 +236,24 @@ HE_HD void box_muller(double u1, double u2, double* z1, double* z2) {
     const double r = x - q;
     const double rr = r * r;
     double sp = 6.066935731106192e-12;
-    sp = fma(sp, rr, -6.688035109811464e-10);
-    sp = fma(sp, rr, 5.692172921967924e-08);
-    sp = fma(sp, rr, -3.598843235212084e-06);
-    sp = fma(sp, rr, 0.00016044118478735975);
-    sp = fma(sp, rr, -0.004681754135318687);
-    sp = fma(sp, rr, 0.07969262624616703);
-    sp = fma(sp, rr, -0.6459640975062462);
-    sp = fma(sp, rr, 1.5707963267948966);
+    sp = fma_k(sp, rr, -6.688035109811464e-10);
+    sp = fma_k(sp, rr, 5.692172921967924e-08);
+    sp = fma_k(sp, rr, -3.598843235212084e-06);
+    sp = fma_k(sp, rr, 0.00016044118478735975);
+    sp = fma_k(sp, rr, -0.004681754135318687);
+    sp = fma_k(sp, rr, 0.07969262624616703);
+    sp = fma_k(sp, rr, -0.6459640975062462);
+    sp = fma_k(sp, rr, 1.5707963267948966);
     const double sn = r * sp;
     double cp = 6.565963114979468e-11;
-    cp = fma(cp, rr, -6.386603083791849e-09);
-    cp = fma(cp, rr, 4.710874778818169e-07);
-    cp = fma(cp, rr, -2.5202042373060596e-05);
-    cp = fma(cp, rr, 0.0009192602748394263);
-    cp = fma(cp, rr, -0.020863480763352957);
-    cp = fma(cp, rr, 0.253669507901048);
-    cp = fma(cp, rr, -1.2337005501361697);
-    const double cs = fma(cp, rr, 1.0);
+    cp = fma_k(cp, rr, -6.386603083791849e-09);
+    cp = fma_k(cp, rr, 4.710874778818169e-07);
+    cp = fma_k(cp, rr, -2.5202042373060596e-05);
+    cp = fma_k(cp, rr, 0.0009192602748394263);
+    cp = fma_k(cp, rr, -0.020863480763352957);
+    cp = fma_k(cp, rr, 0.253669507901048);
+    cp = fma_k(cp, rr, -1.2337005501361697);
+    const double cs = fma_k(cp, rr, 1.0);
     // quadrant qi: (sin, cos) = (sn, cs), (cs, -sn), (-sn, -cs), (-cs, sn) -- as two
     // selects and two exact sign flips (a chained ?: on qi lowers to branches)
     const int qi = (int)q & 3;
@@ -201,21 +273,21 @@ HE_HD void box_muller(double u1, double u2, double* z1, double* z2) {
 HE_HD double erf_small(double x) {
     const double z = x * x;
     double p = -2.783516207210921354903762e-14;
-    p = fma(p, z, 4.463224263286477344931894e-13);
-    p = fma(p, z, -6.711366855164110377934626e-12);
-    p = fma(p, z, 9.422759064650410970620214e-11);
-    p = fma(p, z, -1.229055530171792735298289e-9);
-    p = fma(p, z, 1.480719281587921723954605e-8);
-    p = fma(p, z, -0.00000016365844691234924317393);
-    p = fma(p, z, 0.000001646211436588924740161296);
-    p = fma(p, z, -0.00001492565035840625097746242);
-    p = fma(p, z, 0.0001205533298178966425102734);
-    p = fma(p, z, -0.0008548327023450852832546658);
-    p = fma(p, z, 0.005223977625442187842111847);
-    p = fma(p, z, -0.02686617064513125175943235);
-    p = fma(p, z, 0.1128379167095512573896159);
-    p = fma(p, z, -0.376126389031837524632053);
-    p = fma(p, z, 1.128379167095512573896159);
+    p = fma_k(p, z, 4.463224263286477344931894e-13);
+    p = fma_k(p, z, -6.711366855164110377934626e-12);
+    p = fma_k(p, z, 9.422759064650410970620214e-11);
+    p = fma_k(p, z, -1.229055530171792735298289e-9);
+    p = fma_k(p, z, 1.480719281587921723954605e-8);
+    p = fma_k(p, z, -0.00000016365844691234924317393);
+    p = fma_k(p, z, 0.000001646211436588924740161296);
+    p = fma_k(p, z, -0.00001492565035840625097746242);
+    p = fma_k(p, z, 0.0001205533298178966425102734);
+    p = fma_k(p, z, -0.0008548327023450852832546658);
+    p = fma_k(p, z, 0.005223977625442187842111847);
+    p = fma_k(p, z, -0.02686617064513125175943235);
+    p = fma_k(p, z, 0.1128379167095512573896159);
+    p = fma_k(p, z, -0.376126389031837524632053);
+    p = fma_k(p, z, 1.128379167095512573896159);
     return x * p;
 }
 
@@ -224,14 +296,14 @@ HE_HD double erf_small(double x) {
 HE_HD double erf_small4(double x) {
     const double z = x * x;
     double p = 0.000001646211436588924740161296;
-    p = fma(p, z, -0.00001492565035840625097746242);
-    p = fma(p, z, 0.0001205533298178966425102734);
-    p = fma(p, z, -0.0008548327023450852832546658);
-    p = fma(p, z, 0.005223977625442187842111847);
-    p = fma(p, z, -0.02686617064513125175943235);
-    p = fma(p, z, 0.1128379167095512573896159);
-    p = fma(p, z, -0.376126389031837524632053);
-    p = fma(p, z, 1.128379167095512573896159);
+    p = fma_k(p, z, -0.00001492565035840625097746242);
+    p = fma_k(p, z, 0.0001205533298178966425102734);
+    p = fma_k(p, z, -0.0008548327023450852832546658);
+    p = fma_k(p, z, 0.005223977625442187842111847);
+    p = fma_k(p, z, -0.02686617064513125175943235);
+    p = fma_k(p, z, 0.1128379167095512573896159);
+    p = fma_k(p, z, -0.376126389031837524632053);
+    p = fma_k(p, z, 1.128379167095512573896159);
     return x * p;
 }
 
@@ -297,14 +369,14 @@ HE_HD double log_ratio(double S, double K) {
     const double y = q - 1.0;
     if (!(fabs(y) < 0.0078125)) return log(q);
     double p = 1.0 / 9.0;
-    p = fma(p, y, -1.0 / 8.0);
-    p = fma(p, y, 1.0 / 7.0);
-    p = fma(p, y, -1.0 / 6.0);
-    p = fma(p, y, 1.0 / 5.0);
-    p = fma(p, y, -1.0 / 4.0);
-    p = fma(p, y, 1.0 / 3.0);
-    p = fma(p, y, -0.5);
-    p = fma(p, y, 1.0);
+    p = fma_k(p, y, -1.0 / 8.0);
+    p = fma_k(p, y, 1.0 / 7.0);
+    p = fma_k(p, y, -1.0 / 6.0);
+    p = fma_k(p, y, 1.0 / 5.0);
+    p = fma_k(p, y, -1.0 / 4.0);
+    p = fma_k(p, y, 1.0 / 3.0);
+    p = fma_k(p, y, -0.5);
+    p = fma_k(p, y, 1.0);
     return y * p;
 }
 

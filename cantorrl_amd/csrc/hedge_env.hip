@@ -31,6 +31,7 @@
 #include <string.h>
 
 #include <new>
+#include <type_traits>
 #include <string>
 #include <vector>
 
@@ -590,7 +591,7 @@ __device__ __forceinline__ void market_body(Params p, Market cur, Market bak, in
                 if (n < a0 || n >= a0 + (uint64_t)nsteps) continue;
                 int j = (int)(n - a0) + 1;
                 double dW = p.sqrt_dt * z[h];
-                shS[lane][j] = exp(p.drift + p.sqrt_var * dW);  // rbergomi_sim.py:459-463
+                shS[lane][j] = exp_k(p.drift + p.sqrt_var * dW);  // rbergomi_sim.py:459-463
             }
         }
     }
@@ -1415,6 +1416,491 @@ __global__ __launch_bounds__(kBlock, HE_FUSED_WAVES) void step_market_kernel(Par
 }
 #endif
 
+// ------------------------------------------------------------------ LDS rollout
+// he_rollout, GBM without a book: ONE launch per call, and the market never leaves the
+// chip.  A workgroup owns kLdsEnvs = 64 envs and runs 2 + kLdsProd waves:
+//   wave 0 (reward stepper): the f64 state chain of hedging_env_v2.py:181-262 -- trades,
+//     costs, cash, portfolio value, P&L, reward -- one lane per env over all K steps,
+//     and the reward / terminated stores; it owns the env state;
+//   wave 1 (obs stepper): the positions alone (integer trade logic, :181-200) and the
+//     13-float observation (:109-143), staged in LDS and stored as 16-B vectors;
+//   waves 2.. (producers): the market of the NEXT kLdsM-step block -- Philox4x32-10
+//     normals, the GBM price (rbergomi_sim.py:454-464), rolling-ATM marks
+//     (option_calculator.py:11-27) and the obs greeks (hedging_env_v2.py:79-107) -- as
+//     24-B records {S, C, P, delta_c, gamma, delta_p} into the other LDS buffer while
+//     the steppers consume the current one.
+// kLdsLanes lanes per env, lane `sub` making slots [sub H, sub H + H) of a block; the
+// sequential f64 price chain passes from lane to lane through shuffles.  One workgroup
+// barrier per block hands a buffer over.  The device functions and their operands are
+// market_body's / step_kernel's, so the outputs are the tile kernels' bits (tests: LDS
+// rollouts == tile rollouts == repeated he_step).  HBM traffic is the step I/O of
+// hedging_env_v2.py:175-294 only: actions in, obs / reward / terminated out, and the
+// per-env state + market position once per launch.
+#ifndef HE_LDS_LANES
+#define HE_LDS_LANES 2
+#endif
+#ifndef HE_LDS_M
+#define HE_LDS_M 8
+#endif
+#ifndef HE_LDS_PRIO_REW
+#define HE_LDS_PRIO_REW 0
+#endif
+#ifndef HE_LDS_PRIO_OBS
+#define HE_LDS_PRIO_OBS 2  // the obs wave is the workgroup's critical chain: it wins issue
+#endif
+#ifndef HE_LDS_PRIO_PROD
+#define HE_LDS_PRIO_PROD 1
+#endif
+constexpr int kLdsEnvs = 64;                         // envs per workgroup = one stepper wave
+constexpr int kLdsLanes = HE_LDS_LANES;              // producer lanes per env
+constexpr int kLdsProd = kLdsLanes;                  // producer waves (64 / kLdsLanes envs each)
+constexpr int kLdsPEnvs = kLdsEnvs / kLdsLanes;      // envs per producer wave
+constexpr int kLdsThreads = 64 * (2 + kLdsProd);     // + the reward and the obs stepper waves
+constexpr int kLdsM = HE_LDS_M;                      // slots per LDS market block
+constexpr int kLdsH = kLdsM / kLdsLanes;             // consecutive slots per producer lane
+static_assert(kLdsH * kLdsLanes == kLdsM && kLdsPEnvs * kLdsLanes == kLdsEnvs, "producer lane layout");
+constexpr int kLdsPrefetch = kLdsM % 6 == 0 ? 6 : (kLdsM % 4 == 0 ? 4 : kLdsM);  // steps of actions in flight
+static_assert(kLdsM % kLdsPrefetch == 0, "the action ring index is the slot mod D");
+// min waves per SIMD: 4 workgroups per CU need 4 (2 + kLdsProd) / 4 per SIMD if the hardware
+// spreads every workgroup evenly; one more leaves room for an uneven placement
+#ifndef HE_LDS_MINWAVES
+#define HE_LDS_MINWAVES ((4 * (2 + kLdsProd) + 3) / 4 + 1)
+#endif
+constexpr int kLdsMinWaves = HE_LDS_MINWAVES;
+// LDS: the market records, double-buffered by block, [slot][env]: {S, C} pairs and P
+// (12 B per env-slot, conflict-free lane accesses), and the obs wave's two row staging
+// tiles: 18.9 KB at M = 8, so all 65,536 envs of BASELINE configs[1] resident at once.
+struct LdsMarket {
+    float2 sc[2][kLdsM][kLdsEnvs];
+    float pp[2][kLdsM][kLdsEnvs];
+    float stage[2][kLdsEnvs * kObs];  // the obs wave's row staging, by step parity
+};
+static_assert(sizeof(LdsMarket) <= 40 * 1024, "4 workgroups per CU");
+
+#ifdef HE_LDS_TIMING
+// Diagnostic builds only: per wave role (0 reward, 1 obs, 2-3 producers) and workgroup,
+// {cycles from start to end, cycles spent in barriers (s_memtime), 100 MHz ticks from
+// start to end (s_memrealtime)}, read by he_debug_lds_timing.
+__device__ uint64_t g_lds_tim[4][4096][3];
+#define LDS_T0() uint64_t tim_t0 = __builtin_amdgcn_s_memtime(), tim_bar = 0, tim_r0 = __builtin_amdgcn_s_memrealtime()
+#define LDS_BAR()                                                  \
+    do {                                                           \
+        const uint64_t tb_ = __builtin_amdgcn_s_memtime();         \
+        __syncthreads();                                           \
+        tim_bar += __builtin_amdgcn_s_memtime() - tb_;             \
+    } while (0)
+#define LDS_T1(role)                                                                     \
+    do {                                                                                 \
+        if ((threadIdx.x & 63) == 0 && blockIdx.x < 4096) {                              \
+            g_lds_tim[role][blockIdx.x][0] = __builtin_amdgcn_s_memtime() - tim_t0;      \
+            g_lds_tim[role][blockIdx.x][1] = tim_bar;                                    \
+            g_lds_tim[role][blockIdx.x][2] = __builtin_amdgcn_s_memrealtime() - tim_r0;  \
+        }                                                                                \
+    } while (0)
+#else
+#define LDS_T0() do {} while (0)
+#define LDS_BAR() __syncthreads()
+#define LDS_T1(role) do {} while (0)
+#endif
+
+// Store one workgroup's 64 obs rows (the image, 832 floats) as 3 x 16 B + 4 B per lane:
+// every lane active, no branch.
+__device__ __forceinline__ void flush_obs_full(const float* img, float* out, int64_t row0, int lane) {
+    asm volatile("" ::: "memory");
+    GLOBAL float* dst = (GLOBAL float*)out + row0 * kObs;
+    GLOBAL v4f* d4 = (GLOBAL v4f*)dst;
+    const v4f* s4 = reinterpret_cast<const v4f*>(img);
+    d4[lane] = s4[lane];
+    d4[lane + 64] = s4[lane + 64];
+    d4[lane + 128] = s4[lane + 128];
+    dst[768 + lane] = img[768 + lane];
+    asm volatile("" ::: "memory");
+}
+
+// The stepper waves.  OBS = false: the reward wave; OBS = true: the obs wave.  Both make
+// the same integer decisions from the same actions, so they agree on every position and
+// done flag.  LEAN (the FAST configuration with every output present, lds_lean_config):
+// the per-handle constants in registers and no branch in a step (selects; div_by_nb),
+// so the unrolled steps of a block form one basic block the scheduler can overlap;
+// otherwise the generic step_env / make_obs code.
+//
+// Memory-op discipline (what keeps the stores in flight): every lane is active -- a
+// lane past the last env mirrors env N-1 (same inputs, so its stores write the same
+// values to the same addresses) -- and a full block is straight-line code (unrolled
+// slots, no branch around a load or store), so the waitcnt pass never merges paths with
+// different outstanding memory ops.  (A copy of a pending load's register at a merge,
+// e.g. the action ring at a loop back-edge behind a `break`, costs an s_waitcnt
+// vmcnt(0): every store of the wave drained.)  A partial last block takes a generic loop.
+template <bool LEAN, bool OBS>
+__device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& io, int k_steps, const Market& cur,
+                                            LdsMarket& L, int64_t base) {
+    constexpr int D = kLdsPrefetch;
+    const int lane = threadIdx.x & 63;
+    const int64_t N = p.n;
+    const int nfull = k_steps / kLdsM;          // full blocks
+    const int tail = k_steps - nfull * kLdsM;   // steps of the partial last block
+    const int64_t i0 = base + lane;
+    const int64_t i = i0 < N ? i0 : N - 1;      // lanes past N mirror env N-1
+    const int wrows = (int)((N - base) < kLdsEnvs ? (N - base) : kLdsEnvs);
+    const Mkt rst{p.rstv[0], p.rstv[1], p.rstv[2], p.rstv[3], 0.0};
+    const GLOBAL v2f* gact = (const GLOBAL v2f*)io.act;
+    GLOBAL float* const grew = (GLOBAL float*)io.rew;
+    GLOBAL uint8_t* const gterm = (GLOBAL uint8_t*)io.term;
+    if (OBS) __builtin_amdgcn_s_setprio(HE_LDS_PRIO_OBS);
+    else __builtin_amdgcn_s_setprio(HE_LDS_PRIO_REW);
+    LDS_T0();
+    Env e{};
+    Mkt pre = rst;
+    double pv_last = 0.0;
+    {
+        const uint32_t t0 = s.t[i];
+        const uint32_t pk = s.pos[i];
+        e.t = t0;
+        e.call = unpack_lo(pk);
+        e.put = unpack_hi(pk);
+        e.path = -1;
+        e.s0_small = rst.S < 1e-6f;
+        e.s0 = e.s0_small ? 1.0f : rst.S;
+        if (!OBS) {
+            e.cash = s.cash[i];
+            // the market the env stands at: the block-start record of market_body (f32 S)
+            if (t0 != 0) pre = Mkt{(float)cur.S[i], p.var_f, cur.C[i], cur.P[i], 0.0};
+            pv_last = portfolio_value<false>(p, e, pre);
+        }
+    }
+    float2 ra[D];
+#pragma unroll
+    for (int d = 0; d < D; ++d) ra[d] = ld2(gact, (int64_t)(d < k_steps ? d : k_steps - 1) * N + i);
+
+    // ---- the block loop over a step function step(buf, sl, k, action)
+    auto run = [&](auto&& step) {
+        LDS_BAR();  // block 0 produced
+        for (int b = 0; b < nfull; ++b) {
+#if defined(HE_LDS_DIAG) && HE_LDS_DIAG == 2
+            LDS_BAR();  // diagnostic build: the steppers only keep the barrier count
+            continue;
+#endif
+            const int buf = b & 1;
+#pragma unroll
+            for (int sl = 0; sl < kLdsM; ++sl) {
+                const int k = b * kLdsM + sl;
+                const float2 ak = ra[sl % D];
+                const int kn = k + D;
+                ra[sl % D] = ld2(gact, (int64_t)(kn < k_steps ? kn : k_steps - 1) * N + i);
+                step(buf, sl, k, ak);
+            }
+            LDS_BAR();  // buffer b & 1 handed back, block b + 1 produced
+        }
+        if (tail) {
+#if !(defined(HE_LDS_DIAG) && HE_LDS_DIAG == 2)
+            const int buf = nfull & 1;
+            for (int sl = 0; sl < tail; ++sl) {
+                const int k = nfull * kLdsM + sl;
+                step(buf, sl, k, ld2(gact, (int64_t)k * N + i));
+            }
+#endif
+            LDS_BAR();
+        }
+    };
+
+    if constexpr (LEAN) {
+        // the FAST configuration's constants (fast_config): v2, loss != mse, generate mode
+        const float mt_f = p.mt_f, maxh_f = p.maxh_f, inv_maxh_f = p.inv_maxh_f;
+        const int32_t mt = p.mt, maxh = p.maxh, T = p.T;
+        if (OBS) {
+            const double s0s_d = p.s0s_d, inv_s0s_d = p.inv_s0s_d;
+            const float T_f = p.T_f, inv_T_f = p.inv_T_f, var_f = p.var_f;
+            float preS = pre.S;
+            if (e.t != 0) preS = (float)cur.S[i];
+            auto obs_step = [&](int buf, int sl, int k, float2 ak, auto full) {
+                const float2 r0 = L.sc[buf][sl][lane];
+                const float rP = L.pp[buf][sl][lane];
+                // the obs greeks: greeks_fast of the market price, as market_kernel makes them
+                const float4 g = greeks_fast<true>(p, r0.x, var_f);
+                // (i)-(ii) of step_env: the integer trade logic (:181-200)
+                const int32_t nc = e.call + trade_round(ak.x * mt_f, mt);
+                const int32_t nq = e.put + trade_round(ak.y * mt_f, mt);
+                const int32_t cc = nc < -maxh ? -maxh : (nc > maxh ? maxh : nc);
+                const int32_t qq = nq < -maxh ? -maxh : (nq > maxh ? maxh : nq);
+                const uint32_t t1 = e.t + 1;
+                const bool term = (int32_t)t1 >= T;
+                // make_obs<true> (hedging_env_v2.py:109-143) on the post-step state, or the
+                // reset obs on a terminal step (SB3 autoreset)
+                float o[kObs];
+                o[0] = div_f32_by(r0.x, s0s_d, inv_s0s_d);
+                o[1] = div_f32_by(r0.y, s0s_d, inv_s0s_d);
+                o[2] = div_f32_by(rP, s0s_d, inv_s0s_d);
+                o[3] = div_int_byf((float)cc, maxh_f, inv_maxh_f);
+                o[4] = div_int_byf((float)qq, maxh_f, inv_maxh_f);
+                o[5] = var_f;
+                o[6] = div_int_byf((float)(T - (int32_t)t1), T_f, inv_T_f);
+                o[7] = g.x;
+                o[8] = g.y;
+                o[9] = g.z;
+                o[10] = g.y;
+                o[11] = lag_return(r0.x, preS);
+                o[12] = (preS == 0.0f) ? 0.0f : np_clipf(var_f - var_f, -1.0f, 1.0f);
+                // staged in LDS (two tiles, alternating by step: the next step's row writes
+                // do not wait behind this step's read-back) and stored as whole 16-B lines
+                float* const tile = L.stage[k & 1];
+#pragma unroll
+                for (int c = 0; c < kObs; ++c) tile[lane * kObs + c] = term ? p.rstv[4 + c] : o[c];
+                float* out = io.obs + (int64_t)k * N * kObs;
+                if constexpr (decltype(full)::value) flush_obs_full(tile, out, base, lane);
+                else flush_obs_wave(tile, out, base, wrows, lane);
+                e.t = term ? 0u : t1;
+                e.call = term ? 0 : cc;
+                e.put = term ? 0 : qq;
+                preS = term ? rst.S : r0.x;
+            };
+            if (wrows == kLdsEnvs)
+                run([&](int buf, int sl, int k, float2 ak) { obs_step(buf, sl, k, ak, std::true_type{}); });
+            else
+                run([&](int buf, int sl, int k, float2 ak) { obs_step(buf, sl, k, ak, std::false_type{}); });
+        } else {
+            const double tcpc = p.tcpc, slip_frac = p.slip_frac, lam = p.lam, w = p.w, theta = p.theta;
+            const double shares_d = p.shares_d, inv_shares = p.inv_shares, den = p.den, inv_den = p.inv_den;
+            const double inv_252 = p.inv_252, init_cash = p.initial_cash;
+            const float shares_f = p.shares_f;
+            // step_env's PV0 (:167-168): f32, of the reset market -- one constant here
+            const double pv0 = (double)((shares_f * rst.S + 0.0f) + p.init_cash_f);
+            run([&](int buf, int sl, int k, float2 ak) {
+                const int64_t koff = (int64_t)k * N;
+                const float2 sc = L.sc[buf][sl][lane];
+                const float pP = L.pp[buf][sl][lane];
+                const double pv_prev = (e.t == 0) ? pv0 : pv_last;
+                // (i)-(ii) trades (:181-200)
+                const int32_t nc = e.call + trade_round(ak.x * mt_f, mt);
+                const int32_t nq = e.put + trade_round(ak.y * mt_f, mt);
+                const int32_t cc = nc < -maxh ? -maxh : (nc > maxh ? maxh : nc);
+                const int32_t qq = nq < -maxh ? -maxh : (nq > maxh ? maxh : nq);
+                const int32_t dc = cc - e.call, dp = qq - e.put;
+                // (iii) commission + slippage on the pre-step marks (:203-213)
+                const int32_t adc = dc < 0 ? -dc : dc, adp = dp < 0 ? -dp : dp;
+                const double commission = (double)(adc + adp) * tcpc;
+                const double slc = (((double)adc * (double)pre.C) * 100.0) * slip_frac;
+                const double slp = (((double)adp * (double)pre.P) * 100.0) * slip_frac;
+                const double tc = commission + (slc + slp);
+                const double cash = e.cash - tc;
+                // (iv)-(vi) advance, mark-to-market (:216-238)
+                const uint32_t t1 = e.t + 1;
+                const bool term = (int32_t)t1 >= T;
+                const double optv = ((double)cc * (double)sc.y) * 100.0 + ((double)qq * (double)pP) * 100.0;
+                const double pv = ((double)(shares_f * sc.x) + optv) + cash;
+                const double pnl = pv - pv_prev;
+                const double ps = div_by_nb(pnl, shares_d, inv_shares);
+                // (vii) reward (:243-262)
+                const double term_v = div_by_nb(fabs(ps), den, inv_den);
+                const double rpc = (-w) * term_v;
+                const double tcp = lam * tc;
+                const double thp = theta * div_int_by((double)(T - (int32_t)t1), 252.0, inv_252);
+                const double reward = (rpc - tcp) - thp;
+                grew[koff + i] = (float)reward;
+                gterm[koff + i] = term ? 1 : 0;
+                pv_last = pv;
+                // SB3 autoreset (selects)
+                e.t = term ? 0u : t1;
+                e.call = term ? 0 : cc;
+                e.put = term ? 0 : qq;
+                e.cash = term ? init_cash : cash;
+                pre = Mkt{term ? rst.S : sc.x, rst.v, term ? rst.C : sc.y, term ? rst.P : pP, 0.0};
+            });
+        }
+    } else {
+        if (OBS && e.t != 0) pre = Mkt{(float)cur.S[i], p.var_f, cur.C[i], cur.P[i], 0.0};
+        auto step = [&](int buf, int sl, int k, float2 ak) {
+            const int64_t koff = (int64_t)k * N;
+            const float2 sc = L.sc[buf][sl][lane];
+            const Mkt post{sc.x, p.var_f, sc.y, L.pp[buf][sl][lane], 0.0};
+            if (OBS) {
+                float4 g = p.record_metrics ? greeks_fast<true>(p, post.S, p.var_f) : make_float4(0.f, 0.f, 0.f, 0.f);
+                g.w = lag_return(post.S, pre.S);
+                // (i)-(ii) of step_env: the integer trade logic (:181-200)
+                const int32_t nc = e.call + trade_round(ak.x * p.mt_f, p.mt);
+                const int32_t nq = e.put + trade_round(ak.y * p.mt_f, p.mt);
+                e.call = nc < -p.maxh ? -p.maxh : (nc > p.maxh ? p.maxh : nc);
+                e.put = nq < -p.maxh ? -p.maxh : (nq > p.maxh ? p.maxh : nq);
+                e.t = e.t + 1;
+                const bool term = (int32_t)e.t >= p.T;
+                float o[kObs];
+                make_obs<false>(p, e, post, g, pre.S, pre.v, o);
+                float* const tile = L.stage[k & 1];
+#pragma unroll
+                for (int c = 0; c < kObs; ++c) tile[lane * kObs + c] = term ? p.rstv[4 + c] : o[c];  // SB3 autoreset obs
+                if (io.obs) flush_obs_wave(tile, io.obs + koff * kObs, base, wrows, lane);
+                pre = term ? rst : post;
+                if (term) env_reset_common(p, e);
+            } else {
+                StepOut so;
+                step_env<false, false>(p, e, pre, post, ak.x, ak.y, pv_last, so);
+                pv_last = so.pv;
+                if (grew) grew[koff + i] = (float)so.reward;
+                if (gterm) gterm[koff + i] = so.term ? 1 : 0;
+                pre = so.term ? rst : post;
+                if (so.term) env_reset_common(p, e);
+            }
+        };
+        run(step);
+    }
+    LDS_T1(OBS ? 1 : 0);
+    if (!OBS && i0 < N) {
+        s.t[i] = e.t;
+        s.pos[i] = pack_pos(e.call, e.put);
+        s.cash[i] = e.cash;
+    }
+}
+
+// Producer waves: block bp of 64 envs into LDS buffer bp & 1 while the steppers consume
+// block bp - 1.  pw = producer wave index (kLdsPEnvs envs each).  Lanes past the last
+// env mirror env N-1 like the steppers' (identical values, identical addresses).
+__device__ __forceinline__ void lds_producer(const Params& p, int k_steps, const Market& cur, LdsMarket& W,
+                                             int64_t base, int pw) {
+    const int lane = threadIdx.x & 63;
+    const int sub = lane / kLdsPEnvs;
+    const int le = pw * kLdsPEnvs + (lane % kLdsPEnvs);  // local env of this lane
+    const int64_t N = p.n;
+    const int nb = (k_steps + kLdsM - 1) / kLdsM;
+    const uint32_t T = (uint32_t)p.T;
+    const int64_t pi = (base + le) < N ? base + le : N - 1;
+    const int64_t gid = p.goff + pi;
+    __builtin_amdgcn_s_setprio(HE_LDS_PRIO_PROD);
+    const uint32_t ep0 = cur.ep[pi];
+    const uint32_t t0 = cur.t[pi];
+    double Sbs = cur.S[pi];                          // f64 price before slot 0 of block bp
+    const uint32_t off = t0 >= T ? T : t0;           // a0 = ep T + t (t = T: the next episode)
+    const uint64_t a0 = (uint64_t)ep0 * T + off;     // env-step index of the launch's first step
+    uint32_t tpb = off >= T ? 0u : off;              // episode step before slot 0 of block bp
+    const int sl0 = sub * kLdsH;
+    LDS_T0();
+    for (int bp = 0; bp <= nb; ++bp) {
+#if defined(HE_LDS_DIAG) && HE_LDS_DIAG == 1
+        LDS_BAR();  // diagnostic build: the producers only keep the barrier count
+        continue;
+#endif
+        if (bp < nb) {
+            const int kb = bp * kLdsM;
+            const int len = (k_steps - kb) < kLdsM ? (k_steps - kb) : kLdsM;
+            const uint64_t nf = a0 + (uint64_t)(kb + sl0);
+            const uint32_t tpf = (tpb + (uint32_t)sl0) % T;
+            // (1) the random part of every slot: Philox block m = n / 2 gives the
+            // Box-Muller pair of steps 2m (cos) and 2m + 1 (sin)
+            double ex[kLdsH];
+            double zc = 0.0;
+#pragma unroll
+            for (int h = 0; h < kLdsH; ++h) {
+                ex[h] = 1.0;
+                if (sl0 + h < len) {
+                    const uint64_t n = nf + (uint64_t)h;
+                    double z;
+                    if (h == 0 || (n & 1) == 0) {
+                        double z1, z2;
+#if defined(HE_LDS_SKIP) && (HE_LDS_SKIP & 1)
+                        {   // diagnostic build: no Box-Muller
+                            u32x4 ctr = {(uint32_t)(n >> 1), (uint32_t)(n >> 33), (uint32_t)gid, (uint32_t)((uint64_t)gid >> 32)};
+                            u32x4 x = philox4x32_10(ctr, p.key0, p.key1);
+                            z1 = u01(x.x, x.y) - 0.5;
+                            z2 = u01(x.z, x.w) - 0.5;
+                        }
+#else
+                        normals(p, gid, n >> 1, &z1, &z2);
+#endif
+                        z = (n & 1) ? z2 : z1;
+                        zc = z2;
+                    } else {
+                        z = zc;
+                    }
+                    const double dW = p.sqrt_dt * z;
+#if defined(HE_LDS_SKIP) && (HE_LDS_SKIP & 16)
+                    ex[h] = 1.0 + p.drift + p.sqrt_var * dW;  // diagnostic build: no exp
+#else
+                    ex[h] = exp_k(p.drift + p.sqrt_var * dW);  // rbergomi_sim.py:459-463
+#endif
+                }
+            }
+            // (2) the f64 price chain: the block's growth factors gathered from the env's
+            // kLdsLanes lanes (independent shuffles, one latency), then every lane runs the
+            // whole block's chain itself -- M products, no lane-to-lane hand-off -- keeping
+            // its own slots (Sx) and the price before its first slot (Sin)
+            double eall[kLdsM];
+#pragma unroll
+            for (int r = 0; r < kLdsLanes; ++r)
+#pragma unroll
+                for (int h = 0; h < kLdsH; ++h) eall[r * kLdsH + h] = __shfl(ex[h], (lane % kLdsPEnvs) + r * kLdsPEnvs);
+            double Sx[kLdsH];
+#pragma unroll
+            for (int h = 0; h < kLdsH; ++h) Sx[h] = Sbs;
+            double S = Sbs, Sin = Sbs;
+            {
+                uint32_t tp = tpb;
+#pragma unroll
+                for (int j = 0; j < kLdsM; ++j) {
+                    if (j == sl0) Sin = S;
+                    if (j < len) {
+                        if (tp == 0) S = p.s0;  // autoreset: a new episode starts from S0
+                        const double Sn = S * eall[j];
+                        S = (Sn < 1e-8) ? 1e-8 : Sn;  // np.maximum(., 1e-8), NaN kept
+                        tp = (tp + 1 == T) ? 0u : tp + 1;
+                    }
+#pragma unroll
+                    for (int h = 0; h < kLdsH; ++h) Sx[h] = (j == sl0 + h) ? S : Sx[h];
+                }
+            }
+            Sbs = S;  // price after the block (every lane ran the whole chain)
+            // (3) marks + obs greeks of every slot; the terminal step replays the marks of
+            // the position before it (hedging_env_v2.py:229-231)
+            uint32_t tp = tpf;
+            const int wb = bp & 1;
+#pragma unroll
+            for (int h = 0; h < kLdsH; ++h) {
+                if (sl0 + h < len) {
+                    const bool last = tp + 1 == T;
+                    const double Sprev = (h == 0) ? Sin : Sx[h - 1];
+                    const double Sm = last ? ((tp == 0) ? p.s0 : Sprev) : Sx[h];
+                    float C, P;
+#if defined(HE_LDS_SKIP) && (HE_LDS_SKIP & 2)
+                    C = (float)Sm * 0.02f; P = (float)Sm * 0.018f;  // diagnostic build: no marks
+#else
+                    marks<HE_MODE_GBM>(p, Sm, p.var, &C, &P);
+#endif
+                    const int sl = sl0 + h;
+                    W.sc[wb][sl][le] = make_float2((float)Sx[h], C);
+                    W.pp[wb][sl][le] = P;
+                    if (kb + sl == k_steps - 1) {  // the market position after the launch
+                        const uint32_t q = off + (uint32_t)(k_steps - 1);
+                        cur.ep[pi] = ep0 + q / T;
+                        cur.t[pi] = q % T + 1u;
+                        cur.S[pi] = Sx[h];
+                        cur.C[pi] = C;
+                        cur.P[pi] = P;
+                    }
+                    tp = (tp + 1 == T) ? 0u : tp + 1;
+                }
+            }
+            tpb = (uint32_t)(((uint64_t)tpb + kLdsM) % T);
+        }
+        LDS_BAR();  // block bp handed to the steppers
+    }
+    LDS_T1(2 + (pw < 2 ? pw : 1));
+}
+
+// Wave roles are uniform (readfirstlane), so each role's loop is plain scalar control
+// flow and all execute the same number of barriers; the roles' working sets never coexist.
+// SGPRs capped at 96 (.sgpr_count 94): past 96 the hardware admits one wave per SIMD
+// fewer than the occupancy API and the compiler report (MI355X_MICROARCH.md, Residency),
+// and at 106 the 4 x 6 waves of 4 workgroups no longer fit a CU -- at 65,536 envs the
+// launch ran in two rounds of workgroups (536 vs ~270 us).  The spills go to VGPR lanes.
+template <bool LEAN>
+__global__ __launch_bounds__(kLdsThreads, kLdsMinWaves) __attribute__((amdgpu_num_sgpr(96))) void lds_rollout_kernel(
+    const Params* __restrict__ pc, State s, Io io, int k_steps, Market cur) {
+    __shared__ __attribute__((aligned(16))) LdsMarket lm;
+    const Params& p = *pc;  // read through the scalar cache (a by-value copy spills)
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t base = (int64_t)blockIdx.x * kLdsEnvs;
+    if (wave == 0) lds_stepper<LEAN, false>(p, s, io, k_steps, cur, lm, base);
+    else if (wave == 1) lds_stepper<LEAN, true>(p, s, io, k_steps, cur, lm, base);
+    else lds_producer(p, k_steps, cur, lm, base, wave - 2);
+}
+
 // Explicit reset of envs `ids` (NULL: all).  Generate: the market position of a
 // reset env moves to the start of its next episode.
 template <int MODE>
@@ -1573,6 +2059,7 @@ struct he_env {
     int32_t cur_buf = 0;      // tile buffer of the block being consumed
     int32_t next_state = 0;   // next block: 0 none, 1 generating on `xs` (ev_next), 2 ready
     bool fuse_market = true;  // rollouts: next block's market in the step grid (HE_FUSED_MARKET=0: side stream)
+    bool lds_rollout = true;  // he_rollout (GBM, no book): lds_rollout_kernel (HE_LDS_ROLLOUT=0: tile kernels)
     int32_t prefetch_mode = 0; // 0 auto, 1 never, 2 always: market_kernel(b+1) on `xs` during block b
     hipStream_t xs = nullptr; // library side stream for market prefetch
     hipEvent_t ev_fork = nullptr, ev_next = nullptr;
@@ -1988,7 +2475,48 @@ static bool fast_config(const he_env* env) {
            env->p.s0s_const && env->p.den_const;
 }
 
-static he_status launch_steps(he_env* env, Io io, bool info, int k_total, void* stream) {
+// The lean LDS steppers (branch-free, unguarded Markstein divisions, div_by_nb): the
+// FAST configuration with every output buffer given, and prices and cash where every
+// P&L is 0 or a normal number far from the f64 range ends (S0 and initial cash in
+// [1e-30, 1e30]: a P&L is a difference of portfolio values, a multiple of their ulp).
+static bool lds_lean_config(const he_env* env, const Io& io) {
+    const he_config& c = env->cfg;
+    const double s0 = c.s0, ic = fabs(c.initial_cash);
+    return fast_config(env) && io.obs && io.rew && io.term && s0 >= 1e-30 && s0 <= 1e30 && ic <= 1e30;
+}
+
+// he_rollout through lds_rollout_kernel: GBM, no liability book (HE_LDS_ROLLOUT=0
+// falls back to the market-tile kernels).  The market position `cur` must be where the
+// envs are (no block generated ahead, no mid-block position): materialize_market
+// rewinds it, a no-op after an LDS rollout.  Afterwards `cur` is exact again and the
+// tiles are invalid (the next he_step regenerates its block from `cur`).
+static bool lds_rollout_eligible(const he_env* env) {
+    return env->lds_rollout && env->cfg.mode == HE_MODE_GBM && env->cfg.book_size == 0;
+}
+
+static he_status launch_lds_rollout(he_env* env, const Io& io, int k_total, hipStream_t st) {
+    he_status s = materialize_market(env, st);
+    if (s != HE_OK) return s;
+    const int64_t blocks = (env->cfg.n_envs + kLdsEnvs - 1) / kLdsEnvs;
+    const Params* pc = env->dparams;  // buffer 0's copy: the tile pointers are not used
+    void (*kern)(const Params*, State, Io, int, Market) =
+        lds_lean_config(env, io) ? lds_rollout_kernel<true> : lds_rollout_kernel<false>;
+    if (env->ev_start) {  // one-shot: bracket exactly this dispatch
+        hipEvent_t a = (hipEvent_t)env->ev_start, b = (hipEvent_t)env->ev_stop;
+        env->ev_start = env->ev_stop = nullptr;
+        hipExtLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kLdsThreads), 0, st, a, b, 0, pc, env->s, io,
+                              k_total, env->cur);
+    } else {
+        hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kLdsThreads), 0, st, pc, env->s, io, k_total,
+                           env->cur);
+    }
+    HE_HIP(env, hipGetLastError());
+    env->block_pos = env->cfg.market_block;
+    env->next_state = 0;
+    return HE_OK;
+}
+
+static he_status launch_steps(he_env* env, Io io, bool info, int k_total, void* stream, bool rollout = false) {
     const he_config& c = env->cfg;
     if (c.mode == HE_MODE_REPLAY && !env->rec) return fail(env, HE_ESTATE, "no paths loaded (he_load_paths)");
     if (!env->ready) return fail(env, HE_ESTATE, "he_reset must be called before stepping");
@@ -1999,6 +2527,7 @@ static he_status launch_steps(he_env* env, Io io, bool info, int k_total, void* 
         HE_HIP(env, hipGetLastError());
         return HE_OK;
     }
+    if (rollout && !info && !io.pol_on && lds_rollout_eligible(env)) return launch_lds_rollout(env, io, k_total, st);
     const int32_t M = c.market_block;
     const int64_t N = c.n_envs;
     int done = 0;
@@ -2199,6 +2728,8 @@ he_status he_create(const he_config* cfg, he_env** out) {
         {
             const char* ev = getenv("HE_FUSED_MARKET");
             env->fuse_market = !(ev && ev[0] == '0');
+            const char* el = getenv("HE_LDS_ROLLOUT");
+            env->lds_rollout = !(el && el[0] == '0');
         }
         HE_HIP(env, hipStreamCreateWithFlags(&env->xs, hipStreamNonBlocking));
         HE_HIP(env, hipEventCreateWithFlags(&env->ev_fork, hipEventDisableTiming));
@@ -2354,6 +2885,14 @@ he_status he_host_philox(uint64_t seed, uint64_t env_id, uint64_t n, uint32_t ou
     return HE_OK;
 }
 
+#ifdef HE_LDS_TIMING
+he_status he_debug_lds_timing(void* host, size_t bytes) {
+    const size_t cap = sizeof(g_lds_tim);
+    if (bytes > cap) bytes = cap;
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_lds_tim), bytes, 0, hipMemcpyDeviceToHost) == hipSuccess ? HE_OK : HE_EHIP;
+}
+#endif
+
 #ifdef HE_TIMING
 he_status he_debug_timing(void* host, size_t bytes) {
     const size_t cap = (size_t)5 * 8192 * 2 * 8;
@@ -2406,6 +2945,9 @@ he_status he_seed(he_env* env, const int64_t* env_ids, const uint64_t* seeds, in
         HE_HIP(env, hipMemcpy(env->s.pcg, pcg.data(), pcg.size() * 8, hipMemcpyHostToDevice));
         HE_HIP(env, hipMemcpy(env->s.pcgb, pcgb.data(), pcgb.size() * 4, hipMemcpyHostToDevice));
     } else {
+        // one Philox key per handle: per-env seeding has no generate-mode meaning
+        if (env_ids || count != 1)
+            return fail(env, HE_EINVAL, "generate modes take exactly one seed (the handle's Philox key), no env_ids");
         env->cfg.seed = seeds[0];
         fill_params(env);
         he_status s = sync_dparams(env);
@@ -2482,7 +3024,7 @@ he_status he_rollout(he_env* env, int32_t k_steps, const float* actions, float* 
     io.obs = obs;
     io.rew = reward;
     io.term = terminated;
-    return launch_steps(env, io, false, k_steps, stream);
+    return launch_steps(env, io, false, k_steps, stream, true);
 }
 
 he_status he_rollout_policy(he_env* env, int32_t k_steps, int32_t policy, float* actions_out, float* obs,
@@ -2581,7 +3123,10 @@ he_status he_set_state(he_env* env, const void* host_buf, size_t size) {
         src += f.first;
     }
     env->ready = hdr != 0;
+    // the restored `cur` is the envs' position: drop every block generated from the old
+    // trajectory (a fused rollout leaves next_state 2, a side-stream prefetch 1)
     env->block_pos = env->cfg.market_block;
+    env->next_state = 0;
     return HE_OK;
 }
 

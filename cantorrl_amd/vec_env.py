@@ -242,8 +242,12 @@ class HedgingVecEnv:
         return self._pending_seeds
 
     def seed_envs(self, seeds, env_ids=None):
-        """Per-env reset(seed=...) re-seeding (replay) / Philox key (generate)."""
-        seeds = np.ascontiguousarray(np.asarray(seeds, dtype=np.uint64))
+        """Per-env reset(seed=...) re-seeding (replay).  Generate modes have one Philox
+        key per handle: seeds[0] becomes it (env i's stream is keyed by its global id),
+        and env_ids are refused (he_seed: HE_EINVAL)."""
+        seeds = np.ascontiguousarray(np.asarray(seeds, dtype=np.uint64)).reshape(-1)
+        if self.mode != "replay" and env_ids is None:
+            seeds = seeds[:1]
         ids = None if env_ids is None else np.ascontiguousarray(np.asarray(env_ids, dtype=np.int64))
         st = self.lib.he_seed(self._h, None if ids is None else ids.ctypes.data, seeds.ctypes.data,
                               len(seeds))

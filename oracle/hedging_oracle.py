@@ -632,7 +632,10 @@ class OracleVecEnv:
                     scaled_float_call=fc, scaled_float_put=fp,
                     requested_calls_rounded_clipped=rqc, requested_puts_rounded_clipped=rqp,
                     actual_calls_traded=dc, actual_puts_traded=dp,
-                    initial_S0_for_episode=np.where(self.S0_small, 1.0, self.S0.astype(np.float64)))
+                    initial_S0_for_episode=np.where(self.S0_small, 1.0, self.S0.astype(np.float64)),
+                    # the market after the step, before any autoreset (he_info current_*)
+                    current_stock_price=self.S.copy(), current_call_price=self.C.copy(),
+                    current_put_price=self.P.copy())
         obs = self._obs()
         terminal_obs = np.full_like(obs, np.nan)
         if term.any():

@@ -46,19 +46,43 @@ def test_per_step_bytes_add_up(bench):
     assert bench.STEP_BYTES_PER_ENV["heston"] == 16 + 8 + 48 + 74
 
 
-def test_fused_launch_counts_the_market(bench, monkeypatch):
+def test_achieved_is_priced_on_survey_bytes(bench, monkeypatch):
+    """roofline.achieved uses SURVEY 8(d)'s algorithmic bytes (rollout 66 B per env-step
+    + 120 B per env per launch; he_step 186 B), whatever the kernel moves besides."""
+    n, rk = 65536, 256
+    r = bench.roofline("rollout", n, 0.25, rk, False, "gbm", lds=True)
+    assert r["bytes_per_launch"] == n * (rk * 66 + 120)
+    assert r["kernel"].startswith("lds_rollout_kernel")
+    assert r["kernel_bytes_per_launch"] == n * (rk * 65 + 80) and r["overhead_bytes_per_launch"] == 0
+    assert abs(r["achieved"] - n * (rk * 66 + 120) / 0.25e-3 / 1e9) < 0.1
+    assert abs(r["frac"] - r["achieved"] / bench.HBM_PEAK_GBS) < 1e-4
+    s = bench.roofline("graph", n, 0.005, 1, False, "gbm")
+    assert s["bytes_per_launch"] == n * 186
+
+
+def test_tile_path_reports_the_market_tile_as_overhead(bench, monkeypatch):
     n, rk = 65536, 64
     monkeypatch.setenv("HE_FUSED_MARKET", "1")
     r = bench.roofline("rollout", n, 0.1, rk, False, "gbm")
     step = n * (rk * 89 + 44)
     market = n * (rk * 24 + bench.MARKET_STATE_BYTES)
-    assert r["bytes_per_launch"] == step + market == 481558528  # profiles/r01s21_bench.jsonl
+    # round 1's figure (profiles/r01s21_bench.jsonl) = the 8(d) I/O + the tile round trip
+    assert r["kernel_bytes_per_launch"] + r["overhead_bytes_per_launch"] == step + market == 481558528
+    assert r["bytes_per_launch"] == n * (rk * 66 + 120)
     assert r["kernel"].startswith("step_market_kernel")
-    # a book keeps the market on the side stream: the step kernel's bytes alone
+    # a book keeps the market on the side stream: the step kernel's tile reads only
     rb = bench.roofline("rollout", n, 0.1, rk, True, "gbm")
-    assert rb["bytes_per_launch"] == n * (rk * (89 + 8) + 44)
+    assert rb["kernel_bytes_per_launch"] + rb["overhead_bytes_per_launch"] == n * (rk * (89 + 8) + 44)
     assert rb["kernel"].startswith("step_kernel")
     monkeypatch.setenv("HE_FUSED_MARKET", "0")
     r0 = bench.roofline("rollout", n, 0.1, rk, False, "gbm")
-    assert r0["bytes_per_launch"] == step == 376176640  # profiles/r01s11_bench_all_configs.jsonl
+    assert r0["kernel_bytes_per_launch"] + r0["overhead_bytes_per_launch"] == step == 376176640
     assert abs(r0["frac"] - r0["achieved"] / bench.HBM_PEAK_GBS) < 1e-4
+
+
+def test_lds_path_selection(bench, monkeypatch):
+    monkeypatch.delenv("HE_LDS_ROLLOUT", raising=False)
+    assert bench.lds_rollout(bench.CONFIGS[2]) and bench.lds_rollout(bench.CONFIGS[3])
+    assert not bench.lds_rollout(bench.CONFIGS[4]) and not bench.lds_rollout(bench.CONFIGS[5])
+    monkeypatch.setenv("HE_LDS_ROLLOUT", "0")
+    assert not bench.lds_rollout(bench.CONFIGS[2])

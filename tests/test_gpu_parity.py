@@ -111,8 +111,9 @@ def run_gbm_pair(n, steps, seed, cfg, gen, offset=0, mode="gbm"):
                   "current_step"):
             if k in oinf:
                 assert_same(venv.info_tensor(k).cpu().numpy(), oinf[k].astype(np.int32), f"{k}[{s}]")
-        S_got = venv.info_tensor("current_stock_price").cpu().numpy()
-        assert_same(S_got, orc.S if not oterm.any() else S_got, f"S[{s}]", rtol=1e-6)
+        # the market after the step (pre-reset on terminated envs), every env, every step
+        for k in ("current_stock_price", "current_call_price", "current_put_price"):
+            assert_same(venv.info_tensor(k).cpu().numpy(), oinf[k], f"{k}[{s}]", rtol=1e-6)
         for k in ("per_share_step_pnl", "portfolio_value", "cash", "transaction_costs_total"):
             got = venv.info_tensor(k).cpu().numpy()
             exp = oinf[k]
@@ -191,6 +192,36 @@ def test_state_checkpoint_roundtrip(greeks_site):
     b.set_state(blob)
     o2, r2, _ = b.rollout(acts[K:].contiguous())
     assert torch.equal(o1, o2) and torch.equal(r1, r2)
+
+
+@pytest.mark.parametrize("path", ["lds", "fused", "side"])
+def test_set_state_into_a_stepped_env(path, monkeypatch):
+    """Restoring a checkpoint into an env that has stepped on (the fused grid leaves the
+    next block generated, the side stream a pending prefetch) drops those blocks: the
+    restored env replays exactly what followed the checkpoint, by rollouts and by steps."""
+    from cantorrl_amd.vec_env import HedgingVecEnv
+    monkeypatch.setenv("HE_LDS_ROLLOUT", "1" if path == "lds" else "0")
+    monkeypatch.setenv("HE_FUSED_MARKET", "0" if path == "side" else "1")
+    n, K = 500, 40
+    acts = torch.rand((3 * K, n, 2), device="cuda") * 2.2 - 1.1
+    a = HedgingVecEnv(n, mode="gbm", generate=dict(episode_length=30), seed=3, return_numpy=False, info_keys=())
+    a.reset_tensors()
+    a.rollout(acts[:K].contiguous())
+    blob = a.get_state()
+    o1, r1, t1 = (x.clone() for x in a.rollout(acts[K:2 * K].contiguous()))
+    s1 = [a.step_tensors(acts[2 * K + k], terminal_obs=False)[0].clone() for k in range(5)]
+    a.set_state(blob)
+    o2, r2, t2 = a.rollout(acts[K:2 * K].contiguous())
+    s2 = [a.step_tensors(acts[2 * K + k], terminal_obs=False)[0].clone() for k in range(5)]
+    assert torch.equal(o1, o2) and torch.equal(r1, r2) and torch.equal(t1, t2)
+    for x, y in zip(s1, s2):
+        assert torch.equal(x, y)
+    # and a set_state between single steps (a side-stream prefetch may be pending)
+    a.set_state(blob)
+    s3 = [a.step_tensors(acts[K + k], terminal_obs=False)[0].clone() for k in range(K)]
+    for k in range(K):
+        assert torch.equal(s3[k], o1[k]), k
+    a.close()
 
 
 @pytest.mark.parametrize("n", [1, 255, 257, 65536])
@@ -441,7 +472,9 @@ def test_fused_rollouts_mixed_with_steps_resets_and_checkpoints(mode, monkeypatc
     gen = dict(episode_length=50)
     acts = torch.rand((400, n, 2), device="cuda") * 2.2 - 1.1
     outs = []
-    for fused in ("1", "0"):
+    # LDS rollouts (GBM), the fused tile grid, the side-stream market
+    for lds, fused in (("1", "1"), ("0", "1"), ("0", "0")):
+        monkeypatch.setenv("HE_LDS_ROLLOUT", lds)
         monkeypatch.setenv("HE_FUSED_MARKET", fused)
         env = HedgingVecEnv(n, mode=mode, generate=gen, seed=21, return_numpy=False, info_keys=())
         env.reset_tensors()
@@ -467,9 +500,51 @@ def test_fused_rollouts_mixed_with_steps_resets_and_checkpoints(mode, monkeypatc
                 env.set_state(blob)
         env.close()
         outs.append(got)
-    assert len(outs[0]) == len(outs[1])
-    for i, (a, b) in enumerate(zip(*outs)):
-        assert torch.equal(a, b), i
+    assert len(outs[0]) == len(outs[1]) == len(outs[2])
+    for other in outs[1:]:
+        for i, (a, b) in enumerate(zip(outs[0], other)):
+            assert torch.equal(a, b), i
+
+
+LDS_CASES = {
+    # name: (n_envs, generate kwargs, env kwargs, rollout lengths)
+    "train": (1000, dict(episode_length=40), dict(loss_type="abs", pnl_penalty_weight=0.001, lambda_cost=0.0001,
+                                                    theta_weight=0.0002, slippage_bps=1.0), (64, 64, 30, 100)),
+    "odd_T_ragged": (257, dict(episode_length=25), {}, (1, 5, 12, 13, 11, 37, 64, 3)),
+    "T1": (130, dict(episode_length=1), {}, (7, 12, 1, 20)),
+    "T2_mse_nometrics": (64, dict(episode_length=2, s0=101.25, variance=0.09), dict(loss_type="mse", record_metrics=False,
+                                                                                    initial_cash=1000.0), (9, 24)),
+    "long_K": (3000, dict(), dict(slippage_bps=5.0), (300, 257)),
+}
+
+
+@pytest.mark.parametrize("case", sorted(LDS_CASES))
+def test_lds_rollout_equals_tile_rollout(case, monkeypatch):
+    """lds_rollout_kernel (market made in LDS by producer waves, never in HBM) gives the
+    tile kernels' rollouts bit for bit: obs, rewards, done flags, and the checkpointed
+    state after every call -- odd and ragged env counts, K not a multiple of the LDS
+    block, odd episode lengths (Philox pair parity), T = 1 and 2 (terminal lagged marks at
+    the block start / the reset marks), the non-FAST step (mse, record_metrics off)."""
+    from cantorrl_amd.vec_env import HedgingVecEnv
+    n, gen, kw, ks = LDS_CASES[case]
+    g = torch.Generator(device="cuda")
+    g.manual_seed(17)
+    acts = torch.rand((sum(ks), n, 2), device="cuda", generator=g) * 2.2 - 1.1
+    runs = []
+    for lds in ("1", "0"):
+        monkeypatch.setenv("HE_LDS_ROLLOUT", lds)
+        env = HedgingVecEnv(n, mode="gbm", generate=gen, seed=31, global_env_offset=5, return_numpy=False,
+                            info_keys=(), **kw)
+        got = [env.reset_tensors().clone()]
+        a0 = 0
+        for k in ks:
+            o, r, t = env.rollout(acts[a0:a0 + k].contiguous())
+            got += [o.clone(), r.clone(), t.clone(), torch.from_numpy(env.get_state().copy())]
+            a0 += k
+        env.close()
+        runs.append(got)
+    for i, (a, b) in enumerate(zip(*runs)):
+        assert torch.equal(a, b), (case, i)
 
 
 def _bench_configs():

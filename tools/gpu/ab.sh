@@ -1,17 +1,20 @@
 #!/bin/bash
-# A/B of libhedgeenv builds under tools/ab/*.so: graph-mode he_step and he_rollout(K=64),
-# GBM, 65,536 envs (or $1).  Then the GPU parity suite on the in-tree library.
+# A/B of builds: the headline bench (kernel time of the dominant kernel) with the in-tree
+# library and with every tools/ab/*.so (CANTORRL_HEDGEENV_LIB), configs $CFGS (default 2 3).
+#   gpurun --timeout 900 -- bash tools/gpu/ab.sh <tag>
 set -o pipefail
-cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out
-N=${1:-65536}
-libs=$(ls tools/ab/*.so)
-L=gpurun_out/ab.log
-echo "== he_step graph" > $L
-timeout -k 10 120 ./tools/step_bench $N $libs >> $L 2>&1 || { cat $L; exit 1; }
-echo "== he_rollout K=64" >> $L
-STEP_BENCH_ROLLOUT=64 timeout -k 10 120 ./tools/step_bench $N $libs $libs >> $L 2>&1 || { cat $L; exit 1; }
-cat $L
-if [ -n "$TESTS" ]; then
-  timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_ab.log 2>&1 || { tail -40 gpurun_out/pytest_ab.log; exit 1; }
-  tail -2 gpurun_out/pytest_ab.log
-fi
+TAG=${1:-ab}
+R=$GRAFT_REPO_ROOT; cd $R; O=gpurun_out/$TAG; mkdir -p $O; export TMPDIR=/tmp
+for c in ${CFGS:-2 3}; do
+  for l in default tools/ab/*.so; do
+    b=$(basename $l .so)
+    if [ "$l" = default ]; then unset CANTORRL_HEDGEENV_LIB; else export CANTORRL_HEDGEENV_LIB=$R/$l; fi
+    timeout -k 10 200 python -u bench.py --config $c --no-pmc --no-cpu-baseline --no-step-api $BENCH_ARGS > $O/b_${b}_cfg$c.log 2>&1 || { tail -20 $O/b_${b}_cfg$c.log; exit 1; }
+    python3 -c "
+import json,sys
+l=[json.loads(x) for x in open('$O/b_${b}_cfg$c.log') if x.startswith('{')][0]
+r=l['roofline']
+print('cfg $c %-14s value %.4g  kernel_us %9.2f  frac %.4f  K %s' % ('$b', l['value'], r['kernel_us'], r['frac'], l['config']['rollout_k']))
+"
+  done
+done

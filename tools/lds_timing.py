@@ -1,0 +1,39 @@
+#!/usr/bin/env python3
+"""Per-role barrier waits of lds_rollout_kernel (diagnostic build -DHE_LDS_TIMING).
+
+    CANTORRL_HEDGEENV_LIB=tools/ab/timing.so python tools/lds_timing.py [n_envs] [K]
+
+Roles: 0 reward stepper, 1 obs stepper, 2-3 producers.  For each: mean cycles from the
+first barrier to the end and the share of them spent waiting in barriers (s_memtime).
+"""
+import ctypes
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402
+from cantorrl_amd.vec_env import HedgingVecEnv  # noqa: E402
+
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
+K = int(sys.argv[2]) if len(sys.argv) > 2 else 256
+cfg = bench.CONFIGS[2]
+env = HedgingVecEnv(n, mode="gbm", generate=cfg["gen"], seed=42, return_numpy=False, info_keys=(), **cfg["kw"])
+env.reset_tensors()
+acts = torch.rand((K, n, 2), device="cuda") * 2 - 1
+for _ in range(4):
+    env.rollout(acts)
+torch.cuda.synchronize()
+lib = env.lib
+lib.he_debug_lds_timing.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+buf = np.zeros((4, 4096, 3), np.uint64)
+assert lib.he_debug_lds_timing(buf.ctypes.data, buf.nbytes) == 0
+wg = min((n + 63) // 64, 4096)
+for role, name in enumerate(("reward", "obs", "prod0", "prod1")):
+    tot = buf[role, :wg, 0].astype(np.float64)
+    bar = buf[role, :wg, 1].astype(np.float64)
+    print(f"{name:7s} total {tot.mean():12.0f} cyc  in barriers {bar.mean():12.0f} ({bar.mean() / tot.mean():6.1%})"
+          f"  per step {tot.mean() / K:8.0f}  busy/step {(tot.mean() - bar.mean()) / K:8.0f}"
+          f"  clock {tot.mean() / (buf[role, :wg, 2].astype(np.float64).mean() * 10.0):6.0f} MHz")

@@ -11,7 +11,8 @@ import sys
 def kname(n):
     if "step1_kernel" in n:
         return "step_kernel"
-    for k in ("step_kernel", "market_kernel", "reset_kernel", "table_greeks_kernel", "init_reset_kernel"):
+    for k in ("lds_rollout_kernel", "step_market_kernel", "step_kernel", "market_kernel", "reset_kernel",
+              "table_greeks_kernel", "init_reset_kernel"):
         if k in n:
             return k
     return None
