@@ -117,6 +117,7 @@ EXPORTS = [
     "he_pcg64_seed_state", "he_host_episode_draws", "he_host_philox", "he_host_div_by", "he_host_div_byf", "he_time_next_step", "he_rollout_policy", "he_host_box_muller",
     "he_sync_market", "he_vecnorm_stats_len", "he_vecnorm_scratch_bytes", "he_vecnorm_init", "he_vecnorm_step",
     "he_vecnorm_reset", "he_fixed_european_marks", "he_bs_delta_hedge", "he_count_nonfinite",
+    "he_device_rng", "he_device_math", "he_host_math",
 ]
 
 
@@ -190,6 +191,9 @@ def load(path=LIB_PATH):
         "he_fixed_european_marks": (i32, [vp, i64, i32, ctypes.c_double, vp, vp, vp, vp]),
         "he_bs_delta_hedge": (i32, [vp, i64, i32, ctypes.c_double, ctypes.c_double, vp, vp]),
         "he_count_nonfinite": (i32, [vp, i64, vp, vp]),
+        "he_device_rng": (i32, [u64, vp, vp, i64, vp, vp, vp]),
+        "he_device_math": (i32, [i32, vp, i64, vp, vp]),
+        "he_host_math": (i32, [i32, vp, i64, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

@@ -1901,6 +1901,30 @@ __global__ __launch_bounds__(kLdsThreads, kLdsMinWaves) __attribute__((amdgpu_nu
     else lds_producer(p, k_steps, cur, lm, base, wave - 2);
 }
 
+// Test hooks (he_device_rng / he_device_math): the device build of the generate-mode
+// RNG and math, element-wise, so tests can compare device words and values bit for bit
+// with the host build, rocRAND and the oracle.
+__global__ void device_rng_kernel(uint32_t k0, uint32_t k1, const uint64_t* gid, const uint64_t* n, int64_t count,
+                                  uint32_t* words, double* normals) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= count) return;
+    const u32x4 c = {(uint32_t)n[k], (uint32_t)(n[k] >> 32), (uint32_t)gid[k], (uint32_t)(gid[k] >> 32)};
+    const u32x4 x = philox4x32_10(c, k0, k1);
+    if (words) {
+        words[4 * k] = x.x;
+        words[4 * k + 1] = x.y;
+        words[4 * k + 2] = x.z;
+        words[4 * k + 3] = x.w;
+    }
+    if (normals) box_muller(u01(x.x, x.y), u01(x.z, x.w), normals + 2 * k, normals + 2 * k + 1);
+}
+
+__global__ void device_math_kernel(int32_t op, const double* x, int64_t count, double* out) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= count) return;
+    out[k] = (op == 0) ? exp_k(x[k]) : x[k];
+}
+
 // Explicit reset of envs `ids` (NULL: all).  Generate: the market position of a
 // reset env moves to the start of its next episode.
 template <int MODE>
@@ -2900,6 +2924,29 @@ he_status he_debug_timing(void* host, size_t bytes) {
     return hipMemcpy(host, g_tim, bytes, hipMemcpyDeviceToHost) == hipSuccess ? HE_OK : HE_EHIP;
 }
 #endif
+
+he_status he_device_rng(uint64_t seed, const uint64_t* env_ids, const uint64_t* step_index, int64_t count,
+                        uint32_t* words, double* normals, void* stream) {
+    if (count < 0 || (count > 0 && (!env_ids || !step_index))) return HE_EINVAL;
+    if (count == 0) return HE_OK;
+    hipLaunchKernelGGL(device_rng_kernel, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       (uint32_t)seed, (uint32_t)(seed >> 32), env_ids, step_index, count, words, normals);
+    return hipGetLastError() == hipSuccess ? HE_OK : HE_EHIP;
+}
+
+he_status he_device_math(int32_t op, const double* x, int64_t count, double* out, void* stream) {
+    if (op != 0 || count < 0 || (count > 0 && (!x || !out))) return HE_EINVAL;
+    if (count == 0) return HE_OK;
+    hipLaunchKernelGGL(device_math_kernel, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       op, x, count, out);
+    return hipGetLastError() == hipSuccess ? HE_OK : HE_EHIP;
+}
+
+he_status he_host_math(int32_t op, const double* x, int64_t count, double* out) {
+    if (op != 0 || count < 0 || (count > 0 && (!x || !out))) return HE_EINVAL;
+    for (int64_t k = 0; k < count; ++k) out[k] = exp_k(x[k]);
+    return HE_OK;
+}
 
 he_status he_host_div_by(const double* a, int64_t count, double b, double* out) {
     if ((!a || !out) && count > 0) return HE_EINVAL;

@@ -426,22 +426,28 @@ class HedgingVecEnv:
 
 
 class InfoView:
-    """Lazy list[dict] of per-env infos (SB3 contract) over the device info SoA."""
+    """Lazy list[dict] of per-env infos (SB3 contract) over the device info SoA.
+
+    The step's info buffers (and terminal obs) are snapshotted on the device when the view
+    is made -- the next step overwrites the env's own buffers -- and copied to the host on
+    the first access, so a view read after later steps still shows its own step."""
 
     def __init__(self, venv, done):
         self._v = venv
         self._done = done
         self._cache = {}
         self._host = None
+        self._snap = {k: t.clone() for k, t in venv._info_t.items()}
+        self._tobs_snap = venv._tobs.clone()
 
     def _host_info(self):
         if self._host is None:
-            self._host = {k: t.cpu().numpy() for k, t in self._v._info_t.items()}
+            self._host = {k: t.cpu().numpy() for k, t in self._snap.items()}
         return self._host
 
     def _materialize_done(self, done):
         v = self._v
-        tobs = v._tobs.cpu().numpy()
+        tobs = self._tobs_snap.cpu().numpy()
         h = self._host_info()
         for i in np.nonzero(done)[0]:
             d = self[i]

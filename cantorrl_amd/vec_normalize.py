@@ -78,17 +78,36 @@ class DeviceVecNormalize:
         return p
 
     # ------------------------------------------------------------------ statistics (SB3 attributes)
+    # Reading obs_rms / ret_rms gives a host snapshot; assigning one (any object with
+    # mean, var, count -- an SB3 RunningMeanStd too) copies it into the device statistics.
+    # That is SB3's own sync_envs_normalization (a deepcopy per evaluation); the plain
+    # `eval_env.obs_rms = train_env.obs_rms` of train_ppo_v2.py:208,309 therefore freezes
+    # the evaluation statistics at assignment instead of aliasing the training object.
     @property
     def obs_rms(self):
         s = self._stats.cpu().numpy()
         D = _lib.HE_OBS_DIM
         return _RmsView(s[:D].copy(), s[D:2 * D].copy(), float(s[2 * D]))
 
+    @obs_rms.setter
+    def obs_rms(self, rms):
+        D = _lib.HE_OBS_DIM
+        part = np.concatenate([np.asarray(rms.mean, np.float64).reshape(D), np.asarray(rms.var, np.float64).reshape(D),
+                               [float(rms.count)]])
+        self._stats[: 2 * D + 1].copy_(torch.as_tensor(part))
+
     @property
     def ret_rms(self):
         s = self._stats.cpu().numpy()
         D = _lib.HE_OBS_DIM
         return _RmsView(np.float64(s[2 * D + 1]), np.float64(s[2 * D + 2]), float(s[2 * D + 3]))
+
+    @ret_rms.setter
+    def ret_rms(self, rms):
+        D = _lib.HE_OBS_DIM
+        part = np.array([float(np.asarray(rms.mean).reshape(())), float(np.asarray(rms.var).reshape(())),
+                         float(rms.count)], np.float64)
+        self._stats[2 * D + 1:].copy_(torch.as_tensor(part))
 
     @property
     def returns(self):
@@ -109,17 +128,27 @@ class DeviceVecNormalize:
             self._returns.copy_(torch.as_tensor(np.asarray(st["returns"], np.float64)))
 
     def save(self, path):
-        np.savez(path, **self.get_state())
+        """NPZ content written to exactly `path` (np.savez would append ".npz"; the
+        reference saves to "*.pkl" names and tests os.path.exists on them,
+        train_ppo_v2.py:343-350,400-402,437-450)."""
+        with open(path, "wb") as f:
+            np.savez(f, **self.get_state())
 
     @classmethod
     def load(cls, path, venv):
         """VecNormalize.load(path, venv) for the NPZ written by save()."""
-        z = np.load(path, allow_pickle=False)
+        with open(path, "rb") as f:
+            z = np.load(f, allow_pickle=False)
+            z = {k: z[k] for k in z.files}
+        return cls._from_arrays(z, venv)
+
+    @classmethod
+    def _from_arrays(cls, z, venv):
         clip_obs, clip_reward, gamma, eps = (float(x) for x in z["params"])
         training, norm_obs, norm_reward = (bool(x) for x in z["flags"])
         obj = cls(venv, training=training, norm_obs=norm_obs, norm_reward=norm_reward, clip_obs=clip_obs,
                   clip_reward=clip_reward, gamma=gamma, epsilon=eps)
-        obj.set_state({k: z[k] for k in z.files})
+        obj.set_state(z)
         return obj
 
     # ------------------------------------------------------------------ device path
@@ -219,12 +248,16 @@ class _NormInfoView(InfoView):
     def __init__(self, wrapper, done):
         super().__init__(wrapper.venv, done)
         self._w = wrapper
+        # this step's normalized terminal obs and Monitor sums (the next step overwrites them)
+        self._ntobs = wrapper._tobs_out.clone()
+        self._er = wrapper._ep_ret_done.clone()
+        self._el = wrapper._ep_len_done.clone()
 
     def _materialize_done(self, done):
         w, v = self._w, self._w.venv
-        tobs = w._tobs_out.cpu().numpy()
-        er = w._ep_ret_done.cpu().numpy()
-        el = w._ep_len_done.cpu().numpy()
+        tobs = self._ntobs.cpu().numpy()
+        er = self._er.cpu().numpy()
+        el = self._el.cpu().numpy()
         h = self._host_info()
         for i in np.nonzero(done)[0]:
             d = self[i]

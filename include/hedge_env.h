@@ -294,6 +294,16 @@ he_status he_host_div_by(const double* a, int64_t count, double b, double* out);
 he_status he_host_box_muller(const double* u1, const double* u2, int64_t count, double* z1, double* z2);
 /* f32 twin for the obs quotients by per-handle constants (must equal IEEE a[k] / b). */
 he_status he_host_div_byf(const float* a, int64_t count, float b, float* out);
+/* Device builds of the same RNG for tests (DEVICE pointers, stream-ordered): the 4 Philox
+ * words of (seed, env_ids[k], step_index[k]) into words[4k..4k+3] (= rocRAND
+ * rocrand_init(seed, env_ids[k], 4 step_index[k]) + rocrand4) and the Box-Muller pair the
+ * generate modes draw from them into normals[2k..2k+1]; either output may be NULL. */
+he_status he_device_rng(uint64_t seed, const uint64_t* env_ids, const uint64_t* step_index, int64_t count,
+                        uint32_t* words, double* normals, void* stream);
+/* op 0: the generate-mode price-advance exp (he_math.h exp_k), on the device (DEVICE
+ * pointers) and on the host (HOST pointers), for bit-identity and accuracy tests. */
+he_status he_device_math(int32_t op, const double* x, int64_t count, double* out, void* stream);
+he_status he_host_math(int32_t op, const double* x, int64_t count, double* out);
 
 /* ---- VecNormalize and Monitor on the device ---------------------------------------
  * SB3 2.6.0 VecNormalize (+ RunningMeanStd) as wrapped around the env at

@@ -94,7 +94,9 @@ def philox_words(seed, env_ids, step_index):
     """4 uint32 words for (seed, global env id, env-step index n).
 
     Counter = (lo32(n), hi32(n), lo32(g), hi32(g)), key = (lo32(seed), hi32(seed));
-    identical to rocRAND `rocrand_init(seed, subsequence=g, offset=4*n)` + `rocrand4`.
+    identical to rocRAND `rocrand_init(seed, subsequence=g, offset=4*n)` + `rocrand4` for
+    n < 2^62 (every index an env reaches; rocRAND's offset 4n wraps beyond), checked word for
+    word against rocRAND's own code (oracle/rocrand_words.cpp, tests/test_lib_cpu.py).
     """
     g = np.asarray(env_ids, np.uint64)
     n = np.asarray(step_index, np.uint64)

@@ -143,3 +143,45 @@ def test_box_muller_within_ulps_of_libm():
     ang = 2.0 * np.pi * u2
     assert np.all(np.abs(z1 - rad * np.cos(ang)) <= 8 * np.spacing(rad))
     assert np.all(np.abs(z2 - rad * np.sin(ang)) <= 8 * np.spacing(rad))
+
+
+def test_rocrand_oracle_equals_host_philox_and_numpy():
+    """SURVEY 8(c)'s RNG oracle: rocRAND's own Philox4x32-10, host-compiled from its ROCm 7.2
+    header (oracle/rocrand_words.cpp), equals libhedgeenv's host build and the NumPy
+    restatement word for word over the whole 64-bit (seed, env id, step) range."""
+    from _rng_oracles import coordinates, rocrand_words
+    rng = np.random.default_rng(11)
+    for seed in (0, 42, 2 ** 32 - 1, 2 ** 32, int(rng.integers(0, 2 ** 63)), 2 ** 64 - 1):
+        gid, n = coordinates(rng, 4000)
+        ref = rocrand_words(seed, gid, n)
+        npw = np.stack([np.asarray(w, np.uint32) for w in philox_words(seed, gid, n)], axis=1)
+        assert np.array_equal(ref, npw), seed
+        for k in range(0, gid.size, 97):
+            assert _lib.host_philox(seed, int(gid[k]), int(n[k])) == tuple(int(x) for x in ref[k])
+    # the Random123 / rocRAND known answer
+    assert tuple(rocrand_words(0, [0], [0])[0]) == (0x6627E8D5, 0xE169C58D, 0xBC57AC4C, 0x9B00DBD8)
+
+
+def test_exp_k_within_one_ulp():
+    """he_math.h exp_k (the generate-mode price-advance exp, SGPR-constant polynomial):
+    within 1 ulp of numpy's exp everywhere on |x| < 700, equal to it on the large majority
+    of GBM increments (rbergomi_sim.py:459-463 arguments)."""
+    import ctypes
+    lib = _lib.load()
+    rng = np.random.default_rng(5)
+    gbm = -0.5 * 0.029028 / 252 + np.sqrt(0.029028 / 252) * rng.standard_normal(400_000)
+    wide = rng.uniform(-699.0, 699.0, 400_000)
+    for x, max_diff in ((gbm, 0.05), (wide, 0.08)):
+        x = np.ascontiguousarray(x)
+        out = np.empty_like(x)
+        assert lib.he_host_math(0, x.ctypes.data, x.size, out.ctypes.data) == 0
+        ref = np.exp(x)
+        ulp = np.abs(out.view(np.int64) - ref.view(np.int64))
+        assert ulp.max() <= 1, ulp.max()
+        assert (ulp != 0).mean() < max_diff, (ulp != 0).mean()
+    # edge cases take the library exp
+    x = np.array([0.0, -0.0, 700.5, -745.0, 709.7, np.inf, -np.inf], np.float64)
+    out = np.empty_like(x)
+    assert lib.he_host_math(0, x.ctypes.data, x.size, out.ctypes.data) == 0
+    assert np.array_equal(out[:2], [1.0, 1.0])
+    assert np.allclose(out[2:5], np.exp(x[2:5]), rtol=1e-15) and out[5] == np.inf and out[6] == 0.0

@@ -100,6 +100,45 @@ def test_sb3_api_and_save_load(tmp_path):
     vn.close()
 
 
+def test_stats_assignment_pkl_path_and_stale_infos(tmp_path):
+    """`eval_env.obs_rms = train_env.obs_rms` (train_ppo_v2.py:208,309)
+    copies the statistics in; save/load round-trip under the reference's ".pkl" names
+    (train_ppo_v2.py:343-350,437-450); an info view read after later steps shows its own
+    step."""
+    import os
+    from cantorrl_amd.vec_env import HedgingVecEnv
+    from cantorrl_amd.vec_normalize import DeviceVecNormalize
+    mk = lambda: HedgingVecEnv(32, mode="gbm", generate=dict(episode_length=6), seed=3,  # noqa: E731
+                               info_keys=("call_contracts", "per_share_step_pnl"),
+                               monitor_keywords=("per_share_step_pnl",), **KW)
+    train, ev = DeviceVecNormalize(mk()), DeviceVecNormalize(mk(), training=False, norm_reward=False)
+    train.reset()
+    for _ in range(9):
+        train.step(np.full((32, 2), 0.3, np.float32))
+    ev.obs_rms = train.obs_rms
+    ev.ret_rms = train.ret_rms
+    np.testing.assert_array_equal(ev.obs_rms.mean, train.obs_rms.mean)
+    np.testing.assert_array_equal(ev.obs_rms.var, train.obs_rms.var)
+    assert ev.obs_rms.count == train.obs_rms.count and ev.ret_rms.var == train.ret_rms.var
+    path = str(tmp_path / "final_vecnormalize.pkl")
+    train.save(path)
+    assert os.path.exists(path) and not os.path.exists(path + ".npz")
+    back = DeviceVecNormalize.load(path, mk())
+    np.testing.assert_array_equal(back.obs_rms.mean, train.obs_rms.mean)
+    # infos of step t read after step t+1 (the actions move the positions every step)
+    ev.reset()
+    _, _, _, na = ev.step(np.full((32, 2), 1.0, np.float32))
+    _, _, _, nb = ev.step(np.full((32, 2), 1.0, np.float32))
+    assert na[3]["call_contracts"] == 15 and nb[3]["call_contracts"] == 30
+    venv = ev.venv
+    venv.reset()
+    _, _, _, ia = venv.step(np.full((32, 2), 1.0, np.float32))
+    _, _, _, ib = venv.step(np.full((32, 2), 1.0, np.float32))
+    assert ia[5]["call_contracts"] == 15 and ib[5]["call_contracts"] == 30
+    for e in (train, ev, back):
+        e.close()
+
+
 def test_nonfinite_counter():
     """check_finite: he_count_nonfinite after each step counts non-finite obs/reward
     values on the device.  Replay tables with a NaN mark column (as the shipped
