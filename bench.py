@@ -18,9 +18,14 @@ replays he_step launches captured into hipGraphs, one kernel per step (the
 Gym step API path); `eager` calls he_step from Python every step.  At N=1 the
 JSON line also carries the graph-mode he_step measurement under "step_api".
 For N>1 the script runs under torch.distributed.run, one rank per GPU (weak
-scaling: E envs per rank, env ids offset by rank), and all-gathers per-env
-rewards over RCCL every 256 steps (the rollout-buffer boundary of
-train_ppo_v2.py:48).
+scaling: E envs per rank, env ids offset by rank), and all-gathers the per-env
+episode summaries {return, sum P&L, sum cost, length} (he_episode_summaries) over
+RCCL every 256 steps (the rollout-buffer boundary of train_ppo_v2.py:48).
+`--gpus N` without WORLD_SIZE in the environment makes this process the launcher:
+it runs the PMC pass and the CPU baseline (no GPU call of its own: the PMC pass is a
+rocprofv3 child), then starts `python -m torch.distributed.run --nproc-per-node N
+bench.py ...` as a child process and exits with its status; rank 0 merges the
+launcher's results into its JSON line.
 """
 import argparse
 import ctypes
@@ -117,7 +122,7 @@ CONFIGS = {
 }
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2560)
@@ -134,11 +139,12 @@ def parse():
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC traffic pass")
     ap.add_argument("--probe", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--launch-dry-run", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--workload", choices=["env", "rbergomi"], default="env",
                     help="env: the hedging-env step (headline); rbergomi: the rough-Bergomi MC mark generator")
     ap.add_argument("--rb-paths", type=int, default=2048, help="rbergomi: paths per GPU (x 252 days x call/put)")
     ap.add_argument("--rb-normals", choices=["f64", "f32"], default="f64")
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
 def _cpu_sample(seconds, seed=42, barrier=None):
@@ -199,7 +205,18 @@ def cpu_baseline(seconds):
                 sample=f"oracle/hedging_oracle.py OracleVecEnv GBM, 256 envs per process, {procs} processes "
                        f"x {seconds:.0f} s (NumPy, 1 thread each; {avail} cores in affinity mask)",
                 single_core_value=v1,
-                single_core_sample=f"256 envs x {steps1 // 256} steps ({el1:.1f} s, 1 thread)")
+                single_core_sample=f"256 envs x {steps1 // 256} steps ({el1:.1f} s, 1 thread)",
+                **REFERENCE_CPU)
+
+
+# The reference's own env (hedging_env_v2.py, unmodified, record_metrics=True) on 256 envs,
+# measured in the build container (8-core Xeon, nproc = 8), not on the GPU box:
+# SURVEY.md section 6 / BASELINE.md:18-20
+REFERENCE_CPU = dict(
+    reference_value=4782.0, reference_value_8proc=31904.0,
+    reference_sample="container measurement (build container, nproc=8, not the GPU box): the reference's "
+                     "hedging_env_v2.py, 256 envs, serial DummyVecEnv-style loop = 4,782 env-steps/s on 1 process; "
+                     "8 fork processes x 32 envs = 31,904 env-steps/s (SURVEY.md section 6, BASELINE.md:18-20)")
 
 
 def make_env(args, dev, rank=0, prefetch="auto"):
@@ -218,6 +235,8 @@ class Runner:
     def __init__(self, args, env, mode, acts, stream, dist=None, gathered=None):
         self.args, self.env, self.mode, self.acts, self.stream = args, env, mode, acts, stream
         self.dist, self.gathered = dist, gathered
+        self.summaries = torch.zeros((args.envs, 4), dtype=torch.float32, device=acts.device)
+        self.gathers = 0
         self.lib, self.h = env.lib, env._h
         self.ring = acts.shape[0]
         n = args.envs
@@ -277,10 +296,45 @@ class Runner:
             else:
                 self.rollout(done, cs)
             done += self.chunk
-            if self.dist is not None and done % 256 == 0:
-                # per-env summary gather at the rollout-buffer boundary (train_ppo_v2.py:48)
-                src = self.rr[-1] if self.mode == "rollout" else self.env._rew
-                self.dist.all_gather_into_tensor(self.gathered, src)
+            if self.dist is not None and done % GATHER_EVERY == 0:
+                self.gather(cs)
+
+    def gather(self, cs):
+        """The rollout-buffer boundary (train_ppo_v2.py:48, n_steps = 256): every rank's
+        per-env episode summaries, stream-ordered behind the rollouts that made them."""
+        st = self.lib.he_episode_summaries(self.h, self.summaries.data_ptr(), cs)
+        if st:
+            raise RuntimeError(self.lib.he_last_error(self.h).decode())
+        gather_summaries(self.dist, self.summaries, self.gathered)
+        self.gathers += 1
+
+
+GATHER_EVERY = 256  # train_ppo_v2.py:48 n_steps
+
+
+def gather_summaries(dist, local, gathered):
+    """All-gather the per-env episode summaries [n, 4] {return, sum P&L, sum cost, length}
+    of every rank into gathered [world * n, 4], rank-major: row r * n + i is global env
+    r * n + i (env ids are offset by rank, so this is the single-process [world * n, 4]).
+    RCCL (device tensors, on the current stream) or gloo (host tensors)."""
+    if gathered.is_cuda:
+        dist.all_gather_into_tensor(gathered, local)
+    else:
+        dist.all_gather(list(gathered.chunk(dist.get_world_size())), local)
+    return gathered
+
+
+def summarize_payload(gathered):
+    """The gathered payload in a few numbers (the Monitor-style episode stats the
+    reference logs at the boundary, train_ppo_v2.py:119)."""
+    g = gathered.double().cpu()
+    fin = g[:, 3] > 0
+    nf = int(fin.sum())
+    out = dict(envs=int(g.shape[0]), envs_with_finished_episode=nf)
+    if nf:
+        out.update(mean_return=float(g[fin, 0].mean()), mean_pnl=float(g[fin, 1].mean()),
+                   mean_cost=float(g[fin, 2].mean()), mean_length=float(g[fin, 3].mean()))
+    return out
 
 
 def probe(args):
@@ -614,8 +668,68 @@ def rbergomi_main(args):
         dist.destroy_process_group()
 
 
-def main():
-    args = parse()
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def launcher_cmd(argv, n, port):
+    """The child command of `bench.py --gpus N` (N > 1): one rank per GPU on this node."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *argv]
+
+
+def launch(args, argv):
+    """`--gpus N` without WORLD_SIZE: this process makes no GPU call.  It runs the PMC pass
+    (a rocprofv3 child on one GPU) and the CPU baseline, starts the N ranks as a child
+    process (never exec), hands its results to rank 0 through a file, and returns the
+    child's exit status."""
+    import subprocess
+    import tempfile
+    parent = dict(pmc=None, pmc_note="skipped", cpu_baseline=None)
+    if not args.launch_dry_run:
+        if args.workload == "env" and not args.no_pmc:
+            t, v = pmc_traffic(args)
+            parent.update(pmc=t, pmc_note=v if t is None else None, pmc_counters=v if t is not None else None)
+        if not args.no_cpu_baseline:
+            parent["cpu_baseline"] = (cpu_baseline(args.cpu_seconds) if args.workload == "env"
+                                      else None)
+    fd, path = tempfile.mkstemp(prefix="bench_parent_", suffix=".json", dir="/tmp")
+    with os.fdopen(fd, "w") as fh:
+        json.dump(parent, fh)
+    cmd = launcher_cmd(argv, args.gpus, free_port())
+    env = dict(os.environ, BENCH_PARENT_RESULTS=path)
+    try:
+        if args.launch_dry_run:
+            print(json.dumps(dict(cmd=cmd, parent_results=path, cuda_initialized=torch.cuda.is_initialized())),
+                  flush=True)
+            return 0
+        return subprocess.run(cmd, env=env).returncode
+    finally:
+        os.unlink(path)
+
+
+def parent_results():
+    """What the `--gpus N` launcher measured (rank 0 merges it), or None."""
+    p = os.environ.get("BENCH_PARENT_RESULTS")
+    if not p or not os.path.exists(p):
+        return None
+    with open(p) as fh:
+        return json.load(fh)
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        if args.envs is None and args.workload == "env":
+            args.envs = CONFIGS[args.config]["envs"]
+        if args.rollout_k is None and args.workload == "env":
+            lds0 = args.mode == "rollout" and lds_rollout(CONFIGS[args.config])
+            args.rollout_k = 256 if lds0 else M_BLOCK
+        sys.exit(launch(args, argv))
     if args.workload == "rbergomi":
         rbergomi_main(args)
         return
@@ -630,14 +744,19 @@ def main():
         probe(args)
         return
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    pmc = (None, "skipped")
-    if world == 1 and not args.no_pmc:
-        pmc = pmc_traffic(args)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    pmc = (None, "skipped")
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args.cpu_seconds)   # before the GPU is touched (forks workers)
+    parent = parent_results()
+    if parent is not None:  # ranks of a `--gpus N` launch: the launcher measured these
+        pmc = (parent["pmc"], parent.get("pmc_counters") or parent.get("pmc_note"))
+        cpu = parent["cpu_baseline"]
+    elif world == 1:
+        if not args.no_pmc:
+            pmc = pmc_traffic(args)
+        if not args.no_cpu_baseline:
+            cpu = cpu_baseline(args.cpu_seconds)   # before the GPU is touched (forks workers)
     dist = None
     if world > 1:
         import torch.distributed as dist
@@ -653,7 +772,7 @@ def main():
     g.manual_seed(1234 + rank)
     acts = torch.rand((256, n, 2), device=dev, generator=g) * 2 - 1
     stream = torch.cuda.Stream(device=dev)
-    gathered = torch.empty((world, n), dtype=torch.float32, device=dev) if world > 1 else None
+    gathered = torch.empty((world * n, 4), dtype=torch.float32, device=dev) if world > 1 else None
 
     env = make_env(args, dev, rank)
     runner = Runner(args, env, args.mode, acts, stream, dist, gathered)
@@ -661,6 +780,12 @@ def main():
     K = -(-max(args.steps, MIN_TIMED_STEPS) // runner.chunk) * runner.chunk
     W = -(-args.warmup // runner.chunk) * runner.chunk
     wall, dev_ms = timed(runner, K, W, dist)
+    payload = None
+    if dist is not None:
+        payload = dict(what="he_episode_summaries: per-env {return, sum P&L, sum cost, length} f32 [envs, 4], "
+                            "all_gather_into_tensor over RCCL", every_steps=GATHER_EVERY,
+                       bytes_per_rank=n * 16, gathers=runner.gathers)
+        payload.update(summarize_payload(runner.gathered))
     hev = HipEvents()
     kern_ms = kernel_time_ms(hev, runner, 64 if args.mode == "rollout" else 256)
     env.close()
@@ -716,6 +841,8 @@ def main():
             "step_api": step_api,
             "cpu_baseline": cpu,
         }
+        if payload is not None:
+            line["gather"] = payload
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()

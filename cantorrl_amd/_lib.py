@@ -117,7 +117,7 @@ EXPORTS = [
     "he_pcg64_seed_state", "he_host_episode_draws", "he_host_philox", "he_host_div_by", "he_host_div_byf", "he_time_next_step", "he_rollout_policy", "he_host_box_muller",
     "he_sync_market", "he_vecnorm_stats_len", "he_vecnorm_scratch_bytes", "he_vecnorm_init", "he_vecnorm_step",
     "he_vecnorm_reset", "he_fixed_european_marks", "he_bs_delta_hedge", "he_count_nonfinite",
-    "he_device_rng", "he_device_math", "he_host_math",
+    "he_device_rng", "he_device_math", "he_host_math", "he_episode_summaries",
 ]
 
 
@@ -194,8 +194,12 @@ def load(path=LIB_PATH):
         "he_device_rng": (i32, [u64, vp, vp, i64, vp, vp, vp]),
         "he_device_math": (i32, [i32, vp, i64, vp, vp]),
         "he_host_math": (i32, [i32, vp, i64, vp]),
+        "he_episode_summaries": (i32, [vp, vp, vp]),
     }
+    ab = path != os.path.join(HERE, "lib", "libhedgeenv.so")  # an A/B build of an older tree
     for name, (res, args) in sig.items():
+        if ab and not hasattr(lib, name):
+            continue
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

@@ -29,7 +29,10 @@ FLAGS = [
 # code (Box-Muller, exp, marks, greeks) out of the block loops into VGPR pairs, which
 # then spill (lds_rollout_kernel: 168 VGPRs + 236 B/lane of scratch; without it 80
 # VGPRs, no scratch).  Rematerialising them at the use is cheaper than scratch.
-ENV_FLAGS = ["-mllvm", "-disable-machine-licm"]
+# -phi-node-folding-threshold=8: SimplifyCFG otherwise leaves the autoreset of the LDS
+# reward wave (a dozen selects on `term`, with the episode summaries) as an if/else,
+# whose CFG merges cost waitcnt drains and, there, scratch.
+ENV_FLAGS = ["-mllvm", "-disable-machine-licm", "-mllvm", "-phi-node-folding-threshold=8"]
 
 
 RB_SRC = os.path.join(HERE, "csrc", "rbergomi.hip")

@@ -177,8 +177,11 @@ struct State {
     float* s0;         // replay initial_S0_for_episode; -1 encodes the python 1.0 substitution
     uint64_t* pcg;     // replay [4][N]: state_hi, state_lo, inc_hi, inc_lo
     uint32_t* pcgb;    // replay [2][N]: has_uint32, uinteger
-    double* acc;       // policy rollouts: [7][N] episode sums (reward, pnl, |ps|, tc, rpc, tcp, ps)
-    uint32_t* acc_len; // policy rollouts: [N] episode length so far
+    double* acc;       // rollouts: [7][N] episode sums (reward, pnl, |ps|, tc, rpc, tcp, ps)
+    uint32_t* acc_len; // rollouts: [N] episode length so far
+    float* last;       // [4][N] the last finished episode {return, sum pnl, sum cost, length}
+    double* sum;       // generate-mode rollouts: [3][N] running {return, sum pnl, sum cost}
+    uint32_t* sum_len; // generate-mode rollouts: [N] running episode length
 };
 
 // Generate-mode market position of every env: `cur` = after the last generated
@@ -212,6 +215,7 @@ struct Io {
     he_info info;
     PolIo pol;
     bool pol_on;
+    bool sums;         // he_rollout: keep the episode summaries (State::sum / last)
 };
 
 struct Mkt {
@@ -1153,6 +1157,22 @@ __device__ __forceinline__ void step_body(const Params& pk, int64_t n_envs, cons
         for (int c = 0; c < 7; ++c) acc[c] = s.acc[(int64_t)c * N + i];
         acc_len = s.acc_len[i];
     }
+    // multi-step rollouts: the episode summaries (he_episode_summaries), as lds_stepper
+    constexpr bool SUMS = !SINGLE && !POL && !INFO;
+    const bool sums = SUMS && io.sums;  // he_rollout only: he_step does not pay for them
+    double sm0 = 0.0, sm1 = 0.0, sm2 = 0.0;
+    uint32_t slen = 0;
+    float last0 = 0.f, last1 = 0.f, last2 = 0.f, last3 = 0.f;
+    if (sums && live) {
+        sm0 = s.sum[i];
+        sm1 = s.sum[N + i];
+        sm2 = s.sum[2 * N + i];
+        slen = s.sum_len[i];
+        last0 = s.last[i];
+        last1 = s.last[N + i];
+        last2 = s.last[2 * N + i];
+        last3 = s.last[3 * N + i];
+    }
     bool reset_any = false;
     float* const orow = tile + (wave * kEpw + (lane < kEpw ? lane : 0)) * kObs;
     // step k of every env from market `post` (greeks + lag return `g`) with action ak:
@@ -1205,10 +1225,28 @@ __device__ __forceinline__ void step_body(const Params& pk, int64_t n_envs, cons
                         rec.reserved2 = 0.0;
                         io.pol.rec[r] = rec;
                     }
+                    s.last[i] = (float)acc[0];
+                    s.last[N + i] = (float)acc[1];
+                    s.last[2 * N + i] = (float)acc[3];
+                    s.last[3 * N + i] = (float)acc_len;
 #pragma unroll
                     for (int c = 0; c < 7; ++c) acc[c] = 0.0;
                     acc_len = 0;
                 }
+            }
+            if (SUMS) {
+                const double a0 = sm0 + so.reward, a1 = sm1 + so.pnl, a2 = sm2 + so.tc;
+                const uint32_t n1 = slen + 1u;
+                float f0 = (float)a0, f1 = (float)a1, f2 = (float)a2, f3 = (float)n1;
+                asm volatile("" : "+v"(f0), "+v"(f1), "+v"(f2), "+v"(f3));
+                last0 = so.term ? f0 : last0;
+                last1 = so.term ? f1 : last1;
+                last2 = so.term ? f2 : last2;
+                last3 = so.term ? f3 : last3;
+                sm0 = so.term ? 0.0 : a0;
+                sm1 = so.term ? 0.0 : a1;
+                sm2 = so.term ? 0.0 : a2;
+                slen = so.term ? 0u : n1;
             }
             term = so.term;
             if (INFO) write_info(io.info, i, so, e, post, p.variant);
@@ -1328,6 +1366,16 @@ __device__ __forceinline__ void step_body(const Params& pk, int64_t n_envs, cons
             for (int c = 0; c < 7; ++c) s.acc[(int64_t)c * N + i] = acc[c];
             s.acc_len[i] = acc_len;
         }
+        if (sums) {
+            s.sum[i] = sm0;
+            s.sum[N + i] = sm1;
+            s.sum[2 * N + i] = sm2;
+            s.sum_len[i] = slen;
+            s.last[i] = last0;
+            s.last[N + i] = last1;
+            s.last[2 * N + i] = last2;
+            s.last[3 * N + i] = last3;
+        }
         if (io.trunc) ((GLOBAL uint8_t*)io.trunc)[i] = 0;
     }
     HE_TIM(4);
@@ -1366,6 +1414,8 @@ __global__ __launch_bounds__(kBlock) void step1_kernel(const Params* __restrict_
     io.trunc = sio.trunc;
     io.tobs = sio.tobs;
     io.info = he_info{};
+    io.pol_on = false;
+    io.sums = false;
     step_body<MODE, false, true, BOOK, FAST, false, GS>(*pc, n, tA, tB, tC, s, io, 1, slot0, blockIdx.x);
 }
 
@@ -1568,6 +1618,37 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
             pv_last = portfolio_value<false>(p, e, pre);
         }
     }
+    // the reward wave's episode summaries {return, sum pnl, sum cost, length} of the last
+    // finished episode (he_episode_summaries) and the running sums behind them (s.sum)
+    double sm0 = 0.0, sm1 = 0.0, sm2 = 0.0;
+    uint32_t slen = 0;
+    float last0 = 0.f, last1 = 0.f, last2 = 0.f, last3 = 0.f;
+    if (!OBS) {
+        sm0 = s.sum[i];
+        sm1 = s.sum[N + i];
+        sm2 = s.sum[2 * N + i];
+        slen = s.sum_len[i];
+        last0 = s.last[i];
+        last1 = s.last[N + i];
+        last2 = s.last[2 * N + i];
+        last3 = s.last[3 * N + i];
+    }
+    auto account = [&](double reward, double pnl, double tc, bool term) {
+        const double a0 = sm0 + reward, a1 = sm1 + pnl, a2 = sm2 + tc;
+        const uint32_t n = slen + 1u;
+        // the conversions made unconditionally (opaque): sunk under the selects they turn
+        // them into branches, and the whole autoreset with them
+        float f0 = (float)a0, f1 = (float)a1, f2 = (float)a2, f3 = (float)n;
+        asm volatile("" : "+v"(f0), "+v"(f1), "+v"(f2), "+v"(f3));
+        last0 = term ? f0 : last0;
+        last1 = term ? f1 : last1;
+        last2 = term ? f2 : last2;
+        last3 = term ? f3 : last3;
+        sm0 = term ? 0.0 : a0;
+        sm1 = term ? 0.0 : a1;
+        sm2 = term ? 0.0 : a2;
+        slen = term ? 0u : n;
+    };
     float2 ra[D];
 #pragma unroll
     for (int d = 0; d < D; ++d) ra[d] = ld2(gact, (int64_t)(d < k_steps ? d : k_steps - 1) * N + i);
@@ -1697,6 +1778,7 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
                 const double reward = (rpc - tcp) - thp;
                 grew[koff + i] = (float)reward;
                 gterm[koff + i] = term ? 1 : 0;
+                account(reward, pnl, tc, term);
                 pv_last = pv;
                 // SB3 autoreset (selects)
                 e.t = term ? 0u : t1;
@@ -1736,6 +1818,7 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
                 pv_last = so.pv;
                 if (grew) grew[koff + i] = (float)so.reward;
                 if (gterm) gterm[koff + i] = so.term ? 1 : 0;
+                account(so.reward, so.pnl, so.tc, so.term);
                 pre = so.term ? rst : post;
                 if (so.term) env_reset_common(p, e);
             }
@@ -1744,9 +1827,21 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
     }
     LDS_T1(OBS ? 1 : 0);
     if (!OBS && i0 < N) {
-        s.t[i] = e.t;
-        s.pos[i] = pack_pos(e.call, e.put);
-        s.cash[i] = e.cash;
+        // a fresh (opaque) index: the compiler would otherwise keep every state address of
+        // the prologue live across the block loop, in VGPR pairs, and spill them
+        int64_t j = i;
+        asm volatile("" : "+v"(j));
+        s.t[j] = e.t;
+        s.pos[j] = pack_pos(e.call, e.put);
+        s.cash[j] = e.cash;
+        s.sum[j] = sm0;
+        s.sum[N + j] = sm1;
+        s.sum[2 * N + j] = sm2;
+        s.sum_len[j] = slen;
+        s.last[j] = last0;
+        s.last[N + j] = last1;
+        s.last[2 * N + j] = last2;
+        s.last[3 * N + j] = last3;
     }
 }
 
@@ -1966,6 +2061,8 @@ __global__ __launch_bounds__(kBlock) void reset_kernel(Params p, State s, Market
 #pragma unroll
     for (int c = 0; c < 7; ++c) s.acc[(int64_t)c * p.n + i] = 0.0;
     s.acc_len[i] = 0;
+    for (int c = 0; c < 3; ++c) s.sum[(int64_t)c * p.n + i] = 0.0;
+    s.sum_len[i] = 0;
     if (obs) {
 #pragma unroll
         for (int c = 0; c < kObs; ++c) obs[i * kObs + c] = o[c];
@@ -2361,7 +2458,7 @@ static void launch_step_gs(he_env* env, const Params& p, const Io& io, bool info
         hipLaunchKernelGGL(pk, dim3((unsigned)blocks), dim3(kBlock), 0, st, p, env->s, io, k, slot0);
         return;
     }
-    if (k == 1 && !info) {
+    if (k == 1 && !info && !io.sums) {  // he_step (rollouts keep the episode summaries)
         constexpr bool REPLAY = (MODE == HE_MODE_REPLAY);
         const Params* pc = env->dparams + (REPLAY ? 0 : env->cur_buf);
         const float4* tA = REPLAY ? p.rec : p.tileA;
@@ -2379,7 +2476,7 @@ static void launch_step_gs(he_env* env, const Params& p, const Io& io, bool info
         return;
     }
     void (*kern)(Params, State, Io, int, int);
-    if (k == 1)
+    if (k == 1 && !io.sums)
         kern = info ? step_kernel<MODE, true, true, BOOK, false, false, GS>
                     : step_kernel<MODE, false, true, BOOK, FAST, false, GS>;
     else
@@ -2546,6 +2643,7 @@ static he_status launch_steps(he_env* env, Io io, bool info, int k_total, void* 
     if (!env->ready) return fail(env, HE_ESTATE, "he_reset must be called before stepping");
     DeviceGuard dg(c.device);
     hipStream_t st = (hipStream_t)stream;
+    io.sums = rollout && !io.pol_on;
     if (c.mode == HE_MODE_REPLAY) {
         launch_step<HE_MODE_REPLAY, false, false>(env, env->p, io, info, k_total, 0, st);
         HE_HIP(env, hipGetLastError());
@@ -2709,6 +2807,9 @@ he_status he_create(const he_config* cfg, he_env** out) {
     fs.push_back({(size_t)N * 8, (void**)&env->s.cash, true});
     fs.push_back({(size_t)N * 56, (void**)&env->s.acc, true});
     fs.push_back({(size_t)N * 4, (void**)&env->s.acc_len, true});
+    fs.push_back({(size_t)N * 16, (void**)&env->s.last, true});
+    fs.push_back({(size_t)N * 24, (void**)&env->s.sum, true});
+    fs.push_back({(size_t)N * 4, (void**)&env->s.sum_len, true});
     if (c.mode == HE_MODE_REPLAY) {
         fs.push_back({(size_t)N * 4, (void**)&env->s.path, true});
         fs.push_back({(size_t)N * 4, (void**)&env->s.s0, true});
@@ -3024,9 +3125,10 @@ he_status he_reset(he_env* env, const int64_t* env_ids, int64_t count, float* ob
     if (c.mode == HE_MODE_REPLAY) {
         launch_reset<HE_MODE_REPLAY>(env, env_ids, count, obs_out, inf, st);
     } else {
-        // partial reset: every other env keeps its market position (rewind); full
-        // reset: only wait for a pending prefetch, which writes `cur` too
-        he_status s = env_ids ? materialize_market(env, st) : join_prefetch(env, st);
+        // `cur` must be where the envs are (rewind): a partial reset keeps every other
+        // env on its path, and a reset starts the episode after the env's current one
+        // (cur.ep + 1), not after one a block generated ahead already reached
+        he_status s = materialize_market(env, st);
         if (s != HE_OK) return s;
         env->block_pos = c.market_block;  // tiles regenerated on the next step
         env->next_state = 0;
@@ -3100,6 +3202,19 @@ he_status he_rollout_policy(he_env* env, int32_t k_steps, int32_t policy, float*
         io.pol.count = env->scratch_count;
     }
     return launch_steps(env, io, false, k_steps, stream);
+}
+
+he_status he_episode_summaries(he_env* env, float* out, void* stream) {
+    if (!env || !out) return HE_EINVAL;
+    DeviceGuard dg(env->cfg.device);
+    const int64_t N = env->cfg.n_envs;
+    // [4][N] -> [N][4]: a strided 2D copy on the stream (no kernel)
+    HE_HIP(env, hipMemcpy2DAsync(out, 4 * sizeof(float), env->s.last, sizeof(float), sizeof(float), (size_t)N,
+                                 hipMemcpyDeviceToDevice, (hipStream_t)stream));
+    for (int c = 1; c < 4; ++c)
+        HE_HIP(env, hipMemcpy2DAsync(out + c, 4 * sizeof(float), env->s.last + (size_t)c * N, sizeof(float),
+                                     sizeof(float), (size_t)N, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+    return HE_OK;
 }
 
 he_status he_sync_market(he_env* env, void* stream) {

@@ -351,6 +351,16 @@ class HedgingVecEnv:
         _lib.check(self.lib, self._h, st, "he_rollout")
         return obs, reward, terminated
 
+    def episode_summaries(self, out=None):
+        """[N, 4] f32 device tensor: {return, sum of step P&L, sum of costs, length} of each
+        env's most recently finished episode (he_episode_summaries; generate-mode rollouts
+        and policy rollouts keep them)."""
+        if out is None:
+            out = torch.empty((self.num_envs, 4), dtype=torch.float32, device=self.device)
+        _lib.check(self.lib, self._h, self.lib.he_episode_summaries(self._h, out.data_ptr(), self.stream),
+                   "he_episode_summaries")
+        return out
+
     def rollout_policy(self, k_steps, policy, actions_out=None, obs=None, reward=None, terminated=None,
                        records=None, record_count=None):
         """k_steps fused steps driven by a baseline policy evaluated on the device

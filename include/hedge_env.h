@@ -248,10 +248,18 @@ typedef struct he_episode_record {
  * appends one he_episode_record at records[atomicAdd(record_count, 1)] while that
  * index is < record_capacity (DEVICE pointers; the caller zeroes *record_count).
  * Episode sums run from the last he_reset of the env and are kept by this entry point
- * only (he_step / he_rollout do not update them). */
+ * and by the generate-mode he_rollout (he_step does not update them). */
 he_status he_rollout_policy(he_env* env, int32_t k_steps, int32_t policy, float* actions_out, float* obs,
                             float* reward, uint8_t* terminated, he_episode_record* records,
                             int64_t record_capacity, unsigned long long* record_count, void* stream);
+
+/* Per-env episode summaries, the payload ranks all-gather at rollout boundaries (SURVEY
+ * 8(e); Monitor's episode return / length, train_ppo_v2.py:119, and the evaluation sums
+ * of :481-514): out[N][4] f32 (DEVICE pointer) = {return, sum of step P&L, sum of
+ * transaction costs, length} of each env's most recently finished episode (zeros before
+ * the first).  Maintained by he_rollout in generate modes (the LDS path) and by
+ * he_rollout_policy; the running sums restart at he_reset.  Stream-ordered. */
+he_status he_episode_summaries(he_env* env, float* out, void* stream);
 
 /* Generate modes run market_kernel for block b+1 on a library-owned side stream
  * while the step kernels of block b run on `stream` (he_step, policy rollouts, books;

@@ -13,6 +13,8 @@ mirroring SB3 2.6.0's auto-reset (`train_ppo_v2.py:127-141`).
 
 Outputs `tests/golden/*.npz` (inputs + expected outputs only; no reference
 source).  Re-run:  python oracle/make_golden.py
+G12 (generate mode closed loop, the oracle's GBM market replayed through the
+reference env):  python oracle/make_golden.py --closed-loop
 """
 import os
 import sys
@@ -28,6 +30,7 @@ OUT = os.path.join(REPO, "tests", "golden")
 
 sys.path.insert(0, os.path.join(HERE, "gym_shim"))
 sys.path.insert(0, REF)
+sys.path.insert(1, REPO)
 
 INFO_KEYS = [
     "step_pnl_total", "per_share_step_pnl", "raw_pnl_deviation_abs",
@@ -138,7 +141,98 @@ def run_scenario(name, variant, data, env_kwargs, n_envs, n_steps, seed_base, ac
           f"resets={int(term.sum())} nan_rewards={int(np.isnan(rew).sum())}")
 
 
+def closed_loop(n_envs=16, episodes=2, seed=42):
+    """G12: generate mode pinned to the reference env itself.
+
+    The GBM market of generate mode, as the oracle restates it (Philox4x32-10 normals
+    keyed by (seed, env id, episode * T + t), S_{t+1} = S_t exp((mu - v/2) dt +
+    sqrt(v) sqrt(dt) z), rolling-ATM BS marks; SURVEY 8(d) inputs: S0 = 496.48,
+    v = 0.029028, mu = 0.04, dt = 1/252, T = 252), is written per (env, episode) in the
+    NPZ layout the reference loads (paths / volatilities / call_prices_atm /
+    put_prices_atm, one path per file, so its episode draw integers(1) is always 0) and
+    replayed through the UNMODIFIED hedging_env_v2.HedgingEnv with the train_ppo_v2.py
+    reward settings, DummyVecEnv-style (terminal obs kept, the next episode's env
+    reset).  episodes + 1 episodes of market are made: the last terminal step's
+    post-reset obs is the next episode's reset obs."""
+    from oracle.hedging_oracle import OracleVecEnv
+    T = 252
+    gen = dict(s0=496.48001098632812, variance=0.029028, mu=0.04, dt=1 / 252, episode_length=T)
+    train = dict(loss_type="abs", pnl_penalty_weight=0.001, lambda_cost=0.0001,
+                 theta_weight=0.0002, slippage_bps=1.0, record_metrics=True)  # train_ppo_v2.py:74-80
+    orc = OracleVecEnv(n_envs, mode="gbm", gen=dict(gen, seed=seed, env_offset=0),
+                       **{k: v for k, v in train.items()})
+    orc.seed_envs_at(np.arange(n_envs), [seed] * n_envs)
+    E = episodes + 1
+    S = np.zeros((n_envs, E, T + 1))
+    for e in range(E):
+        orc.g_ep[:] = e
+        orc.S64[:] = gen["s0"]
+        S[:, e, 0] = gen["s0"]
+        for t in range(T):
+            orc.t[:] = t
+            orc._gbm_advance(np.ones(n_envs, bool))
+            S[:, e, t + 1] = orc.S64
+    C, P = orc._gbm_marks(S[..., :T].reshape(-1), None)
+    C = C.reshape(n_envs, E, T)
+    P = P.reshape(n_envs, E, T)
+    V = np.full((n_envs, E, T + 1), gen["variance"])
+    cls = _ref_modules()[2]
+    rng = np.random.default_rng(20251016)
+    n_steps = episodes * T
+    actions = make_actions(rng, n_steps, n_envs, "random")
+    actions = (actions * np.float32(1.05)).astype(np.float32)  # past +-1 too (clip)
+
+    def env_for(i, e):
+        with tempfile.TemporaryDirectory() as td:
+            path = os.path.join(td, "data.npz")
+            np.savez(path, paths=S[i, e][None], volatilities=V[i, e][None], call_prices_atm=C[i, e][None],
+                     put_prices_atm=P[i, e][None])
+            env = cls(path, **train)
+        o, _ = env.reset(seed=seed + i)
+        return env, o
+
+    with np.errstate(all="ignore"):
+        envs, reset_obs, ep = [], np.zeros((n_envs, 13), np.float32), np.zeros(n_envs, np.int64)
+        for i in range(n_envs):
+            env, o = env_for(i, 0)
+            envs.append(env)
+            reset_obs[i] = o
+        obs = np.zeros((n_steps, n_envs, 13), np.float32)
+        term_obs = np.full((n_steps, n_envs, 13), np.nan, np.float32)
+        rew = np.zeros((n_steps, n_envs), np.float64)
+        term = np.zeros((n_steps, n_envs), bool)
+        info = {k: np.full((n_steps, n_envs), np.nan, np.float64) for k in INFO_KEYS}
+        for k in INT_KEYS:
+            info[k] = np.zeros((n_steps, n_envs), np.int64)
+        for s in range(n_steps):
+            for i in range(n_envs):
+                o, r, te, tr, inf = envs[i].step(actions[s, i])
+                assert tr is False
+                rew[s, i] = r
+                term[s, i] = bool(te)
+                for k in INFO_KEYS:
+                    if k in inf:
+                        info[k][s, i] = inf[k]
+                if te:
+                    term_obs[s, i] = o
+                    ep[i] += 1
+                    envs[i], o = env_for(i, ep[i])
+                obs[s, i] = o
+    out = dict(
+        variant=np.int64(2), n_envs=np.int64(n_envs), n_steps=np.int64(n_steps), seed=np.int64(seed),
+        gen_json=np.array(__import__("json").dumps(gen)), config_json=np.array(__import__("json").dumps(train)),
+        market_S=S, market_C=C, market_P=P,
+        actions=actions, reset_obs=reset_obs, obs=obs, terminal_obs=term_obs, reward=rew, terminated=term)
+    for k in INFO_KEYS:
+        out["info_" + k] = info[k]
+    np.savez_compressed(os.path.join(OUT, "g12_closed_loop.npz"), **out)
+    print(f"g12_closed_loop: envs={n_envs} steps={n_steps} resets={int(term.sum())}")
+
+
 def main():
+    if "--closed-loop" in sys.argv:
+        closed_loop()
+        return
     os.makedirs(OUT, exist_ok=True)
     rng = np.random.default_rng(20250629)
     paths = np.load(os.path.join(REF, "data", "paths.npy"))

@@ -593,3 +593,122 @@ def test_full_size_slice_matches_oracle(config):
             terms += int(oterm.sum())
     assert terms == m  # every env finished its first episode at t = 252
     venv.close()
+
+
+@pytest.mark.parametrize("path", ["lds", "tile", "book"])
+def test_episode_summaries_match_oracle(path, monkeypatch):
+    """he_episode_summaries (the per-env payload ranks all-gather): the
+    {return, sum of step P&L, sum of transaction costs, length} of each env's last finished
+    episode equal the oracle's sums of reward / step_pnl_total / transaction_costs_total
+    over the same steps (f64 sums in step order, f32 out; P&L bar PNL_RTOL) -- through the
+    LDS rollout, the tile rollout and the tile rollout with a liability book, over rollout
+    calls that split episodes, with he_reset restarting the running sums."""
+    from cantorrl_amd.vec_env import HedgingVecEnv
+    monkeypatch.setenv("HE_LDS_ROLLOUT", "1" if path == "lds" else "0")
+    n, T, seed = 300, 23, 5
+    cfg = dict(loss_type="abs", pnl_penalty_weight=0.001, lambda_cost=0.0001, theta_weight=0.0002, slippage_bps=1.0)
+    gen = dict(s0=496.48001098632812, variance=0.029028, mu=0.04, dt=1 / 252, episode_length=T)
+    if path == "book":
+        gen["book"] = BOOK8
+    rng = np.random.default_rng(seed)
+    ks = (64, 9, 40, 100)
+    acts = rng.uniform(-1.05, 1.05, size=(sum(ks), n, 2)).astype(np.float32)
+    venv = HedgingVecEnv(n, mode="gbm", generate=gen, seed=seed, info_keys=(), return_numpy=False, **cfg)
+    orc = OracleVecEnv(n, mode="gbm", gen=dict(gen, seed=seed, env_offset=0), **cfg)
+    orc.seed_envs_at(np.arange(n), [seed] * n)
+    orc.reset()
+    venv.reset_tensors()
+    assert not venv.episode_summaries().any()
+    run = np.zeros((3, n))
+    length = np.zeros(n, np.int64)
+    last = np.zeros((n, 4))
+    a0 = 0
+    for k in ks:
+        _, grew, _ = venv.rollout(torch.from_numpy(acts[a0:a0 + k]).cuda())
+        grew = grew.cpu().numpy()
+        for s in range(a0, a0 + k):
+            _, orew, oterm, _, oinf = orc.step(acts[s])
+            assert_same(grew[s - a0], orew.astype(np.float32), f"reward[{s}]", rtol=PNL_RTOL, atol=1e-9)
+            run += np.stack([orew, oinf["step_pnl_total"], oinf["transaction_costs_total"]])
+            length += 1
+            done = np.asarray(oterm, bool)
+            last[done] = np.stack([run[0], run[1], run[2], length], axis=1)[done]
+            run[:, done] = 0.0
+            length[done] = 0
+        a0 += k
+        got = venv.episode_summaries().cpu().numpy()
+        assert_same(got[:, 3], last[:, 3].astype(np.float32), f"length after {a0}")
+        assert_same(got[:, 0], last[:, 0].astype(np.float32), f"return after {a0}", rtol=PNL_RTOL, atol=1e-6)
+        for c, name in ((1, "pnl"), (2, "cost")):
+            scale = np.abs(last[:, c]).max() + 1.0
+            assert_same(got[:, c], last[:, c].astype(np.float32), f"{name} after {a0}", rtol=PNL_RTOL,
+                        atol=PNL_RTOL * scale)
+    # he_reset restarts the running sums; the last finished episode stays reported
+    before = venv.episode_summaries().clone()
+    venv.reset_tensors()
+    orc.reset()
+    assert torch.equal(venv.episode_summaries(), before)
+    _, grew, _ = venv.rollout(torch.from_numpy(acts[:T]).cuda())
+    grew = grew.cpu().numpy()
+    run[:] = 0.0
+    for s in range(T):
+        _, orew, _, _, oinf = orc.step(acts[s])
+        assert_same(grew[s], orew.astype(np.float32), f"reward after reset[{s}]", rtol=PNL_RTOL, atol=1e-9)
+        run += np.stack([orew, oinf["step_pnl_total"], oinf["transaction_costs_total"]])
+    got = venv.episode_summaries().cpu().numpy()
+    assert (got[:, 3] == T).all()
+    assert_same(got[:, 0], run[0].astype(np.float32), "return after reset", rtol=PNL_RTOL, atol=1e-6)
+    venv.close()
+
+
+@pytest.mark.parametrize("api", ["step", "rollout_lds", "rollout_tile"])
+def test_generate_mode_matches_reference_closed_loop(api, monkeypatch):
+    """G12 (tests/golden/g12_closed_loop.npz): GPU generate mode against the UNMODIFIED
+    reference env replaying the generate-mode market (oracle/make_golden.py
+    --closed-loop; 16 envs x 2 episodes of 252 steps, seed 42, SURVEY 8(d) inputs).
+    he_step with every info field, and he_rollout through lds_rollout_kernel and through
+    the tile kernels: obs columns, done flags, integer fields bit-exact, greeks at
+    OBS_RTOL, rewards and the f64 P&L fields at PNL_RTOL."""
+    import json
+    from cantorrl_amd.vec_env import HedgingVecEnv
+    z = np.load(os.path.join(GOLDEN, "g12_closed_loop.npz"), allow_pickle=False)
+    d = {k: z[k] for k in z.files}
+    gen, cfg = json.loads(str(d["gen_json"])), json.loads(str(d["config_json"]))
+    n, steps = int(d["n_envs"]), int(d["n_steps"])
+    monkeypatch.setenv("HE_LDS_ROLLOUT", "0" if api == "rollout_tile" else "1")
+    env = HedgingVecEnv(n, mode="gbm", generate=gen, seed=int(d["seed"]), return_numpy=False,
+                        info_keys=all_info_keys() if api == "step" else (), **cfg)
+    compare_obs(env.reset_tensors().cpu().numpy(), d["reset_obs"], "reset_obs")
+    if api == "step":
+        for s in range(steps):
+            obs, rew, term, _ = env.step_tensors(torch.from_numpy(d["actions"][s]).cuda())
+            torch.cuda.synchronize()
+            done = d["terminated"][s]
+            assert_same(term.cpu().numpy().astype(bool), done, f"terminated[{s}]")
+            assert_same(rew.cpu().numpy(), d["reward"][s].astype(np.float32), f"reward[{s}]", rtol=PNL_RTOL, atol=1e-9)
+            compare_obs(obs.cpu().numpy(), d["obs"][s], f"obs[{s}]")
+            if done.any():
+                compare_obs(env._tobs.cpu().numpy()[done], d["terminal_obs"][s][done], f"terminal_obs[{s}]")
+            for k in GOLD_INFO:
+                exp = d["info_" + k][s]
+                got = env.info_tensor(k).cpu().numpy().astype(exp.dtype)
+                if exp.dtype.kind == "i":
+                    assert_same(got, exp, f"info_{k}[{s}]")
+                else:
+                    assert_same(got, exp, f"info_{k}[{s}]", rtol=PNL_RTOL, atol=1e-9)
+    else:
+        obs, rew, term = env.rollout(torch.from_numpy(d["actions"]).cuda())
+        torch.cuda.synchronize()
+        assert_same(term.cpu().numpy().astype(bool), d["terminated"], "terminated")
+        assert_same(rew.cpu().numpy(), d["reward"].astype(np.float32), "reward", rtol=PNL_RTOL, atol=1e-9)
+        compare_obs(obs.cpu().numpy(), d["obs"], "obs")
+        # the last finished episode of every env (he_episode_summaries) from the golden
+        summ = env.episode_summaries().cpu().numpy()
+        T = int(gen["episode_length"])
+        last = slice(steps - T, steps)
+        assert (summ[:, 3] == T).all()
+        assert_same(summ[:, 0], d["reward"][last].sum(0).astype(np.float32), "episode return", rtol=PNL_RTOL,
+                    atol=1e-6)
+        assert_same(summ[:, 2], d["info_transaction_costs_total"][last].sum(0).astype(np.float32), "episode cost",
+                    rtol=PNL_RTOL, atol=1e-6)
+    env.close()

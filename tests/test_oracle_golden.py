@@ -85,3 +85,31 @@ def test_bs_price_matches_option_calculator():
     assert_same(pd, z["put_delta"], "put_delta", rtol=1e-13)
     assert_same(g, z["gamma"], "gamma", rtol=1e-12)
     assert_same(v, z["vega"], "vega", rtol=1e-12)
+
+
+def load_closed_loop():
+    import json
+    z = np.load(os.path.join(GOLDEN, "g12_closed_loop.npz"), allow_pickle=False)
+    d = {k: z[k] for k in z.files}
+    return json.loads(str(d["gen_json"])), json.loads(str(d["config_json"])), d
+
+
+def test_oracle_generate_mode_matches_reference_closed_loop():
+    """G12: the oracle's generate mode (its own GBM market, made inside the env) equals
+    the unmodified reference env replaying that market (oracle/make_golden.py
+    --closed-loop): every obs, reward, done flag, terminal obs and info field, bit for
+    bit, over 2 episodes x 16 envs."""
+    gen, cfg, d = load_closed_loop()
+    n, seed = int(d["n_envs"]), int(d["seed"])
+    env = OracleVecEnv(n, mode="gbm", gen=dict(gen, seed=seed, env_offset=0), **cfg)
+    env.seed_envs_at(np.arange(n), [seed] * n)
+    assert_same(env.reset(), d["reset_obs"], "reset_obs")
+    for s in range(int(d["n_steps"])):
+        o, r, te, to, inf = env.step(d["actions"][s])
+        assert_same(te, d["terminated"][s], f"terminated[{s}]")
+        assert_same(r, d["reward"][s], f"reward[{s}]")
+        assert_same(o, d["obs"][s], f"obs[{s}]")
+        if te.any():
+            assert_same(to[te], d["terminal_obs"][s][te], f"terminal_obs[{s}]")
+        for k in INFO_FIELDS:
+            assert_same(np.asarray(inf[k]).astype(d["info_" + k].dtype), d["info_" + k][s], f"info_{k}[{s}]")
