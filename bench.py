@@ -312,6 +312,22 @@ class Runner:
 GATHER_EVERY = 256  # train_ppo_v2.py:48 n_steps
 
 
+def init_dist(local):
+    """One rank per GPU over RCCL (backend "nccl").  BENCH_DIST_BACKEND=gloo is the
+    rehearsal of the N-rank path on a box with fewer GPUs than ranks (ranks share
+    device local % device_count, host-side collectives); the driver's runs use RCCL."""
+    import torch.distributed as dist
+    backend = os.environ.get("BENCH_DIST_BACKEND", "nccl")
+    ndev = torch.cuda.device_count()
+    dev_index = local if backend == "nccl" else local % max(ndev, 1)
+    torch.cuda.set_device(dev_index)
+    if backend == "nccl":
+        dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
+    else:
+        dist.init_process_group(backend)
+    return dist, backend
+
+
 def gather_summaries(dist, local, gathered):
     """All-gather the per-env episode summaries [n, 4] {return, sum P&L, sum cost, length}
     of every rank into gathered [world * n, 4], rank-major: row r * n + i is global env
@@ -320,7 +336,7 @@ def gather_summaries(dist, local, gathered):
     if gathered.is_cuda:
         dist.all_gather_into_tensor(gathered, local)
     else:
-        dist.all_gather(list(gathered.chunk(dist.get_world_size())), local)
+        dist.all_gather(list(gathered.chunk(dist.get_world_size())), local.to(gathered.device))
     return gathered
 
 
@@ -483,7 +499,9 @@ def timed(runner, K, W, dist):
         dist.barrier()
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
-    t = torch.tensor([wall], dtype=torch.float64, device=torch.device("cuda", torch.cuda.current_device()))
+    host = dist is not None and dist.get_backend() == "gloo"
+    t = torch.tensor([wall], dtype=torch.float64,
+                     device="cpu" if host else torch.device("cuda", torch.cuda.current_device()))
     if dist is not None:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item()), ev0.elapsed_time(ev1)
@@ -757,11 +775,9 @@ def main(argv=None):
             pmc = pmc_traffic(args)
         if not args.no_cpu_baseline:
             cpu = cpu_baseline(args.cpu_seconds)   # before the GPU is touched (forks workers)
-    dist = None
+    dist, backend = None, None
     if world > 1:
-        import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dist, backend = init_dist(local)
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
@@ -772,7 +788,8 @@ def main(argv=None):
     g.manual_seed(1234 + rank)
     acts = torch.rand((256, n, 2), device=dev, generator=g) * 2 - 1
     stream = torch.cuda.Stream(device=dev)
-    gathered = torch.empty((world * n, 4), dtype=torch.float32, device=dev) if world > 1 else None
+    gathered = (torch.empty((world * n, 4), dtype=torch.float32, device=dev if backend == "nccl" else "cpu")
+                if world > 1 else None)
 
     env = make_env(args, dev, rank)
     runner = Runner(args, env, args.mode, acts, stream, dist, gathered)
@@ -783,7 +800,8 @@ def main(argv=None):
     payload = None
     if dist is not None:
         payload = dict(what="he_episode_summaries: per-env {return, sum P&L, sum cost, length} f32 [envs, 4], "
-                            "all_gather_into_tensor over RCCL", every_steps=GATHER_EVERY,
+                            "all-gathered to [world * envs, 4]", backend="rccl" if backend == "nccl" else backend,
+                       every_steps=GATHER_EVERY,
                        bytes_per_rank=n * 16, gathers=runner.gathers)
         payload.update(summarize_payload(runner.gathered))
     hev = HipEvents()

@@ -1,24 +1,43 @@
 #!/bin/bash
-# Measurement pass on the GPU box: GPU parity suite, smoke, default bench (PMC traffic +
-# CPU baseline, graph-mode step API), and a rocprofv3 kernel-trace summary of the default bench.
-#   gpurun --timeout 1100 -- bash tools/gpu/round.sh <tag>
+# Round measurements.  Phase "tests": the whole -m gpu suite + smoke().  Phase "bench":
+# the headline bench line (PMC traffic + CPU baseline + step API), the same command under
+# rocprofv3 --kernel-trace --stats, configs 3-5, and the 2-rank rehearsal of the --gpus N
+# launcher (gloo collectives, both ranks on this box's one GPU).
+#   gpurun --timeout 1200 -- bash tools/gpu/round.sh <tag> tests|bench
 set -o pipefail
-TAG=${1:-run}
-R=$GRAFT_REPO_ROOT; cd $R; O=gpurun_out/$TAG; mkdir -p $O
-export TMPDIR=/tmp
-echo "[$(date +%T)] pytest -m gpu"
-timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1 \
-  || { echo "pytest failed"; tail -40 $O/pytest_gpu.log; exit 1; }
-tail -3 $O/pytest_gpu.log
-echo "[$(date +%T)] smoke"
-timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
-tail -1 $O/smoke.log
-echo "[$(date +%T)] bench default"
-timeout -k 10 400 python -u bench.py > $O/b_default.log 2>&1 || { tail -20 $O/b_default.log; exit 1; }
-grep "^{" $O/b_default.log
-echo "[$(date +%T)] rocprofv3 kernel trace"
+TAG=${1:-round}; PHASE=${2:-bench}
+R=$GRAFT_REPO_ROOT; cd $R; O=$R/gpurun_out/$TAG; mkdir -p $O; export TMPDIR=/tmp
+if [ "$PHASE" = tests ]; then
+  echo "[$(date +%T)] pytest -m gpu"
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1 \
+    || { echo "pytest failed"; grep -E "FAIL|Error|assert" $O/pytest_gpu.log | head -30; tail -30 $O/pytest_gpu.log; exit 1; }
+  tail -2 $O/pytest_gpu.log
+  echo "[$(date +%T)] smoke"
+  timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
+  tail -3 $O/smoke.log
+  exit 0
+fi
+echo "[$(date +%T)] bench (default: PMC + CPU baseline + step API)"
+timeout -k 10 400 python -u bench.py > $O/bench.log 2>&1 || { tail -20 $O/bench.log; exit 1; }
+grep "^{" $O/bench.log > $O/bench.jsonl
+echo "[$(date +%T)] bench under rocprofv3 --kernel-trace --stats"
 cd /tmp
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $R/$O/prof -o run --output-format csv -- python3 $R/bench.py --no-cpu-baseline --no-pmc --no-step-api > $R/$O/b_prof.log 2>&1 || { tail -20 $R/$O/b_prof.log; exit 1; }
-grep "^{" $R/$O/b_prof.log
-find $R/$O/prof -name "*kernel_stats.csv"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 $R/bench.py --no-pmc --no-cpu-baseline --no-step-api > $O/bench_rocprof.log 2>&1 || { tail -20 $O/bench_rocprof.log; exit 1; }
+cd $R
+grep "^{" $O/bench_rocprof.log > $O/bench_under_rocprof.jsonl
+for c in 3 4 5; do
+  echo "[$(date +%T)] bench config $c"
+  timeout -k 10 300 python -u bench.py --config $c --no-pmc --no-cpu-baseline --no-step-api > $O/b_cfg$c.log 2>&1 || { tail -20 $O/b_cfg$c.log; exit 1; }
+  grep "^{" $O/b_cfg$c.log >> $O/bench_cfg345.jsonl
+done
+echo "[$(date +%T)] --gpus 2 rehearsal (gloo, one GPU)"
+BENCH_DIST_BACKEND=gloo timeout -k 10 300 python -u bench.py --gpus 2 --no-pmc --no-cpu-baseline --no-step-api --steps 512 --warmup 256 > $O/b_gpus2.log 2>&1 || { tail -30 $O/b_gpus2.log; exit 1; }
+grep "^{" $O/b_gpus2.log > $O/bench_gpus2_rehearsal.jsonl
+python3 - <<PY
+import json
+for f in ("bench.jsonl", "bench_under_rocprof.jsonl", "bench_cfg345.jsonl", "bench_gpus2_rehearsal.jsonl"):
+    for l in open("$O/" + f):
+        d = json.loads(l); r = d.get("roofline", {})
+        print(f, d["config"].get("config_index"), d["n_gpus"], "%.4g" % d["value"], r.get("kernel_us"), r.get("frac"), r.get("traffic_over_bytes"), d.get("gather", {}).get("envs_with_finished_episode"))
+PY
 echo "[$(date +%T)] done"
