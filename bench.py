@@ -74,8 +74,8 @@ MARKET_STATE_BYTES = 72
 
 
 def lds_rollout(cfg):
-    """he_rollout runs lds_rollout_kernel (GBM without a book, unless HE_LDS_ROLLOUT=0)."""
-    return cfg["mode"] == "gbm" and not cfg["gen"].get("book") and os.environ.get("HE_LDS_ROLLOUT", "1") != "0"
+    """he_rollout runs lds_rollout_kernel (GBM, with or without a book, unless HE_LDS_ROLLOUT=0)."""
+    return cfg["mode"] == "gbm" and os.environ.get("HE_LDS_ROLLOUT", "1") != "0"
 
 
 def fused_market():
@@ -367,11 +367,13 @@ def probe(args):
     env.close()
 
 
-def pmc_traffic(args):
-    """HBM bytes per step-kernel launch from rocprofv3 PMC counters, one counter per
-    pass (MI355X_MICROARCH.md "HBM": FETCH_SIZE reads 1/2 of a wide coalesced read on
-    gfx950, so bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024).  Runs BEFORE this process
-    touches the GPU; the profiled program is a child (`rocprofv3 ... -- python3`)."""
+STEP_KERNELS = r"step1?_kernel|step_market_kernel|lds_rollout_kernel"
+
+
+def pmc_pass(args, counters, kernels=STEP_KERNELS):
+    """One rocprofv3 --pmc pass of `bench.py --probe` (a child process: this one has not
+    touched the GPU) -> {kernel short name: {counter: mean per dispatch}} for the
+    kernels matching `kernels` (the first dispatches of each skipped: warm-up)."""
     import csv
     import glob
     import re
@@ -380,29 +382,74 @@ def pmc_traffic(args):
     import tempfile
     if shutil.which("rocprofv3") is None:
         return None, "rocprofv3 not found"
+    with tempfile.TemporaryDirectory(dir="/tmp") as td:
+        cmd = ["rocprofv3", "--pmc", *counters, "--output-format", "csv", "-d", td, "-o", "pmc", "--",
+               sys.executable, os.path.abspath(__file__), "--probe", "--envs", str(args.envs),
+               "--config", str(args.config), "--mode", args.mode, "--rollout-k", str(args.rollout_k)]
+        try:
+            subprocess.run(cmd, check=True, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
+                           timeout=240, cwd="/tmp", env=dict(os.environ, TMPDIR="/tmp"))
+        except Exception as e:  # noqa: BLE001
+            return None, f"rocprofv3 --pmc {' '.join(counters)} failed: {e}"
+        rows = {}
+        for fn in glob.glob(os.path.join(td, "**", "*counter_collection.csv"), recursive=True):
+            with open(fn) as fh:
+                for r in csv.DictReader(fh):
+                    m = re.search(kernels, r.get("Kernel_Name", ""))
+                    if m and r.get("Counter_Name") in counters:
+                        k = m.group(0)
+                        rows.setdefault(k, {}).setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
+    if not rows:
+        return None, f"no {counters} rows for {kernels}"
+    skip = 2 if args.mode == "rollout" else 8
+    return {k: {c: float(np.mean(v[skip:] if len(v) > 2 * skip else v)) for c, v in d.items()}
+            for k, d in rows.items()}, None
+
+
+def pmc_traffic(args):
+    """HBM bytes per step-kernel launch from rocprofv3 PMC counters, one counter per
+    pass (MI355X_MICROARCH.md "HBM": FETCH_SIZE reads 1/2 of a wide coalesced read on
+    gfx950, so bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024).  Runs BEFORE this process
+    touches the GPU; the profiled program is a child (`rocprofv3 ... -- python3`)."""
     vals = {}
     for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
-        with tempfile.TemporaryDirectory(dir="/tmp") as td:
-            cmd = ["rocprofv3", "--pmc", ctr, "--output-format", "csv", "-d", td, "-o", "pmc", "--",
-                   sys.executable, os.path.abspath(__file__), "--probe", "--envs", str(args.envs),
-                   "--config", str(args.config), "--mode", args.mode, "--rollout-k", str(args.rollout_k)]
-            try:
-                subprocess.run(cmd, check=True, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
-                               timeout=240, cwd="/tmp", env=dict(os.environ, TMPDIR="/tmp"))
-            except Exception as e:  # noqa: BLE001
-                return None, f"rocprofv3 --pmc {ctr} failed: {e}"
-            rows = []
-            for f in glob.glob(os.path.join(td, "**", "*counter_collection.csv"), recursive=True):
-                with open(f) as fh:
-                    for r in csv.DictReader(fh):
-                        if re.search(r"step1?_kernel|step_market_kernel|lds_rollout_kernel", r.get("Kernel_Name", "")) and r.get("Counter_Name") == ctr:
-                            rows.append(float(r["Counter_Value"]))
-            if not rows:
-                return None, f"no {ctr} rows for the step kernel"
-            skip = 2 if args.mode == "rollout" else 8
-            vals[ctr] = float(np.mean(rows[skip:] if len(rows) > 2 * skip else rows))
+        res, err = pmc_pass(args, [ctr])
+        if res is None:
+            return None, err
+        vals[ctr] = sum(d[ctr] for d in res.values() if ctr in d)
     traffic = (2.0 * vals["FETCH_SIZE"] + vals["WRITE_SIZE"]) * 1024.0
     return traffic, vals
+
+
+VALU_COUNTERS = ["SQ_INSTS_VALU", "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64",
+                 "SQ_INSTS_VALU_TRANS_F64", "GRBM_GUI_ACTIVE"]
+FP64_VECTOR_PEAK_TFLOPS = 78.6  # half the 157.3 TF f32 vector rate (MI355X_MICROARCH.md): f64 FMA issues at 1/2
+
+
+def pmc_valu(args):
+    """The VALU side of the step and market kernels (one --pmc pass): per dispatch, wave
+    instructions per SIMD-cycle (cycles = GRBM_GUI_ACTIVE / 8, the guide's per-XCD sum)
+    against the issue bound of the kernel's f64 / other mix (a wave64 VALU instruction
+    every 2 cycles per SIMD, f64 every 4), and the f64 FLOP count per dispatch."""
+    res, err = pmc_pass(args, VALU_COUNTERS, STEP_KERNELS + "|market_kernel")
+    if res is None:
+        return None, err
+    out = {}
+    for k, d in res.items():
+        if "SQ_INSTS_VALU" not in d or not d.get("GRBM_GUI_ACTIVE"):
+            continue
+        f64 = sum(d.get(c, 0.0) for c in VALU_COUNTERS[1:5])
+        share = f64 / d["SQ_INSTS_VALU"] if d["SQ_INSTS_VALU"] else 0.0
+        cycles = d["GRBM_GUI_ACTIVE"] / 8.0
+        issue = d["SQ_INSTS_VALU"] / (cycles * 1024.0)
+        bound = 1.0 / (2.0 * (1.0 - share) + 4.0 * share)
+        out[k] = dict(valu_insts=d["SQ_INSTS_VALU"], f64_share=round(share, 4),
+                      issue_per_simd_cycle=round(issue, 4), issue_bound_per_simd_cycle=round(bound, 4),
+                      valu_issue_frac=round(issue / bound, 4),
+                      f64_flop=64.0 * (2.0 * d.get("SQ_INSTS_VALU_FMA_F64", 0.0) + d.get("SQ_INSTS_VALU_ADD_F64", 0.0)
+                                       + d.get("SQ_INSTS_VALU_MUL_F64", 0.0)),
+                      cycles_profiled=cycles)
+    return out, None
 
 
 class HipEvents:
@@ -516,7 +563,7 @@ def roofline(mode, n, kern_ms, rk, book=False, market="gbm", lds=False):
     if mode == "rollout":
         survey = n * (rk * SURVEY_ROLLOUT_B + SURVEY_ROLLOUT_STATE_B)
         if lds:
-            own = n * (rk * LDS_STEP_B + LDS_STATE_B)
+            own = n * (rk * LDS_STEP_B + LDS_STATE_B + (16 if book else 0))  # + the book's running max
             kname = ("lds_rollout_kernel (he_rollout, K=%d fused steps; the market made in LDS by "
                      "producer waves, never written to HBM)" % rk)
         else:
@@ -711,6 +758,9 @@ def launch(args, argv):
         if args.workload == "env" and not args.no_pmc:
             t, v = pmc_traffic(args)
             parent.update(pmc=t, pmc_note=v if t is None else None, pmc_counters=v if t is not None else None)
+            if CONFIGS[args.config]["gen"].get("book"):
+                vv, note = pmc_valu(args)
+                parent.update(valu=vv, valu_note=note)
         if not args.no_cpu_baseline:
             parent["cpu_baseline"] = (cpu_baseline(args.cpu_seconds) if args.workload == "env"
                                       else None)
@@ -765,14 +815,19 @@ def main(argv=None):
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     pmc = (None, "skipped")
+    valu = (None, "skipped")
     cpu = None
+    has_book = bool(CONFIGS[args.config]["gen"].get("book"))
     parent = parent_results()
     if parent is not None:  # ranks of a `--gpus N` launch: the launcher measured these
         pmc = (parent["pmc"], parent.get("pmc_counters") or parent.get("pmc_note"))
+        valu = (parent.get("valu"), parent.get("valu_note"))
         cpu = parent["cpu_baseline"]
     elif world == 1:
         if not args.no_pmc:
             pmc = pmc_traffic(args)
+            if has_book:  # VALU-bound configurations: the instruction-issue side
+                valu = pmc_valu(args)
         if not args.no_cpu_baseline:
             cpu = cpu_baseline(args.cpu_seconds)   # before the GPU is touched (forks workers)
     dist, backend = None, None
@@ -808,13 +863,28 @@ def main(argv=None):
     kern_ms = kernel_time_ms(hev, runner, 64 if args.mode == "rollout" else 256)
     env.close()
 
-    has_book = bool(cfg["gen"].get("book"))
     roof = roofline(args.mode, n, kern_ms, args.rollout_k, has_book, tile_layout(cfg["mode"], n), lds)
     if not lds:  # the tile path: market_kernel makes the HBM market tile
         roof["tile_layout"] = tile_layout(cfg["mode"], n)
         mkt_ms = market_time_ms(hev, args, dev, acts, stream)
         roof["market_kernel_us_per_64_steps"] = round(mkt_ms * 1e3, 3)
         roof["market_kernel_us_per_step"] = round(mkt_ms * 1e3 / M_BLOCK, 3)
+        steps_per_launch = args.rollout_k if args.mode == "rollout" else 1
+        if mkt_ms / M_BLOCK > kern_ms / steps_per_launch:
+            roof["dominant_kernel"] = "market_kernel (the HBM market tile, %.1f us per step vs %.1f for the steps)" % (
+                mkt_ms * 1e3 / M_BLOCK, kern_ms * 1e3 / steps_per_launch)
+    if valu[0]:
+        # the dominant kernel by profiled cycles; with a book it is VALU-bound: its issue
+        # rate against the bound of its f64 mix, and its f64 FLOP rate at the live duration
+        dom = max(valu[0], key=lambda k: valu[0][k]["cycles_profiled"])
+        v = dict(valu[0][dom])
+        if dom == "lds_rollout_kernel" or (dom.startswith("step") and "market" not in dom):
+            v["f64_tflops"] = round(v["f64_flop"] / (kern_ms * 1e-3) / 1e12, 3)
+            v["f64_frac_of_vector_peak"] = round(v["f64_tflops"] / FP64_VECTOR_PEAK_TFLOPS, 4)
+        roof["valu"] = dict(kernel=dom, peak_f64_tflops=FP64_VECTOR_PEAK_TFLOPS, **v)
+        roof["valu_by_kernel"] = valu[0]
+    elif valu[1] != "skipped":
+        roof["valu_note"] = valu[1]
     if pmc[0] is not None:
         roof["traffic"] = int(pmc[0])
         roof["traffic_over_bytes"] = round(pmc[0] / roof["bytes_per_launch"], 4)

@@ -111,6 +111,7 @@ struct BookOpt {
     int32_t type, expiry;
     double K, H, q100;
     double lnK, lnH, lnH2K;   // log K, log H, 2 log H - log K (host)
+    double invK;              // 1 / K (host)
 };
 
 struct Params {
@@ -161,7 +162,7 @@ struct Params {
     // liability book (generate modes)
     int32_t book_n;
     const BookOpt* book;    // device copy [book_n], read through the scalar cache
-    const double* book_tab; // [m][3] = {sqrt(m dt), 1 / sqrt(m dt), exp(-r m dt)}, m = 0..max expiry
+    const double* book_tab; // [m][4] = {sqrt(m dt), 1 / sqrt(m dt), exp(-r m dt), exp(r m dt)}, m = 0..max expiry
     double book_rst;        // book value of the reset market (t = 0, S0, v0)
     double* tileC;          // [M+1][N] f64 book value of every slot
 #ifdef HE_TIMING
@@ -422,79 +423,142 @@ __device__ __forceinline__ void marks(const Params& p, double S64, double var64,
 // (option_calculator.py:11-27, intrinsic when tau <= 0 or sig <= 0).  Up-and-out call
 // (q = 0, Hull, "Options, Futures and Other Derivatives", barrier options):
 // c_uo = c - c_ui, worthless once S touched H at a step date or when H <= K.
-// tab[m] = {sqrt(m dt), 1 / sqrt(m dt), exp(-r m dt)} (tau = m dt as in book_option)
+// tab[m] = {sqrt(m dt), 1 / sqrt(m dt), exp(-r m dt), exp(r m dt)} (tau = m dt as in book_option)
 __global__ void book_tab_kernel(double* tab, int32_t n, double dt, double r) {
     const int m = blockIdx.x * blockDim.x + threadIdx.x;
     if (m >= n) return;
     const double tau = (double)m * dt;
     const double sq = sqrt(tau);
-    tab[3 * m] = sq;
-    tab[3 * m + 1] = 1.0 / sq;
-    tab[3 * m + 2] = exp(-r * tau);
+    tab[4 * m] = sq;
+    tab[4 * m + 1] = 1.0 / sq;
+    tab[4 * m + 2] = exp(-r * tau);
+    tab[4 * m + 3] = exp(r * tau);
 }
 
 // Per env-step constants shared by the book's options: log S once (log(S/K) =
 // log S - log K), 1/sigma, and lam of the barrier formula; per option the
-// tau-dependent sqrt(tau), 1/sqrt(tau) and exp(-r tau) come from a table indexed by
-// the remaining steps m = expiry - t (tau = m dt, the same f64 product as before).
+// tau-dependent sqrt(tau), 1/sqrt(tau), exp(-r tau) and exp(r tau) come from a table
+// indexed by the remaining steps m = expiry - t (tau = m dt, the same f64 product).
 struct BookEnv {
     double S, lnS, sig, isig, s2, lam;
 };
 
-// (N(a), N(-a)) from one erfc(|a|/sqrt2) on every lane.  ndtr_pair's erf branch for
-// |a| < 1 would make a wave of mixed d's run both branches; the book (an extension
-// without a reference, checked against oracle/hedging_oracle.py through the P&L in
-// tests/test_gpu_parity.py) takes the erfc form throughout: the same values to
-// ~1e-16 absolute.
-__device__ __forceinline__ void ncdf_pair(double a, double* pos, double* neg) {
-    const double y = 0.5 * erfc(fabs(a) * 0.70710678118654752440);
-    const bool p = a > 0.0;
-    *pos = p ? 1.0 - y : y;
-    *neg = p ? y : 1.0 - y;
+// The normal tail Q(a) = Phi(-a), a >= 0, as phi(a) R(a) with the Mills ratio
+// R(a) = sqrt(pi/2) erfcx(a / sqrt 2) a degree-20 polynomial in u = A - B / (a + c), c = 3.5:
+// the Chebyshev fit on a in [0, 38.6] (Q underflows past it) re-expanded in powers of u
+// (coefficients below 0.49 in magnitude, so Horner loses nothing), 2.6e-13 relative on Q
+// against scipy.special.ndtr (tools/mills_fit.py).  Branch-free -- every lane of a wave
+// runs the same instructions whatever its d -- and phi is the caller's: d1 and d2 of a
+// Black-Scholes price share one exp (S phi(d1) = K e^{-r tau} phi(d2)).  Replaces two
+// library erfc per pair, each with its own exp and range branches (the book is an
+// extension without a reference; its bar is the oracle's P&L at 1e-5, test_gpu_parity.py).
+constexpr double kMillsA = 1.1813471502590676, kMillsB = 7.6347150259067362, kMillsC = 3.5;
+constexpr double kMillsMax = 37.4;                       // phi(37.4) ~ 1e-304: the tail is 0 past it
+constexpr double kInvSqrt2Pi = 0.39894228040143267794;
+__device__ __forceinline__ double mills(double a) {
+    const double d = a + kMillsC;                        // in [3.5, 41]: no special cases
+    double y = __builtin_amdgcn_rcp(d);
+    y = fma(fma(-d, y, 1.0), y, y);                      // two Newton steps: 1 / d to the last bits
+    y = fma(fma(-d, y, 1.0), y, y);
+    const double u = fma(-kMillsB, y, kMillsA);
+    double r = -4.4206737983570504e-10;
+    r = fma_k(r, u, -3.8907837965992227e-09);
+    r = fma_k(r, u, -1.6735307803068382e-09);
+    r = fma_k(r, u, 3.5462265542512339e-08);
+    r = fma_k(r, u, 6.1229321472110077e-08);
+    r = fma_k(r, u, -1.4934329903924975e-07);
+    r = fma_k(r, u, -5.8954452073183568e-07);
+    r = fma_k(r, u, 1.6391429736383158e-07);
+    r = fma_k(r, u, 4.1122801372346195e-06);
+    r = fma_k(r, u, 3.4217038844164288e-06);
+    r = fma_k(r, u, -2.7074245209317019e-05);
+    r = fma_k(r, u, -4.4835109354094885e-05);
+    r = fma_k(r, u, 0.00021086542652290141);
+    r = fma_k(r, u, 0.00039784937176197925);
+    r = fma_k(r, u, -0.002353960594219441);
+    r = fma_k(r, u, -0.0013327285592737549);
+    r = fma_k(r, u, 0.034655415072285041);
+    r = fma_k(r, u, -0.13151258275835945);
+    r = fma_k(r, u, 0.29927575053510824);
+    r = fma_k(r, u, -0.48122354789588401);
+    r = fma_k(r, u, 0.30783718216692846);
+    return r;
 }
 
-__device__ __forceinline__ double ncdf(double a) {
-    const double y = 0.5 * erfc(fabs(a) * 0.70710678118654752440);
-    return (a > 0.0) ? 1.0 - y : y;
+// |d| clamped to the range of the fit, and its phi
+__device__ __forceinline__ double tail_arg(double d) {
+    const double a = fabs(d);
+    return a < kMillsMax ? a : kMillsMax;                // NaN -> kMillsMax (the price is NaN anyway)
+}
+__device__ __forceinline__ double phi_of(double a) { return exp_k(-0.5 * (a * a)) * kInvSqrt2Pi; }
+
+// N(d) and N(-d) from the tail q = Q(|d|)
+__device__ __forceinline__ void ncdf_from_tail(double d, double q, double* pos, double* neg) {
+    const bool p = d > 0.0;
+    *pos = p ? 1.0 - q : q;
+    *neg = p ? q : 1.0 - q;
 }
 
+// One book option (branch-free in the lane-varying quantities: remaining steps, running max).
 __device__ __forceinline__ double book_option(const Params& p, const BookOpt& o, const BookEnv& b, int32_t m,
                                               double runmax) {
-    if (o.type == HE_BOOK_UO_CALL && runmax >= o.H) return 0.0;
     const double K = o.K, S = b.S, r = p.r_d;
-    if (m <= 0 || b.sig <= 0.0) {   // tau = m dt <= 0
-        const double ic = S - K, ip = K - S;
-        if (o.type == HE_BOOK_PUT) return (ip < 0.0) ? 0.0 : ip;
-        return (ic < 0.0) ? 0.0 : ic;
-    }
-    if (o.type == HE_BOOK_UO_CALL && o.H <= K) return 0.0;
-    const double tau = (double)m * p.dt;
-    const double* e = p.book_tab + 3 * m;
+    const bool live = m > 0 && b.sig > 0.0;             // tau = m dt > 0 (else intrinsic)
+    const int32_t mc = live ? m : 1;                    // a valid table row either way
+    const double tau = (double)mc * p.dt;
+    const double* e = p.book_tab + 4 * mc;
     const double sst = b.sig * e[0];
     const double isst = b.isig * e[1];
     const double d1 = ((b.lnS - o.lnK) + (r + 0.5 * b.s2) * tau) * isst;
     const double d2 = d1 - sst;
     const double Kd = K * e[2];
+    const double SoKd = S * (o.invK * e[3]);            // S / (K e^{-r tau}) = phi(d2) / phi(d1)
+    const double a1 = tail_arg(d1), a2 = tail_arg(d2);
+    const double ph1 = phi_of(a1);
+    const double q1 = ph1 * mills(a1), q2 = (ph1 * SoKd) * mills(a2);
     double n1, m1, n2, m2;
-    ncdf_pair(d1, &n1, &m1);
-    ncdf_pair(d2, &n2, &m2);
+    ncdf_from_tail(d1, q1, &n1, &m1);
+    ncdf_from_tail(d2, q2, &n2, &m2);
     double v;
-    if (o.type == HE_BOOK_PUT) {
+    if (o.type == HE_BOOK_PUT) {                         // o.type: uniform over the wave
         v = Kd * m2 - S * m1;
+        const double ip = K - S;
+        v = live ? v : ((ip < 0.0) ? 0.0 : ip);
     } else {
         v = S * n1 - Kd * n2;
         if (o.type == HE_BOOK_UO_CALL) {
+            // c_uo = c - c_ui (Hull); the tails of x1 - sst, y - sst, y1 - sst from those of
+            // x1, y, y1 (phi(x - sst) = phi(x) exp(x sst - sst^2 / 2))
             const double ls = b.lam * sst;
             const double lhs = o.lnH - b.lnS;                    // log(H / S)
             const double x1 = -lhs * isst + ls;                  // log(S / H) / sst + lam sst
             const double y = (o.lnH2K - b.lnS) * isst + ls;      // log(H^2 / (S K)) / sst + lam sst
             const double y1 = lhs * isst + ls;
-            const double p2l = exp((2.0 * b.lam) * lhs);          // (H/S)^(2 lam)
-            const double p2l2 = exp((2.0 * b.lam - 2.0) * lhs);   // (H/S)^(2 lam - 2)
-            const double cui = S * ncdf(x1) - Kd * ncdf(x1 - sst) - S * p2l * (ncdf(-y) - ncdf(-y1)) +
-                               Kd * p2l2 * (ncdf(-y + sst) - ncdf(-y1 + sst));
+            const double ert = e[3];                             // e^{r tau}
+            const double ax = tail_arg(x1), ay = tail_arg(y), ay1 = tail_arg(y1);
+            const double px = phi_of(ax), py = phi_of(ay), py1 = phi_of(ay1);
+            const double sh = exp_k(-lhs);                       // S / H
+            const double hs = exp_k(lhs);                        // H / S
+            const double ax_ = tail_arg(x1 - sst), ay_ = tail_arg(y - sst), ay1_ = tail_arg(y1 - sst);
+            const double qx = px * mills(ax), qx_ = (px * (sh * ert)) * mills(ax_);
+            const double qy = py * mills(ay), qy_ = (py * ((hs * hs) * (S * o.invK) * ert)) * mills(ay_);
+            const double qy1 = py1 * mills(ay1), qy1_ = (py1 * (hs * ert)) * mills(ay1_);
+            double nx, mx, nx_, mx_, ny, my, ny_, my_, ny1, my1, ny1_, my1_;
+            ncdf_from_tail(x1, qx, &nx, &mx);
+            ncdf_from_tail(x1 - sst, qx_, &nx_, &mx_);
+            ncdf_from_tail(y, qy, &ny, &my);
+            ncdf_from_tail(y - sst, qy_, &ny_, &my_);
+            ncdf_from_tail(y1, qy1, &ny1, &my1);
+            ncdf_from_tail(y1 - sst, qy1_, &ny1_, &my1_);
+            const double p2l = exp_k((2.0 * b.lam) * lhs);       // (H/S)^(2 lam)
+            const double p2l2 = p2l * (sh * sh);                 // (H/S)^(2 lam - 2)
+            const double cui = S * nx - Kd * nx_ - S * p2l * (my - my1) + Kd * p2l2 * (my_ - my1_);
             v = v - cui;
+            v = (runmax >= o.H || o.H <= K) ? 0.0 : v;          // knocked out / worthless
         }
+        const double ic = S - K;
+        v = live ? v : ((ic < 0.0) ? 0.0 : ic);
+        if (o.type == HE_BOOK_UO_CALL) v = (runmax >= o.H) ? 0.0 : v;
     }
     return (v < 0.0) ? 0.0 : v;   // python max(price, 0)
 }
@@ -1501,31 +1565,47 @@ __global__ __launch_bounds__(kBlock, HE_FUSED_WAVES) void step_market_kernel(Par
 #ifndef HE_LDS_PRIO_PROD
 #define HE_LDS_PRIO_PROD 1
 #endif
+#ifndef HE_LDS_LANES_BOOK
+#define HE_LDS_LANES_BOOK 4  // a liability book: its marks are most of the producers' work
+#endif
 constexpr int kLdsEnvs = 64;                         // envs per workgroup = one stepper wave
-constexpr int kLdsLanes = HE_LDS_LANES;              // producer lanes per env
-constexpr int kLdsProd = kLdsLanes;                  // producer waves (64 / kLdsLanes envs each)
-constexpr int kLdsPEnvs = kLdsEnvs / kLdsLanes;      // envs per producer wave
-constexpr int kLdsThreads = 64 * (2 + kLdsProd);     // + the reward and the obs stepper waves
 constexpr int kLdsM = HE_LDS_M;                      // slots per LDS market block
-constexpr int kLdsH = kLdsM / kLdsLanes;             // consecutive slots per producer lane
-static_assert(kLdsH * kLdsLanes == kLdsM && kLdsPEnvs * kLdsLanes == kLdsEnvs, "producer lane layout");
 constexpr int kLdsPrefetch = kLdsM % 6 == 0 ? 6 : (kLdsM % 4 == 0 ? 4 : kLdsM);  // steps of actions in flight
 static_assert(kLdsM % kLdsPrefetch == 0, "the action ring index is the slot mod D");
-// min waves per SIMD: 4 workgroups per CU need 4 (2 + kLdsProd) / 4 per SIMD if the hardware
-// spreads every workgroup evenly; one more leaves room for an uneven placement
-#ifndef HE_LDS_MINWAVES
-#define HE_LDS_MINWAVES ((4 * (2 + kLdsProd) + 3) / 4 + 1)
+
+// Workgroup geometry of one market configuration: `lanes` producer lanes per env in
+// `lanes` producer waves (64 / lanes envs each), each lane making H consecutive slots.
+// min waves per SIMD (GBM): 4 workgroups per CU need 4 (2 + prod) / 4 per SIMD if the
+// hardware spreads every workgroup evenly; one more leaves room for an uneven placement.
+// With a book the kernel is VALU-bound: 128 VGPRs (4 waves per SIMD) for the marks.
+template <int MODE, bool BOOK>
+struct LdsGeom {
+    static constexpr bool HESTON = MODE == HE_MODE_HESTON;
+    static constexpr int lanes = BOOK ? HE_LDS_LANES_BOOK : HE_LDS_LANES;
+    static constexpr int prod = lanes;
+    static constexpr int penvs = kLdsEnvs / lanes;
+    static constexpr int threads = 64 * (2 + prod);  // + the reward and the obs stepper waves
+    static constexpr int H = kLdsM / lanes;
+#ifdef HE_LDS_MINWAVES
+    static constexpr int minwaves = BOOK ? 4 : HE_LDS_MINWAVES;
+#else
+    static constexpr int minwaves = BOOK ? 4 : (4 * (2 + prod) + 3) / 4 + 1;
 #endif
-constexpr int kLdsMinWaves = HE_LDS_MINWAVES;
+    static_assert(H * lanes == kLdsM && penvs * lanes == kLdsEnvs, "producer lane layout");
+};
+
 // LDS: the market records, double-buffered by block, [slot][env]: {S, C} pairs and P
-// (12 B per env-slot, conflict-free lane accesses), and the obs wave's two row staging
-// tiles: 18.9 KB at M = 8, so all 65,536 envs of BASELINE configs[1] resident at once.
-struct LdsMarket {
+// (12 B per env-slot, conflict-free lane accesses), the obs wave's two row staging
+// tiles, and with a book its f64 value per slot: 19.7 KB at M = 8 (GBM), so all 65,536
+// envs of BASELINE configs[1] are resident at once; 27.9 KB with a book.
+template <int MODE, bool BOOK>
+struct LdsMarketT {
     float2 sc[2][kLdsM][kLdsEnvs];
     float pp[2][kLdsM][kLdsEnvs];
-    float stage[2][kLdsEnvs * kObs];  // the obs wave's row staging, by step parity
+    float stage[2][kLdsEnvs * kObs];                                   // obs row staging, by step parity
+    double bk[BOOK ? 2 : 1][BOOK ? kLdsM : 1][kLdsEnvs];                // book value of every slot
 };
-static_assert(sizeof(LdsMarket) <= 40 * 1024, "4 workgroups per CU");
+static_assert(sizeof(LdsMarketT<HE_MODE_GBM, false>) <= 40 * 1024, "4 workgroups per CU");
 
 #ifdef HE_LDS_TIMING
 // Diagnostic builds only: per wave role (0 reward, 1 obs, 2-3 producers) and workgroup,
@@ -1581,9 +1661,9 @@ __device__ __forceinline__ void flush_obs_full(const float* img, float* out, int
 // different outstanding memory ops.  (A copy of a pending load's register at a merge,
 // e.g. the action ring at a loop back-edge behind a `break`, costs an s_waitcnt
 // vmcnt(0): every store of the wave drained.)  A partial last block takes a generic loop.
-template <bool LEAN, bool OBS>
+template <int MODE, bool BOOK, bool LEAN, bool OBS>
 __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& io, int k_steps, const Market& cur,
-                                            LdsMarket& L, int64_t base) {
+                                            LdsMarketT<MODE, BOOK>& L, int64_t base) {
     constexpr int D = kLdsPrefetch;
     const int lane = threadIdx.x & 63;
     const int64_t N = p.n;
@@ -1592,7 +1672,7 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
     const int64_t i0 = base + lane;
     const int64_t i = i0 < N ? i0 : N - 1;      // lanes past N mirror env N-1
     const int wrows = (int)((N - base) < kLdsEnvs ? (N - base) : kLdsEnvs);
-    const Mkt rst{p.rstv[0], p.rstv[1], p.rstv[2], p.rstv[3], 0.0};
+    const Mkt rst{p.rstv[0], p.rstv[1], p.rstv[2], p.rstv[3], BOOK ? p.book_rst : 0.0};
     const GLOBAL v2f* gact = (const GLOBAL v2f*)io.act;
     GLOBAL float* const grew = (GLOBAL float*)io.rew;
     GLOBAL uint8_t* const gterm = (GLOBAL uint8_t*)io.term;
@@ -1614,8 +1694,13 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
         if (!OBS) {
             e.cash = s.cash[i];
             // the market the env stands at: the block-start record of market_body (f32 S)
-            if (t0 != 0) pre = Mkt{(float)cur.S[i], p.var_f, cur.C[i], cur.P[i], 0.0};
-            pv_last = portfolio_value<false>(p, e, pre);
+            if (t0 != 0) {
+                const double Sc = cur.S[i];
+                // the book at the block start: market_body's slot 0 (same function, operands)
+                const double Bc = BOOK ? book_value(p, Sc, p.var, (int32_t)t0, cur.M[i]) : 0.0;
+                pre = Mkt{(float)Sc, p.var_f, cur.C[i], cur.P[i], Bc};
+            }
+            pv_last = portfolio_value<BOOK>(p, e, pre);
         }
     }
     // the reward wave's episode summaries {return, sum pnl, sum cost, length} of the last
@@ -1743,8 +1828,10 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
             const double shares_d = p.shares_d, inv_shares = p.inv_shares, den = p.den, inv_den = p.inv_den;
             const double inv_252 = p.inv_252, init_cash = p.initial_cash;
             const float shares_f = p.shares_f;
-            // step_env's PV0 (:167-168): f32, of the reset market -- one constant here
-            const double pv0 = (double)((shares_f * rst.S + 0.0f) + p.init_cash_f);
+            // step_env's PV0 (:167-168): f32, of the reset market -- one constant here (+ the
+            // reset market's book)
+            double pv0 = (double)((shares_f * rst.S + 0.0f) + p.init_cash_f);
+            if (BOOK) pv0 = pv0 + rst.B;
             run([&](int buf, int sl, int k, float2 ak) {
                 const int64_t koff = (int64_t)k * N;
                 const float2 sc = L.sc[buf][sl][lane];
@@ -1767,7 +1854,8 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
                 const uint32_t t1 = e.t + 1;
                 const bool term = (int32_t)t1 >= T;
                 const double optv = ((double)cc * (double)sc.y) * 100.0 + ((double)qq * (double)pP) * 100.0;
-                const double pv = ((double)(shares_f * sc.x) + optv) + cash;
+                double pv = ((double)(shares_f * sc.x) + optv) + cash;
+                if (BOOK) pv = pv + L.bk[buf][sl][lane];  // liability book (extension): after cash
                 const double pnl = pv - pv_prev;
                 const double ps = div_by_nb(pnl, shares_d, inv_shares);
                 // (vii) reward (:243-262)
@@ -1793,7 +1881,7 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
         auto step = [&](int buf, int sl, int k, float2 ak) {
             const int64_t koff = (int64_t)k * N;
             const float2 sc = L.sc[buf][sl][lane];
-            const Mkt post{sc.x, p.var_f, sc.y, L.pp[buf][sl][lane], 0.0};
+            const Mkt post{sc.x, p.var_f, sc.y, L.pp[buf][sl][lane], BOOK ? L.bk[buf][sl][lane] : 0.0};
             if (OBS) {
                 float4 g = p.record_metrics ? greeks_fast<true>(p, post.S, p.var_f) : make_float4(0.f, 0.f, 0.f, 0.f);
                 g.w = lag_return(post.S, pre.S);
@@ -1814,7 +1902,7 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
                 if (term) env_reset_common(p, e);
             } else {
                 StepOut so;
-                step_env<false, false>(p, e, pre, post, ak.x, ak.y, pv_last, so);
+                step_env<BOOK, false>(p, e, pre, post, ak.x, ak.y, pv_last, so);
                 pv_last = so.pv;
                 if (grew) grew[koff + i] = (float)so.reward;
                 if (gterm) gterm[koff + i] = so.term ? 1 : 0;
@@ -1848,8 +1936,11 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
 // Producer waves: block bp of 64 envs into LDS buffer bp & 1 while the steppers consume
 // block bp - 1.  pw = producer wave index (kLdsPEnvs envs each).  Lanes past the last
 // env mirror env N-1 like the steppers' (identical values, identical addresses).
-__device__ __forceinline__ void lds_producer(const Params& p, int k_steps, const Market& cur, LdsMarket& W,
-                                             int64_t base, int pw) {
+template <int MODE, bool BOOK>
+__device__ __forceinline__ void lds_producer(const Params& p, int k_steps, const Market& cur,
+                                             LdsMarketT<MODE, BOOK>& W, int64_t base, int pw) {
+    using G = LdsGeom<MODE, BOOK>;
+    constexpr int kLdsLanes = G::lanes, kLdsPEnvs = G::penvs, kLdsH = G::H;
     const int lane = threadIdx.x & 63;
     const int sub = lane / kLdsPEnvs;
     const int le = pw * kLdsPEnvs + (lane % kLdsPEnvs);  // local env of this lane
@@ -1862,6 +1953,7 @@ __device__ __forceinline__ void lds_producer(const Params& p, int k_steps, const
     const uint32_t ep0 = cur.ep[pi];
     const uint32_t t0 = cur.t[pi];
     double Sbs = cur.S[pi];                          // f64 price before slot 0 of block bp
+    double Mbs = BOOK ? cur.M[pi] : 0.0;             // book: running max of S before it
     const uint32_t off = t0 >= T ? T : t0;           // a0 = ep T + t (t = T: the next episode)
     const uint64_t a0 = (uint64_t)ep0 * T + off;     // env-step index of the launch's first step
     uint32_t tpb = off >= T ? 0u : off;              // episode step before slot 0 of block bp
@@ -1921,26 +2013,37 @@ __device__ __forceinline__ void lds_producer(const Params& p, int k_steps, const
             for (int r = 0; r < kLdsLanes; ++r)
 #pragma unroll
                 for (int h = 0; h < kLdsH; ++h) eall[r * kLdsH + h] = __shfl(ex[h], (lane % kLdsPEnvs) + r * kLdsPEnvs);
-            double Sx[kLdsH];
+            double Sx[kLdsH], Mx[kLdsH];
 #pragma unroll
             for (int h = 0; h < kLdsH; ++h) Sx[h] = Sbs;
-            double S = Sbs, Sin = Sbs;
+#pragma unroll
+            for (int h = 0; h < kLdsH; ++h) Mx[h] = Mbs;
+            double S = Sbs, Sin = Sbs, Mr = Mbs;
             {
                 uint32_t tp = tpb;
 #pragma unroll
                 for (int j = 0; j < kLdsM; ++j) {
                     if (j == sl0) Sin = S;
                     if (j < len) {
-                        if (tp == 0) S = p.s0;  // autoreset: a new episode starts from S0
+                        if (tp == 0) {  // autoreset: a new episode starts from S0
+                            S = p.s0;
+                            if (BOOK) Mr = p.s0;
+                        }
                         const double Sn = S * eall[j];
                         S = (Sn < 1e-8) ? 1e-8 : Sn;  // np.maximum(., 1e-8), NaN kept
+                        if (BOOK) Mr = np_max(Mr, S);   // market_body's barrier monitor
                         tp = (tp + 1 == T) ? 0u : tp + 1;
                     }
 #pragma unroll
                     for (int h = 0; h < kLdsH; ++h) Sx[h] = (j == sl0 + h) ? S : Sx[h];
+                    if (BOOK) {
+#pragma unroll
+                        for (int h = 0; h < kLdsH; ++h) Mx[h] = (j == sl0 + h) ? Mr : Mx[h];
+                    }
                 }
             }
             Sbs = S;  // price after the block (every lane ran the whole chain)
+            if (BOOK) Mbs = Mr;
             // (3) marks + obs greeks of every slot; the terminal step replays the marks of
             // the position before it (hedging_env_v2.py:229-231)
             uint32_t tp = tpf;
@@ -1960,6 +2063,9 @@ __device__ __forceinline__ void lds_producer(const Params& p, int k_steps, const
                     const int sl = sl0 + h;
                     W.sc[wb][sl][le] = make_float2((float)Sx[h], C);
                     W.pp[wb][sl][le] = P;
+                    // the book after the step into slot sl (episode step tp + 1, the new S,
+                    // not lagged): market_body's tileC
+                    if (BOOK) W.bk[wb][sl][le] = book_value(p, Sx[h], p.var, (int32_t)(tp + 1), Mx[h]);
                     if (kb + sl == k_steps - 1) {  // the market position after the launch
                         const uint32_t q = off + (uint32_t)(k_steps - 1);
                         cur.ep[pi] = ep0 + q / T;
@@ -1967,6 +2073,7 @@ __device__ __forceinline__ void lds_producer(const Params& p, int k_steps, const
                         cur.S[pi] = Sx[h];
                         cur.C[pi] = C;
                         cur.P[pi] = P;
+                        if (BOOK) cur.M[pi] = Mx[h];
                     }
                     tp = (tp + 1 == T) ? 0u : tp + 1;
                 }
@@ -1984,16 +2091,17 @@ __device__ __forceinline__ void lds_producer(const Params& p, int k_steps, const
 // fewer than the occupancy API and the compiler report (MI355X_MICROARCH.md, Residency),
 // and at 106 the 4 x 6 waves of 4 workgroups no longer fit a CU -- at 65,536 envs the
 // launch ran in two rounds of workgroups (536 vs ~270 us).  The spills go to VGPR lanes.
-template <bool LEAN>
-__global__ __launch_bounds__(kLdsThreads, kLdsMinWaves) __attribute__((amdgpu_num_sgpr(96))) void lds_rollout_kernel(
-    const Params* __restrict__ pc, State s, Io io, int k_steps, Market cur) {
-    __shared__ __attribute__((aligned(16))) LdsMarket lm;
+template <int MODE, bool BOOK, bool LEAN>
+__global__ __launch_bounds__((LdsGeom<MODE, BOOK>::threads), (LdsGeom<MODE, BOOK>::minwaves))
+    __attribute__((amdgpu_num_sgpr(96))) void lds_rollout_kernel(const Params* __restrict__ pc, State s, Io io,
+                                                                 int k_steps, Market cur) {
+    __shared__ __attribute__((aligned(16))) LdsMarketT<MODE, BOOK> lm;
     const Params& p = *pc;  // read through the scalar cache (a by-value copy spills)
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int64_t base = (int64_t)blockIdx.x * kLdsEnvs;
-    if (wave == 0) lds_stepper<LEAN, false>(p, s, io, k_steps, cur, lm, base);
-    else if (wave == 1) lds_stepper<LEAN, true>(p, s, io, k_steps, cur, lm, base);
-    else lds_producer(p, k_steps, cur, lm, base, wave - 2);
+    if (wave == 0) lds_stepper<MODE, BOOK, LEAN, false>(p, s, io, k_steps, cur, lm, base);
+    else if (wave == 1) lds_stepper<MODE, BOOK, LEAN, true>(p, s, io, k_steps, cur, lm, base);
+    else lds_producer<MODE, BOOK>(p, k_steps, cur, lm, base, wave - 2);
 }
 
 // Test hooks (he_device_rng / he_device_math): the device build of the generate-mode
@@ -2612,7 +2720,7 @@ static bool lds_lean_config(const he_env* env, const Io& io) {
 // rewinds it, a no-op after an LDS rollout.  Afterwards `cur` is exact again and the
 // tiles are invalid (the next he_step regenerates its block from `cur`).
 static bool lds_rollout_eligible(const he_env* env) {
-    return env->lds_rollout && env->cfg.mode == HE_MODE_GBM && env->cfg.book_size == 0;
+    return env->lds_rollout && env->cfg.mode == HE_MODE_GBM;
 }
 
 static he_status launch_lds_rollout(he_env* env, const Io& io, int k_total, hipStream_t st) {
@@ -2620,16 +2728,23 @@ static he_status launch_lds_rollout(he_env* env, const Io& io, int k_total, hipS
     if (s != HE_OK) return s;
     const int64_t blocks = (env->cfg.n_envs + kLdsEnvs - 1) / kLdsEnvs;
     const Params* pc = env->dparams;  // buffer 0's copy: the tile pointers are not used
-    void (*kern)(const Params*, State, Io, int, Market) =
-        lds_lean_config(env, io) ? lds_rollout_kernel<true> : lds_rollout_kernel<false>;
+    const bool book = env->cfg.book_size > 0, lean = lds_lean_config(env, io);
+    void (*kern)(const Params*, State, Io, int, Market);
+    int threads;
+    if (book) {
+        kern = lean ? lds_rollout_kernel<HE_MODE_GBM, true, true> : lds_rollout_kernel<HE_MODE_GBM, true, false>;
+        threads = LdsGeom<HE_MODE_GBM, true>::threads;
+    } else {
+        kern = lean ? lds_rollout_kernel<HE_MODE_GBM, false, true> : lds_rollout_kernel<HE_MODE_GBM, false, false>;
+        threads = LdsGeom<HE_MODE_GBM, false>::threads;
+    }
     if (env->ev_start) {  // one-shot: bracket exactly this dispatch
         hipEvent_t a = (hipEvent_t)env->ev_start, b = (hipEvent_t)env->ev_stop;
         env->ev_start = env->ev_stop = nullptr;
-        hipExtLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kLdsThreads), 0, st, a, b, 0, pc, env->s, io,
-                              k_total, env->cur);
+        hipExtLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(threads), 0, st, a, b, 0, pc, env->s, io, k_total,
+                              env->cur);
     } else {
-        hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kLdsThreads), 0, st, pc, env->s, io, k_total,
-                           env->cur);
+        hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(threads), 0, st, pc, env->s, io, k_total, env->cur);
     }
     HE_HIP(env, hipGetLastError());
     env->block_pos = env->cfg.market_block;
@@ -2872,12 +2987,13 @@ he_status he_create(const he_config* cfg, he_env** out) {
             hb[k].lnK = log(hb[k].K);
             hb[k].lnH = log(hb[k].H);
             hb[k].lnH2K = 2.0 * hb[k].lnH - hb[k].lnK;
+            hb[k].invK = 1.0 / hb[k].K;
         }
         HE_HIP(env, hipMalloc(&env->dbook, HE_BOOK_MAX * sizeof(BookOpt)));
         HE_HIP(env, hipMemcpy(env->dbook, hb, c.book_size * sizeof(BookOpt), hipMemcpyHostToDevice));
         int32_t max_exp = 1;
         for (int k = 0; k < c.book_size; ++k) max_exp = (c.book[k].expiry > max_exp) ? c.book[k].expiry : max_exp;
-        HE_HIP(env, hipMalloc(&env->dbook_tab, (size_t)3 * (size_t)(max_exp + 1) * sizeof(double)));
+        HE_HIP(env, hipMalloc(&env->dbook_tab, (size_t)4 * (size_t)(max_exp + 1) * sizeof(double)));
         hipLaunchKernelGGL(book_tab_kernel, dim3((unsigned)((max_exp + 256) / 256)), dim3(256), 0, 0, env->dbook_tab,
                            max_exp + 1, c.dt, c.risk_free_rate);
         HE_HIP(env, hipGetLastError());

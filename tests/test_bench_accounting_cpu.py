@@ -83,6 +83,6 @@ def test_tile_path_reports_the_market_tile_as_overhead(bench, monkeypatch):
 def test_lds_path_selection(bench, monkeypatch):
     monkeypatch.delenv("HE_LDS_ROLLOUT", raising=False)
     assert bench.lds_rollout(bench.CONFIGS[2]) and bench.lds_rollout(bench.CONFIGS[3])
-    assert not bench.lds_rollout(bench.CONFIGS[4]) and not bench.lds_rollout(bench.CONFIGS[5])
+    assert bench.lds_rollout(bench.CONFIGS[4]) and not bench.lds_rollout(bench.CONFIGS[5])  # GBM + book; Heston
     monkeypatch.setenv("HE_LDS_ROLLOUT", "0")
     assert not bench.lds_rollout(bench.CONFIGS[2])

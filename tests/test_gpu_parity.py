@@ -200,7 +200,7 @@ def test_set_state_into_a_stepped_env(path, monkeypatch):
     next block generated, the side stream a pending prefetch) drops those blocks: the
     restored env replays exactly what followed the checkpoint, by rollouts and by steps."""
     from cantorrl_amd.vec_env import HedgingVecEnv
-    monkeypatch.setenv("HE_LDS_ROLLOUT", "1" if path == "lds" else "0")
+    monkeypatch.setenv("HE_LDS_ROLLOUT", "0" if path.endswith("tile") else "1")
     monkeypatch.setenv("HE_FUSED_MARKET", "0" if path == "side" else "1")
     n, K = 500, 40
     acts = torch.rand((3 * K, n, 2), device="cuda") * 2.2 - 1.1
@@ -515,6 +515,15 @@ LDS_CASES = {
     "T2_mse_nometrics": (64, dict(episode_length=2, s0=101.25, variance=0.09), dict(loss_type="mse", record_metrics=False,
                                                                                     initial_cash=1000.0), (9, 24)),
     "long_K": (3000, dict(), dict(slippage_bps=5.0), (300, 257)),
+    # liability books (extension): the producers mark the book per slot into LDS
+    "book8": (1000, dict(episode_length=40, book=BOOK8), dict(loss_type="abs", pnl_penalty_weight=0.001,
+                                                             lambda_cost=0.0001, theta_weight=0.0002,
+                                                             slippage_bps=1.0), (64, 37, 100, 9)),
+    "book_barrier_ragged": (333, dict(episode_length=29, book=[dict(type="uo_call", strike=496.0, barrier=520.0,
+                                                                     expiry=40, quantity=-50.0),
+                                                                dict(type="put", strike=480.0, expiry=20,
+                                                                     quantity=-10.0)]),
+                            dict(loss_type="mse", record_metrics=False), (5, 64, 13, 71)),
 }
 
 
@@ -595,7 +604,7 @@ def test_full_size_slice_matches_oracle(config):
     venv.close()
 
 
-@pytest.mark.parametrize("path", ["lds", "tile", "book"])
+@pytest.mark.parametrize("path", ["lds", "tile", "book", "book_tile"])
 def test_episode_summaries_match_oracle(path, monkeypatch):
     """he_episode_summaries (the per-env payload ranks all-gather): the
     {return, sum of step P&L, sum of transaction costs, length} of each env's last finished
@@ -604,11 +613,11 @@ def test_episode_summaries_match_oracle(path, monkeypatch):
     LDS rollout, the tile rollout and the tile rollout with a liability book, over rollout
     calls that split episodes, with he_reset restarting the running sums."""
     from cantorrl_amd.vec_env import HedgingVecEnv
-    monkeypatch.setenv("HE_LDS_ROLLOUT", "1" if path == "lds" else "0")
+    monkeypatch.setenv("HE_LDS_ROLLOUT", "0" if path.endswith("tile") else "1")
     n, T, seed = 300, 23, 5
     cfg = dict(loss_type="abs", pnl_penalty_weight=0.001, lambda_cost=0.0001, theta_weight=0.0002, slippage_bps=1.0)
     gen = dict(s0=496.48001098632812, variance=0.029028, mu=0.04, dt=1 / 252, episode_length=T)
-    if path == "book":
+    if path.startswith("book"):
         gen["book"] = BOOK8
     rng = np.random.default_rng(seed)
     ks = (64, 9, 40, 100)

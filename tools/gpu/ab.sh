@@ -5,7 +5,7 @@
 set -o pipefail
 TAG=${1:-ab}
 R=$GRAFT_REPO_ROOT; cd $R; O=gpurun_out/$TAG; mkdir -p $O; export TMPDIR=/tmp
-for c in ${CFGS:-2 3}; do
+for c in ${CFGS:-2 3 4}; do
   for l in default tools/ab/*.so; do
     b=$(basename $l .so)
     if [ "$l" = default ]; then unset CANTORRL_HEDGEENV_LIB; else export CANTORRL_HEDGEENV_LIB=$R/$l; fi

@@ -1,11 +1,18 @@
 #!/bin/bash
-# book path: GPU parity (book + policy tests), then bench configs 4 and 5
+# Configs 4/5 (liability book): kernel timeline (rocprofv3 --kernel-trace) of the bench and
+# the PMC instruction mix of market_kernel / step_kernel.
+#   gpurun --timeout 900 -- bash tools/gpu/book.sh <tag> [configs]
 set -o pipefail
-TAG=${1:-book}
-cd $GRAFT_REPO_ROOT; O=gpurun_out/$TAG; mkdir -p $O; export TMPDIR=/tmp
-timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
-tail -1 $O/pytest.log
-for c in 4 5; do
-  timeout -k 10 300 python -u bench.py --config $c --no-cpu-baseline --no-step-api --no-pmc > $O/b_cfg$c.log 2>&1 || { tail -20 $O/b_cfg$c.log; exit 1; }
-  grep "^{" $O/b_cfg$c.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); r=d['roofline']; print(d['config']['config_index'], '%.3g'%d['value'], r['kernel_us'], r['frac'], r['market_kernel_us_per_64_steps'])"
+TAG=${1:-book}; CFGS=${2:-4 5}
+R=$GRAFT_REPO_ROOT; cd $R; O=$R/gpurun_out/$TAG; mkdir -p $O; export TMPDIR=/tmp
+for c in $CFGS; do
+  echo "[$(date +%T)] config $c timeline"
+  cd /tmp
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/tl$c -o run -- python3 $R/bench.py --config $c --no-pmc --no-cpu-baseline --no-step-api --steps 512 --warmup 128 > $O/tl$c.log 2>&1 || { tail -20 $O/tl$c.log; exit 1; }
+  cd $R
+  grep "^{" $O/tl$c.log
+  python3 tools/timeline.py $O/tl$c
+  echo "[$(date +%T)] config $c pmc"
+  timeout -k 10 400 bash tools/gpu/pmc.sh $TAG/pmc$c --config $c > $O/pmc$c.log 2>&1 || { tail -20 $O/pmc$c.log; exit 1; }
+  cat $O/pmc$c.log
 done
