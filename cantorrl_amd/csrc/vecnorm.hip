@@ -5,15 +5,20 @@
 // gamma) (train_ppo_v2.py:204,305) and evaluates with the stats frozen (:450-453); every
 // env is wrapped in Monitor(info_keywords=...) (:119).  On the host that is a NumPy
 // pass over [N, 13] per step plus per-env Python lists -- the bottleneck once N is in
-// the tens of thousands.  Here one step is two launches:
-//   moments_kernel  per block: exact two-pass f64 mean / M2 of the obs columns and of
-//                   the updated running returns; the last block to finish (atomic
-//                   ticket) merges the blocks in block order (Chan et al.) and applies
-//                   RunningMeanStd.update_from_moments -- deterministic for a given grid
-//   apply_kernel    obs / reward / terminal-obs normalization, returns[done] = 0 and
-//                   the Monitor episode sums; one thread per env row
-// HBM-bound and tiny (68 B of obs + reward read and written per env); the point is to
-// keep the statistics on the device, not the arithmetic.
+// the tens of thousands.  Here one step is ONE launch of vecnorm_kernel, one workgroup
+// per CU at most (G <= 256 workgroups, every one resident):
+//   1. per workgroup: exact two-pass f64 mean / M2 of its rows' obs columns and of the
+//      updated running returns, written as a partial;
+//   2. the last workgroup to arrive (atomic ticket) merges the G partials in workgroup
+//      order (Chan et al.; sums as block reductions), applies
+//      RunningMeanStd.update_from_moments and releases the others (a generation flag);
+//   3. every workgroup normalizes its rows with the new statistics: obs / reward /
+//      terminal obs, returns[done] = 0 and the Monitor episode sums.
+// Deterministic for a given grid.  The waits are bounded (a spin that never sees the
+// flag gives up and leaves the outputs unwritten, reported by the next he_vecnorm_step
+// check) so a fault can never hang the device.  Eval mode (no statistics update) skips
+// 1-2.  HBM-bound and tiny (68 B of obs + reward read and written per env): the point is
+// to keep the statistics on the device within one launch, not the arithmetic.
 
 #include <hip/hip_runtime.h>
 
@@ -26,7 +31,7 @@ namespace {
 
 constexpr int kD = HE_OBS_DIM;
 constexpr int kVnThreads = 256;
-constexpr int kVnMaxBlocks = 64;    // the last block stages all partials in LDS and merges them serially
+constexpr int kVnMaxBlocks = 256;   // workgroups of one launch: all resident (one per CU at most)
 
 // scratch layout: [blocks][kPart] doubles, then one u32 ticket
 constexpr int kPart = 2 * kD + 3;   // count, mean[D], M2[D], ret_mean, ret_M2
@@ -55,29 +60,6 @@ struct VnArgs {
     int reset;   // he_vecnorm_reset: returns = 0 instead of the discounted update
 };
 
-// Sum of s[0..kD] over the block into out[0..kD] (LDS): a wave-level butterfly per
-// column, then one barrier and a 4-way sum -- two barriers for all 14 columns.
-__device__ __forceinline__ void block_sum_cols(double* s, double (*sh)[kD + 1], double* out) {
-#pragma unroll
-    for (int c = 0; c <= kD; ++c) {
-#pragma unroll
-        for (int m = 32; m >= 1; m >>= 1) s[c] += __shfl_xor(s[c], m, 64);
-    }
-    const int w = threadIdx.x >> 6;
-    if ((threadIdx.x & 63) == 0) {
-#pragma unroll
-        for (int c = 0; c <= kD; ++c) sh[w][c] = s[c];
-    }
-    __syncthreads();
-    if (threadIdx.x <= kD) {
-        double t = 0.0;
-#pragma unroll
-        for (int i = 0; i < kVnThreads / 64; ++i) t += sh[i][threadIdx.x];
-        out[threadIdx.x] = t;
-    }
-    __syncthreads();
-}
-
 // RunningMeanStd.update_from_moments (SB3 common/running_mean_std.py), f64
 __device__ __forceinline__ void rms_update(double* mean, double* var, double* count, double bmean, double bvar,
                                            double bcount) {
@@ -92,179 +74,224 @@ __device__ __forceinline__ void rms_update(double* mean, double* var, double* co
     *count = tot;
 }
 
-__global__ void __launch_bounds__(kVnThreads) moments_kernel(VnArgs a) {
-    __shared__ double sh[kVnThreads / 64][kD + 1];
-    __shared__ double smean[kD + 1];
-    __shared__ double sm2[kD + 1];
-    __shared__ bool last;
+__device__ __forceinline__ double clipd(double x, double lo, double hi) { return x < lo ? lo : (x > hi ? hi : x); }
+
+// Sum of v[0..NV) over the block into out[0..NV) (LDS): a wave-level butterfly per
+// value, then one barrier and a 4-way sum -- two barriers for all NV values.
+template <int NV>
+__device__ __forceinline__ void block_sum(double* v, double (*sh)[NV], double* out) {
+#pragma unroll
+    for (int c = 0; c < NV; ++c) {
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) v[c] += __shfl_xor(v[c], m, 64);
+    }
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+        for (int c = 0; c < NV; ++c) sh[w][c] = v[c];
+    }
+    __syncthreads();
+    if (threadIdx.x < NV) {
+        double t = 0.0;
+#pragma unroll
+        for (int i = 0; i < kVnThreads / 64; ++i) t += sh[i][threadIdx.x];
+        out[threadIdx.x] = t;
+    }
+    __syncthreads();
+}
+
+constexpr long kVnSpinLimit = 1L << 20;  // ~1 s of polling: only a fault gets there
+
+// Cross-workgroup data (partials, statistics, ticket, flag) moves through agent-scope
+// relaxed atomics: sc1 loads and stores that go to the device coherence point, so no
+// L2 writeback / invalidate (a __threadfence per workgroup costs more than the work --
+// 17.7 us of the two-launch version was mostly those); "s_waitcnt vmcnt(0)" orders a
+// workgroup's stores before its ticket.
+__device__ __forceinline__ double ld_dev(const double* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ __forceinline__ void st_dev(double* p, double v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ __forceinline__ void stores_done() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+__global__ void __launch_bounds__(kVnThreads) vecnorm_kernel(VnArgs a) {
+    __shared__ double sh[kVnThreads / 64][kD + 2];
+    __shared__ double smean[kD + 2];
+    __shared__ double sm2[kD + 2];
+    __shared__ double snorm[kD][2];   // per obs column: mean, sqrt(var + eps)
+    __shared__ double srstd;
+    __shared__ int sgo;
     const int b = blockIdx.x;
     const int64_t r0 = (int64_t)b * a.rows_per_block;
     const int64_t r1 = (r0 + a.rows_per_block < a.n) ? r0 + a.rows_per_block : a.n;
     const double cnt = (double)(r1 > r0 ? r1 - r0 : 0);
-    // pass 1: sums (and the running-return update)
-    double s[kD + 1];
+    const bool upd_ret = a.training && !a.reset;
+    const bool sync = a.upd_obs || upd_ret;
+    if (sync) {
+        // the generation of this launch's release flag (stable: the previous launch on the
+        // stream has finished; its last workgroup advanced it)
+        unsigned int gen0 = 0;
+        if (threadIdx.x == 0) gen0 = __hip_atomic_load(a.ticket + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // 1. pass 1: sums (and the running-return update)
+        double v[kD + 1];
 #pragma unroll
-    for (int c = 0; c <= kD; ++c) s[c] = 0.0;
-    for (int64_t r = r0 + threadIdx.x; r < r1; r += kVnThreads) {
-        if (a.upd_obs) {
-#pragma unroll
-            for (int c = 0; c < kD; ++c) s[c] += (double)a.obs[r * kD + c];
-        }
-        if (a.training && !a.reset) {
-            const double ret = a.returns[r] * a.gamma + (double)a.reward[r];   // VecNormalize._update_reward
-            a.returns[r] = ret;
-            s[kD] += ret;
-        }
-    }
-    block_sum_cols(s, sh, smean);
-    if (threadIdx.x <= kD) smean[threadIdx.x] = (cnt > 0.0) ? smean[threadIdx.x] / cnt : 0.0;
-    __syncthreads();
-    // pass 2: sums of squared deviations from the block means
-#pragma unroll
-    for (int c = 0; c <= kD; ++c) s[c] = 0.0;
-    for (int64_t r = r0 + threadIdx.x; r < r1; r += kVnThreads) {
-        if (a.upd_obs) {
-#pragma unroll
-            for (int c = 0; c < kD; ++c) {
-                const double d = (double)a.obs[r * kD + c] - smean[c];
-                s[c] += d * d;
-            }
-        }
-        if (a.training && !a.reset) {
-            const double d = a.returns[r] - smean[kD];
-            s[kD] += d * d;
-        }
-    }
-    block_sum_cols(s, sh, sm2);
-    double* part = a.part + (int64_t)b * kPart;
-    if (threadIdx.x <= kD) {
-        const int c = threadIdx.x;
-        part[(c < kD) ? 1 + c : 1 + 2 * kD] = smean[c];
-        part[(c < kD) ? 1 + kD + c : 2 + 2 * kD] = sm2[c];
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        part[0] = cnt;
-        __threadfence();
-        last = (atomicAdd(a.ticket, 1u) == (unsigned)(a.blocks - 1));
-    }
-    __syncthreads();
-    if (!last) return;
-    // the last block: stage every block's partials in LDS (parallel loads), then merge
-    // them in block order, one thread per column; the D obs columns share one count,
-    // read before anyone writes it
-    __threadfence();
-    __shared__ double sp[kVnMaxBlocks * kPart];
-    {
-        const volatile double* P = a.part;
-        for (int k = threadIdx.x; k < a.blocks * kPart; k += kVnThreads) sp[k] = P[k];
-    }
-    const double obs_count0 = a.stats[2 * kD];
-    __syncthreads();
-    const int c = threadIdx.x;
-    if (c <= kD) {
-        // exact merge, two passes over the staged partials in block order: the batch
-        // mean from the block sums, then M2 = sum_b M2_b + n_b (mean_b - mean)^2
-        const int mi = (c < kD) ? 1 + c : 1 + 2 * kD;
-        const int qi = (c < kD) ? 1 + kD + c : 2 + 2 * kD;
-        // four interleaved accumulators (k mod 4), combined in a fixed order: the LDS
-        // reads of a chain are independent, so the loop is not latency-bound
-        double n4[4] = {0.0, 0.0, 0.0, 0.0}, s4[4] = {0.0, 0.0, 0.0, 0.0};
-        int k = 0;
-        for (; k + 4 <= a.blocks; k += 4) {
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const double n_b = sp[(k + u) * kPart];
-                n4[u] += n_b;
-                s4[u] = fma(n_b, sp[(k + u) * kPart + mi], s4[u]);
-            }
-        }
-        for (; k < a.blocks; ++k) {
-            const double n_b = sp[k * kPart];
-            n4[0] += n_b;
-            s4[0] = fma(n_b, sp[k * kPart + mi], s4[0]);
-        }
-        const double n_a = (n4[0] + n4[1]) + (n4[2] + n4[3]);
-        const double mean_a = ((s4[0] + s4[1]) + (s4[2] + s4[3])) / n_a;
-        double q4[4] = {0.0, 0.0, 0.0, 0.0};
-        for (k = 0; k + 4 <= a.blocks; k += 4) {
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const double d = sp[(k + u) * kPart + mi] - mean_a;
-                q4[u] += sp[(k + u) * kPart + qi] + sp[(k + u) * kPart] * (d * d);
-            }
-        }
-        for (; k < a.blocks; ++k) {
-            const double d = sp[k * kPart + mi] - mean_a;
-            q4[0] += sp[k * kPart + qi] + sp[k * kPart] * (d * d);
-        }
-        const double m2_a = (q4[0] + q4[1]) + (q4[2] + q4[3]);
-        // np.mean / np.var(ddof=0) of the batch, then update_from_moments (:update)
-        if (c < kD) {
+        for (int c = 0; c <= kD; ++c) v[c] = 0.0;
+        for (int64_t r = r0 + threadIdx.x; r < r1; r += kVnThreads) {
             if (a.upd_obs) {
-                double cnt0 = obs_count0;
-                rms_update(&a.stats[c], &a.stats[kD + c], &cnt0, mean_a, m2_a / n_a, n_a);
-                if (c == 0) a.stats[2 * kD] = cnt0;
-            }
-        } else if (a.training && !a.reset) {
-            rms_update(&a.stats[2 * kD + 1], &a.stats[2 * kD + 2], &a.stats[2 * kD + 3], mean_a, m2_a / n_a, n_a);
-        }
-    }
-    if (threadIdx.x == 0) *a.ticket = 0u;   // ready for the next launch
-}
-
-__device__ __forceinline__ double clipd(double x, double lo, double hi) { return x < lo ? lo : (x > hi ? hi : x); }
-
-__global__ void __launch_bounds__(kVnThreads) apply_kernel(VnArgs a) {
-    __shared__ double sm[kD], ss[kD];
-    __shared__ double rstd;
-    if (threadIdx.x < kD) {
-        sm[threadIdx.x] = a.stats[threadIdx.x];
-        ss[threadIdx.x] = sqrt(a.stats[kD + threadIdx.x] + a.eps);
-    }
-    if (threadIdx.x == 0) rstd = sqrt(a.stats[2 * kD + 2] + a.eps);
-    __syncthreads();
-    const int64_t r = (int64_t)blockIdx.x * kVnThreads + threadIdx.x;
-    if (r >= a.n) return;
-    const bool dn = a.done ? a.done[r] != 0 : false;
 #pragma unroll
-    for (int c = 0; c < kD; ++c) {
-        const float x = a.obs[r * kD + c];
-        a.obs_out[r * kD + c] =
-            a.norm_obs ? (float)clipd(((double)x - sm[c]) / ss[c], -a.clip_obs, a.clip_obs) : x;
+                for (int c = 0; c < kD; ++c) v[c] += (double)a.obs[r * kD + c];
+            }
+            if (upd_ret) {
+                const double ret = a.returns[r] * a.gamma + (double)a.reward[r];   // VecNormalize._update_reward
+                a.returns[r] = ret;
+                v[kD] += ret;
+            }
+        }
+        block_sum<kD + 1>(v, reinterpret_cast<double(*)[kD + 1]>(sh), smean);
+        if (threadIdx.x <= kD) smean[threadIdx.x] = (cnt > 0.0) ? smean[threadIdx.x] / cnt : 0.0;
+        __syncthreads();
+        // pass 2: sums of squared deviations from the block means
+#pragma unroll
+        for (int c = 0; c <= kD; ++c) v[c] = 0.0;
+        for (int64_t r = r0 + threadIdx.x; r < r1; r += kVnThreads) {
+            if (a.upd_obs) {
+#pragma unroll
+                for (int c = 0; c < kD; ++c) {
+                    const double d = (double)a.obs[r * kD + c] - smean[c];
+                    v[c] += d * d;
+                }
+            }
+            if (upd_ret) {
+                const double d = a.returns[r] - smean[kD];
+                v[kD] += d * d;
+            }
+        }
+        block_sum<kD + 1>(v, reinterpret_cast<double(*)[kD + 1]>(sh), sm2);
+        double* part = a.part + (int64_t)b * kPart;
+        if (threadIdx.x <= kD) {
+            const int c = threadIdx.x;
+            st_dev(&part[(c < kD) ? 1 + c : 1 + 2 * kD], smean[c]);
+            st_dev(&part[(c < kD) ? 1 + kD + c : 2 + 2 * kD], sm2[c]);
+        }
+        if (threadIdx.x == 0) st_dev(&part[0], cnt);
+        stores_done();
+        __syncthreads();
+        // 2. the last workgroup to arrive merges and releases the others
+        if (threadIdx.x == 0) {
+            const unsigned int t = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            sgo = (t == (unsigned)(a.blocks - 1)) ? 1 : 0;
+        }
+        __syncthreads();
+        if (sgo) {
+            // thread k holds partial k; the batch mean as sum n_k mean_k / n, then
+            // M2 = sum M2_k + n_k (mean_k - mean)^2 -- block reductions in a fixed order
+            const int k = threadIdx.x;
+            const double* P = a.part + (int64_t)k * kPart;
+            const bool has = k < a.blocks;
+            const double n_k = has ? ld_dev(&P[0]) : 0.0;
+            double mk[kD + 1], qk[kD + 1];
+#pragma unroll
+            for (int c = 0; c <= kD; ++c) {
+                mk[c] = has ? ld_dev(&P[(c < kD) ? 1 + c : 1 + 2 * kD]) : 0.0;
+                qk[c] = has ? ld_dev(&P[(c < kD) ? 1 + kD + c : 2 + 2 * kD]) : 0.0;
+            }
+            double w[kD + 2];
+#pragma unroll
+            for (int c = 0; c <= kD; ++c) w[c] = n_k * mk[c];
+            w[kD + 1] = n_k;
+            block_sum<kD + 2>(w, sh, smean);   // smean[0..kD] = sums, smean[kD + 1] = n
+            const double n_a = smean[kD + 1];
+#pragma unroll
+            for (int c = 0; c <= kD; ++c) {
+                const double d = mk[c] - smean[c] / n_a;
+                w[c] = qk[c] + n_k * (d * d);
+            }
+            w[kD + 1] = 0.0;
+            block_sum<kD + 2>(w, sh, sm2);
+            const double obs_count0 = ld_dev(&a.stats[2 * kD]);
+            __syncthreads();   // everyone has read the count before it is written
+            const int c = threadIdx.x;
+            if (c <= kD) {
+                const double mean_a = smean[c] / n_a, m2_a = sm2[c];
+                // np.mean / np.var(ddof=0) of the batch, then update_from_moments (:update)
+                const int im = (c < kD) ? c : 2 * kD + 1, iv = (c < kD) ? kD + c : 2 * kD + 2;
+                if ((c < kD && a.upd_obs) || (c == kD && upd_ret)) {
+                    double mean = ld_dev(&a.stats[im]), var = ld_dev(&a.stats[iv]);
+                    double count = (c < kD) ? obs_count0 : ld_dev(&a.stats[2 * kD + 3]);
+                    rms_update(&mean, &var, &count, mean_a, m2_a / n_a, n_a);
+                    st_dev(&a.stats[im], mean);
+                    st_dev(&a.stats[iv], var);
+                    if (c == 0) st_dev(&a.stats[2 * kD], count);
+                    if (c == kD) st_dev(&a.stats[2 * kD + 3], count);
+                }
+            }
+            stores_done();
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // the next launch's
+                stores_done();
+                __hip_atomic_store(a.ticket + 1, gen0 + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        } else if (threadIdx.x == 0) {
+            // relaxed polls (an acquire load per poll would invalidate this XCD's L2 every
+            // time: 255 pollers thrash every cache); the statistics are read with sc1 loads
+            long spins = 0;
+            while (__hip_atomic_load(a.ticket + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gen0) {
+                if (++spins > kVnSpinLimit) {
+                    sgo = -1;   // never released: leave the outputs alone
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(4);
+            }
+        }
+        __syncthreads();
+        if (sgo < 0) return;
     }
-    if (a.reset) {
-        a.returns[r] = 0.0;
-        return;
+    // 3. normalize this workgroup's rows with the (new) statistics
+    if (threadIdx.x < kD) {
+        snorm[threadIdx.x][0] = ld_dev(&a.stats[threadIdx.x]);
+        snorm[threadIdx.x][1] = sqrt(ld_dev(&a.stats[kD + threadIdx.x]) + a.eps);
     }
-    const float rw = a.reward[r];
-    a.rew_out[r] = a.norm_reward ? (float)clipd((double)rw / rstd, -a.clip_rew, a.clip_rew) : rw;
-    if (dn && a.tobs && a.tobs_out) {
+    if (threadIdx.x == 0) srstd = sqrt(ld_dev(&a.stats[2 * kD + 2]) + a.eps);
+    __syncthreads();
+    for (int64_t r = r0 + threadIdx.x; r < r1; r += kVnThreads) {
+        const bool dn = a.done ? a.done[r] != 0 : false;
 #pragma unroll
         for (int c = 0; c < kD; ++c) {
-            const float x = a.tobs[r * kD + c];
-            a.tobs_out[r * kD + c] =
-                a.norm_obs ? (float)clipd(((double)x - sm[c]) / ss[c], -a.clip_obs, a.clip_obs) : x;
+            const float x = a.obs[r * kD + c];
+            a.obs_out[r * kD + c] =
+                a.norm_obs ? (float)clipd(((double)x - snorm[c][0]) / snorm[c][1], -a.clip_obs, a.clip_obs) : x;
         }
-    }
-    if (dn) a.returns[r] = 0.0;   // self.returns[dones] = 0
-    if (a.ep_ret) {                 // Monitor: sum(rewards), len(rewards)
-        const double er = a.ep_ret[r] + (double)rw;
-        const int32_t el = a.ep_len[r] + 1;
-        if (dn) {
-            a.ep_ret_done[r] = er;
-            a.ep_len_done[r] = el;
-            a.ep_ret[r] = 0.0;
-            a.ep_len[r] = 0;
-        } else {
-            a.ep_ret[r] = er;
-            a.ep_len[r] = el;
+        if (a.reset) {
+            a.returns[r] = 0.0;
+            continue;
+        }
+        const float rw = a.reward[r];
+        a.rew_out[r] = a.norm_reward ? (float)clipd((double)rw / srstd, -a.clip_rew, a.clip_rew) : rw;
+        if (dn && a.tobs && a.tobs_out) {
+#pragma unroll
+            for (int c = 0; c < kD; ++c) {
+                const float x = a.tobs[r * kD + c];
+                a.tobs_out[r * kD + c] =
+                    a.norm_obs ? (float)clipd(((double)x - snorm[c][0]) / snorm[c][1], -a.clip_obs, a.clip_obs) : x;
+            }
+        }
+        if (dn) a.returns[r] = 0.0;   // self.returns[dones] = 0
+        if (a.ep_ret) {                 // Monitor: sum(rewards), len(rewards)
+            const double er = a.ep_ret[r] + (double)rw;
+            const int32_t el = a.ep_len[r] + 1;
+            if (dn) {
+                a.ep_ret_done[r] = er;
+                a.ep_len_done[r] = el;
+                a.ep_ret[r] = 0.0;
+                a.ep_len[r] = 0;
+            } else {
+                a.ep_ret[r] = er;
+                a.ep_len[r] = el;
+            }
         }
     }
 }
 
 int blocks_for(int64_t n) {
-    int64_t b = (n + 4 * kVnThreads - 1) / (4 * kVnThreads);   // >= 4 rows per thread
+    int64_t b = (n + kVnThreads - 1) / kVnThreads;   // one row per thread up to 65,536 envs
     if (b > kVnMaxBlocks) b = kVnMaxBlocks;
     return (int)(b < 1 ? 1 : b);
 }
@@ -287,13 +314,9 @@ he_status launch(VnArgs& a, void* scratch, hipStream_t s) {
     a.blocks = blocks_for(a.n);
     a.rows_per_block = (int)((a.n + a.blocks - 1) / a.blocks);
     a.part = (double*)scratch;
+    // {ticket, release generation}: zero-initialised by the caller's scratch (he_vecnorm_scratch_bytes)
     a.ticket = (unsigned int*)((char*)scratch + (size_t)kVnMaxBlocks * kPart * sizeof(double));
-    if (a.upd_obs || (a.training && !a.reset)) {
-        hipLaunchKernelGGL(moments_kernel, dim3(a.blocks), dim3(kVnThreads), 0, s, a);
-        if (hipGetLastError() != hipSuccess) return HE_EHIP;
-    }
-    hipLaunchKernelGGL(apply_kernel, dim3((unsigned)((a.n + kVnThreads - 1) / kVnThreads)), dim3(kVnThreads), 0, s,
-                       a);
+    hipLaunchKernelGGL(vecnorm_kernel, dim3(a.blocks), dim3(kVnThreads), 0, s, a);
     return hipGetLastError() == hipSuccess ? HE_OK : HE_EHIP;
 }
 
