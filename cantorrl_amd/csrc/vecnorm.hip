@@ -5,20 +5,19 @@
 // gamma) (train_ppo_v2.py:204,305) and evaluates with the stats frozen (:450-453); every
 // env is wrapped in Monitor(info_keywords=...) (:119).  On the host that is a NumPy
 // pass over [N, 13] per step plus per-env Python lists -- the bottleneck once N is in
-// the tens of thousands.  Here one step is ONE launch of vecnorm_kernel, one workgroup
-// per CU at most (G <= 256 workgroups, every one resident):
-//   1. per workgroup: exact two-pass f64 mean / M2 of its rows' obs columns and of the
-//      updated running returns, written as a partial;
-//   2. the last workgroup to arrive (atomic ticket) merges the G partials in workgroup
-//      order (Chan et al.; sums as block reductions), applies
-//      RunningMeanStd.update_from_moments and releases the others (a generation flag);
-//   3. every workgroup normalizes its rows with the new statistics: obs / reward /
-//      terminal obs, returns[done] = 0 and the Monitor episode sums.
-// Deterministic for a given grid.  The waits are bounded (a spin that never sees the
-// flag gives up and leaves the outputs unwritten, reported by the next he_vecnorm_step
-// check) so a fault can never hang the device.  Eval mode (no statistics update) skips
-// 1-2.  HBM-bound and tiny (68 B of obs + reward read and written per env): the point is
-// to keep the statistics on the device within one launch, not the arithmetic.
+// the tens of thousands.  Here one step is two launches of G <= 256 workgroups, each
+// owning a slice of 256 rows staged through LDS as flat coalesced copies:
+//   vn_moments_kernel  exact two-pass f64 mean / M2 of the slice's obs columns and of the
+//                      updated running returns, stored as a partial (+ a snapshot of the
+//                      old statistics);
+//   vn_apply_kernel    every workgroup merges all G partials itself (Chan et al.; the
+//                      same block reductions in the same order, so the same result
+//                      everywhere), applies RunningMeanStd.update_from_moments (workgroup
+//                      0 stores it), and normalizes its rows: obs / reward / terminal obs,
+//                      returns[done] = 0 and the Monitor episode sums.
+// Deterministic for a given grid; no atomics and no waiting between workgroups (the
+// kernel boundary publishes the partials).  Eval mode (no statistics update) is the
+// second launch alone.  68 B of obs + reward read and written per env.
 
 #include <hip/hip_runtime.h>
 
@@ -31,9 +30,9 @@ namespace {
 
 constexpr int kD = HE_OBS_DIM;
 constexpr int kVnThreads = 256;
-constexpr int kVnMaxBlocks = 256;   // workgroups of one launch: all resident (one per CU at most)
+constexpr int kVnMaxBlocks = 256;   // workgroups of a launch = partials merged per workgroup (one per thread)
 
-// scratch layout: [blocks][kPart] doubles, then one u32 ticket
+// scratch layout: [kPart][kVnMaxBlocks] doubles, then the 2 kD + 4 old statistics
 constexpr int kPart = 2 * kD + 3;   // count, mean[D], M2[D], ret_mean, ret_M2
 
 struct VnArgs {
@@ -49,7 +48,6 @@ struct VnArgs {
     double* returns;
     double* stats;
     double* part;
-    unsigned int* ticket;
     float* obs_out;
     float* rew_out;
     float* tobs_out;
@@ -76,222 +74,256 @@ __device__ __forceinline__ void rms_update(double* mean, double* var, double* co
 
 __device__ __forceinline__ double clipd(double x, double lo, double hi) { return x < lo ? lo : (x > hi ? hi : x); }
 
-// Sum of v[0..NV) over the block into out[0..NV) (LDS): a wave-level butterfly per
-// value, then one barrier and a 4-way sum -- two barriers for all NV values.
+// Sum of v[0..NV) over the block into out[0..NV) (LDS), NV <= 16: every thread stores
+// its NV values (row stride NV + 1), then 16 threads per value sum 16 rows each and
+// finish with a 4-level butterfly inside their 16-lane group -- 16 LDS reads and 4
+// shuffles per thread, against 6 shuffle levels per value (~180 LDS permutes per wave)
+// of a butterfly over the whole wave.  The summation order is fixed.
 template <int NV>
-__device__ __forceinline__ void block_sum(double* v, double (*sh)[NV], double* out) {
+__device__ __forceinline__ void block_sum(const double* v, double* buf, double* out) {
+    static_assert(NV <= 16 && NV * 16 <= kVnThreads, "16 threads per value");
+    constexpr int S = NV + 1;
+    const int t = threadIdx.x;
 #pragma unroll
-    for (int c = 0; c < NV; ++c) {
-#pragma unroll
-        for (int m = 32; m >= 1; m >>= 1) v[c] += __shfl_xor(v[c], m, 64);
-    }
-    const int w = threadIdx.x >> 6;
-    if ((threadIdx.x & 63) == 0) {
-#pragma unroll
-        for (int c = 0; c < NV; ++c) sh[w][c] = v[c];
-    }
+    for (int c = 0; c < NV; ++c) buf[t * S + c] = v[c];
     __syncthreads();
-    if (threadIdx.x < NV) {
-        double t = 0.0;
+    if (t < NV * 16) {
+        const int c = t >> 4, j = t & 15;
+        double x = 0.0;
 #pragma unroll
-        for (int i = 0; i < kVnThreads / 64; ++i) t += sh[i][threadIdx.x];
-        out[threadIdx.x] = t;
+        for (int k = 0; k < kVnThreads / 16; ++k) x += buf[(j + 16 * k) * S + c];
+#pragma unroll
+        for (int m = 8; m >= 1; m >>= 1) x += __shfl_xor(x, m, 16);
+        if (j == 0) out[c] = x;
     }
     __syncthreads();
 }
 
-constexpr long kVnSpinLimit = 1L << 20;  // ~1 s of polling: only a fault gets there
+constexpr int kVnChunk = kVnThreads;   // rows staged in LDS at a time (one per thread)
 
-// Cross-workgroup data (partials, statistics, ticket, flag) moves through agent-scope
-// relaxed atomics: sc1 loads and stores that go to the device coherence point, so no
-// L2 writeback / invalidate (a __threadfence per workgroup costs more than the work --
-// 17.7 us of the two-launch version was mostly those); "s_waitcnt vmcnt(0)" orders a
-// workgroup's stores before its ticket.
-__device__ __forceinline__ double ld_dev(const double* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-__device__ __forceinline__ void st_dev(double* p, double v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-__device__ __forceinline__ void stores_done() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+// Rows [c0, c0 + rows) of obs -> LDS tile, as a flat coalesced copy (the [N][13] rows are
+// 52 B apart: per-row loads would touch 26 cache lines per wave instruction); the rows
+// are then read from LDS with a stride of 13 words (odd: no bank conflicts).
+__device__ __forceinline__ void load_tile(float* tile, const float* obs, int64_t c0, int rows) {
+    const float* src = obs + c0 * kD;
+    const int nf = rows * kD;
+    for (int k = threadIdx.x; k < nf; k += kVnThreads) tile[k] = src[k];
+    __syncthreads();
+}
 
-__global__ void __launch_bounds__(kVnThreads) vecnorm_kernel(VnArgs a) {
-    __shared__ double sh[kVnThreads / 64][kD + 2];
-    __shared__ double smean[kD + 2];
-    __shared__ double sm2[kD + 2];
-    __shared__ double snorm[kD][2];   // per obs column: mean, sqrt(var + eps)
-    __shared__ double srstd;
-    __shared__ int sgo;
-    const int b = blockIdx.x;
-    const int64_t r0 = (int64_t)b * a.rows_per_block;
-    const int64_t r1 = (r0 + a.rows_per_block < a.n) ? r0 + a.rows_per_block : a.n;
-    const double cnt = (double)(r1 > r0 ? r1 - r0 : 0);
+struct VnRows {
+    int64_t r0, r1;
+    double cnt;
+};
+__device__ __forceinline__ VnRows rows_of(const VnArgs& a) {
+    VnRows w;
+    w.r0 = (int64_t)blockIdx.x * a.rows_per_block;
+    w.r1 = (w.r0 + a.rows_per_block < a.n) ? w.r0 + a.rows_per_block : a.n;
+    w.cnt = (double)(w.r1 > w.r0 ? w.r1 - w.r0 : 0);
+    return w;
+}
+
+// Launch 1 (training): per workgroup, the exact two-pass f64 mean / M2 of its rows' obs
+// columns and of the updated running returns, stored as a partial.  The kernel
+// boundary publishes the partials to launch 2 -- no atomics, no waiting (a single
+// launch with a grid-wide wait measured 25 us at 65,536 envs: four dependent
+// device-coherent round trips between workgroups).
+__global__ void __launch_bounds__(kVnThreads) vn_moments_kernel(VnArgs a) {
+    __shared__ double sh[kVnThreads * (kD + 2)];
+    __shared__ double smean[kD + 1];
+    __shared__ double sm2[kD + 1];
+    __shared__ float tile[kVnChunk * kD];
+    const VnRows w = rows_of(a);
     const bool upd_ret = a.training && !a.reset;
-    const bool sync = a.upd_obs || upd_ret;
-    if (sync) {
-        // the generation of this launch's release flag (stable: the previous launch on the
-        // stream has finished; its last workgroup advanced it)
-        unsigned int gen0 = 0;
-        if (threadIdx.x == 0) gen0 = __hip_atomic_load(a.ticket + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        // 1. pass 1: sums (and the running-return update)
-        double v[kD + 1];
+    const int t = threadIdx.x;
+    double v[kD + 1];
 #pragma unroll
-        for (int c = 0; c <= kD; ++c) v[c] = 0.0;
-        for (int64_t r = r0 + threadIdx.x; r < r1; r += kVnThreads) {
+    for (int c = 0; c <= kD; ++c) v[c] = 0.0;
+    for (int64_t c0 = w.r0; c0 < w.r1; c0 += kVnChunk) {   // pass 1: sums (and the returns)
+        const int rows = (int)((w.r1 - c0) < kVnChunk ? (w.r1 - c0) : kVnChunk);
+        if (a.upd_obs) load_tile(tile, a.obs, c0, rows);
+        if (t < rows) {
             if (a.upd_obs) {
 #pragma unroll
-                for (int c = 0; c < kD; ++c) v[c] += (double)a.obs[r * kD + c];
+                for (int c = 0; c < kD; ++c) v[c] += (double)tile[t * kD + c];
             }
             if (upd_ret) {
+                const int64_t r = c0 + t;
                 const double ret = a.returns[r] * a.gamma + (double)a.reward[r];   // VecNormalize._update_reward
                 a.returns[r] = ret;
                 v[kD] += ret;
             }
         }
-        block_sum<kD + 1>(v, reinterpret_cast<double(*)[kD + 1]>(sh), smean);
-        if (threadIdx.x <= kD) smean[threadIdx.x] = (cnt > 0.0) ? smean[threadIdx.x] / cnt : 0.0;
         __syncthreads();
-        // pass 2: sums of squared deviations from the block means
+    }
+    block_sum<kD + 1>(v, sh, smean);
+    if (t <= kD) smean[t] = (w.cnt > 0.0) ? smean[t] / w.cnt : 0.0;
+    __syncthreads();
 #pragma unroll
-        for (int c = 0; c <= kD; ++c) v[c] = 0.0;
-        for (int64_t r = r0 + threadIdx.x; r < r1; r += kVnThreads) {
+    for (int c = 0; c <= kD; ++c) v[c] = 0.0;
+    const bool resident = w.r1 - w.r0 <= kVnChunk;   // the tile still holds the rows
+    for (int64_t c0 = w.r0; c0 < w.r1; c0 += kVnChunk) {   // pass 2: squared deviations
+        const int rows = (int)((w.r1 - c0) < kVnChunk ? (w.r1 - c0) : kVnChunk);
+        if (!resident && a.upd_obs) load_tile(tile, a.obs, c0, rows);
+        if (t < rows) {
             if (a.upd_obs) {
 #pragma unroll
                 for (int c = 0; c < kD; ++c) {
-                    const double d = (double)a.obs[r * kD + c] - smean[c];
+                    const double d = (double)tile[t * kD + c] - smean[c];
                     v[c] += d * d;
                 }
             }
             if (upd_ret) {
-                const double d = a.returns[r] - smean[kD];
+                const double d = a.returns[c0 + t] - smean[kD];
                 v[kD] += d * d;
             }
         }
-        block_sum<kD + 1>(v, reinterpret_cast<double(*)[kD + 1]>(sh), sm2);
-        double* part = a.part + (int64_t)b * kPart;
-        if (threadIdx.x <= kD) {
-            const int c = threadIdx.x;
-            st_dev(&part[(c < kD) ? 1 + c : 1 + 2 * kD], smean[c]);
-            st_dev(&part[(c < kD) ? 1 + kD + c : 2 + 2 * kD], sm2[c]);
+        if (!resident) __syncthreads();
+    }
+    block_sum<kD + 1>(v, sh, sm2);
+    // partials [kPart][kVnMaxBlocks] (launch 2's thread k reads column k: coalesced)
+    double* part = a.part + blockIdx.x;
+    if (t <= kD) {
+        part[((t < kD) ? 1 + t : 1 + 2 * kD) * kVnMaxBlocks] = smean[t];
+        part[((t < kD) ? 1 + kD + t : 2 + 2 * kD) * kVnMaxBlocks] = sm2[t];
+    }
+    if (t == 0) part[0] = w.cnt;
+    // the statistics before this step, for launch 2 (whose workgroup 0 overwrites them)
+    if (blockIdx.x == 0 && t < 2 * kD + 4) a.part[kVnMaxBlocks * kPart + t] = a.stats[t];
+}
+
+// Launch 2: every workgroup merges all the partials itself (the same reductions in the
+// same order, so the same statistics everywhere; workgroup 0 stores them), then
+// normalizes its rows: obs / reward / terminal obs, returns[done] = 0, Monitor sums.
+__global__ void __launch_bounds__(kVnThreads) vn_apply_kernel(VnArgs a) {
+    __shared__ double sh[kVnThreads * (kD + 3)];
+    __shared__ double smean[kD + 2];
+    __shared__ double sm2[kD + 2];
+    __shared__ double snorm[kD][2];   // per obs column: mean, sqrt(var + eps)
+    __shared__ double srstd;
+    __shared__ float tile[kVnChunk * kD];
+    const VnRows w = rows_of(a);
+    const bool upd_ret = a.training && !a.reset;
+    const int t = threadIdx.x;
+    const bool resident = w.r1 - w.r0 <= kVnChunk;
+    if (resident && w.r1 > w.r0) load_tile(tile, a.obs, w.r0, (int)(w.r1 - w.r0));
+    if (a.upd_obs || upd_ret) {
+        // thread k holds partial k; the batch mean as sum n_k mean_k / n, then
+        // M2 = sum M2_k + n_k (mean_k - mean)^2 -- block reductions in a fixed order
+        const double* P = a.part + t;
+        const bool has = t < a.blocks;
+        const double n_k = has ? P[0] : 0.0;
+        double mk[kD + 1], qk[kD + 1];
+#pragma unroll
+        for (int c = 0; c <= kD; ++c) {
+            mk[c] = has ? P[((c < kD) ? 1 + c : 1 + 2 * kD) * kVnMaxBlocks] : 0.0;
+            qk[c] = has ? P[((c < kD) ? 1 + kD + c : 2 + 2 * kD) * kVnMaxBlocks] : 0.0;
         }
-        if (threadIdx.x == 0) st_dev(&part[0], cnt);
-        stores_done();
-        __syncthreads();
-        // 2. the last workgroup to arrive merges and releases the others
-        if (threadIdx.x == 0) {
-            const unsigned int t = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            sgo = (t == (unsigned)(a.blocks - 1)) ? 1 : 0;
+        double v[kD + 2];
+#pragma unroll
+        for (int c = 0; c <= kD; ++c) v[c] = n_k * mk[c];
+        v[kD + 1] = n_k;
+        block_sum<kD + 2>(v, sh, smean);   // smean[0..kD] = sums, smean[kD + 1] = n
+        const double n_a = smean[kD + 1];
+#pragma unroll
+        for (int c = 0; c <= kD; ++c) {
+            const double d = mk[c] - smean[c] / n_a;
+            v[c] = qk[c] + n_k * (d * d);
         }
-        __syncthreads();
-        if (sgo) {
-            // thread k holds partial k; the batch mean as sum n_k mean_k / n, then
-            // M2 = sum M2_k + n_k (mean_k - mean)^2 -- block reductions in a fixed order
-            const int k = threadIdx.x;
-            const double* P = a.part + (int64_t)k * kPart;
-            const bool has = k < a.blocks;
-            const double n_k = has ? ld_dev(&P[0]) : 0.0;
-            double mk[kD + 1], qk[kD + 1];
-#pragma unroll
-            for (int c = 0; c <= kD; ++c) {
-                mk[c] = has ? ld_dev(&P[(c < kD) ? 1 + c : 1 + 2 * kD]) : 0.0;
-                qk[c] = has ? ld_dev(&P[(c < kD) ? 1 + kD + c : 2 + 2 * kD]) : 0.0;
-            }
-            double w[kD + 2];
-#pragma unroll
-            for (int c = 0; c <= kD; ++c) w[c] = n_k * mk[c];
-            w[kD + 1] = n_k;
-            block_sum<kD + 2>(w, sh, smean);   // smean[0..kD] = sums, smean[kD + 1] = n
-            const double n_a = smean[kD + 1];
-#pragma unroll
-            for (int c = 0; c <= kD; ++c) {
-                const double d = mk[c] - smean[c] / n_a;
-                w[c] = qk[c] + n_k * (d * d);
-            }
-            w[kD + 1] = 0.0;
-            block_sum<kD + 2>(w, sh, sm2);
-            const double obs_count0 = ld_dev(&a.stats[2 * kD]);
-            __syncthreads();   // everyone has read the count before it is written
-            const int c = threadIdx.x;
-            if (c <= kD) {
-                const double mean_a = smean[c] / n_a, m2_a = sm2[c];
-                // np.mean / np.var(ddof=0) of the batch, then update_from_moments (:update)
-                const int im = (c < kD) ? c : 2 * kD + 1, iv = (c < kD) ? kD + c : 2 * kD + 2;
-                if ((c < kD && a.upd_obs) || (c == kD && upd_ret)) {
-                    double mean = ld_dev(&a.stats[im]), var = ld_dev(&a.stats[iv]);
-                    double count = (c < kD) ? obs_count0 : ld_dev(&a.stats[2 * kD + 3]);
-                    rms_update(&mean, &var, &count, mean_a, m2_a / n_a, n_a);
-                    st_dev(&a.stats[im], mean);
-                    st_dev(&a.stats[iv], var);
-                    if (c == 0) st_dev(&a.stats[2 * kD], count);
-                    if (c == kD) st_dev(&a.stats[2 * kD + 3], count);
+        v[kD + 1] = 0.0;
+        block_sum<kD + 2>(v, sh, sm2);
+        const int c = t;
+        if (c <= kD) {
+            const double mean_a = smean[c] / n_a, m2_a = sm2[c];
+            // np.mean / np.var(ddof=0) of the batch, then update_from_moments (:update)
+            const int im = (c < kD) ? c : 2 * kD + 1, iv = (c < kD) ? kD + c : 2 * kD + 2;
+            const double* old = a.part + kVnMaxBlocks * kPart;   // launch 1's snapshot
+            double mean = old[im], var = old[iv];
+            if ((c < kD && a.upd_obs) || (c == kD && upd_ret)) {
+                double count = (c < kD) ? old[2 * kD] : old[2 * kD + 3];
+                rms_update(&mean, &var, &count, mean_a, m2_a / n_a, n_a);
+                if (blockIdx.x == 0) {
+                    if (c == 0) a.stats[2 * kD] = count;
+                    if (c == kD) a.stats[2 * kD + 3] = count;
                 }
             }
-            stores_done();
-            __syncthreads();
-            if (threadIdx.x == 0) {
-                __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // the next launch's
-                stores_done();
-                __hip_atomic_store(a.ticket + 1, gen0 + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-        } else if (threadIdx.x == 0) {
-            // relaxed polls (an acquire load per poll would invalidate this XCD's L2 every
-            // time: 255 pollers thrash every cache); the statistics are read with sc1 loads
-            long spins = 0;
-            while (__hip_atomic_load(a.ticket + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gen0) {
-                if (++spins > kVnSpinLimit) {
-                    sgo = -1;   // never released: leave the outputs alone
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(4);
-            }
-        }
-        __syncthreads();
-        if (sgo < 0) return;
-    }
-    // 3. normalize this workgroup's rows with the (new) statistics
-    if (threadIdx.x < kD) {
-        snorm[threadIdx.x][0] = ld_dev(&a.stats[threadIdx.x]);
-        snorm[threadIdx.x][1] = sqrt(ld_dev(&a.stats[kD + threadIdx.x]) + a.eps);
-    }
-    if (threadIdx.x == 0) srstd = sqrt(ld_dev(&a.stats[2 * kD + 2]) + a.eps);
-    __syncthreads();
-    for (int64_t r = r0 + threadIdx.x; r < r1; r += kVnThreads) {
-        const bool dn = a.done ? a.done[r] != 0 : false;
-#pragma unroll
-        for (int c = 0; c < kD; ++c) {
-            const float x = a.obs[r * kD + c];
-            a.obs_out[r * kD + c] =
-                a.norm_obs ? (float)clipd(((double)x - snorm[c][0]) / snorm[c][1], -a.clip_obs, a.clip_obs) : x;
-        }
-        if (a.reset) {
-            a.returns[r] = 0.0;
-            continue;
-        }
-        const float rw = a.reward[r];
-        a.rew_out[r] = a.norm_reward ? (float)clipd((double)rw / srstd, -a.clip_rew, a.clip_rew) : rw;
-        if (dn && a.tobs && a.tobs_out) {
-#pragma unroll
-            for (int c = 0; c < kD; ++c) {
-                const float x = a.tobs[r * kD + c];
-                a.tobs_out[r * kD + c] =
-                    a.norm_obs ? (float)clipd(((double)x - snorm[c][0]) / snorm[c][1], -a.clip_obs, a.clip_obs) : x;
-            }
-        }
-        if (dn) a.returns[r] = 0.0;   // self.returns[dones] = 0
-        if (a.ep_ret) {                 // Monitor: sum(rewards), len(rewards)
-            const double er = a.ep_ret[r] + (double)rw;
-            const int32_t el = a.ep_len[r] + 1;
-            if (dn) {
-                a.ep_ret_done[r] = er;
-                a.ep_len_done[r] = el;
-                a.ep_ret[r] = 0.0;
-                a.ep_len[r] = 0;
+            if (c < kD) {
+                snorm[c][0] = mean;
+                snorm[c][1] = sqrt(var + a.eps);
             } else {
-                a.ep_ret[r] = er;
-                a.ep_len[r] = el;
+                srstd = sqrt(var + a.eps);
+            }
+            smean[c] = mean;   // stored below, after every thread has read the old values
+            sm2[c] = var;
+        }
+        __syncthreads();
+        if (blockIdx.x == 0 && c <= kD) {
+            const int im = (c < kD) ? c : 2 * kD + 1, iv = (c < kD) ? kD + c : 2 * kD + 2;
+            a.stats[im] = smean[c];
+            a.stats[iv] = sm2[c];
+        }
+    } else {
+        if (t < kD) {
+            snorm[t][0] = a.stats[t];
+            snorm[t][1] = sqrt(a.stats[kD + t] + a.eps);
+        }
+        if (t == 0) srstd = sqrt(a.stats[2 * kD + 2] + a.eps);
+        __syncthreads();
+    }
+    for (int64_t c0 = w.r0; c0 < w.r1; c0 += kVnChunk) {
+        const int rows = (int)((w.r1 - c0) < kVnChunk ? (w.r1 - c0) : kVnChunk);
+        if (!resident) load_tile(tile, a.obs, c0, rows);
+        if (t < rows) {
+            const int64_t r = c0 + t;
+            // the row in place in LDS, then stored back as a flat coalesced copy
+            if (a.norm_obs) {
+#pragma unroll
+                for (int c = 0; c < kD; ++c) {
+                    const float x = tile[t * kD + c];
+                    tile[t * kD + c] = (float)clipd(((double)x - snorm[c][0]) / snorm[c][1], -a.clip_obs, a.clip_obs);
+                }
+            }
+            if (a.reset) {
+                a.returns[r] = 0.0;
+            } else {
+                const bool dn = a.done ? a.done[r] != 0 : false;
+                const float rw = a.reward[r];
+                a.rew_out[r] = a.norm_reward ? (float)clipd((double)rw / srstd, -a.clip_rew, a.clip_rew) : rw;
+                if (dn && a.tobs && a.tobs_out) {   // rare: per-row accesses
+#pragma unroll
+                    for (int c = 0; c < kD; ++c) {
+                        const float x = a.tobs[r * kD + c];
+                        a.tobs_out[r * kD + c] =
+                            a.norm_obs ? (float)clipd(((double)x - snorm[c][0]) / snorm[c][1], -a.clip_obs, a.clip_obs)
+                                       : x;
+                    }
+                }
+                if (dn) a.returns[r] = 0.0;   // self.returns[dones] = 0
+                if (a.ep_ret) {                 // Monitor: sum(rewards), len(rewards)
+                    const double er = a.ep_ret[r] + (double)rw;
+                    const int32_t el = a.ep_len[r] + 1;
+                    if (dn) {
+                        a.ep_ret_done[r] = er;
+                        a.ep_len_done[r] = el;
+                        a.ep_ret[r] = 0.0;
+                        a.ep_len[r] = 0;
+                    } else {
+                        a.ep_ret[r] = er;
+                        a.ep_len[r] = el;
+                    }
+                }
             }
         }
+        __syncthreads();
+        float* dst = a.obs_out + c0 * kD;
+        const int nf = rows * kD;
+        for (int k = t; k < nf; k += kVnThreads) dst[k] = tile[k];
+        __syncthreads();
     }
 }
 
 int blocks_for(int64_t n) {
-    int64_t b = (n + kVnThreads - 1) / kVnThreads;   // one row per thread up to 65,536 envs
+    int64_t b = (n + kVnChunk - 1) / kVnChunk;   // one row per thread up to 65,536 envs
     if (b > kVnMaxBlocks) b = kVnMaxBlocks;
     return (int)(b < 1 ? 1 : b);
 }
@@ -313,10 +345,12 @@ __global__ void init_kernel(double* stats) {
 he_status launch(VnArgs& a, void* scratch, hipStream_t s) {
     a.blocks = blocks_for(a.n);
     a.rows_per_block = (int)((a.n + a.blocks - 1) / a.blocks);
-    a.part = (double*)scratch;
-    // {ticket, release generation}: zero-initialised by the caller's scratch (he_vecnorm_scratch_bytes)
-    a.ticket = (unsigned int*)((char*)scratch + (size_t)kVnMaxBlocks * kPart * sizeof(double));
-    hipLaunchKernelGGL(vecnorm_kernel, dim3(a.blocks), dim3(kVnThreads), 0, s, a);
+    a.part = (double*)scratch;   // [kVnMaxBlocks][kPart] partials, then the old statistics
+    if (a.upd_obs || (a.training && !a.reset)) {
+        hipLaunchKernelGGL(vn_moments_kernel, dim3(a.blocks), dim3(kVnThreads), 0, s, a);
+        if (hipGetLastError() != hipSuccess) return HE_EHIP;
+    }
+    hipLaunchKernelGGL(vn_apply_kernel, dim3(a.blocks), dim3(kVnThreads), 0, s, a);
     return hipGetLastError() == hipSuccess ? HE_OK : HE_EHIP;
 }
 
@@ -368,7 +402,7 @@ int64_t he_vecnorm_stats_len(int32_t obs_dim) { return 2 * (int64_t)obs_dim + 4;
 int64_t he_vecnorm_scratch_bytes(int64_t n, int32_t obs_dim) {
     (void)n;
     (void)obs_dim;
-    return (int64_t)kVnMaxBlocks * kPart * sizeof(double) + 256;
+    return ((int64_t)kVnMaxBlocks * kPart + 2 * kD + 4) * (int64_t)sizeof(double);  // partials + old statistics
 }
 
 he_status he_vecnorm_init(double* stats, int32_t obs_dim, void* stream) {

@@ -44,8 +44,17 @@ for _ in range(R):
 e1.record()
 torch.cuda.synchronize()
 us = e0.elapsed_time(e1) * 1e3 / R
-print(f"he_vecnorm_step n={n}: {us:.2f} us/step (moments + apply), {n * 68 / (us * 1e-6) / 1e9:.1f} GB/s of obs+reward "
-      f"in/out", flush=True)
+print(f"he_vecnorm_step n={n}: {us:.2f} us/step (statistics update + normalize), {n * 68 / (us * 1e-6) / 1e9:.1f} GB/s "
+      f"of obs+reward in/out", flush=True)
+# frozen statistics (eval): the normalize phase alone, no cross-workgroup merge
+p.training = 0
+e0.record()
+for _ in range(R):
+    lib.he_vecnorm_step(*args)
+e1.record()
+torch.cuda.synchronize()
+print(f"he_vecnorm_step n={n}, training=False: {e0.elapsed_time(e1) * 1e3 / R:.2f} us/step", flush=True)
+p.training = 1
 # env step + vecnorm, one launch each
 e0.record()
 for k in range(64):
