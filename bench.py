@@ -74,8 +74,9 @@ MARKET_STATE_BYTES = 72
 
 
 def lds_rollout(cfg):
-    """he_rollout runs lds_rollout_kernel (GBM, with or without a book, unless HE_LDS_ROLLOUT=0)."""
-    return cfg["mode"] == "gbm" and os.environ.get("HE_LDS_ROLLOUT", "1") != "0"
+    """he_rollout runs lds_rollout_kernel (GBM or Heston, with or without a book, unless
+    HE_LDS_ROLLOUT=0)."""
+    return cfg["mode"] in ("gbm", "heston") and os.environ.get("HE_LDS_ROLLOUT", "1") != "0"
 
 
 def fused_market():
@@ -563,7 +564,8 @@ def roofline(mode, n, kern_ms, rk, book=False, market="gbm", lds=False):
     if mode == "rollout":
         survey = n * (rk * SURVEY_ROLLOUT_B + SURVEY_ROLLOUT_STATE_B)
         if lds:
-            own = n * (rk * LDS_STEP_B + LDS_STATE_B + (16 if book else 0))  # + the book's running max
+            # + the book's running max, + Heston's f64 variance (each read + written)
+            own = n * (rk * LDS_STEP_B + LDS_STATE_B + (16 if book else 0) + (16 if market == "heston" else 0))
             kname = ("lds_rollout_kernel (he_rollout, K=%d fused steps; the market made in LDS by "
                      "producer waves, never written to HBM)" % rk)
         else:

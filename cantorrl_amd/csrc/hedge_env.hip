@@ -1581,15 +1581,17 @@ static_assert(kLdsM % kLdsPrefetch == 0, "the action ring index is the slot mod 
 template <int MODE, bool BOOK>
 struct LdsGeom {
     static constexpr bool HESTON = MODE == HE_MODE_HESTON;
-    static constexpr int lanes = BOOK ? HE_LDS_LANES_BOOK : HE_LDS_LANES;
+    // Heston: two normals, a sqrt and a per-step Black-Scholes constant set per slot --
+    // producer-bound like a book, so it takes the book's lane count
+    static constexpr int lanes = (BOOK || HESTON) ? HE_LDS_LANES_BOOK : HE_LDS_LANES;
     static constexpr int prod = lanes;
     static constexpr int penvs = kLdsEnvs / lanes;
     static constexpr int threads = 64 * (2 + prod);  // + the reward and the obs stepper waves
     static constexpr int H = kLdsM / lanes;
 #ifdef HE_LDS_MINWAVES
-    static constexpr int minwaves = BOOK ? 4 : HE_LDS_MINWAVES;
+    static constexpr int minwaves = (BOOK || HESTON) ? 4 : HE_LDS_MINWAVES;
 #else
-    static constexpr int minwaves = BOOK ? 4 : (4 * (2 + prod) + 3) / 4 + 1;
+    static constexpr int minwaves = (BOOK || HESTON) ? 4 : (4 * (2 + prod) + 3) / 4 + 1;
 #endif
     static_assert(H * lanes == kLdsM && penvs * lanes == kLdsEnvs, "producer lane layout");
 };
@@ -1604,8 +1606,10 @@ struct LdsMarketT {
     float pp[2][kLdsM][kLdsEnvs];
     float stage[2][kLdsEnvs * kObs];                                   // obs row staging, by step parity
     double bk[BOOK ? 2 : 1][BOOK ? kLdsM : 1][kLdsEnvs];                // book value of every slot
+    float vv[MODE == HE_MODE_HESTON ? 2 : 1][MODE == HE_MODE_HESTON ? kLdsM : 1][kLdsEnvs];  // Heston: f32 v_t
 };
 static_assert(sizeof(LdsMarketT<HE_MODE_GBM, false>) <= 40 * 1024, "4 workgroups per CU");
+static_assert(sizeof(LdsMarketT<HE_MODE_HESTON, true>) <= 40 * 1024, "4 workgroups per CU");
 
 #ifdef HE_LDS_TIMING
 // Diagnostic builds only: per wave role (0 reward, 1 obs, 2-3 producers) and workgroup,
@@ -1665,6 +1669,8 @@ template <int MODE, bool BOOK, bool LEAN, bool OBS>
 __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& io, int k_steps, const Market& cur,
                                             LdsMarketT<MODE, BOOK>& L, int64_t base) {
     constexpr int D = kLdsPrefetch;
+    constexpr bool HESTON = MODE == HE_MODE_HESTON;
+    static_assert(!(LEAN && HESTON), "the lean steppers take the constant GBM variance");
     const int lane = threadIdx.x & 63;
     const int64_t N = p.n;
     const int nfull = k_steps / kLdsM;          // full blocks
@@ -1696,9 +1702,10 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
             // the market the env stands at: the block-start record of market_body (f32 S)
             if (t0 != 0) {
                 const double Sc = cur.S[i];
+                const double Vc = HESTON ? cur.v[i] : p.var;
                 // the book at the block start: market_body's slot 0 (same function, operands)
-                const double Bc = BOOK ? book_value(p, Sc, p.var, (int32_t)t0, cur.M[i]) : 0.0;
-                pre = Mkt{(float)Sc, p.var_f, cur.C[i], cur.P[i], Bc};
+                const double Bc = BOOK ? book_value(p, Sc, Vc, (int32_t)t0, cur.M[i]) : 0.0;
+                pre = Mkt{(float)Sc, HESTON ? (float)Vc : p.var_f, cur.C[i], cur.P[i], Bc};
             }
             pv_last = portfolio_value<BOOK>(p, e, pre);
         }
@@ -1877,13 +1884,15 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
             });
         }
     } else {
-        if (OBS && e.t != 0) pre = Mkt{(float)cur.S[i], p.var_f, cur.C[i], cur.P[i], 0.0};
+        if (OBS && e.t != 0) pre = Mkt{(float)cur.S[i], HESTON ? (float)cur.v[i] : p.var_f, cur.C[i], cur.P[i], 0.0};
         auto step = [&](int buf, int sl, int k, float2 ak) {
             const int64_t koff = (int64_t)k * N;
             const float2 sc = L.sc[buf][sl][lane];
-            const Mkt post{sc.x, p.var_f, sc.y, L.pp[buf][sl][lane], BOOK ? L.bk[buf][sl][lane] : 0.0};
+            const float vk = HESTON ? L.vv[HESTON ? buf : 0][HESTON ? sl : 0][lane] : p.var_f;
+            const Mkt post{sc.x, vk, sc.y, L.pp[buf][sl][lane], BOOK ? L.bk[buf][sl][lane] : 0.0};
             if (OBS) {
-                float4 g = p.record_metrics ? greeks_fast<true>(p, post.S, p.var_f) : make_float4(0.f, 0.f, 0.f, 0.f);
+                // the obs greeks of market_body's greeks records (Heston: of the slot's v)
+                float4 g = p.record_metrics ? greeks_fast<!HESTON>(p, post.S, post.v) : make_float4(0.f, 0.f, 0.f, 0.f);
                 g.w = lag_return(post.S, pre.S);
                 // (i)-(ii) of step_env: the integer trade logic (:181-200)
                 const int32_t nc = e.call + trade_round(ak.x * p.mt_f, p.mt);
@@ -1940,6 +1949,7 @@ template <int MODE, bool BOOK>
 __device__ __forceinline__ void lds_producer(const Params& p, int k_steps, const Market& cur,
                                              LdsMarketT<MODE, BOOK>& W, int64_t base, int pw) {
     using G = LdsGeom<MODE, BOOK>;
+    constexpr bool HESTON = G::HESTON;
     constexpr int kLdsLanes = G::lanes, kLdsPEnvs = G::penvs, kLdsH = G::H;
     const int lane = threadIdx.x & 63;
     const int sub = lane / kLdsPEnvs;
@@ -1953,6 +1963,7 @@ __device__ __forceinline__ void lds_producer(const Params& p, int k_steps, const
     const uint32_t ep0 = cur.ep[pi];
     const uint32_t t0 = cur.t[pi];
     double Sbs = cur.S[pi];                          // f64 price before slot 0 of block bp
+    double Vbs = HESTON ? cur.v[pi] : 0.0;           // Heston: f64 variance before it
     double Mbs = BOOK ? cur.M[pi] : 0.0;             // book: running max of S before it
     const uint32_t off = t0 >= T ? T : t0;           // a0 = ep T + t (t = T: the next episode)
     const uint64_t a0 = (uint64_t)ep0 * T + off;     // env-step index of the launch's first step
@@ -1969,39 +1980,99 @@ __device__ __forceinline__ void lds_producer(const Params& p, int k_steps, const
             const int len = (k_steps - kb) < kLdsM ? (k_steps - kb) : kLdsM;
             const uint64_t nf = a0 + (uint64_t)(kb + sl0);
             const uint32_t tpf = (tpb + (uint32_t)sl0) % T;
-            // (1) the random part of every slot: Philox block m = n / 2 gives the
-            // Box-Muller pair of steps 2m (cos) and 2m + 1 (sin)
-            double ex[kLdsH];
-            double zc = 0.0;
+            double ex[kLdsH];   // own slots' growth factors S_j / S_{j-1} (before the clamp)
+            double Vx[kLdsH];   // Heston: own slots' v after the step
+            double Vin = Vbs;   // Heston: v before the lane's first slot
+            if constexpr (!HESTON) {
+                // (1) the random part of every slot: Philox block m = n / 2 gives the
+                // Box-Muller pair of steps 2m (cos) and 2m + 1 (sin)
+                double zc = 0.0;
 #pragma unroll
-            for (int h = 0; h < kLdsH; ++h) {
-                ex[h] = 1.0;
-                if (sl0 + h < len) {
-                    const uint64_t n = nf + (uint64_t)h;
-                    double z;
-                    if (h == 0 || (n & 1) == 0) {
-                        double z1, z2;
+                for (int h = 0; h < kLdsH; ++h) {
+                    ex[h] = 1.0;
+                    Vx[h] = 0.0;
+                    if (sl0 + h < len) {
+                        const uint64_t n = nf + (uint64_t)h;
+                        double z;
+                        if (h == 0 || (n & 1) == 0) {
+                            double z1, z2;
 #if defined(HE_LDS_SKIP) && (HE_LDS_SKIP & 1)
-                        {   // diagnostic build: no Box-Muller
-                            u32x4 ctr = {(uint32_t)(n >> 1), (uint32_t)(n >> 33), (uint32_t)gid, (uint32_t)((uint64_t)gid >> 32)};
-                            u32x4 x = philox4x32_10(ctr, p.key0, p.key1);
-                            z1 = u01(x.x, x.y) - 0.5;
-                            z2 = u01(x.z, x.w) - 0.5;
+                            {   // diagnostic build: no Box-Muller
+                                u32x4 ctr = {(uint32_t)(n >> 1), (uint32_t)(n >> 33), (uint32_t)gid, (uint32_t)((uint64_t)gid >> 32)};
+                                u32x4 x = philox4x32_10(ctr, p.key0, p.key1);
+                                z1 = u01(x.x, x.y) - 0.5;
+                                z2 = u01(x.z, x.w) - 0.5;
+                            }
+#else
+                            normals(p, gid, n >> 1, &z1, &z2);
+#endif
+                            z = (n & 1) ? z2 : z1;
+                            zc = z2;
+                        } else {
+                            z = zc;
                         }
-#else
-                        normals(p, gid, n >> 1, &z1, &z2);
-#endif
-                        z = (n & 1) ? z2 : z1;
-                        zc = z2;
-                    } else {
-                        z = zc;
-                    }
-                    const double dW = p.sqrt_dt * z;
+                        const double dW = p.sqrt_dt * z;
 #if defined(HE_LDS_SKIP) && (HE_LDS_SKIP & 16)
-                    ex[h] = 1.0 + p.drift + p.sqrt_var * dW;  // diagnostic build: no exp
+                        ex[h] = 1.0 + p.drift + p.sqrt_var * dW;  // diagnostic build: no exp
 #else
-                    ex[h] = exp_k(p.drift + p.sqrt_var * dW);  // rbergomi_sim.py:459-463
+                        ex[h] = exp_k(p.drift + p.sqrt_var * dW);  // rbergomi_sim.py:459-463
 #endif
+                    }
+                }
+            } else {
+                // (1) Heston (market_body's full-truncation Euler, rbergomi_sim.py:454-458):
+                // Philox block n -> (z1, z2) per step; dw1 drives v, rho dw1 + sqrt(1 - rho^2)
+                // dw2 the price
+                double w1[kLdsH], ws[kLdsH];
+#pragma unroll
+                for (int h = 0; h < kLdsH; ++h) {
+                    w1[h] = 0.0;
+                    ws[h] = 0.0;
+                    if (sl0 + h < len) {
+                        double z1, z2;
+                        normals(p, gid, nf + (uint64_t)h, &z1, &z2);
+                        const double dw1 = p.sqrt_dt * z1, dw2 = p.sqrt_dt * z2;
+                        w1[h] = dw1;
+                        ws[h] = p.h_rho * dw1 + p.h_sqrt1mrho2 * dw2;
+                    }
+                }
+                // (2a) the variance chain of the whole block in every lane (dw1 gathered from
+                // the env's lanes): M sqrt, no exp; the lane keeps vp and sqrt(vp) of its slots
+                double w1all[kLdsM];
+#pragma unroll
+                for (int r = 0; r < kLdsLanes; ++r)
+#pragma unroll
+                    for (int h = 0; h < kLdsH; ++h) w1all[r * kLdsH + h] = __shfl(w1[h], (lane % kLdsPEnvs) + r * kLdsPEnvs);
+                double vpx[kLdsH], sqx[kLdsH];
+#pragma unroll
+                for (int h = 0; h < kLdsH; ++h) vpx[h] = sqx[h] = Vx[h] = 0.0;
+                double v = Vbs;
+                uint32_t tq = tpb;
+#pragma unroll
+                for (int j = 0; j < kLdsM; ++j) {
+                    if (j == sl0) Vin = v;
+                    double vp = 0.0, sq = 0.0;
+                    if (j < len) {
+                        if (tq == 0) v = p.var;  // autoreset: a new episode starts from v0
+                        vp = v < 0.0 ? 0.0 : v;  // full truncation
+                        sq = sqrt(vp);
+                        v = (v + p.h_kappa * (p.h_theta - vp) * p.dt) + p.h_xi * sq * w1all[j];
+                        tq = (tq + 1 == T) ? 0u : tq + 1;
+                    }
+#pragma unroll
+                    for (int h = 0; h < kLdsH; ++h) {
+                        vpx[h] = (j == sl0 + h) ? vp : vpx[h];
+                        sqx[h] = (j == sl0 + h) ? sq : sqx[h];
+                        Vx[h] = (j == sl0 + h) ? v : Vx[h];
+                    }
+                }
+                Vbs = v;
+                // (2b) the lane's own growth factors exp(drift + diff), market_body's operands
+#pragma unroll
+                for (int h = 0; h < kLdsH; ++h) {
+                    const double drift = (p.mu - 0.5 * vpx[h]) * p.dt;
+                    const double diff = sqx[h] * ws[h];
+                    ex[h] = (sl0 + h < len) ? exp(drift + diff) : 1.0;
                 }
             }
             // (2) the f64 price chain: the block's growth factors gathered from the env's
@@ -2054,23 +2125,27 @@ __device__ __forceinline__ void lds_producer(const Params& p, int k_steps, const
                     const bool last = tp + 1 == T;
                     const double Sprev = (h == 0) ? Sin : Sx[h - 1];
                     const double Sm = last ? ((tp == 0) ? p.s0 : Sprev) : Sx[h];
+                    const double Vh = HESTON ? Vx[h] : p.var;
+                    const double Vm = HESTON ? (last ? ((tp == 0) ? p.var : ((h == 0) ? Vin : Vx[h > 0 ? h - 1 : 0])) : Vh) : p.var;
                     float C, P;
 #if defined(HE_LDS_SKIP) && (HE_LDS_SKIP & 2)
                     C = (float)Sm * 0.02f; P = (float)Sm * 0.018f;  // diagnostic build: no marks
 #else
-                    marks<HE_MODE_GBM>(p, Sm, p.var, &C, &P);
+                    marks<MODE>(p, Sm, Vm, &C, &P);
 #endif
                     const int sl = sl0 + h;
                     W.sc[wb][sl][le] = make_float2((float)Sx[h], C);
                     W.pp[wb][sl][le] = P;
+                    if (HESTON) W.vv[HESTON ? wb : 0][HESTON ? sl : 0][le] = (float)Vh;
                     // the book after the step into slot sl (episode step tp + 1, the new S,
                     // not lagged): market_body's tileC
-                    if (BOOK) W.bk[wb][sl][le] = book_value(p, Sx[h], p.var, (int32_t)(tp + 1), Mx[h]);
+                    if (BOOK) W.bk[wb][sl][le] = book_value(p, Sx[h], Vh, (int32_t)(tp + 1), Mx[h]);
                     if (kb + sl == k_steps - 1) {  // the market position after the launch
                         const uint32_t q = off + (uint32_t)(k_steps - 1);
                         cur.ep[pi] = ep0 + q / T;
                         cur.t[pi] = q % T + 1u;
                         cur.S[pi] = Sx[h];
+                        if (HESTON) cur.v[pi] = Vh;
                         cur.C[pi] = C;
                         cur.P[pi] = P;
                         if (BOOK) cur.M[pi] = Mx[h];
@@ -2714,13 +2789,13 @@ static bool lds_lean_config(const he_env* env, const Io& io) {
     return fast_config(env) && io.obs && io.rew && io.term && s0 >= 1e-30 && s0 <= 1e30 && ic <= 1e30;
 }
 
-// he_rollout through lds_rollout_kernel: GBM, no liability book (HE_LDS_ROLLOUT=0
+// he_rollout through lds_rollout_kernel: GBM or Heston, with or without a book (HE_LDS_ROLLOUT=0
 // falls back to the market-tile kernels).  The market position `cur` must be where the
 // envs are (no block generated ahead, no mid-block position): materialize_market
 // rewinds it, a no-op after an LDS rollout.  Afterwards `cur` is exact again and the
 // tiles are invalid (the next he_step regenerates its block from `cur`).
 static bool lds_rollout_eligible(const he_env* env) {
-    return env->lds_rollout && env->cfg.mode == HE_MODE_GBM;
+    return env->lds_rollout && (env->cfg.mode == HE_MODE_GBM || env->cfg.mode == HE_MODE_HESTON);
 }
 
 static he_status launch_lds_rollout(he_env* env, const Io& io, int k_total, hipStream_t st) {
@@ -2731,7 +2806,10 @@ static he_status launch_lds_rollout(he_env* env, const Io& io, int k_total, hipS
     const bool book = env->cfg.book_size > 0, lean = lds_lean_config(env, io);
     void (*kern)(const Params*, State, Io, int, Market);
     int threads;
-    if (book) {
+    if (env->cfg.mode == HE_MODE_HESTON) {  // generic steppers (the lean ones take a constant variance)
+        kern = book ? lds_rollout_kernel<HE_MODE_HESTON, true, false> : lds_rollout_kernel<HE_MODE_HESTON, false, false>;
+        threads = book ? LdsGeom<HE_MODE_HESTON, true>::threads : LdsGeom<HE_MODE_HESTON, false>::threads;
+    } else if (book) {
         kern = lean ? lds_rollout_kernel<HE_MODE_GBM, true, true> : lds_rollout_kernel<HE_MODE_GBM, true, false>;
         threads = LdsGeom<HE_MODE_GBM, true>::threads;
     } else {

@@ -506,6 +506,7 @@ def test_fused_rollouts_mixed_with_steps_resets_and_checkpoints(mode, monkeypatc
             assert torch.equal(a, b), i
 
 
+HESTON_GEN = dict(heston_kappa=2.0, heston_theta=0.029028, heston_xi=0.3, heston_rho=-0.7)
 LDS_CASES = {
     # name: (n_envs, generate kwargs, env kwargs, rollout lengths)
     "train": (1000, dict(episode_length=40), dict(loss_type="abs", pnl_penalty_weight=0.001, lambda_cost=0.0001,
@@ -524,6 +525,19 @@ LDS_CASES = {
                                                                 dict(type="put", strike=480.0, expiry=20,
                                                                      quantity=-10.0)]),
                             dict(loss_type="mse", record_metrics=False), (5, 64, 13, 71)),
+    # Heston (the producers run the variance chain; v per slot in LDS)
+    "heston": (1000, dict(episode_length=40, **HESTON_GEN), dict(loss_type="abs", pnl_penalty_weight=0.001,
+                                                                lambda_cost=0.0001, theta_weight=0.0002,
+                                                                slippage_bps=1.0), (64, 37, 100, 9)),
+    "heston_T2": (130, dict(episode_length=2, **HESTON_GEN), {}, (7, 12, 1, 20)),
+    "heston_T1": (67, dict(episode_length=1, **HESTON_GEN), dict(record_metrics=False), (9, 3)),
+    "heston_barrier_ragged": (333, dict(episode_length=29, **HESTON_GEN,
+                                        book=[dict(type="uo_call", strike=496.0, barrier=520.0, expiry=40,
+                                                   quantity=-50.0),
+                                              dict(type="put", strike=480.0, expiry=20, quantity=-10.0)]),
+                              dict(loss_type="mse", record_metrics=False), (5, 64, 13, 71)),
+    "heston_hot_xi": (257, dict(episode_length=25, heston_kappa=0.5, heston_theta=0.09, heston_xi=2.5,
+                                heston_rho=0.3, variance=0.04), {}, (1, 5, 12, 13, 11, 37, 64, 3)),
 }
 
 
@@ -542,8 +556,8 @@ def test_lds_rollout_equals_tile_rollout(case, monkeypatch):
     runs = []
     for lds in ("1", "0"):
         monkeypatch.setenv("HE_LDS_ROLLOUT", lds)
-        env = HedgingVecEnv(n, mode="gbm", generate=gen, seed=31, global_env_offset=5, return_numpy=False,
-                            info_keys=(), **kw)
+        env = HedgingVecEnv(n, mode="heston" if case.startswith("heston") else "gbm", generate=gen, seed=31,
+                            global_env_offset=5, return_numpy=False, info_keys=(), **kw)
         got = [env.reset_tensors().clone()]
         a0 = 0
         for k in ks:
