@@ -760,9 +760,8 @@ def launch(args, argv):
         if args.workload == "env" and not args.no_pmc:
             t, v = pmc_traffic(args)
             parent.update(pmc=t, pmc_note=v if t is None else None, pmc_counters=v if t is not None else None)
-            if CONFIGS[args.config]["gen"].get("book"):
-                vv, note = pmc_valu(args)
-                parent.update(valu=vv, valu_note=note)
+            vv, note = pmc_valu(args)
+            parent.update(valu=vv, valu_note=note)
         if not args.no_cpu_baseline:
             parent["cpu_baseline"] = (cpu_baseline(args.cpu_seconds) if args.workload == "env"
                                       else None)
@@ -828,8 +827,9 @@ def main(argv=None):
     elif world == 1:
         if not args.no_pmc:
             pmc = pmc_traffic(args)
-            if has_book:  # VALU-bound configurations: the instruction-issue side
-                valu = pmc_valu(args)
+            # the instruction-issue side: the LDS kernel makes the market on chip, so every
+            # configuration is partly VALU-bound (with a book or Heston, mostly)
+            valu = pmc_valu(args)
         if not args.no_cpu_baseline:
             cpu = cpu_baseline(args.cpu_seconds)   # before the GPU is touched (forks workers)
     dist, backend = None, None

@@ -1566,7 +1566,13 @@ __global__ __launch_bounds__(kBlock, HE_FUSED_WAVES) void step_market_kernel(Par
 #define HE_LDS_PRIO_PROD 1
 #endif
 #ifndef HE_LDS_LANES_BOOK
-#define HE_LDS_LANES_BOOK 4  // a liability book: its marks are most of the producers' work
+// a liability book or Heston: 2 producer waves (4 waves per workgroup, 4 workgroups per
+// CU at 128 VGPRs) -- same-box A/B against 4 (r02 g2): config 4 1.11e10 -> 1.21e10,
+// config 5 1.19e10 -> 1.25e10 env-steps/s
+#define HE_LDS_LANES_BOOK 2
+#endif
+#ifndef HE_LDS_MINWAVES_BOOK
+#define HE_LDS_MINWAVES_BOOK 4
 #endif
 constexpr int kLdsEnvs = 64;                         // envs per workgroup = one stepper wave
 constexpr int kLdsM = HE_LDS_M;                      // slots per LDS market block
@@ -1589,9 +1595,9 @@ struct LdsGeom {
     static constexpr int threads = 64 * (2 + prod);  // + the reward and the obs stepper waves
     static constexpr int H = kLdsM / lanes;
 #ifdef HE_LDS_MINWAVES
-    static constexpr int minwaves = (BOOK || HESTON) ? 4 : HE_LDS_MINWAVES;
+    static constexpr int minwaves = (BOOK || HESTON) ? HE_LDS_MINWAVES_BOOK : HE_LDS_MINWAVES;
 #else
-    static constexpr int minwaves = (BOOK || HESTON) ? 4 : (4 * (2 + prod) + 3) / 4 + 1;
+    static constexpr int minwaves = (BOOK || HESTON) ? HE_LDS_MINWAVES_BOOK : (4 * (2 + prod) + 3) / 4 + 1;
 #endif
     static_assert(H * lanes == kLdsM && penvs * lanes == kLdsEnvs, "producer lane layout");
 };

@@ -7,14 +7,15 @@
 // pass over [N, 13] per step plus per-env Python lists -- the bottleneck once N is in
 // the tens of thousands.  Here one step is two launches of G <= 256 workgroups, each
 // owning a slice of 256 rows staged through LDS as flat coalesced copies:
-//   vn_moments_kernel  exact two-pass f64 mean / M2 of the slice's obs columns and of the
-//                      updated running returns, stored as a partial (+ a snapshot of the
-//                      old statistics);
-//   vn_apply_kernel    every workgroup merges all G partials itself (Chan et al.; the
-//                      same block reductions in the same order, so the same result
-//                      everywhere), applies RunningMeanStd.update_from_moments (workgroup
-//                      0 stores it), and normalizes its rows: obs / reward / terminal obs,
-//                      returns[done] = 0 and the Monitor episode sums.
+//   vn_moments_kernel  one pass of f64 sums of d and d^2, d = x - shift (the batch's row 0
+//                      for obs, the old running mean for the returns), over the slice's obs
+//                      columns and updated running returns, stored as a partial (+ a
+//                      snapshot of the old statistics and the shifts);
+//   vn_apply_kernel    every workgroup merges all G partials itself (one block reduction in
+//                      a fixed order, so the same result everywhere), applies
+//                      RunningMeanStd.update_from_moments (workgroup 0 stores it), and
+//                      normalizes its rows by (x - mean) * (1 / sqrt(var + eps)): obs /
+//                      reward / terminal obs, returns[done] = 0 and the Monitor episode sums.
 // Deterministic for a given grid; no atomics and no waiting between workgroups (the
 // kernel boundary publishes the partials).  Eval mode (no statistics update) is the
 // second launch alone.  68 B of obs + reward read and written per env.
@@ -32,8 +33,9 @@ constexpr int kD = HE_OBS_DIM;
 constexpr int kVnThreads = 256;
 constexpr int kVnMaxBlocks = 256;   // workgroups of a launch = partials merged per workgroup (one per thread)
 
-// scratch layout: [kPart][kVnMaxBlocks] doubles, then the 2 kD + 4 old statistics
-constexpr int kPart = 2 * kD + 3;   // count, mean[D], M2[D], ret_mean, ret_M2
+// scratch layout: [kPart][kVnMaxBlocks] doubles, then the 2 kD + 4 old statistics and
+// the kD + 1 shifts of the sums
+constexpr int kPart = 2 * kD + 3;   // count, S1[D + 1] (obs, returns), S2[D + 1]
 
 struct VnArgs {
     int64_t n;
@@ -74,26 +76,27 @@ __device__ __forceinline__ void rms_update(double* mean, double* var, double* co
 
 __device__ __forceinline__ double clipd(double x, double lo, double hi) { return x < lo ? lo : (x > hi ? hi : x); }
 
-// Sum of v[0..NV) over the block into out[0..NV) (LDS), NV <= 16: every thread stores
-// its NV values (row stride NV + 1), then 16 threads per value sum 16 rows each and
-// finish with a 4-level butterfly inside their 16-lane group -- 16 LDS reads and 4
-// shuffles per thread, against 6 shuffle levels per value (~180 LDS permutes per wave)
-// of a butterfly over the whole wave.  The summation order is fixed.
+// Sum of v[0..NV) over the block into out[0..NV) (LDS), NV <= 32: every thread stores
+// its NV values (row stride NV + 1), then TPV = 16 (NV <= 16) or 8 threads per value sum
+// 256 / TPV rows each and finish with a butterfly inside their TPV-lane group -- against
+// 6 shuffle levels per value (~180 LDS permutes per wave) of a butterfly over the whole
+// wave.  The summation order is fixed.
 template <int NV>
 __device__ __forceinline__ void block_sum(const double* v, double* buf, double* out) {
-    static_assert(NV <= 16 && NV * 16 <= kVnThreads, "16 threads per value");
+    constexpr int TPV = NV <= 16 ? 16 : 8;
+    static_assert(NV <= 32 && NV * TPV <= kVnThreads, "threads per value");
     constexpr int S = NV + 1;
     const int t = threadIdx.x;
 #pragma unroll
     for (int c = 0; c < NV; ++c) buf[t * S + c] = v[c];
     __syncthreads();
-    if (t < NV * 16) {
-        const int c = t >> 4, j = t & 15;
+    if (t < NV * TPV) {
+        const int c = t / TPV, j = t % TPV;
         double x = 0.0;
 #pragma unroll
-        for (int k = 0; k < kVnThreads / 16; ++k) x += buf[(j + 16 * k) * S + c];
+        for (int k = 0; k < kVnThreads / TPV; ++k) x += buf[(j + TPV * k) * S + c];
 #pragma unroll
-        for (int m = 8; m >= 1; m >>= 1) x += __shfl_xor(x, m, 16);
+        for (int m = TPV / 2; m >= 1; m >>= 1) x += __shfl_xor(x, m, TPV);
         if (j == 0) out[c] = x;
     }
     __syncthreads();
@@ -123,151 +126,135 @@ __device__ __forceinline__ VnRows rows_of(const VnArgs& a) {
     return w;
 }
 
-// Launch 1 (training): per workgroup, the exact two-pass f64 mean / M2 of its rows' obs
-// columns and of the updated running returns, stored as a partial.  The kernel
-// boundary publishes the partials to launch 2 -- no atomics, no waiting (a single
-// launch with a grid-wide wait measured 25 us at 65,536 envs: four dependent
+// Launch 1 (training): per workgroup, the sums of the deviations d = x - x0 and d^2 of
+// its rows' obs columns (x0 = the batch's row 0: a data point, so d is centred to within
+// the batch's spread and S2 - S1^2 / n keeps ~all of f64's digits) and of the updated
+// running returns (shifted by the old running mean), in one pass, stored as a partial.
+// The kernel boundary publishes the partials to launch 2 -- no atomics, no waiting (a
+// single launch with a grid-wide wait measured 25 us at 65,536 envs: four dependent
 // device-coherent round trips between workgroups).
 __global__ void __launch_bounds__(kVnThreads) vn_moments_kernel(VnArgs a) {
-    __shared__ double sh[kVnThreads * (kD + 2)];
-    __shared__ double smean[kD + 1];
-    __shared__ double sm2[kD + 1];
+    __shared__ double sh[kVnThreads * (kPart + 1)];
+    __shared__ double ssum[kPart];
     __shared__ float tile[kVnChunk * kD];
     const VnRows w = rows_of(a);
     const bool upd_ret = a.training && !a.reset;
     const int t = threadIdx.x;
-    double v[kD + 1];
+    double sft[kD + 1];
 #pragma unroll
-    for (int c = 0; c <= kD; ++c) v[c] = 0.0;
-    for (int64_t c0 = w.r0; c0 < w.r1; c0 += kVnChunk) {   // pass 1: sums (and the returns)
+    for (int c = 0; c < kD; ++c) sft[c] = (double)a.obs[c];
+    sft[kD] = a.stats[2 * kD + 1];
+    double v[kPart - 1];
+#pragma unroll
+    for (int c = 0; c < kPart - 1; ++c) v[c] = 0.0;
+    for (int64_t c0 = w.r0; c0 < w.r1; c0 += kVnChunk) {
         const int rows = (int)((w.r1 - c0) < kVnChunk ? (w.r1 - c0) : kVnChunk);
         if (a.upd_obs) load_tile(tile, a.obs, c0, rows);
         if (t < rows) {
             if (a.upd_obs) {
 #pragma unroll
-                for (int c = 0; c < kD; ++c) v[c] += (double)tile[t * kD + c];
+                for (int c = 0; c < kD; ++c) {
+                    const double d = (double)tile[t * kD + c] - sft[c];
+                    v[c] += d;
+                    v[kD + 1 + c] += d * d;
+                }
             }
             if (upd_ret) {
                 const int64_t r = c0 + t;
                 const double ret = a.returns[r] * a.gamma + (double)a.reward[r];   // VecNormalize._update_reward
                 a.returns[r] = ret;
-                v[kD] += ret;
+                const double d = ret - sft[kD];
+                v[kD] += d;
+                v[2 * kD + 1] += d * d;
             }
         }
         __syncthreads();
     }
-    block_sum<kD + 1>(v, sh, smean);
-    if (t <= kD) smean[t] = (w.cnt > 0.0) ? smean[t] / w.cnt : 0.0;
-    __syncthreads();
-#pragma unroll
-    for (int c = 0; c <= kD; ++c) v[c] = 0.0;
-    const bool resident = w.r1 - w.r0 <= kVnChunk;   // the tile still holds the rows
-    for (int64_t c0 = w.r0; c0 < w.r1; c0 += kVnChunk) {   // pass 2: squared deviations
-        const int rows = (int)((w.r1 - c0) < kVnChunk ? (w.r1 - c0) : kVnChunk);
-        if (!resident && a.upd_obs) load_tile(tile, a.obs, c0, rows);
-        if (t < rows) {
-            if (a.upd_obs) {
-#pragma unroll
-                for (int c = 0; c < kD; ++c) {
-                    const double d = (double)tile[t * kD + c] - smean[c];
-                    v[c] += d * d;
-                }
-            }
-            if (upd_ret) {
-                const double d = a.returns[c0 + t] - smean[kD];
-                v[kD] += d * d;
-            }
-        }
-        if (!resident) __syncthreads();
-    }
-    block_sum<kD + 1>(v, sh, sm2);
-    // partials [kPart][kVnMaxBlocks] (launch 2's thread k reads column k: coalesced)
+    block_sum<kPart - 1>(v, sh, ssum);
+    // partials [kPart][kVnMaxBlocks] (launch 2's thread k reads column k: coalesced):
+    // count, S1[kD + 1], S2[kD + 1]
     double* part = a.part + blockIdx.x;
-    if (t <= kD) {
-        part[((t < kD) ? 1 + t : 1 + 2 * kD) * kVnMaxBlocks] = smean[t];
-        part[((t < kD) ? 1 + kD + t : 2 + 2 * kD) * kVnMaxBlocks] = sm2[t];
-    }
+    if (t < kPart - 1) part[(1 + t) * kVnMaxBlocks] = ssum[t];
     if (t == 0) part[0] = w.cnt;
-    // the statistics before this step, for launch 2 (whose workgroup 0 overwrites them)
-    if (blockIdx.x == 0 && t < 2 * kD + 4) a.part[kVnMaxBlocks * kPart + t] = a.stats[t];
+    // the statistics before this step and the shifts, for launch 2 (whose workgroup 0
+    // overwrites the statistics)
+    double* snap = a.part + kVnMaxBlocks * kPart;
+    if (blockIdx.x == 0 && t < 2 * kD + 4) snap[t] = a.stats[t];
+    if (blockIdx.x == 0 && t <= kD) snap[2 * kD + 4 + t] = sft[t];
 }
 
-// Launch 2: every workgroup merges all the partials itself (the same reductions in the
-// same order, so the same statistics everywhere; workgroup 0 stores them), then
+// Launch 2: every workgroup merges all the partials itself (one block reduction in a
+// fixed order, so the same statistics everywhere; workgroup 0 stores them), then
 // normalizes its rows: obs / reward / terminal obs, returns[done] = 0, Monitor sums.
 __global__ void __launch_bounds__(kVnThreads) vn_apply_kernel(VnArgs a) {
-    __shared__ double sh[kVnThreads * (kD + 3)];
-    __shared__ double smean[kD + 2];
-    __shared__ double sm2[kD + 2];
-    __shared__ double snorm[kD][2];   // per obs column: mean, sqrt(var + eps)
-    __shared__ double srstd;
+    __shared__ double sh[kVnThreads * (kPart + 1)];
+    __shared__ double ssum[kPart];
+    __shared__ double snorm[kD][2];   // per obs column: mean, 1 / sqrt(var + eps)
+    __shared__ double srinv;
     __shared__ float tile[kVnChunk * kD];
     const VnRows w = rows_of(a);
     const bool upd_ret = a.training && !a.reset;
     const int t = threadIdx.x;
     const bool resident = w.r1 - w.r0 <= kVnChunk;
-    if (resident && w.r1 > w.r0) load_tile(tile, a.obs, w.r0, (int)(w.r1 - w.r0));
+    // the rows' loads first: they are in flight while the partials are merged
+    float xr[kD];
+    const int nres = resident ? (int)(w.r1 - w.r0) * kD : 0;
+    const float* src = a.obs + w.r0 * kD;
+#pragma unroll
+    for (int q = 0; q < kD; ++q) {
+        const int k = t + q * kVnThreads;
+        xr[q] = k < nres ? src[k] : 0.0f;
+    }
     if (a.upd_obs || upd_ret) {
-        // thread k holds partial k; the batch mean as sum n_k mean_k / n, then
-        // M2 = sum M2_k + n_k (mean_k - mean)^2 -- block reductions in a fixed order
         const double* P = a.part + t;
         const bool has = t < a.blocks;
-        const double n_k = has ? P[0] : 0.0;
-        double mk[kD + 1], qk[kD + 1];
+        double v[kPart];
 #pragma unroll
-        for (int c = 0; c <= kD; ++c) {
-            mk[c] = has ? P[((c < kD) ? 1 + c : 1 + 2 * kD) * kVnMaxBlocks] : 0.0;
-            qk[c] = has ? P[((c < kD) ? 1 + kD + c : 2 + 2 * kD) * kVnMaxBlocks] : 0.0;
-        }
-        double v[kD + 2];
-#pragma unroll
-        for (int c = 0; c <= kD; ++c) v[c] = n_k * mk[c];
-        v[kD + 1] = n_k;
-        block_sum<kD + 2>(v, sh, smean);   // smean[0..kD] = sums, smean[kD + 1] = n
-        const double n_a = smean[kD + 1];
-#pragma unroll
-        for (int c = 0; c <= kD; ++c) {
-            const double d = mk[c] - smean[c] / n_a;
-            v[c] = qk[c] + n_k * (d * d);
-        }
-        v[kD + 1] = 0.0;
-        block_sum<kD + 2>(v, sh, sm2);
+        for (int c = 0; c < kPart; ++c) v[c] = has ? P[c * kVnMaxBlocks] : 0.0;
+        block_sum<kPart>(v, sh, ssum);   // ssum[0] = n, [1 .. kD + 1] = S1, then S2
         const int c = t;
         if (c <= kD) {
-            const double mean_a = smean[c] / n_a, m2_a = sm2[c];
-            // np.mean / np.var(ddof=0) of the batch, then update_from_moments (:update)
-            const int im = (c < kD) ? c : 2 * kD + 1, iv = (c < kD) ? kD + c : 2 * kD + 2;
             const double* old = a.part + kVnMaxBlocks * kPart;   // launch 1's snapshot
+            const double n_a = ssum[0], s1 = ssum[1 + c], s2 = ssum[2 + kD + c];
+            // np.mean / np.var(ddof=0) of the batch from the shifted sums, then
+            // RunningMeanStd.update_from_moments
+            const double mean_a = old[2 * kD + 4 + c] + s1 / n_a;
+            const double m2 = s2 - s1 * (s1 / n_a);
+            const double var_a = (m2 > 0.0 ? m2 : 0.0) / n_a;
+            const int im = (c < kD) ? c : 2 * kD + 1, iv = (c < kD) ? kD + c : 2 * kD + 2;
             double mean = old[im], var = old[iv];
             if ((c < kD && a.upd_obs) || (c == kD && upd_ret)) {
                 double count = (c < kD) ? old[2 * kD] : old[2 * kD + 3];
-                rms_update(&mean, &var, &count, mean_a, m2_a / n_a, n_a);
+                rms_update(&mean, &var, &count, mean_a, var_a, n_a);
                 if (blockIdx.x == 0) {
                     if (c == 0) a.stats[2 * kD] = count;
                     if (c == kD) a.stats[2 * kD + 3] = count;
+                    a.stats[im] = mean;
+                    a.stats[iv] = var;
                 }
             }
             if (c < kD) {
                 snorm[c][0] = mean;
-                snorm[c][1] = sqrt(var + a.eps);
+                snorm[c][1] = 1.0 / sqrt(var + a.eps);
             } else {
-                srstd = sqrt(var + a.eps);
+                srinv = 1.0 / sqrt(var + a.eps);
             }
-            smean[c] = mean;   // stored below, after every thread has read the old values
-            sm2[c] = var;
         }
         __syncthreads();
-        if (blockIdx.x == 0 && c <= kD) {
-            const int im = (c < kD) ? c : 2 * kD + 1, iv = (c < kD) ? kD + c : 2 * kD + 2;
-            a.stats[im] = smean[c];
-            a.stats[iv] = sm2[c];
-        }
     } else {
         if (t < kD) {
             snorm[t][0] = a.stats[t];
-            snorm[t][1] = sqrt(a.stats[kD + t] + a.eps);
+            snorm[t][1] = 1.0 / sqrt(a.stats[kD + t] + a.eps);
         }
-        if (t == 0) srstd = sqrt(a.stats[2 * kD + 2] + a.eps);
+        if (t == 0) srinv = 1.0 / sqrt(a.stats[2 * kD + 2] + a.eps);
+        __syncthreads();
+    }
+    if (resident) {
+#pragma unroll
+        for (int q = 0; q < kD; ++q) {
+            const int k = t + q * kVnThreads;
+            if (k < nres) tile[k] = xr[q];
+        }
         __syncthreads();
     }
     for (int64_t c0 = w.r0; c0 < w.r1; c0 += kVnChunk) {
@@ -280,7 +267,7 @@ __global__ void __launch_bounds__(kVnThreads) vn_apply_kernel(VnArgs a) {
 #pragma unroll
                 for (int c = 0; c < kD; ++c) {
                     const float x = tile[t * kD + c];
-                    tile[t * kD + c] = (float)clipd(((double)x - snorm[c][0]) / snorm[c][1], -a.clip_obs, a.clip_obs);
+                    tile[t * kD + c] = (float)clipd(((double)x - snorm[c][0]) * snorm[c][1], -a.clip_obs, a.clip_obs);
                 }
             }
             if (a.reset) {
@@ -288,13 +275,13 @@ __global__ void __launch_bounds__(kVnThreads) vn_apply_kernel(VnArgs a) {
             } else {
                 const bool dn = a.done ? a.done[r] != 0 : false;
                 const float rw = a.reward[r];
-                a.rew_out[r] = a.norm_reward ? (float)clipd((double)rw / srstd, -a.clip_rew, a.clip_rew) : rw;
+                a.rew_out[r] = a.norm_reward ? (float)clipd((double)rw * srinv, -a.clip_rew, a.clip_rew) : rw;
                 if (dn && a.tobs && a.tobs_out) {   // rare: per-row accesses
 #pragma unroll
                     for (int c = 0; c < kD; ++c) {
                         const float x = a.tobs[r * kD + c];
                         a.tobs_out[r * kD + c] =
-                            a.norm_obs ? (float)clipd(((double)x - snorm[c][0]) / snorm[c][1], -a.clip_obs, a.clip_obs)
+                            a.norm_obs ? (float)clipd(((double)x - snorm[c][0]) * snorm[c][1], -a.clip_obs, a.clip_obs)
                                        : x;
                     }
                 }
@@ -318,7 +305,7 @@ __global__ void __launch_bounds__(kVnThreads) vn_apply_kernel(VnArgs a) {
         float* dst = a.obs_out + c0 * kD;
         const int nf = rows * kD;
         for (int k = t; k < nf; k += kVnThreads) dst[k] = tile[k];
-        __syncthreads();
+        if (!resident) __syncthreads();
     }
 }
 
@@ -402,7 +389,7 @@ int64_t he_vecnorm_stats_len(int32_t obs_dim) { return 2 * (int64_t)obs_dim + 4;
 int64_t he_vecnorm_scratch_bytes(int64_t n, int32_t obs_dim) {
     (void)n;
     (void)obs_dim;
-    return ((int64_t)kVnMaxBlocks * kPart + 2 * kD + 4) * (int64_t)sizeof(double);  // partials + old statistics
+    return ((int64_t)kVnMaxBlocks * kPart + 3 * kD + 5) * (int64_t)sizeof(double);  // partials + old statistics + shifts
 }
 
 he_status he_vecnorm_init(double* stats, int32_t obs_dim, void* stream) {
