@@ -163,6 +163,7 @@ struct Params {
     int32_t book_n;
     const BookOpt* book;    // device copy [book_n], read through the scalar cache
     const double* book_tab; // [m][4] = {sqrt(m dt), 1 / sqrt(m dt), exp(-r m dt), exp(r m dt)}, m = 0..max expiry
+    int32_t book_rows;      // max expiry + 1
     double book_rst;        // book value of the reset market (t = 0, S0, v0)
     double* tileC;          // [M+1][N] f64 book value of every slot
 #ifdef HE_TIMING
@@ -501,12 +502,12 @@ __device__ __forceinline__ void ncdf_from_tail(double d, double q, double* pos, 
 
 // One book option (branch-free in the lane-varying quantities: remaining steps, running max).
 __device__ __forceinline__ double book_option(const Params& p, const BookOpt& o, const BookEnv& b, int32_t m,
-                                              double runmax) {
+                                              double runmax, const double* tab) {
     const double K = o.K, S = b.S, r = p.r_d;
     const bool live = m > 0 && b.sig > 0.0;             // tau = m dt > 0 (else intrinsic)
     const int32_t mc = live ? m : 1;                    // a valid table row either way
     const double tau = (double)mc * p.dt;
-    const double* e = p.book_tab + 4 * mc;
+    const double* e = tab + 4 * mc;
     const double sst = b.sig * e[0];
     const double isst = b.isig * e[1];
     const double d1 = ((b.lnS - o.lnK) + (r + 0.5 * b.s2) * tau) * isst;
@@ -564,8 +565,9 @@ __device__ __forceinline__ double book_option(const Params& p, const BookOpt& o,
 }
 
 // sum_k q_k * 100 * V_k after step t of the episode (variance var: GBM constant,
-// Heston the env's v_t).
-__device__ __forceinline__ double book_value(const Params& p, double S, double var, int32_t t, double runmax) {
+// Heston the env's v_t).  tab: the tau table, p.book_tab or its LDS copy.
+__device__ __forceinline__ double book_value(const Params& p, double S, double var, int32_t t, double runmax,
+                                             const double* tab) {
     BookEnv b;
     b.S = S;
     b.lnS = log(S);
@@ -574,11 +576,17 @@ __device__ __forceinline__ double book_value(const Params& p, double S, double v
     b.s2 = b.sig * b.sig;
     b.lam = (p.r_d + 0.5 * b.s2) / b.s2;
     double B = 0.0;
+#ifdef HE_BOOK_UNROLL
+#pragma unroll HE_BOOK_UNROLL
+#endif
     for (int k = 0; k < p.book_n; ++k) {
         const BookOpt o = p.book[k];
-        B = B + o.q100 * book_option(p, o, b, o.expiry - t, runmax);
+        B = B + o.q100 * book_option(p, o, b, o.expiry - t, runmax, tab);
     }
     return B;
+}
+__device__ __forceinline__ double book_value(const Params& p, double S, double var, int32_t t, double runmax) {
+    return book_value(p, S, var, t, runmax, p.book_tab);
 }
 
 // Box-Muller pair of the Philox block of (seed, global env id, env-step index n).
@@ -1576,7 +1584,11 @@ __global__ __launch_bounds__(kBlock, HE_FUSED_WAVES) void step_market_kernel(Par
 #endif
 constexpr int kLdsEnvs = 64;                         // envs per workgroup = one stepper wave
 constexpr int kLdsM = HE_LDS_M;                      // slots per LDS market block
+#ifdef HE_LDS_PREFETCH
+constexpr int kLdsPrefetch = HE_LDS_PREFETCH;  // A/B builds
+#else
 constexpr int kLdsPrefetch = kLdsM % 6 == 0 ? 6 : (kLdsM % 4 == 0 ? 4 : kLdsM);  // steps of actions in flight
+#endif
 static_assert(kLdsM % kLdsPrefetch == 0, "the action ring index is the slot mod D");
 
 // Workgroup geometry of one market configuration: `lanes` producer lanes per env in
@@ -1606,6 +1618,10 @@ struct LdsGeom {
 // (12 B per env-slot, conflict-free lane accesses), the obs wave's two row staging
 // tiles, and with a book its f64 value per slot: 19.7 KB at M = 8 (GBM), so all 65,536
 // envs of BASELINE configs[1] are resident at once; 27.9 KB with a book.
+// Book tau-table rows held in LDS (8 KB): a book whose latest expiry is past it takes the
+// tile kernels (lds_rollout_eligible).  The producers' per-option table reads are then LDS
+// reads instead of L1/L2 gathers on their critical chain.
+constexpr int kLdsBookRows = 256;
 template <int MODE, bool BOOK>
 struct LdsMarketT {
     float2 sc[2][kLdsM][kLdsEnvs];
@@ -1613,9 +1629,10 @@ struct LdsMarketT {
     float stage[2][kLdsEnvs * kObs];                                   // obs row staging, by step parity
     double bk[BOOK ? 2 : 1][BOOK ? kLdsM : 1][kLdsEnvs];                // book value of every slot
     float vv[MODE == HE_MODE_HESTON ? 2 : 1][MODE == HE_MODE_HESTON ? kLdsM : 1][kLdsEnvs];  // Heston: f32 v_t
+    double btab[BOOK ? kLdsBookRows : 1][4];  // the book's tau table (p.book_tab), copied at launch start
 };
-static_assert(sizeof(LdsMarketT<HE_MODE_GBM, false>) <= 40 * 1024, "4 workgroups per CU");
-static_assert(sizeof(LdsMarketT<HE_MODE_HESTON, true>) <= 40 * 1024, "4 workgroups per CU");
+static_assert(kLdsM > 8 || sizeof(LdsMarketT<HE_MODE_GBM, false>) <= 40 * 1024, "4 workgroups per CU");
+static_assert(kLdsM > 8 || sizeof(LdsMarketT<HE_MODE_HESTON, true>) <= 40 * 1024, "4 workgroups per CU");
 
 #ifdef HE_LDS_TIMING
 // Diagnostic builds only: per wave role (0 reward, 1 obs, 2-3 producers) and workgroup,
@@ -2145,7 +2162,7 @@ __device__ __forceinline__ void lds_producer(const Params& p, int k_steps, const
                     if (HESTON) W.vv[HESTON ? wb : 0][HESTON ? sl : 0][le] = (float)Vh;
                     // the book after the step into slot sl (episode step tp + 1, the new S,
                     // not lagged): market_body's tileC
-                    if (BOOK) W.bk[wb][sl][le] = book_value(p, Sx[h], Vh, (int32_t)(tp + 1), Mx[h]);
+                    if (BOOK) W.bk[wb][sl][le] = book_value(p, Sx[h], Vh, (int32_t)(tp + 1), Mx[h], &W.btab[0][0]);
                     if (kb + sl == k_steps - 1) {  // the market position after the launch
                         const uint32_t q = off + (uint32_t)(k_steps - 1);
                         cur.ep[pi] = ep0 + q / T;
@@ -2180,6 +2197,11 @@ __global__ __launch_bounds__((LdsGeom<MODE, BOOK>::threads), (LdsGeom<MODE, BOOK
     const Params& p = *pc;  // read through the scalar cache (a by-value copy spills)
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int64_t base = (int64_t)blockIdx.x * kLdsEnvs;
+    if constexpr (BOOK) {  // the tau table into LDS (rows <= kLdsBookRows: lds_rollout_eligible)
+        const int nv = 4 * p.book_rows;
+        for (int k = threadIdx.x; k < nv; k += LdsGeom<MODE, BOOK>::threads) (&lm.btab[0][0])[k] = p.book_tab[k];
+        __syncthreads();
+    }
     if (wave == 0) lds_stepper<MODE, BOOK, LEAN, false>(p, s, io, k_steps, cur, lm, base);
     else if (wave == 1) lds_stepper<MODE, BOOK, LEAN, true>(p, s, io, k_steps, cur, lm, base);
     else lds_producer<MODE, BOOK>(p, k_steps, cur, lm, base, wave - 2);
@@ -2362,6 +2384,7 @@ struct he_env {
     Params* dparams = nullptr;  // device copies of tile_params(env, 0 / 1) for step1_kernel
     BookOpt* dbook = nullptr;   // liability book, device copy (generate modes)
     double* dbook_tab = nullptr;  // book tau table (book_option)
+    int32_t book_rows = 0;        // its rows: max expiry + 1
     unsigned long long* scratch_count = nullptr;  // he_rollout_policy without records
     double book_rst = 0.0;      // book value of the reset market (host copy)
     int64_t n_paths = 0;
@@ -2503,6 +2526,7 @@ static void fill_params(he_env* env) {
     p.book_n = is_generate(env) ? c.book_size : 0;
     p.book = env->dbook;
     p.book_tab = env->dbook_tab;
+    p.book_rows = env->book_rows;
     p.book_rst = env->book_rst;
     p.tileC = nullptr;
 #ifdef HE_TIMING
@@ -2801,7 +2825,8 @@ static bool lds_lean_config(const he_env* env, const Io& io) {
 // rewinds it, a no-op after an LDS rollout.  Afterwards `cur` is exact again and the
 // tiles are invalid (the next he_step regenerates its block from `cur`).
 static bool lds_rollout_eligible(const he_env* env) {
-    return env->lds_rollout && (env->cfg.mode == HE_MODE_GBM || env->cfg.mode == HE_MODE_HESTON);
+    return env->lds_rollout && (env->cfg.mode == HE_MODE_GBM || env->cfg.mode == HE_MODE_HESTON) &&
+           (env->cfg.book_size == 0 || env->book_rows <= kLdsBookRows);
 }
 
 static he_status launch_lds_rollout(he_env* env, const Io& io, int k_total, hipStream_t st) {
@@ -3078,6 +3103,7 @@ he_status he_create(const he_config* cfg, he_env** out) {
         int32_t max_exp = 1;
         for (int k = 0; k < c.book_size; ++k) max_exp = (c.book[k].expiry > max_exp) ? c.book[k].expiry : max_exp;
         HE_HIP(env, hipMalloc(&env->dbook_tab, (size_t)4 * (size_t)(max_exp + 1) * sizeof(double)));
+        env->book_rows = max_exp + 1;
         hipLaunchKernelGGL(book_tab_kernel, dim3((unsigned)((max_exp + 256) / 256)), dim3(256), 0, 0, env->dbook_tab,
                            max_exp + 1, c.dt, c.risk_free_rate);
         HE_HIP(env, hipGetLastError());
