@@ -27,7 +27,9 @@ cd $R
 grep "^{" $O/bench_rocprof.log > $O/bench_under_rocprof.jsonl
 for c in 3 4 5; do
   echo "[$(date +%T)] bench config $c"
-  timeout -k 10 300 python -u bench.py --config $c --no-pmc --no-cpu-baseline --no-step-api > $O/b_cfg$c.log 2>&1 || { tail -20 $O/b_cfg$c.log; exit 1; }
+  # configs 4 and 5 (book / Heston: producer-bound) with the PMC passes: traffic + VALU issue
+  pmc=--no-pmc; [ $c != 3 ] && pmc=""
+  timeout -k 10 400 python -u bench.py --config $c $pmc --no-cpu-baseline --no-step-api > $O/b_cfg$c.log 2>&1 || { tail -20 $O/b_cfg$c.log; exit 1; }
   grep "^{" $O/b_cfg$c.log >> $O/bench_cfg345.jsonl
 done
 echo "[$(date +%T)] --gpus 2 rehearsal (gloo, one GPU)"
@@ -38,6 +40,6 @@ import json
 for f in ("bench.jsonl", "bench_under_rocprof.jsonl", "bench_cfg345.jsonl", "bench_gpus2_rehearsal.jsonl"):
     for l in open("$O/" + f):
         d = json.loads(l); r = d.get("roofline", {})
-        print(f, d["config"].get("config_index"), d["n_gpus"], "%.4g" % d["value"], r.get("kernel_us"), r.get("frac"), r.get("traffic_over_bytes"), d.get("gather", {}).get("envs_with_finished_episode"))
+        print(f, d["config"].get("config_index"), d["n_gpus"], "%.4g" % d["value"], r.get("kernel_us"), r.get("frac"), r.get("traffic_over_bytes"), (r.get("valu") or {}).get("valu_issue_frac"), d.get("gather", {}).get("envs_with_finished_episode"))
 PY
 echo "[$(date +%T)] done"
