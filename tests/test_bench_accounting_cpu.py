@@ -83,6 +83,11 @@ def test_tile_path_reports_the_market_tile_as_overhead(bench, monkeypatch):
 def test_lds_path_selection(bench, monkeypatch):
     monkeypatch.delenv("HE_LDS_ROLLOUT", raising=False)
     assert bench.lds_rollout(bench.CONFIGS[2]) and bench.lds_rollout(bench.CONFIGS[3])
-    assert bench.lds_rollout(bench.CONFIGS[4]) and not bench.lds_rollout(bench.CONFIGS[5])  # GBM + book; Heston
+    assert bench.lds_rollout(bench.CONFIGS[4]) and bench.lds_rollout(bench.CONFIGS[5])  # GBM + book; Heston + book
+    # the LDS kernel's own bytes: + 16 per env for the book's running max, + 16 for Heston's v
+    n, rk = 131072, 256
+    r5 = bench.roofline("rollout", n, 1.0, rk, True, "heston", lds=True)
+    assert r5["kernel_bytes_per_launch"] == n * (rk * 65 + 80 + 16 + 16)
+    assert r5["overhead_bytes_per_launch"] == 0 and r5["kernel"].startswith("lds_rollout_kernel")
     monkeypatch.setenv("HE_LDS_ROLLOUT", "0")
     assert not bench.lds_rollout(bench.CONFIGS[2])
