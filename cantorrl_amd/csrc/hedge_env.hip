@@ -344,6 +344,29 @@ __device__ __forceinline__ float4 greeks_fast(const Params& p, float S, float v)
     return make_float4(cd, gam, pd, 0.0f);
 }
 
+// greeks_fast<true> for the lean LDS obs stepper: the handle's sigma, tenor and sst are
+// normal (lds_lean_config), so the uniform branches are gone, and the S <= 1e-6 case is
+// a select over the main path's result (which it computes for every lane) instead of a
+// divergent if/else.  Same operations and operands, so the same bits as greeks_fast<true>.
+__device__ __forceinline__ float4 greeks_lean(float S, float num_drift, float inv_sst_f, float sstf) {
+    const float K = rintf(S);
+    const float Kc = np_maxf(K, 1e-6f);
+    const float num = logf(S / Kc) + num_drift;   // f32 in the reference too
+    const float d1 = num * inv_sst_f;
+    const float x = d1 * 0.70710678118654752f;
+    const float tail = 0.5f * erfcf(fabsf(x));
+    float cd = (x >= 0.0f) ? 1.0f - tail : tail;
+    float pd = (x >= 0.0f) ? -tail : tail - 1.0f;
+    const float gd = S * sstf;
+    float gam = (fabsf(gd) < 1e-9f) ? 0.0f
+                                    : (expf(-0.5f * (d1 * d1)) * 0.398942280401432678f) * __builtin_amdgcn_rcpf(gd);
+    const bool tiny = S <= 1e-6f;  // weak python 1e-6 compares as float32(1e-6)
+    cd = tiny ? ((K == 0.0f) ? 0.5f : ((K > 0.0f) ? 0.0f : 1.0f)) : cd;
+    pd = tiny ? ((K == 0.0f) ? -0.5f : ((K < 0.0f) ? 0.0f : -1.0f)) : pd;
+    gam = tiny ? 0.0f : gam;
+    return make_float4(cd, gam, pd, 0.0f);
+}
+
 // ------------------------------------------------------------------ observation
 // S_t / S_{t-1} - 1 clipped to +-1, 0 when S_{t-1} == 0 (hedging_env_v2.py:129-136):
 // a function of the market alone, so it is computed where the market is (market_kernel
@@ -1564,6 +1587,9 @@ __global__ __launch_bounds__(kBlock, HE_FUSED_WAVES) void step_market_kernel(Par
 #ifndef HE_LDS_M
 #define HE_LDS_M 8
 #endif
+#ifndef HE_LDS_HOIST
+#define HE_LDS_HOIST 0  // A/B: obs-wave constants forced into VGPRs (1: greeks, 2: reset obs)
+#endif
 #ifndef HE_LDS_PRIO_REW
 #define HE_LDS_PRIO_REW 0
 #endif
@@ -1806,13 +1832,26 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
         if (OBS) {
             const double s0s_d = p.s0s_d, inv_s0s_d = p.inv_s0s_d;
             const float T_f = p.T_f, inv_T_f = p.inv_T_f, var_f = p.var_f;
+            // the per-step constants held in VGPRs (opaque: the scalar reloads they would
+            // otherwise be rematerialized as share lgkmcnt with the LDS traffic)
+            float gnd = p.g_num_drift, gis = p.g_inv_sst_f, gsf = p.g_sst_f;
+#if HE_LDS_HOIST & 1
+            asm volatile("" : "+v"(gnd), "+v"(gis), "+v"(gsf));
+#endif
+            float ro[kObs];
+#pragma unroll
+            for (int c = 0; c < kObs; ++c) ro[c] = p.rstv[4 + c];
+#if HE_LDS_HOIST & 2
+#pragma unroll
+            for (int c = 0; c < kObs; ++c) asm volatile("" : "+v"(ro[c]));
+#endif
             float preS = pre.S;
             if (e.t != 0) preS = (float)cur.S[i];
             auto obs_step = [&](int buf, int sl, int k, float2 ak, auto full) {
                 const float2 r0 = L.sc[buf][sl][lane];
                 const float rP = L.pp[buf][sl][lane];
                 // the obs greeks: greeks_fast of the market price, as market_kernel makes them
-                const float4 g = greeks_fast<true>(p, r0.x, var_f);
+                const float4 g = greeks_lean(r0.x, gnd, gis, gsf);
                 // (i)-(ii) of step_env: the integer trade logic (:181-200)
                 const int32_t nc = e.call + trade_round(ak.x * mt_f, mt);
                 const int32_t nq = e.put + trade_round(ak.y * mt_f, mt);
@@ -1840,7 +1879,7 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
                 // do not wait behind this step's read-back) and stored as whole 16-B lines
                 float* const tile = L.stage[k & 1];
 #pragma unroll
-                for (int c = 0; c < kObs; ++c) tile[lane * kObs + c] = term ? p.rstv[4 + c] : o[c];
+                for (int c = 0; c < kObs; ++c) tile[lane * kObs + c] = term ? ro[c] : o[c];
                 float* out = io.obs + (int64_t)k * N * kObs;
                 if constexpr (decltype(full)::value) flush_obs_full(tile, out, base, lane);
                 else flush_obs_wave(tile, out, base, wrows, lane);
@@ -2816,7 +2855,10 @@ static bool fast_config(const he_env* env) {
 static bool lds_lean_config(const he_env* env, const Io& io) {
     const he_config& c = env->cfg;
     const double s0 = c.s0, ic = fabs(c.initial_cash);
-    return fast_config(env) && io.obs && io.rew && io.term && s0 >= 1e-30 && s0 <= 1e30 && ic <= 1e30;
+    const Params& p = env->p;
+    const bool normal_greeks = !p.tenor_small && p.g_sigma > 1e-6f && p.g_sst >= 1e-9;  // greeks_lean
+    return fast_config(env) && io.obs && io.rew && io.term && s0 >= 1e-30 && s0 <= 1e30 && ic <= 1e30 &&
+           normal_greeks;
 }
 
 // he_rollout through lds_rollout_kernel: GBM or Heston, with or without a book (HE_LDS_ROLLOUT=0
