@@ -17,7 +17,11 @@ GROUPS = [
      "SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_LDS", "SQ_ACTIVE_INST_VMEM"],
     ["SQ_WAVE_CYCLES", "SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_INSTS_SALU", "SQ_INSTS_VMEM_WR", "SQ_INSTS_VMEM_RD",
      "SQ_LDS_BANK_CONFLICT", "SQ_ACTIVE_INST_SCA"],
+    ["SQ_WAVE_CYCLES", "SQC_ICACHE_REQ", "SQC_ICACHE_HITS", "SQC_ICACHE_MISSES", "SQC_ICACHE_MISSES_DUPLICATE",
+     "SQ_IFETCH", "SQ_WAIT_INST_LDS", "SQ_INST_CYCLES_SALU"],
 ]
+if os.environ.get("PMC_GROUPS"):  # e.g. PMC_GROUPS=2 for the instruction-cache group only
+    GROUPS = [GROUPS[int(k)] for k in os.environ["PMC_GROUPS"].split(",")]
 
 args = bench.parse(sys.argv[1:])
 cfg = bench.CONFIGS[args.config]
