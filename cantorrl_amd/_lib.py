@@ -116,7 +116,7 @@ EXPORTS = [
     "he_num_episodes", "he_get_config", "he_state_size", "he_get_state", "he_set_state",
     "he_pcg64_seed_state", "he_host_episode_draws", "he_host_philox", "he_host_div_by", "he_host_div_byf", "he_time_next_step", "he_rollout_policy", "he_host_box_muller",
     "he_sync_market", "he_vecnorm_stats_len", "he_vecnorm_scratch_bytes", "he_vecnorm_init", "he_vecnorm_step",
-    "he_vecnorm_reset", "he_fixed_european_marks", "he_bs_delta_hedge", "he_count_nonfinite",
+    "he_vecnorm_apply", "he_vecnorm_attach", "he_vecnorm_reset", "he_fixed_european_marks", "he_bs_delta_hedge", "he_count_nonfinite",
     "he_device_rng", "he_device_math", "he_host_math", "he_episode_summaries",
 ]
 
@@ -187,6 +187,8 @@ def load(path=LIB_PATH):
         "he_vecnorm_scratch_bytes": (i64, [i64, i32]),
         "he_vecnorm_init": (i32, [vp, i32, vp]),
         "he_vecnorm_step": (i32, [ctypes.POINTER(HeVecnormParams), i64] + [vp] * 14 + [vp]),
+        "he_vecnorm_apply": (i32, [ctypes.POINTER(HeVecnormParams), i64] + [vp] * 14 + [vp]),
+        "he_vecnorm_attach": (i32, [vp, ctypes.POINTER(HeVecnormParams), vp, vp, vp]),
         "he_vecnorm_reset": (i32, [ctypes.POINTER(HeVecnormParams), i64] + [vp] * 5 + [vp]),
         "he_fixed_european_marks": (i32, [vp, i64, i32, ctypes.c_double, vp, vp, vp, vp]),
         "he_bs_delta_hedge": (i32, [vp, i64, i32, ctypes.c_double, ctypes.c_double, vp, vp]),

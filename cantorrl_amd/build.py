@@ -40,7 +40,7 @@ RB_DEPS = [RB_SRC, os.path.join(HERE, "csrc", "he_math.h"), os.path.join(REPO, "
 RB_OUT = os.path.join(HERE, "lib", "librbergomi.so")
 VN_SRC = os.path.join(HERE, "csrc", "vecnorm.hip")
 AN_SRC = os.path.join(HERE, "csrc", "analytics.hip")
-DEPS = DEPS + [VN_SRC, AN_SRC]
+DEPS = DEPS + [VN_SRC, AN_SRC, os.path.join(HERE, "csrc", "vn_moments.h")]
 TARGETS = [([SRC, VN_SRC, AN_SRC], DEPS, OUT, ENV_FLAGS), ([RB_SRC], RB_DEPS, RB_OUT, [])]
 
 

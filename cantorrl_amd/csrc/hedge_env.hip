@@ -32,6 +32,8 @@
 
 #include <new>
 #include <type_traits>
+
+#include "vn_moments.h"
 #include <string>
 #include <vector>
 
@@ -1514,6 +1516,35 @@ __global__ __launch_bounds__(kBlock) void step1_kernel(const Params* __restrict_
     step_body<MODE, false, true, BOOK, FAST, false, GS>(*pc, n, tA, tB, tC, s, io, 1, slot0, blockIdx.x);
 }
 
+// he_step with VecNormalize attached (he_vecnorm_attach): step1_kernel, then the first half
+// of the VecNormalize step (vn_moments.h) over the rows this workgroup has just written --
+// read back from L2 after the barrier -- instead of a separate moments launch; the
+// caller's he_vecnorm_apply is then the second half alone.
+static_assert(kBlock == vn::kVnThreads && kEpb == vn::kVnChunk, "one step workgroup = one moments partial");
+template <int MODE, bool BOOK, bool FAST, bool GS>
+__global__ __launch_bounds__(kBlock) void step1_vn_kernel(const Params* __restrict__ pc, int64_t n, const float4* tA,
+                                                          const float4* tB, const double* tC, State s, StepIo sio,
+                                                          int slot0, vn::MomentsArgs vm) {
+    Io io;
+    io.act = sio.act;
+    io.obs = sio.obs;
+    io.rew = sio.rew;
+    io.term = sio.term;
+    io.trunc = sio.trunc;
+    io.tobs = sio.tobs;
+    io.info = he_info{};
+    io.pol_on = false;
+    io.sums = false;
+    step_body<MODE, false, true, BOOK, FAST, false, GS>(*pc, n, tA, tB, tC, s, io, 1, slot0, blockIdx.x);
+    __syncthreads();  // the workgroup's obs / reward rows are visible to all its threads
+    vn::moments_body(vm, blockIdx.x);
+}
+
+// The same moments after any other he_step launch (info requested, a fused market block).
+__global__ __launch_bounds__(vn::kVnThreads) void vn_moments_after_step_kernel(vn::MomentsArgs vm) {
+    vn::moments_body(vm, blockIdx.x);
+}
+
 // Rollout block with the next block's market in the same grid: workgroups
 // [0, step_blocks) step block b from tile pk (as step_kernel), the rest generate block
 // b+1 into tile pm (as market_kernel, workgroup bid - step_blocks).  One dispatch per
@@ -2421,6 +2452,9 @@ struct he_env {
     float rstv[4 + kObs] = {};  // host copy of the reset market + obs (generate)
     float* rst = nullptr;     // reset market + obs (generate)
     Params* dparams = nullptr;  // device copies of tile_params(env, 0 / 1) for step1_kernel
+    bool vn_on = false;          // he_vecnorm_attach: he_step also runs the VecNormalize moments
+    bool vn_fused = false;       // ... and this he_step ran them in step1_vn_kernel
+    vn::MomentsArgs vn{};
     BookOpt* dbook = nullptr;   // liability book, device copy (generate modes)
     double* dbook_tab = nullptr;  // book tau table (book_option)
     int32_t book_rows = 0;        // its rows: max expiry + 1
@@ -2716,6 +2750,17 @@ static void launch_step_gs(he_env* env, const Params& p, const Io& io, bool info
         const float4* tA = REPLAY ? p.rec : p.tileA;
         const float4* tB = REPLAY ? p.recg : p.tileB;
         StepIo sio{io.act, io.obs, io.rew, io.term, io.trunc, io.tobs};
+        if (env->vn_on) {  // + the VecNormalize moments in the same launch
+            vn::MomentsArgs vm = env->vn;
+            vm.obs = io.obs;
+            vm.reward = io.rew;
+            hipEvent_t a = (hipEvent_t)env->ev_start, b = (hipEvent_t)env->ev_stop;
+            env->ev_start = env->ev_stop = nullptr;
+            hipExtLaunchKernelGGL((step1_vn_kernel<MODE, BOOK, FAST, GS>), dim3((unsigned)blocks), dim3(kBlock), 0, st, a,
+                                  b, 0, pc, p.n, tA, tB, (const double*)p.tileC, env->s, sio, slot0, vm);
+            env->vn_fused = true;
+            return;
+        }
         if (env->ev_start) {
             hipEvent_t a = (hipEvent_t)env->ev_start, b = (hipEvent_t)env->ev_stop;
             env->ev_start = env->ev_stop = nullptr;
@@ -3426,7 +3471,46 @@ he_status he_step(he_env* env, const float* actions, float* obs, float* reward, 
         const void* const* f = reinterpret_cast<const void* const*>(info);
         for (size_t k = 0; k < sizeof(he_info) / sizeof(void*); ++k) want_info |= f[k] != nullptr;
     }
-    return launch_steps(env, io, want_info, 1, stream);
+    if (env->vn_on && (!obs || !reward))
+        return fail(env, HE_EINVAL, "he_vecnorm_attach: he_step needs the obs and reward buffers");
+    env->vn_fused = false;
+    he_status s = launch_steps(env, io, want_info, 1, stream);
+    if (s != HE_OK || !env->vn_on || env->vn_fused) return s;
+    // VecNormalize attached, and this step took another kernel: the moments after it
+    vn::MomentsArgs vm = env->vn;
+    vm.obs = obs;
+    vm.reward = reward;
+    const int64_t blocks = (env->cfg.n_envs + kEpb - 1) / kEpb;
+    hipLaunchKernelGGL(vn_moments_after_step_kernel, dim3((unsigned)blocks), dim3(vn::kVnThreads), 0,
+                       (hipStream_t)stream, vm);
+    HE_HIP(env, hipGetLastError());
+    return HE_OK;
+}
+
+he_status he_vecnorm_attach(he_env* env, const he_vecnorm_params* p, double* returns, double* stats, void* scratch) {
+    if (!env) return HE_EINVAL;
+    if (!p) {  // detach
+        env->vn_on = false;
+        return HE_OK;
+    }
+    if (p->obs_dim != kObs || !isfinite(p->gamma)) return fail(env, HE_EINVAL, "bad he_vecnorm_params");
+    if (!returns || !stats || !scratch) return fail(env, HE_EINVAL, "returns / stats / scratch are NULL");
+    if (env->cfg.n_envs > (int64_t)vn::kVnMaxBlocks * kEpb)
+        return fail(env, HE_EINVAL, "he_vecnorm_attach covers up to %d envs (use he_vecnorm_step)",
+                    vn::kVnMaxBlocks * kEpb);
+    vn::MomentsArgs m = {};
+    m.n = env->cfg.n_envs;
+    m.rows_per_block = kEpb;
+    m.upd_obs = p->training && p->norm_obs;
+    m.upd_ret = p->training != 0;
+    m.shift_mean = 1;
+    m.gamma = p->gamma;
+    m.returns = returns;
+    m.stats = stats;
+    m.part = (double*)scratch;
+    env->vn = m;
+    env->vn_on = m.upd_obs || m.upd_ret;
+    return HE_OK;
 }
 
 he_status he_rollout(he_env* env, int32_t k_steps, const float* actions, float* obs, float* reward,

@@ -26,16 +26,17 @@
 #include <stdint.h>
 
 #include "../../include/hedge_env.h"
+#include "vn_moments.h"
 
 namespace {
 
-constexpr int kD = HE_OBS_DIM;
-constexpr int kVnThreads = 256;
-constexpr int kVnMaxBlocks = 256;   // workgroups of a launch = partials merged per workgroup (one per thread)
-
-// scratch layout: [kPart][kVnMaxBlocks] doubles, then the 2 kD + 4 old statistics and
-// the kD + 1 shifts of the sums
-constexpr int kPart = 2 * kD + 3;   // count, S1[D + 1] (obs, returns), S2[D + 1]
+using vn::kD;
+using vn::kPart;
+using vn::kVnChunk;
+using vn::kVnMaxBlocks;
+using vn::kVnThreads;
+using vn::block_sum;
+using vn::load_tile;
 
 struct VnArgs {
     int64_t n;
@@ -76,44 +77,6 @@ __device__ __forceinline__ void rms_update(double* mean, double* var, double* co
 
 __device__ __forceinline__ double clipd(double x, double lo, double hi) { return x < lo ? lo : (x > hi ? hi : x); }
 
-// Sum of v[0..NV) over the block into out[0..NV) (LDS), NV <= 32: every thread stores
-// its NV values (row stride NV + 1), then TPV = 16 (NV <= 16) or 8 threads per value sum
-// 256 / TPV rows each and finish with a butterfly inside their TPV-lane group -- against
-// 6 shuffle levels per value (~180 LDS permutes per wave) of a butterfly over the whole
-// wave.  The summation order is fixed.
-template <int NV>
-__device__ __forceinline__ void block_sum(const double* v, double* buf, double* out) {
-    constexpr int TPV = NV <= 16 ? 16 : 8;
-    static_assert(NV <= 32 && NV * TPV <= kVnThreads, "threads per value");
-    constexpr int S = NV + 1;
-    const int t = threadIdx.x;
-#pragma unroll
-    for (int c = 0; c < NV; ++c) buf[t * S + c] = v[c];
-    __syncthreads();
-    if (t < NV * TPV) {
-        const int c = t / TPV, j = t % TPV;
-        double x = 0.0;
-#pragma unroll
-        for (int k = 0; k < kVnThreads / TPV; ++k) x += buf[(j + TPV * k) * S + c];
-#pragma unroll
-        for (int m = TPV / 2; m >= 1; m >>= 1) x += __shfl_xor(x, m, TPV);
-        if (j == 0) out[c] = x;
-    }
-    __syncthreads();
-}
-
-constexpr int kVnChunk = kVnThreads;   // rows staged in LDS at a time (one per thread)
-
-// Rows [c0, c0 + rows) of obs -> LDS tile, as a flat coalesced copy (the [N][13] rows are
-// 52 B apart: per-row loads would touch 26 cache lines per wave instruction); the rows
-// are then read from LDS with a stride of 13 words (odd: no bank conflicts).
-__device__ __forceinline__ void load_tile(float* tile, const float* obs, int64_t c0, int rows) {
-    const float* src = obs + c0 * kD;
-    const int nf = rows * kD;
-    for (int k = threadIdx.x; k < nf; k += kVnThreads) tile[k] = src[k];
-    __syncthreads();
-}
-
 struct VnRows {
     int64_t r0, r1;
     double cnt;
@@ -126,61 +89,27 @@ __device__ __forceinline__ VnRows rows_of(const VnArgs& a) {
     return w;
 }
 
-// Launch 1 (training): per workgroup, the sums of the deviations d = x - x0 and d^2 of
-// its rows' obs columns (x0 = the batch's row 0: a data point, so d is centred to within
-// the batch's spread and S2 - S1^2 / n keeps ~all of f64's digits) and of the updated
-// running returns (shifted by the old running mean), in one pass, stored as a partial.
-// The kernel boundary publishes the partials to launch 2 -- no atomics, no waiting (a
-// single launch with a grid-wide wait measured 25 us at 65,536 envs: four dependent
-// device-coherent round trips between workgroups).
+// Launch 1 (training): the moments partials of each workgroup's rows (vn_moments.h;
+// the obs shift is the batch's row 0).  The kernel boundary publishes the partials to
+// launch 2 -- no atomics, no waiting (a single launch with a grid-wide wait measured
+// 25 us at 65,536 envs: four dependent device-coherent round trips between workgroups).
+__device__ __forceinline__ vn::MomentsArgs moments_args(const VnArgs& a) {
+    vn::MomentsArgs m = {};
+    m.n = a.n;
+    m.rows_per_block = a.rows_per_block;
+    m.upd_obs = a.upd_obs;
+    m.upd_ret = a.training && !a.reset;
+    m.shift_mean = 0;
+    m.gamma = a.gamma;
+    m.obs = a.obs;
+    m.reward = a.reward;
+    m.returns = a.returns;
+    m.stats = a.stats;
+    m.part = a.part;
+    return m;
+}
 __global__ void __launch_bounds__(kVnThreads) vn_moments_kernel(VnArgs a) {
-    __shared__ double sh[kVnThreads * (kPart + 1)];
-    __shared__ double ssum[kPart];
-    __shared__ float tile[kVnChunk * kD];
-    const VnRows w = rows_of(a);
-    const bool upd_ret = a.training && !a.reset;
-    const int t = threadIdx.x;
-    double sft[kD + 1];
-#pragma unroll
-    for (int c = 0; c < kD; ++c) sft[c] = (double)a.obs[c];
-    sft[kD] = a.stats[2 * kD + 1];
-    double v[kPart - 1];
-#pragma unroll
-    for (int c = 0; c < kPart - 1; ++c) v[c] = 0.0;
-    for (int64_t c0 = w.r0; c0 < w.r1; c0 += kVnChunk) {
-        const int rows = (int)((w.r1 - c0) < kVnChunk ? (w.r1 - c0) : kVnChunk);
-        if (a.upd_obs) load_tile(tile, a.obs, c0, rows);
-        if (t < rows) {
-            if (a.upd_obs) {
-#pragma unroll
-                for (int c = 0; c < kD; ++c) {
-                    const double d = (double)tile[t * kD + c] - sft[c];
-                    v[c] += d;
-                    v[kD + 1 + c] += d * d;
-                }
-            }
-            if (upd_ret) {
-                const int64_t r = c0 + t;
-                const double ret = a.returns[r] * a.gamma + (double)a.reward[r];   // VecNormalize._update_reward
-                a.returns[r] = ret;
-                const double d = ret - sft[kD];
-                v[kD] += d;
-                v[2 * kD + 1] += d * d;
-            }
-        }
-        __syncthreads();
-    }
-    block_sum<kPart - 1>(v, sh, ssum);
-    // partials [kPart][kVnMaxBlocks] (launch 2's thread k reads column k: coalesced):
-    // count, S1[kD + 1], S2[kD + 1]
-    double* part = a.part + blockIdx.x;
-    if (t < kPart - 1) part[(1 + t) * kVnMaxBlocks] = ssum[t];
-    if (t == 0) part[0] = w.cnt;
-    // the statistics before this step and the shifts, for launch 2 (whose workgroup 0
-    // overwrites the statistics)
-    double* snap = a.part + kVnMaxBlocks * kPart;
-    if (blockIdx.x == 0 && t < 2 * kD + 4) snap[t] = a.stats[t];
-    if (blockIdx.x == 0 && t <= kD) snap[2 * kD + 4 + t] = sft[t];
+    vn::moments_body(moments_args(a), blockIdx.x);
 }
 
 // Launch 2: every workgroup merges all the partials itself (one block reduction in a
@@ -249,19 +178,55 @@ __global__ void __launch_bounds__(kVnThreads) vn_apply_kernel(VnArgs a) {
         if (t == 0) srinv = 1.0 / sqrt(a.stats[2 * kD + 2] + a.eps);
         __syncthreads();
     }
+    // the rows' own work (reward, returns, terminal obs, Monitor): thread t, row r0 + t
+    auto row_work = [&](int64_t r) {
+        if (a.reset) {
+            a.returns[r] = 0.0;
+            return;
+        }
+        const bool dn = a.done ? a.done[r] != 0 : false;
+        const float rw = a.reward[r];
+        a.rew_out[r] = a.norm_reward ? (float)clipd((double)rw * srinv, -a.clip_rew, a.clip_rew) : rw;
+        if (dn && a.tobs && a.tobs_out) {   // rare: per-row accesses
+#pragma unroll
+            for (int c = 0; c < kD; ++c) {
+                const float x = a.tobs[r * kD + c];
+                a.tobs_out[r * kD + c] =
+                    a.norm_obs ? (float)clipd(((double)x - snorm[c][0]) * snorm[c][1], -a.clip_obs, a.clip_obs) : x;
+            }
+        }
+        if (dn) a.returns[r] = 0.0;   // self.returns[dones] = 0
+        if (a.ep_ret) {                 // Monitor: sum(rewards), len(rewards)
+            const double er = a.ep_ret[r] + (double)rw;
+            const int32_t el = a.ep_len[r] + 1;
+            if (dn) {
+                a.ep_ret_done[r] = er;
+                a.ep_len_done[r] = el;
+            }
+            a.ep_ret[r] = dn ? 0.0 : er;
+            a.ep_len[r] = dn ? 0 : el;
+        }
+    };
     if (resident) {
+        // the obs element-wise straight from the registers the loads landed in: element
+        // k of the slice is column k % 13 (the slice starts at a row boundary)
+        float* dst = a.obs_out + w.r0 * kD;
 #pragma unroll
         for (int q = 0; q < kD; ++q) {
             const int k = t + q * kVnThreads;
-            if (k < nres) tile[k] = xr[q];
+            if (k < nres) {
+                const int c = k % kD;
+                dst[k] = a.norm_obs ? (float)clipd(((double)xr[q] - snorm[c][0]) * snorm[c][1], -a.clip_obs, a.clip_obs)
+                                    : xr[q];
+            }
         }
-        __syncthreads();
+        if (t < (int)(w.r1 - w.r0)) row_work(w.r0 + t);
+        return;
     }
     for (int64_t c0 = w.r0; c0 < w.r1; c0 += kVnChunk) {
         const int rows = (int)((w.r1 - c0) < kVnChunk ? (w.r1 - c0) : kVnChunk);
-        if (!resident) load_tile(tile, a.obs, c0, rows);
+        load_tile(tile, a.obs, c0, rows);
         if (t < rows) {
-            const int64_t r = c0 + t;
             // the row in place in LDS, then stored back as a flat coalesced copy
             if (a.norm_obs) {
 #pragma unroll
@@ -270,42 +235,13 @@ __global__ void __launch_bounds__(kVnThreads) vn_apply_kernel(VnArgs a) {
                     tile[t * kD + c] = (float)clipd(((double)x - snorm[c][0]) * snorm[c][1], -a.clip_obs, a.clip_obs);
                 }
             }
-            if (a.reset) {
-                a.returns[r] = 0.0;
-            } else {
-                const bool dn = a.done ? a.done[r] != 0 : false;
-                const float rw = a.reward[r];
-                a.rew_out[r] = a.norm_reward ? (float)clipd((double)rw * srinv, -a.clip_rew, a.clip_rew) : rw;
-                if (dn && a.tobs && a.tobs_out) {   // rare: per-row accesses
-#pragma unroll
-                    for (int c = 0; c < kD; ++c) {
-                        const float x = a.tobs[r * kD + c];
-                        a.tobs_out[r * kD + c] =
-                            a.norm_obs ? (float)clipd(((double)x - snorm[c][0]) * snorm[c][1], -a.clip_obs, a.clip_obs)
-                                       : x;
-                    }
-                }
-                if (dn) a.returns[r] = 0.0;   // self.returns[dones] = 0
-                if (a.ep_ret) {                 // Monitor: sum(rewards), len(rewards)
-                    const double er = a.ep_ret[r] + (double)rw;
-                    const int32_t el = a.ep_len[r] + 1;
-                    if (dn) {
-                        a.ep_ret_done[r] = er;
-                        a.ep_len_done[r] = el;
-                        a.ep_ret[r] = 0.0;
-                        a.ep_len[r] = 0;
-                    } else {
-                        a.ep_ret[r] = er;
-                        a.ep_len[r] = el;
-                    }
-                }
-            }
+            row_work(c0 + t);
         }
         __syncthreads();
         float* dst = a.obs_out + c0 * kD;
         const int nf = rows * kD;
         for (int k = t; k < nf; k += kVnThreads) dst[k] = tile[k];
-        if (!resident) __syncthreads();
+        __syncthreads();
     }
 }
 
@@ -329,11 +265,11 @@ __global__ void init_kernel(double* stats) {
     }
 }
 
-he_status launch(VnArgs& a, void* scratch, hipStream_t s) {
+he_status launch(VnArgs& a, void* scratch, hipStream_t s, bool moments = true) {
     a.blocks = blocks_for(a.n);
     a.rows_per_block = (int)((a.n + a.blocks - 1) / a.blocks);
     a.part = (double*)scratch;   // [kVnMaxBlocks][kPart] partials, then the old statistics
-    if (a.upd_obs || (a.training && !a.reset)) {
+    if (moments && (a.upd_obs || (a.training && !a.reset))) {
         hipLaunchKernelGGL(vn_moments_kernel, dim3(a.blocks), dim3(kVnThreads), 0, s, a);
         if (hipGetLastError() != hipSuccess) return HE_EHIP;
     }
@@ -398,11 +334,11 @@ he_status he_vecnorm_init(double* stats, int32_t obs_dim, void* stream) {
     return hipGetLastError() == hipSuccess ? HE_OK : HE_EHIP;
 }
 
-he_status he_vecnorm_step(const he_vecnorm_params* p, int64_t n, const float* obs, const float* reward,
-                          const uint8_t* done, const float* terminal_obs, double* returns, double* stats,
-                          void* scratch, float* obs_out, float* reward_out, float* terminal_obs_out,
-                          double* ep_return, int32_t* ep_length, double* ep_return_done, int32_t* ep_length_done,
-                          void* stream) {
+static he_status vecnorm_step(const he_vecnorm_params* p, int64_t n, const float* obs, const float* reward,
+                              const uint8_t* done, const float* terminal_obs, double* returns, double* stats,
+                              void* scratch, float* obs_out, float* reward_out, float* terminal_obs_out,
+                              double* ep_return, int32_t* ep_length, double* ep_return_done,
+                              int32_t* ep_length_done, void* stream, bool moments) {
     if (!params_ok(p) || n < 0) return HE_EINVAL;
     if (n == 0) return HE_OK;
     if (!obs || !reward || !returns || !stats || !scratch || !obs_out || !reward_out) return HE_EINVAL;
@@ -422,7 +358,26 @@ he_status he_vecnorm_step(const he_vecnorm_params* p, int64_t n, const float* ob
     a.ep_len = ep_length;
     a.ep_ret_done = ep_return_done;
     a.ep_len_done = ep_length_done;
-    return launch(a, scratch, (hipStream_t)stream);
+    return launch(a, scratch, (hipStream_t)stream, moments);
+}
+
+he_status he_vecnorm_step(const he_vecnorm_params* p, int64_t n, const float* obs, const float* reward,
+                          const uint8_t* done, const float* terminal_obs, double* returns, double* stats,
+                          void* scratch, float* obs_out, float* reward_out, float* terminal_obs_out,
+                          double* ep_return, int32_t* ep_length, double* ep_return_done, int32_t* ep_length_done,
+                          void* stream) {
+    return vecnorm_step(p, n, obs, reward, done, terminal_obs, returns, stats, scratch, obs_out, reward_out,
+                        terminal_obs_out, ep_return, ep_length, ep_return_done, ep_length_done, stream, true);
+}
+
+he_status he_vecnorm_apply(const he_vecnorm_params* p, int64_t n, const float* obs, const float* reward,
+                           const uint8_t* done, const float* terminal_obs, double* returns, double* stats,
+                           void* scratch, float* obs_out, float* reward_out, float* terminal_obs_out,
+                           double* ep_return, int32_t* ep_length, double* ep_return_done, int32_t* ep_length_done,
+                           void* stream) {
+    if (n > (int64_t)kVnMaxBlocks * kVnThreads) return HE_EINVAL;   // the fused partials cover <= 65,536 rows
+    return vecnorm_step(p, n, obs, reward, done, terminal_obs, returns, stats, scratch, obs_out, reward_out,
+                        terminal_obs_out, ep_return, ep_length, ep_return_done, ep_length_done, stream, false);
 }
 
 he_status he_vecnorm_reset(const he_vecnorm_params* p, int64_t n, const float* obs, double* returns, double* stats,

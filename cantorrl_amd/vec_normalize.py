@@ -14,6 +14,7 @@ Statistics are saved with `save(path)` as NPZ (no pickle) and restored with
 `DeviceVecNormalize.load(path, venv)`.
 """
 import ctypes
+import os
 import time
 
 import numpy as np
@@ -54,6 +55,11 @@ class DeviceVecNormalize:
         self._ep_ret_done = torch.zeros(n, dtype=torch.float64, device=dev)
         self._ep_len_done = torch.zeros(n, dtype=torch.int32, device=dev)
         self._check(self.lib.he_vecnorm_init(self._p(self._stats), D, self._stream()), "he_vecnorm_init")
+        # the moments half of each training step inside the env's he_step launch
+        # (he_vecnorm_attach; up to 65,536 envs), then he_vecnorm_apply; else he_vecnorm_step
+        self._fusable = (getattr(venv, "_h", None) is not None and n <= 65536
+                         and os.environ.get("CANTORRL_VN_FUSED", "1") != "0")
+        self._attached = None
         self._actions_pending = None
         self._t_start = time.time()
 
@@ -164,15 +170,37 @@ class DeviceVecNormalize:
     def step_tensors(self, actions):
         """(normalized obs, normalized reward, terminated, truncated) device tensors;
         the normalized terminal obs of done envs are in `terminal_obs_tensor`."""
+        p = self._params()
+        fused = self._attach(p)
         obs, rew, term, trunc = self.venv.step_tensors(actions)
-        st = self.lib.he_vecnorm_step(ctypes.byref(self._params()), self.num_envs, self._p(obs), self._p(rew),
+        fn = self.lib.he_vecnorm_apply if fused else self.lib.he_vecnorm_step
+        st = fn(ctypes.byref(p), self.num_envs, self._p(obs), self._p(rew),
                                       self._p(term), self._p(self.venv._tobs), self._p(self._returns),
                                       self._p(self._stats), self._p(self._scratch), self._p(self._obs_out),
                                       self._p(self._rew_out), self._p(self._tobs_out), self._p(self._ep_ret),
                                       self._p(self._ep_len), self._p(self._ep_ret_done), self._p(self._ep_len_done),
                                       self._stream())
-        self._check(st, "he_vecnorm_step")
+        self._check(st, "he_vecnorm_apply" if fused else "he_vecnorm_step")
         return self._obs_out, self._rew_out, term, trunc
+
+    def _attach(self, p):
+        """Attach (or detach) the statistics to the env's he_step for this step's
+        parameters; returns whether he_step now runs the moments."""
+        want = self._fusable and bool(p.training)
+        key = (p.training, p.norm_obs, p.gamma) if want else None
+        if key != self._attached:
+            h = self.venv._h
+            st = self.lib.he_vecnorm_attach(h, ctypes.byref(p) if want else None, self._p(self._returns),
+                                            self._p(self._stats), self._p(self._scratch))
+            self._check(st, "he_vecnorm_attach")
+            self._attached = key
+        return want
+
+    def close(self):
+        if self._attached is not None and getattr(self.venv, "_h", None) is not None:
+            self.lib.he_vecnorm_attach(self.venv._h, None, None, None, None)
+            self._attached = None
+        self.venv.close()
 
     @property
     def terminal_obs_tensor(self):
@@ -236,9 +264,6 @@ class DeviceVecNormalize:
 
     def seed(self, seed=None):
         return self.venv.seed(seed)
-
-    def close(self):
-        self.venv.close()
 
 
 class _NormInfoView(InfoView):

@@ -321,7 +321,8 @@ he_status he_host_math(int32_t op, const double* x, int64_t count, double* out);
  *
  * stats: device f64 [2 D + 4] = obs_mean[D], obs_var[D], obs_count, ret_mean, ret_var,
  * ret_count (RunningMeanStd(shape=(D,)) and RunningMeanStd(shape=())).  The batch
- * moments are exact two-pass f64 per block, merged in block order (deterministic). */
+ * moments are one-pass f64 sums of shifted values per block, merged in block order
+ * (deterministic). */
 typedef struct he_vecnorm_params {
     int32_t obs_dim;        /* D; 13 (HE_OBS_DIM) is the one supported */
     int32_t training;       /* update obs_rms / ret_rms / returns */
@@ -354,6 +355,20 @@ he_status he_vecnorm_step(const he_vecnorm_params* p, int64_t n, const float* ob
                           void* scratch, float* obs_out, float* reward_out, float* terminal_obs_out,
                           double* ep_return, int32_t* ep_length, double* ep_return_done,
                           int32_t* ep_length_done, void* stream);
+
+/* The same step split in two, for n <= 65,536 (one moments partial per he_step
+ * workgroup): he_vecnorm_attach(env, p, returns, stats, scratch) makes every later
+ * he_step on `env` also run the first half -- the batch moments of the obs and reward it
+ * writes, and returns = returns * gamma + reward -- in its own launch (no effect unless
+ * p->training; p = NULL detaches); he_vecnorm_apply, with the arguments of
+ * he_vecnorm_step and the same buffers, is then the second half alone: the statistics
+ * update and the normalization.  Replaces he_vecnorm_step's moments launch. */
+he_status he_vecnorm_attach(he_env* env, const he_vecnorm_params* p, double* returns, double* stats, void* scratch);
+he_status he_vecnorm_apply(const he_vecnorm_params* p, int64_t n, const float* obs, const float* reward,
+                           const uint8_t* done, const float* terminal_obs, double* returns, double* stats,
+                           void* scratch, float* obs_out, float* reward_out, float* terminal_obs_out,
+                           double* ep_return, int32_t* ep_length, double* ep_return_done,
+                           int32_t* ep_length_done, void* stream);
 
 /* VecNormalize.reset: returns = 0; obs_rms.update(obs) (training && norm_obs);
  * obs_out normalized (norm_obs, else a copy). */

@@ -164,3 +164,43 @@ def test_nonfinite_counter():
     assert dirty.nonfinite_count() > 0
     clean.close()
     dirty.close()
+
+
+@pytest.mark.parametrize("info", [False, True])
+def test_fused_moments_equal_separate_launch(info, monkeypatch):
+    """he_vecnorm_attach + he_vecnorm_apply (the moments in he_step's own launch, or after
+    an info step in a separate one) against he_vecnorm_step: the same normalized obs and
+    rewards to f32 rounding, the same statistics to 1e-12 (the sums' shift differs: the
+    old running mean against the batch's row 0)."""
+    from cantorrl_amd.vec_env import HedgingVecEnv
+    from cantorrl_amd.vec_normalize import DeviceVecNormalize
+    outs = []
+    for fused in ("1", "0"):
+        monkeypatch.setenv("CANTORRL_VN_FUSED", fused)
+        env = HedgingVecEnv(3000, mode="gbm", generate=GEN, seed=11, device=DEV, return_numpy=False,
+                            info_keys=("cash",) if info else (), **KW)
+        vn = DeviceVecNormalize(env, gamma=0.97)
+        assert vn._fusable == (fused == "1")
+        vn.reset_tensors()
+        g = torch.Generator(device=DEV)
+        g.manual_seed(3)
+        got = []
+        for k in range(30):
+            a = torch.rand((3000, 2), device=DEV, generator=g) * 2 - 1
+            o, r, t, _ = vn.step_tensors(a)
+            got.append((o.clone(), r.clone()))
+            if k == 12:  # eval steps in between detach and re-attach
+                vn.training = False
+                vn.step_tensors(a)
+                vn.training = True
+        torch.cuda.synchronize()
+        outs.append((got, vn.obs_rms, vn.ret_rms, vn.returns.copy()))
+        vn.close()
+    (ga, ra, qa, ta), (gb, rb, qb, tb) = outs
+    for k, ((oa, wa), (ob, wb)) in enumerate(zip(ga, gb)):
+        torch.testing.assert_close(oa, ob, rtol=0, atol=2e-6, msg=f"obs step {k}")
+        torch.testing.assert_close(wa, wb, rtol=1e-6, atol=1e-7, msg=f"reward step {k}")
+    np.testing.assert_allclose(ra.mean, rb.mean, rtol=1e-12, atol=1e-14)
+    np.testing.assert_allclose(ra.var, rb.var, rtol=1e-10, atol=1e-16)
+    np.testing.assert_allclose(qa.var, qb.var, rtol=1e-10)
+    np.testing.assert_array_equal(ta, tb)

@@ -55,13 +55,39 @@ e1.record()
 torch.cuda.synchronize()
 print(f"he_vecnorm_step n={n}, training=False: {e0.elapsed_time(e1) * 1e3 / R:.2f} us/step", flush=True)
 p.training = 1
+# the second half alone (he_vecnorm_apply): what a step costs on top of he_step when the
+# moments run inside he_step's launch (he_vecnorm_attach)
+e0.record()
+for _ in range(R):
+    lib.he_vecnorm_apply(*args)
+e1.record()
+torch.cuda.synchronize()
+print(f"he_vecnorm_apply n={n} (statistics update + normalize; moments fused into he_step): "
+      f"{e0.elapsed_time(e1) * 1e3 / R:.2f} us/step", flush=True)
 # env step + vecnorm, one launch each
 e0.record()
 for k in range(64):
     vn.step_tensors(acts[k])
 e1.record()
 torch.cuda.synchronize()
-print(f"env he_step + vecnorm, eager: {e0.elapsed_time(e1) * 1e3 / 64:.2f} us/step", flush=True)
+print(f"env he_step + vecnorm, eager, moments fused into he_step: {e0.elapsed_time(e1) * 1e3 / 64:.2f} us/step",
+      flush=True)
+vn._fusable = False  # detach: he_step, then he_vecnorm_step (moments + apply)
+vn.step_tensors(acts[0])
+torch.cuda.synchronize()
+e0.record()
+for k in range(64):
+    vn.step_tensors(acts[k])
+e1.record()
+torch.cuda.synchronize()
+print(f"env he_step + vecnorm, eager, separate moments launch: {e0.elapsed_time(e1) * 1e3 / 64:.2f} us/step",
+      flush=True)
+e0.record()
+for k in range(64):
+    env.step_tensors(acts[k])
+e1.record()
+torch.cuda.synchronize()
+print(f"env he_step alone, eager: {e0.elapsed_time(e1) * 1e3 / 64:.2f} us/step", flush=True)
 env.close()
 
 g = torch.Generator(device=dev).manual_seed(0)

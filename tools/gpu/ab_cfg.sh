@@ -8,7 +8,7 @@ cd $GRAFT_REPO_ROOT; O=gpurun_out/$TAG; mkdir -p $O; export TMPDIR=/tmp
 timeout -k 10 300 python -u -m pytest tests/test_vecnorm_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest_vn.log 2>&1 || { tail -30 $O/pytest_vn.log; exit 1; }
 tail -1 $O/pytest_vn.log
 timeout -k 10 200 python -u tools/aux_time.py > $O/aux_time.log 2>&1 || { tail -20 $O/aux_time.log; exit 1; }
-head -4 $O/aux_time.log
+head -8 $O/aux_time.log
 R=$GRAFT_REPO_ROOT
 (cd /tmp && timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $R/$O/auxprof -o run -- python3 $R/tools/aux_time.py > $R/$O/aux_prof.log 2>&1) || { tail -20 $O/aux_prof.log; exit 1; }
 python3 tools/kstats.py $O/auxprof | grep -E "vn_|step1" || true
