@@ -133,7 +133,9 @@ def test_gbm_matches_oracle_across_episodes(greeks_site):
     gen = dict(s0=496.48001098632812, variance=0.029028, mu=0.04, dt=1 / 252, episode_length=40)
     stats = run_gbm_pair(256, 130, 42, cfg, gen)
     # the f64 price path agrees to the last f32 bit almost everywhere
-    assert stats["pnl_exact"] >= 0.99 * stats["pnl_total"], stats
+    # every P&L bit for bit (the f64 chain of step_env on the same market bits); the
+    # tolerance above is the north_star bar, this is what the build delivers
+    assert stats["pnl_exact"] == stats["pnl_total"], stats
 
 
 def test_gbm_mse_v1_and_offset(greeks_site):
@@ -247,7 +249,7 @@ def test_heston_matches_oracle():
     gen = dict(s0=496.48001098632812, variance=0.04, mu=0.04, dt=1 / 252, episode_length=30,
                heston_kappa=1.5, heston_theta=0.035, heston_xi=0.6, heston_rho=-0.7)
     stats = run_gbm_pair(256, 75, 11, cfg, gen, mode="heston")
-    assert stats["pnl_exact"] >= 0.95 * stats["pnl_total"], stats
+    assert stats["pnl_exact"] == stats["pnl_total"], stats  # bit for bit, as for GBM
 
 
 def test_partial_reset_keeps_other_envs_on_their_paths():
