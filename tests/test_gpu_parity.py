@@ -89,7 +89,11 @@ def test_replay_matches_reference_golden(fname):
     env.close()
 
 
-def run_gbm_pair(n, steps, seed, cfg, gen, offset=0, mode="gbm"):
+def run_gbm_pair(n, steps, seed, cfg, gen, offset=0, mode="gbm", pnl_rtol=0.0):
+    """GPU generate mode against the oracle, step by step: integers and the market info bit
+    for bit, the P&L fields and rewards bit for bit too unless pnl_rtol > 0 (north_star's
+    bar, PNL_RTOL: the liability book's own pricer is not the oracle's scipy ndtr), and the
+    obs through compare_obs."""
     from cantorrl_amd.vec_env import HedgingVecEnv
     rng = np.random.default_rng(seed)
     acts = rng.uniform(-1.05, 1.05, size=(steps, n, 2)).astype(np.float32)
@@ -111,17 +115,19 @@ def run_gbm_pair(n, steps, seed, cfg, gen, offset=0, mode="gbm"):
                   "current_step"):
             if k in oinf:
                 assert_same(venv.info_tensor(k).cpu().numpy(), oinf[k].astype(np.int32), f"{k}[{s}]")
-        # the market after the step (pre-reset on terminated envs), every env, every step
+        # the market after the step (pre-reset on terminated envs), every env, every step:
+        # the same f64 chain on the same Philox bits -> the same f32 marks, bit for bit
         for k in ("current_stock_price", "current_call_price", "current_put_price"):
-            assert_same(venv.info_tensor(k).cpu().numpy(), oinf[k], f"{k}[{s}]", rtol=1e-6)
+            assert_same(venv.info_tensor(k).cpu().numpy(), oinf[k], f"{k}[{s}]")
         for k in ("per_share_step_pnl", "portfolio_value", "cash", "transaction_costs_total"):
             got = venv.info_tensor(k).cpu().numpy()
             exp = oinf[k]
-            assert_same(got, exp, f"{k}[{s}]", rtol=PNL_RTOL, atol=1e-9)
+            assert_same(got, exp, f"{k}[{s}]", rtol=pnl_rtol, atol=1e-9 if pnl_rtol else 0.0)
             if k == "per_share_step_pnl":
                 stats["pnl_exact"] += int((got == exp).sum())
                 stats["pnl_total"] += got.size
-        assert_same(rew.cpu().numpy(), orew.astype(np.float32), f"reward[{s}]", rtol=PNL_RTOL, atol=1e-9)
+        assert_same(rew.cpu().numpy(), orew.astype(np.float32), f"reward[{s}]",
+                    rtol=pnl_rtol, atol=1e-9 if pnl_rtol else 0.0)
         compare_obs(obs.cpu().numpy(), oo, f"obs[{s}]")
     venv.close()
     return stats
@@ -292,7 +298,7 @@ def test_book_of_8_europeans_matches_oracle(greeks_site):
     cfg = dict(loss_type="abs", pnl_penalty_weight=0.001, lambda_cost=0.0001, theta_weight=0.0002,
                slippage_bps=1.0)
     gen = dict(s0=496.48001098632812, variance=0.029028, mu=0.04, dt=1 / 252, episode_length=40, book=BOOK8)
-    run_gbm_pair(256, 100, 21, cfg, gen)
+    run_gbm_pair(256, 100, 21, cfg, gen, pnl_rtol=PNL_RTOL)
 
 
 def test_book_heston_up_and_out_matches_oracle():
@@ -304,7 +310,7 @@ def test_book_heston_up_and_out_matches_oracle():
             dict(type="call", strike=500.0, expiry=30, quantity=10.0)]
     gen = dict(s0=496.48001098632812, variance=0.04, mu=0.04, dt=1 / 252, episode_length=30,
                heston_kappa=1.5, heston_theta=0.035, heston_xi=0.6, heston_rho=-0.7, book=book)
-    run_gbm_pair(256, 75, 13, cfg, gen, mode="heston")
+    run_gbm_pair(256, 75, 13, cfg, gen, mode="heston", pnl_rtol=PNL_RTOL)
 
 
 def test_book_rollout_equals_repeated_steps_and_checkpoint(greeks_site):
