@@ -187,6 +187,48 @@ def test_sharding_invariance_global_env_offset(greeks_site):
     assert torch.equal(rw, torch.cat([rl, rh], dim=1))
 
 
+@pytest.mark.parametrize("mode", ["gbm_book", "heston_barrier"])
+def test_sharding_invariance_lds_books_and_heston(mode):
+    """The same 2-way shard identity through lds_rollout_kernel with the producers' other
+    markets: GBM with the 8-option book, Heston with the barrier book (bench configs 4 and
+    5 in miniature, over an autoreset), plus a checkpoint taken and restored mid-run."""
+    from cantorrl_amd.vec_env import HedgingVecEnv
+    book8 = [dict(type=t, strike=k, expiry=e, quantity=q) for t, k, e, q in (
+        ("call", 500.0, 20, -20.0), ("put", 480.0, 20, -15.0), ("call", 520.0, 40, -10.0), ("put", 500.0, 30, -25.0))]
+    if mode == "gbm_book":
+        kw = dict(mode="gbm", generate=dict(episode_length=30, book=book8))
+    else:
+        kw = dict(mode="heston", generate=dict(episode_length=30, heston_kappa=2.0, heston_theta=0.029028,
+                                               heston_xi=0.3, heston_rho=-0.7,
+                                               book=[dict(type="uo_call", strike=496.0, barrier=530.0, expiry=30,
+                                                          quantity=-50.0)]))
+    n, K = 384, 70
+    g = torch.Generator(device="cuda")
+    g.manual_seed(5)
+    acts = torch.rand((K, n, 2), device="cuda", generator=g) * 2 - 1
+    whole = HedgingVecEnv(n, seed=9, return_numpy=False, info_keys=(), **kw)
+    lo = HedgingVecEnv(n // 2, seed=9, return_numpy=False, info_keys=(), **kw)
+    hi = HedgingVecEnv(n // 2, seed=9, global_env_offset=n // 2, return_numpy=False, info_keys=(), **kw)
+    for e in (whole, lo, hi):
+        e.reset_tensors()
+    ow, rw, tw = whole.rollout(acts[:40].contiguous())
+    ol, rl, tl = lo.rollout(acts[:40, : n // 2].contiguous())
+    blob = hi.get_state()
+    oh, rh, th = hi.rollout(acts[:40, n // 2:].contiguous())
+    assert torch.equal(ow, torch.cat([ol, oh], dim=1)) and torch.equal(rw, torch.cat([rl, rh], dim=1))
+    assert torch.equal(tw, torch.cat([tl, th], dim=1)) and bool(tw.any())   # an autoreset inside
+    # restore hi to before its rollout and replay it: the same outputs again
+    hi.set_state(blob)
+    oh2, rh2, _ = hi.rollout(acts[:40, n // 2:].contiguous())
+    assert torch.equal(oh, oh2) and torch.equal(rh, rh2)
+    ow, rw, _ = whole.rollout(acts[40:].contiguous())
+    ol, rl, _ = lo.rollout(acts[40:, : n // 2].contiguous())
+    oh, rh, _ = hi.rollout(acts[40:, n // 2:].contiguous())
+    assert torch.equal(ow, torch.cat([ol, oh], dim=1)) and torch.equal(rw, torch.cat([rl, rh], dim=1))
+    for e in (whole, lo, hi):
+        e.close()
+
+
 def test_state_checkpoint_roundtrip(greeks_site):
     from cantorrl_amd.vec_env import HedgingVecEnv
     n, K = 300, 20
