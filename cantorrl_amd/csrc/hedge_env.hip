@@ -1527,7 +1527,7 @@ __global__ __launch_bounds__(kBlock) void step1_kernel(const Params* __restrict_
 // of the VecNormalize step (vn_moments.h) over the rows this workgroup has just written --
 // read back from L2 after the barrier -- instead of a separate moments launch; the
 // caller's he_vecnorm_apply is then the second half alone.
-static_assert(kBlock == vn::kVnThreads && kEpb == vn::kVnChunk, "one step workgroup = one moments partial");
+static_assert(kBlock == vn::kVnThreads && kEpb <= vn::kVnChunk, "one step workgroup = one moments partial");
 template <int MODE, bool BOOK, bool FAST, bool GS>
 __global__ __launch_bounds__(kBlock) void step1_vn_kernel(const Params* __restrict__ pc, int64_t n, const float4* tA,
                                                           const float4* tB, const double* tC, State s, StepIo sio,
@@ -3502,6 +3502,8 @@ he_status he_vecnorm_attach(he_env* env, const he_vecnorm_params* p, double* ret
     }
     if (p->obs_dim != kObs || !isfinite(p->gamma)) return fail(env, HE_EINVAL, "bad he_vecnorm_params");
     if (!returns || !stats || !scratch) return fail(env, HE_EINVAL, "returns / stats / scratch are NULL");
+    if (kEpb != vn::kVnChunk)  // he_vecnorm_apply merges one partial per 256 rows
+        return fail(env, HE_EINVAL, "he_vecnorm_attach needs 256 envs per step workgroup (HE_STEP_EPW=64)");
     if (env->cfg.n_envs > (int64_t)vn::kVnMaxBlocks * kEpb)
         return fail(env, HE_EINVAL, "he_vecnorm_attach covers up to %d envs (use he_vecnorm_step)",
                     vn::kVnMaxBlocks * kEpb);

@@ -192,7 +192,10 @@ class DeviceVecNormalize:
             h = self.venv._h
             st = self.lib.he_vecnorm_attach(h, ctypes.byref(p) if want else None, self._p(self._returns),
                                             self._p(self._stats), self._p(self._scratch))
-            self._check(st, "he_vecnorm_attach")
+            if st != _lib.HE_OK and want:  # a build without the fused path: two launches
+                self._fusable, want, key = False, False, None
+            else:
+                self._check(st, "he_vecnorm_attach")
             self._attached = key
         return want
 
