@@ -365,9 +365,18 @@ HE_HD double norm_pdf(double x) {
 // 2^-7 of 1 whenever S >= 64, where log1p of y = q - 1 (exact, Sterbenz) is a
 // 9-term alternating series (truncation < y^10/10); elsewhere ocml log.
 HE_HD double log_ratio(double S, double K) {
+#if defined(HE_LOGRATIO_RCP) && defined(__HIP_DEVICE_COMPILE__)
+    // A/B: y = (S - K) / K by a reciprocal and two Newton steps (S - K exact: Sterbenz)
+    double r = __builtin_amdgcn_rcp(K);
+    r = fma(fma(-K, r, 1.0), r, r);
+    r = fma(fma(-K, r, 1.0), r, r);
+    const double y = (S - K) * r;
+    if (!(fabs(y) < 0.0078125)) return log(S / K);
+#else
     const double q = S / K;
     const double y = q - 1.0;
     if (!(fabs(y) < 0.0078125)) return log(q);
+#endif
     double p = 1.0 / 9.0;
     p = fma_k(p, y, -1.0 / 8.0);
     p = fma_k(p, y, 1.0 / 7.0);
