@@ -199,11 +199,23 @@ class DeviceVecNormalize:
             self._attached = key
         return want
 
+    def _detach(self):
+        """The env handle keeps device pointers into this object's buffers while attached:
+        drop them before the buffers go (close, garbage collection)."""
+        h = getattr(self.venv, "_h", None)
+        if getattr(self, "_attached", None) is not None and h is not None and h.value:
+            self.lib.he_vecnorm_attach(h, None, None, None, None)
+        self._attached = None
+
     def close(self):
-        if self._attached is not None and getattr(self.venv, "_h", None) is not None:
-            self.lib.he_vecnorm_attach(self.venv._h, None, None, None, None)
-            self._attached = None
+        self._detach()
         self.venv.close()
+
+    def __del__(self):
+        try:
+            self._detach()
+        except Exception:  # noqa: BLE001 -- interpreter shutdown
+            pass
 
     @property
     def terminal_obs_tensor(self):

@@ -362,7 +362,9 @@ he_status he_vecnorm_step(const he_vecnorm_params* p, int64_t n, const float* ob
  * writes, and returns = returns * gamma + reward -- in its own launch (no effect unless
  * p->training; p = NULL detaches); he_vecnorm_apply, with the arguments of
  * he_vecnorm_step and the same buffers, is then the second half alone: the statistics
- * update and the normalization.  Replaces he_vecnorm_step's moments launch. */
+ * update and the normalization.  Replaces he_vecnorm_step's moments launch.  Call
+ * he_vecnorm_apply once after each he_step on the attached env, and detach before the
+ * returns / stats / scratch buffers are freed (the handle keeps their pointers). */
 he_status he_vecnorm_attach(he_env* env, const he_vecnorm_params* p, double* returns, double* stats, void* scratch);
 he_status he_vecnorm_apply(const he_vecnorm_params* p, int64_t n, const float* obs, const float* reward,
                            const uint8_t* done, const float* terminal_obs, double* returns, double* stats,
