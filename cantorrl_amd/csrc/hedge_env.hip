@@ -166,6 +166,7 @@ struct Params {
     const BookOpt* book;    // device copy [book_n], read through the scalar cache
     const double* book_tab; // [m][4] = {sqrt(m dt), 1 / sqrt(m dt), exp(-r m dt), exp(r m dt)}, m = 0..max expiry
     int32_t book_rows;      // max expiry + 1
+    double bk_sig, bk_isig, bk_s2, bk_lam;  // book_value's volatility terms at the constant variance
     double book_rst;        // book value of the reset market (t = 0, S0, v0)
     double* tileC;          // [M+1][N] f64 book value of every slot
 #ifdef HE_TIMING
@@ -591,15 +592,23 @@ __device__ __forceinline__ double book_option(const Params& p, const BookOpt& o,
 
 // sum_k q_k * 100 * V_k after step t of the episode (variance var: GBM constant,
 // Heston the env's v_t).  tab: the tau table, p.book_tab or its LDS copy.
+template <bool CONST_VAR = false>
 __device__ __forceinline__ double book_value(const Params& p, double S, double var, int32_t t, double runmax,
                                              const double* tab) {
     BookEnv b;
     b.S = S;
     b.lnS = log(S);
-    b.sig = sqrt(var < 0.0 ? 0.0 : var);
-    b.isig = 1.0 / b.sig;
-    b.s2 = b.sig * b.sig;
-    b.lam = (p.r_d + 0.5 * b.s2) / b.s2;
+    if (CONST_VAR) {  // var == p.var: the host's values of the same expressions
+        b.sig = p.bk_sig;
+        b.isig = p.bk_isig;
+        b.s2 = p.bk_s2;
+        b.lam = p.bk_lam;
+    } else {
+        b.sig = sqrt(var < 0.0 ? 0.0 : var);
+        b.isig = 1.0 / b.sig;
+        b.s2 = b.sig * b.sig;
+        b.lam = (p.r_d + 0.5 * b.s2) / b.s2;
+    }
     double B = 0.0;
 #ifdef HE_BOOK_UNROLL
 #pragma unroll HE_BOOK_UNROLL
@@ -2239,7 +2248,7 @@ __device__ __forceinline__ void lds_producer(const Params& p, int k_steps, const
                     if (HESTON) W.vv[HESTON ? wb : 0][HESTON ? sl : 0][le] = (float)Vh;
                     // the book after the step into slot sl (episode step tp + 1, the new S,
                     // not lagged): market_body's tileC
-                    if (BOOK) W.bk[wb][sl][le] = book_value(p, Sx[h], Vh, (int32_t)(tp + 1), Mx[h], &W.btab[0][0]);
+                    if (BOOK) W.bk[wb][sl][le] = book_value<!HESTON>(p, Sx[h], Vh, (int32_t)(tp + 1), Mx[h], &W.btab[0][0]);
                     if (kb + sl == k_steps - 1) {  // the market position after the launch
                         const uint32_t q = off + (uint32_t)(k_steps - 1);
                         cur.ep[pi] = ep0 + q / T;
@@ -2604,6 +2613,12 @@ static void fill_params(he_env* env) {
     p.rec = env->rec;
     p.recg = env->recg;
     p.book_n = is_generate(env) ? c.book_size : 0;
+    // book_value's sigma terms at the handle's variance, the device's operations in the same
+    // order (IEEE sqrt and division: the same bits) -- the GBM producers read them
+    p.bk_sig = sqrt(p.var < 0.0 ? 0.0 : p.var);
+    p.bk_isig = 1.0 / p.bk_sig;
+    p.bk_s2 = p.bk_sig * p.bk_sig;
+    p.bk_lam = (p.r_d + 0.5 * p.bk_s2) / p.bk_s2;
     p.book = env->dbook;
     p.book_tab = env->dbook_tab;
     p.book_rows = env->book_rows;
