@@ -594,7 +594,7 @@ __device__ __forceinline__ double book_option(const Params& p, const BookOpt& o,
 // Heston the env's v_t).  tab: the tau table, p.book_tab or its LDS copy.
 template <bool CONST_VAR = false>
 __device__ __forceinline__ double book_value(const Params& p, double S, double var, int32_t t, double runmax,
-                                             const double* tab) {
+                                             const double* tab, const BookOpt* opts = nullptr) {
     BookEnv b;
     b.S = S;
     b.lnS = log(S);
@@ -614,7 +614,14 @@ __device__ __forceinline__ double book_value(const Params& p, double S, double v
 #pragma unroll HE_BOOK_UNROLL
 #endif
     for (int k = 0; k < p.book_n; ++k) {
-        const BookOpt o = p.book[k];
+        BookOpt o;
+        if (opts) {  // an LDS copy: the type and expiry back in SGPRs (uniform branches)
+            o = opts[k];
+            o.type = __builtin_amdgcn_readfirstlane(o.type);
+            o.expiry = __builtin_amdgcn_readfirstlane(o.expiry);
+        } else {
+            o = p.book[k];
+        }
         B = B + o.q100 * book_option(p, o, b, o.expiry - t, runmax, tab);
     }
     return B;
@@ -1634,6 +1641,9 @@ __global__ __launch_bounds__(kBlock, HE_FUSED_WAVES) void step_market_kernel(Par
 #ifndef HE_LDS_M
 #define HE_LDS_M 8
 #endif
+#ifndef HE_LDS_BOOK_OPTS
+#define HE_LDS_BOOK_OPTS 1  // the book's options read from an LDS copy (config 4: 10.38 -> 8.98 ms per launch; 0: from the scalar cache)
+#endif
 #ifndef HE_LDS_HOIST
 #define HE_LDS_HOIST 0  // A/B: obs-wave constants forced into VGPRs (1: greeks, 2: reset obs)
 #endif
@@ -1703,6 +1713,9 @@ struct LdsMarketT {
     double bk[BOOK ? 2 : 1][BOOK ? kLdsM : 1][kLdsEnvs];                // book value of every slot
     float vv[MODE == HE_MODE_HESTON ? 2 : 1][MODE == HE_MODE_HESTON ? kLdsM : 1][kLdsEnvs];  // Heston: f32 v_t
     double btab[BOOK ? kLdsBookRows : 1][4];  // the book's tau table (p.book_tab), copied at launch start
+#if HE_LDS_BOOK_OPTS
+    BookOpt bopt[BOOK ? HE_BOOK_MAX : 1];     // the book's options, copied at launch start
+#endif
 };
 static_assert(kLdsM > 8 || sizeof(LdsMarketT<HE_MODE_GBM, false>) <= 40 * 1024, "4 workgroups per CU");
 static_assert(kLdsM > 8 || sizeof(LdsMarketT<HE_MODE_HESTON, true>) <= 40 * 1024, "4 workgroups per CU");
@@ -2248,7 +2261,12 @@ __device__ __forceinline__ void lds_producer(const Params& p, int k_steps, const
                     if (HESTON) W.vv[HESTON ? wb : 0][HESTON ? sl : 0][le] = (float)Vh;
                     // the book after the step into slot sl (episode step tp + 1, the new S,
                     // not lagged): market_body's tileC
+#if HE_LDS_BOOK_OPTS
+                    if (BOOK) W.bk[wb][sl][le] = book_value<!HESTON>(p, Sx[h], Vh, (int32_t)(tp + 1), Mx[h], &W.btab[0][0],
+                                                                     &W.bopt[0]);
+#else
                     if (BOOK) W.bk[wb][sl][le] = book_value<!HESTON>(p, Sx[h], Vh, (int32_t)(tp + 1), Mx[h], &W.btab[0][0]);
+#endif
                     if (kb + sl == k_steps - 1) {  // the market position after the launch
                         const uint32_t q = off + (uint32_t)(k_steps - 1);
                         cur.ep[pi] = ep0 + q / T;
@@ -2286,6 +2304,9 @@ __global__ __launch_bounds__((LdsGeom<MODE, BOOK>::threads), (LdsGeom<MODE, BOOK
     if constexpr (BOOK) {  // the tau table into LDS (rows <= kLdsBookRows: lds_rollout_eligible)
         const int nv = 4 * p.book_rows;
         for (int k = threadIdx.x; k < nv; k += LdsGeom<MODE, BOOK>::threads) (&lm.btab[0][0])[k] = p.book_tab[k];
+#if HE_LDS_BOOK_OPTS
+        if ((int)threadIdx.x < p.book_n) lm.bopt[threadIdx.x] = p.book[threadIdx.x];
+#endif
         __syncthreads();
     }
     if (wave == 0) lds_stepper<MODE, BOOK, LEAN, false>(p, s, io, k_steps, cur, lm, base);
