@@ -13,7 +13,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 # CANTORRL_HEDGEENV_LIB: an alternative build (diagnostic / A-B builds under tools/ab/)
 LIB_PATH = os.environ.get("CANTORRL_HEDGEENV_LIB") or os.path.join(HERE, "lib", "libhedgeenv.so")
 
-HE_ABI_VERSION = 2
+HE_ABI_VERSION = 3
 HE_BOOK_MAX = 8
 HE_OBS_DIM = 13
 BOOK_TYPES = {"call": 0, "put": 1, "uo_call": 2}
@@ -21,6 +21,10 @@ HE_OK, HE_EINVAL, HE_ESHAPE, HE_EHIP, HE_ENOMEM, HE_ESTATE = range(6)
 HE_MODE_REPLAY, HE_MODE_GBM, HE_MODE_HESTON = range(3)
 HE_LOSS_MSE, HE_LOSS_ABS, HE_LOSS_CVAR, HE_LOSS_OTHER = range(4)
 MODES = {"replay": HE_MODE_REPLAY, "gbm": HE_MODE_GBM, "heston": HE_MODE_HESTON}
+# he_mark: rolling ATM (rbergomi_sim.py:418,437-446) or the fixed-strike European of
+# option_price_assignment.py:10-21,33-49
+HE_MARK_ROLLING_ATM, HE_MARK_FIXED_EUROPEAN = range(2)
+MARKS = {"rolling_atm": HE_MARK_ROLLING_ATM, "fixed_european": HE_MARK_FIXED_EUROPEAN}
 
 
 def loss_code(loss_type):
@@ -73,7 +77,7 @@ class HeConfig(ctypes.Structure):
         ("market_block", ctypes.c_int32),
         ("market_prefetch", ctypes.c_int32),
         ("book_size", ctypes.c_int32),
-        ("reserved_i", ctypes.c_int32),
+        ("mark", ctypes.c_int32),
         ("book", HeBookOption * HE_BOOK_MAX),
         ("reserved", ctypes.c_double * 7),
     ]

@@ -59,20 +59,8 @@ __global__ void __launch_bounds__(kAnThreads) euro_marks_kernel(const double* __
         Sprev = S;
         if (vols) vols[i * T1 + t] = sig;
         const double T = fmax(1.0 - (double)t / 252.0, 0.0);    // np.clip(1 - t/252, 0, None) (:38)
-        // black_scholes_vectorized (:10-21)
-        const double Ts = (T <= 0.0) ? 1e-8 : T;
-        const double ss = (sig < 1e-8) ? 1e-8 : sig;             // NaN stays NaN
-        const double sqT = sqrt(Ts);
-        const double d1 = (log(S / K) + (r + 0.5 * (ss * ss)) * Ts) / (ss * sqT);
-        const double d2 = d1 - ss * sqT;
-        const double Kd = K * exp(-r * Ts);
-        double c = S * he::ndtr(d1) - Kd * he::ndtr(d2);
-        double p = Kd * he::ndtr(-d2) - S * he::ndtr(-d1);
-        if (T <= 0.0) {                                           // np.where(T <= 0, intrinsic, .)
-            const double KT = K * exp(-r * T);
-            c = he::np_max(S - KT, 0.0);
-            p = he::np_max(KT - S, 0.0);
-        }
+        double c, p;
+        he::bs_vectorized(S, K, T, r, sig, &c, &p);               // black_scholes_vectorized (:10-21)
         calls[i * T1 + t] = c;
         puts[i * T1 + t] = p;
     }

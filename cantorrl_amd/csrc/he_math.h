@@ -414,6 +414,33 @@ HE_HD void bs_call_put(double S, double K, const BSConst& c, double* call, doubl
     *put = (pv < 0.0) ? 0.0 : pv;
 }
 
+// black_scholes_vectorized (src/sim/option_price_assignment.py:10-21) for one element,
+// f64, the reference's operation order: T_safe = 1e-8 for T <= 0, sigma_safe = 1e-8 for
+// sigma < 1e-8 (NaN stays NaN), no floor at 0, and the intrinsic value against the
+// discounted strike K e^{-r T} when T <= 0.  ndtr(x) and ndtr(-x) from one erf / erfc
+// evaluation (ndtr_pair: each bit-identical to its own ndtr call).  The fixed-strike
+// European mark (he_mark HE_MARK_FIXED_EUROPEAN) and he_fixed_european_marks.
+HE_HD void bs_vectorized(double S, double K, double T, double r, double sigma, double* call, double* put) {
+    const double Ts = (T <= 0.0) ? 1e-8 : T;
+    const double ss = (sigma < 1e-8) ? 1e-8 : sigma;
+    const double sqT = sqrt(Ts);
+    const double d1 = (log(S / K) + (r + 0.5 * (ss * ss)) * Ts) / (ss * sqT);
+    const double d2 = d1 - ss * sqT;
+    const double Kd = K * exp(-r * Ts);
+    double n1, m1, n2, m2;
+    ndtr_pair(d1, &n1, &m1);
+    ndtr_pair(d2, &n2, &m2);
+    double c = S * n1 - Kd * n2;
+    double p = Kd * m2 - S * m1;
+    if (T <= 0.0) {   // np.where(T <= 0, intrinsic, .)
+        const double KT = K * exp(-r * T);
+        c = np_max(S - KT, 0.0);
+        p = np_max(KT - S, 0.0);
+    }
+    *call = c;
+    *put = p;
+}
+
 // ---------------------------------------------------------------- PCG64 (numpy)
 // numpy/random/src/pcg64: 128-bit LCG, XSL-RR output; next32 keeps the high
 // half of a 64-bit draw buffered (has_uint32/uinteger).

@@ -145,6 +145,8 @@ struct Params {
     float var_f;
     double sqrt_var, drift, sqrt_dt, mu, dt;
     BSConst bs;             // constant-sigma BS constants (GBM)
+    int32_t mark;           // he_mark of the generated C / P
+    double fe_K;            // HE_MARK_FIXED_EUROPEAN: K = round(S0) (option_price_assignment.py:36)
     float g_sigma, g_num_drift;  // constant-variance greeks: sigma, (r+0.5 sigma**2)*T (f32)
     double g_sst;                // sigma*sqrt(T) (f64)
     double g_inv_sst;            // 1/(sigma*sqrt(T))
@@ -421,12 +423,24 @@ __device__ __forceinline__ void make_obs(const Params& p, const Env& e, const Mk
 }
 
 // ------------------------------------------------------------------ marks
-// f64 Black-Scholes marks at K = round(S) (rolling ATM, rbergomi_sim.py:418,437-446),
-// handed to the env as f32.
-template <int MODE>
-__device__ __forceinline__ void marks(const Params& p, double S64, double var64, float* C, float* P) {
-    double K = rint(S64);
+// f64 Black-Scholes marks of the market at episode step t, handed to the env as f32.
+// HE_MARK_ROLLING_ATM: the 30-day option at K = round(S) (rbergomi_sim.py:418,437-446).
+// HE_MARK_FIXED_EUROPEAN (FE = true: the kernel tests p.mark, a uniform branch): the
+// episode's option struck at round(S0) with T = max(1 - t/252, 0) years left, through
+// black_scholes_vectorized (option_price_assignment.py:10-21,36-38).
+template <int MODE, bool FE = true>
+__device__ __forceinline__ void marks(const Params& p, double S64, double var64, uint32_t t, float* C, float* P) {
     double c, q;
+    if (FE && p.mark == HE_MARK_FIXED_EUROPEAN) {
+        // np.clip(1 - time_grid / 252, 0, None): t / 252 correctly rounded (div_int_by)
+        const double tau = 1.0 - div_int_by((double)t, 252.0, p.inv_252);
+        const double sig = (MODE == HE_MODE_HESTON) ? sqrt(var64 < 0.0 ? 0.0 : var64) : p.sqrt_var;
+        bs_vectorized(S64, p.fe_K, tau < 0.0 ? 0.0 : tau, p.r_d, sig, &c, &q);
+        *C = (float)c;
+        *P = (float)q;
+        return;
+    }
+    double K = rint(S64);
     if (MODE == HE_MODE_HESTON) {
         BSConst h;
         double sig = sqrt(var64 < 0.0 ? 0.0 : var64);
@@ -787,7 +801,7 @@ __device__ __forceinline__ void market_body(Params p, Market cur, Market bak, in
 #if defined(HE_MKT_SKIP) && (HE_MKT_SKIP & 2)
             C = (float)S64; P = (float)v64;  // diagnostic build: no marks
 #else
-            marks<MODE>(p, S64, v64, &C, &P);
+            marks<MODE>(p, S64, v64, tj, &C, &P);
 #endif
         } else if (T == 1u) {  // lagged marks of t = T-1 = 0: the reset marks
             C = p.rstv[2];
@@ -796,7 +810,7 @@ __device__ __forceinline__ void market_body(Params p, Market cur, Market bak, in
             C = C0v;
             P = P0v;
         } else {               // lagged marks of t = T-1: slot j-1 (hedging_env_v2.py:229-231)
-            marks<MODE>(p, shS[lane][j - 1], HESTON ? shV[lane][j - 1] : p.var, &C, &P);
+            marks<MODE>(p, shS[lane][j - 1], HESTON ? shV[lane][j - 1] : p.var, T - 1u, &C, &P);
         }
         if (j == nsteps) {
             cur.C[i] = C;
@@ -858,7 +872,7 @@ __global__ void init_reset_kernel(Params p, float* rst) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
     p.s0s_const = 0;  // S0 is what this kernel computes: divide by the env's own max(S0, 25)
     float C, P;
-    marks<MODE>(p, p.s0, p.var, &C, &P);
+    marks<MODE>(p, p.s0, p.var, 0u, &C, &P);
     Mkt m{(float)p.s0, p.var_f, C, P};
     Env e;
     e.t = 0;
@@ -2067,7 +2081,7 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
 // Producer waves: block bp of 64 envs into LDS buffer bp & 1 while the steppers consume
 // block bp - 1.  pw = producer wave index (kLdsPEnvs envs each).  Lanes past the last
 // env mirror env N-1 like the steppers' (identical values, identical addresses).
-template <int MODE, bool BOOK>
+template <int MODE, bool BOOK, bool LEAN>
 __device__ __forceinline__ void lds_producer(const Params& p, int k_steps, const Market& cur,
                                              LdsMarketT<MODE, BOOK>& W, int64_t base, int pw) {
     using G = LdsGeom<MODE, BOOK>;
@@ -2253,7 +2267,8 @@ __device__ __forceinline__ void lds_producer(const Params& p, int k_steps, const
 #if defined(HE_LDS_SKIP) && (HE_LDS_SKIP & 2)
                     C = (float)Sm * 0.02f; P = (float)Sm * 0.018f;  // diagnostic build: no marks
 #else
-                    marks<MODE>(p, Sm, Vm, &C, &P);
+                    // the episode step of the marks: the slot's (tp + 1), or tp for the lagged ones
+                    marks<MODE, !LEAN>(p, Sm, Vm, last ? tp : tp + 1u, &C, &P);
 #endif
                     const int sl = sl0 + h;
                     W.sc[wb][sl][le] = make_float2((float)Sx[h], C);
@@ -2287,6 +2302,60 @@ __device__ __forceinline__ void lds_producer(const Params& p, int k_steps, const
     LDS_T1(2 + (pw < 2 ? pw : 1));
 }
 
+// Role placement.  A workgroup's 4 waves land on the CU's 4 SIMDs (in the cyclic order
+// 0 -> 2 -> 1 -> 3 from a varying start, MI355X_MICROARCH.md "LDS"), so with role = wave
+// index the role a SIMD hosts depends on where each resident workgroup's placement
+// started, and one SIMD can carry several obs steppers (the critical chain) while another
+// has none.  HE_LDS_BALANCE: every workgroup takes a ticket from a per-CU counter (one
+// atomic per workgroup) and its waves take role = (SIMD id + ticket) mod 4 -- a bijection
+// over its 4 distinct SIMDs, and across the 4 workgroups resident on a CU (consecutive
+// tickets) every SIMD hosts one wave of each role.  Wave-to-SIMD placement not
+// one-per-SIMD (never seen) falls back to role = wave index.
+#ifndef HE_LDS_BALANCE
+#define HE_LDS_BALANCE 0
+#endif
+#if HE_LDS_BALANCE || defined(HE_LDS_HWID)
+__device__ uint32_t g_cu_ticket[4096];
+#endif
+#ifdef HE_LDS_HWID
+// Diagnostic builds only: {HW_ID, XCC_ID, ticket, role} of every wave of the last launch
+// (he_debug_lds_hwid)
+__device__ uint32_t g_lds_hwid[16384][4][4];
+#endif
+__device__ __forceinline__ uint32_t hw_cu_key(uint32_t hw, uint32_t xcc) {
+    // XCC 4 bits | SE_ID 3 | SH_ID 1 | CU_ID 4
+    return ((xcc & 15u) << 8) | (((hw >> 13) & 7u) << 5) | (((hw >> 12) & 1u) << 4) | ((hw >> 8) & 15u);
+}
+template <int NWAVES>
+__device__ __forceinline__ int lds_role(int wave) {
+#if HE_LDS_BALANCE || defined(HE_LDS_HWID)
+    if constexpr (NWAVES == 4) {
+        __shared__ uint32_t sh_place[5];
+        const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);     // HW_REG_HW_ID, 32 bits
+        const uint32_t xcc = __builtin_amdgcn_s_getreg((15 << 11) | 20);   // HW_REG_XCC_ID
+        const uint32_t simd = (hw >> 4) & 3u;
+        if ((threadIdx.x & 63) == 0) sh_place[wave] = simd;
+        if (threadIdx.x == 0) sh_place[4] = atomicAdd(&g_cu_ticket[hw_cu_key(hw, xcc & 15u)], 1u);
+        __syncthreads();
+        const uint32_t m = (1u << sh_place[0]) | (1u << sh_place[1]) | (1u << sh_place[2]) | (1u << sh_place[3]);
+        int role = wave;
+#if HE_LDS_BALANCE
+        if (m == 15u) role = (int)((simd + sh_place[4]) & 3u);
+#endif
+#ifdef HE_LDS_HWID
+        if ((threadIdx.x & 63) == 0 && blockIdx.x < 16384) {
+            g_lds_hwid[blockIdx.x][wave][0] = hw;
+            g_lds_hwid[blockIdx.x][wave][1] = xcc;
+            g_lds_hwid[blockIdx.x][wave][2] = sh_place[4];
+            g_lds_hwid[blockIdx.x][wave][3] = (uint32_t)role | (m << 8);
+        }
+#endif
+        return __builtin_amdgcn_readfirstlane(role);
+    }
+#endif
+    return wave;
+}
+
 // Wave roles are uniform (readfirstlane), so each role's loop is plain scalar control
 // flow and all execute the same number of barriers; the roles' working sets never coexist.
 // SGPRs capped at 96 (.sgpr_count 94): past 96 the hardware admits one wave per SIMD
@@ -2299,7 +2368,7 @@ __global__ __launch_bounds__((LdsGeom<MODE, BOOK>::threads), (LdsGeom<MODE, BOOK
                                                                  int k_steps, Market cur) {
     __shared__ __attribute__((aligned(16))) LdsMarketT<MODE, BOOK> lm;
     const Params& p = *pc;  // read through the scalar cache (a by-value copy spills)
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wave = lds_role<LdsGeom<MODE, BOOK>::threads / 64>(__builtin_amdgcn_readfirstlane(threadIdx.x >> 6));
     const int64_t base = (int64_t)blockIdx.x * kLdsEnvs;
     if constexpr (BOOK) {  // the tau table into LDS (rows <= kLdsBookRows: lds_rollout_eligible)
         const int nv = 4 * p.book_rows;
@@ -2311,7 +2380,7 @@ __global__ __launch_bounds__((LdsGeom<MODE, BOOK>::threads), (LdsGeom<MODE, BOOK
     }
     if (wave == 0) lds_stepper<MODE, BOOK, LEAN, false>(p, s, io, k_steps, cur, lm, base);
     else if (wave == 1) lds_stepper<MODE, BOOK, LEAN, true>(p, s, io, k_steps, cur, lm, base);
-    else lds_producer<MODE, BOOK>(p, k_steps, cur, lm, base, wave - 2);
+    else lds_producer<MODE, BOOK, LEAN>(p, k_steps, cur, lm, base, wave - 2);
 }
 
 // Test hooks (he_device_rng / he_device_math): the device build of the generate-mode
@@ -2591,6 +2660,8 @@ static void fill_params(he_env* env) {
     p.bs.b = sig * sqrt(T);
     p.bs.inv_b = 1.0 / p.bs.b;
     p.bs.disc = exp(-r * T);
+    p.mark = c.mark;
+    p.fe_K = rint(c.s0);   // np.round(paths[:, 0]): every generated episode starts at s0
     // hedging_env_v2.py:84,95-99 for a constant f32 variance (numpy scalar powf)
     float vf = (float)c.variance;
     float vmax = (vf != vf) ? vf : (vf > 1e-8f ? vf : 1e-8f);
@@ -2945,8 +3016,9 @@ static bool lds_lean_config(const he_env* env, const Io& io) {
     const double s0 = c.s0, ic = fabs(c.initial_cash);
     const Params& p = env->p;
     const bool normal_greeks = !p.tenor_small && p.g_sigma > 1e-6f && p.g_sst >= 1e-9;  // greeks_lean
+    // the lean kernels' producers make rolling-ATM marks only (marks<MODE, false>)
     return fast_config(env) && io.obs && io.rew && io.term && s0 >= 1e-30 && s0 <= 1e30 && ic <= 1e30 &&
-           normal_greeks;
+           normal_greeks && c.mark == HE_MARK_ROLLING_ATM;
 }
 
 // he_rollout through lds_rollout_kernel: GBM or Heston, with or without a book (HE_LDS_ROLLOUT=0
@@ -3140,6 +3212,10 @@ he_status he_create(const he_config* cfg, he_env** out) {
         return fail(env, HE_EINVAL, "book_size must be in [0, %d]", HE_BOOK_MAX);
     if (c.book_size > 0 && c.mode == HE_MODE_REPLAY)
         return fail(env, HE_EINVAL, "the liability book needs a generate mode (GBM / Heston)");
+    if (c.mark != HE_MARK_ROLLING_ATM && c.mark != HE_MARK_FIXED_EUROPEAN)
+        return fail(env, HE_EINVAL, "bad mark %d (he_mark)", c.mark);
+    if (c.mark != HE_MARK_ROLLING_ATM && c.mode == HE_MODE_REPLAY)
+        return fail(env, HE_EINVAL, "replay mode reads its marks from the table (mark must be HE_MARK_ROLLING_ATM)");
     for (int k = 0; k < c.book_size; ++k)
         if (c.book[k].type < HE_BOOK_CALL || c.book[k].type > HE_BOOK_UO_CALL)
             return fail(env, HE_EINVAL, "book[%d].type %d is not an he_book_type", k, c.book[k].type);
@@ -3371,6 +3447,14 @@ he_status he_debug_lds_timing(void* host, size_t bytes) {
     const size_t cap = sizeof(g_lds_tim);
     if (bytes > cap) bytes = cap;
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_lds_tim), bytes, 0, hipMemcpyDeviceToHost) == hipSuccess ? HE_OK : HE_EHIP;
+}
+#endif
+
+#ifdef HE_LDS_HWID
+he_status he_debug_lds_hwid(void* host, size_t bytes) {
+    const size_t cap = sizeof(g_lds_hwid);
+    if (bytes > cap) bytes = cap;
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_lds_hwid), bytes, 0, hipMemcpyDeviceToHost) == hipSuccess ? HE_OK : HE_EHIP;
 }
 #endif
 
@@ -3640,9 +3724,13 @@ he_status he_get_config(const he_env* env, he_config* out) {
     return HE_OK;
 }
 
+// Checkpoint blob: an 8-byte header {ready flag, format << 8}, then every state field.
+// The format changes with the field list (3: + the episode summaries of ABI v3).
+constexpr uint64_t kStateFormat = 3;
+
 size_t he_state_size(const he_env* env) {
     if (!env) return 0;
-    size_t n = 8;  // header: ready flag
+    size_t n = 8;  // header: ready flag | format << 8
     for (auto& f : env->fields) n += f.first;
     return n;
 }
@@ -3658,7 +3746,7 @@ he_status he_get_state(he_env* env, void* host_buf, size_t size) {
         HE_HIP(env, hipDeviceSynchronize());
     }
     char* dst = (char*)host_buf;
-    uint64_t hdr = env->ready ? 1u : 0u;
+    uint64_t hdr = (env->ready ? 1u : 0u) | (kStateFormat << 8);
     memcpy(dst, &hdr, 8);
     dst += 8;
     for (auto& f : env->fields) {
@@ -3670,6 +3758,13 @@ he_status he_get_state(he_env* env, void* host_buf, size_t size) {
 
 he_status he_set_state(he_env* env, const void* host_buf, size_t size) {
     if (!env || !host_buf) return HE_EINVAL;
+    if (size >= 8) {
+        uint64_t h0;
+        memcpy(&h0, host_buf, 8);
+        if ((h0 >> 8) != kStateFormat)
+            return fail(env, HE_EINVAL, "checkpoint format %llu != %llu: saved by another libhedgeenv version",
+                        (unsigned long long)(h0 >> 8), (unsigned long long)kStateFormat);
+    }
     if (size != he_state_size(env)) return fail(env, HE_EINVAL, "state buffer size %zu != %zu", size, he_state_size(env));
     DeviceGuard dg(env->cfg.device);
     HE_HIP(env, hipDeviceSynchronize());
@@ -3681,7 +3776,7 @@ he_status he_set_state(he_env* env, const void* host_buf, size_t size) {
         HE_HIP(env, hipMemcpy(f.second, src, f.first, hipMemcpyHostToDevice));
         src += f.first;
     }
-    env->ready = hdr != 0;
+    env->ready = (hdr & 0xFF) != 0;
     // the restored `cur` is the envs' position: drop every block generated from the old
     // trajectory (a fused rollout leaves next_state 2, a side-stream prefetch 1)
     env->block_pos = env->cfg.market_block;

@@ -33,7 +33,7 @@ V1_DEFAULTS["transaction_cost_per_contract"] = 0.05
 
 GENERATE_DEFAULTS = dict(s0=496.48001098632812, variance=0.029028, mu=0.04, dt=1 / 252,
                          episode_length=252, heston_kappa=2.0, heston_theta=0.029028,
-                         heston_xi=0.3, heston_rho=-0.7)
+                         heston_xi=0.3, heston_rho=-0.7, mark="rolling_atm")
 
 MONITOR_KEYWORDS = ("per_share_step_pnl", "raw_pnl_deviation_abs", "transaction_costs_total")
 
@@ -66,6 +66,9 @@ class HedgingVecEnv:
     Replay mode (reference semantics): pass `data_file_path` (NPZ with paths,
     volatilities, call_prices_atm, put_prices_atm) or `tables=(S, v, C, P)`.
     Generate modes: `mode="gbm"` / `"heston"`, market in `generate=dict(...)`;
+    `generate["mark"]` = "rolling_atm" (default: the 30-day ATM option re-struck every
+    step, rbergomi_sim.py:418,437-446) or "fixed_european" (one option per episode at
+    K = round(S0), T = max(1 - t/252, 0), option_price_assignment.py:10-21,33-49).
     `generate["book"]` = list of up to 8 dicts {type: "call"|"put"|"uo_call",
     strike, expiry (steps), quantity (contracts, < 0 short), barrier} is the
     per-env liability book (extension, include/hedge_env.h he_book_option).
@@ -128,6 +131,12 @@ class HedgingVecEnv:
         cfg.heston_xi = float(gen["heston_xi"])
         cfg.heston_rho = float(gen["heston_rho"])
         cfg.market_block = int(market_block)
+        mark = gen["mark"]
+        if mark not in _lib.MARKS:
+            raise ValueError(f"mark must be one of {sorted(_lib.MARKS)}, not {mark!r}")
+        if mode == "replay" and mark != "rolling_atm":
+            raise ValueError("replay mode reads its marks from the table (mark='rolling_atm')")
+        cfg.mark = _lib.MARKS[mark]
         if book:
             if mode == "replay":
                 raise ValueError("the liability book needs a generate mode (gbm / heston)")

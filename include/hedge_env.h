@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define HE_ABI_VERSION 2
+#define HE_ABI_VERSION 3
 #define HE_BOOK_MAX 8
 #define HE_OBS_DIM 13
 #define HE_ACT_DIM 2
@@ -65,6 +65,19 @@ typedef enum he_mode {
     HE_MODE_GBM = 1,     /* generate: GBM + Philox, BS rolling-ATM marks       */
     HE_MODE_HESTON = 2   /* generate: Heston full-truncation Euler (extension) */
 } he_mode;
+
+/* How generate modes mark the two hedge instruments C, P at env step t (replay reads
+ * them from the table).  Both keep the env's terminal-step lag (hedging_env_v2.py:229-231). */
+typedef enum he_mark {
+    HE_MARK_ROLLING_ATM = 0,    /* 30-day call/put struck at K = round(S_t), re-struck every step:
+                                   the reference generator's marks (rbergomi_sim.py:418,437-446),
+                                   option_calculator.py:11-27 form                               */
+    HE_MARK_FIXED_EUROPEAN = 1  /* one call/put per episode struck at K = round(S_0), expiring
+                                   one year after the episode start: T = max(1 - t/252, 0),
+                                   black_scholes_vectorized (option_price_assignment.py:10-21,
+                                   33-49) at the market's volatility (GBM: sqrt(variance);
+                                   Heston: sqrt(max(v_t, 0)))                                   */
+} he_mark;
 
 typedef enum he_loss {
     HE_LOSS_MSE = 0,
@@ -134,7 +147,7 @@ typedef struct he_config {
                                    the step grid on `stream` (step_market_kernel), the
                                    other paths on the side stream                    */
     int32_t book_size;          /* generate modes: options in the liability book (0..8) */
-    int32_t reserved_i;
+    int32_t mark;               /* generate modes: he_mark (replay: must be ROLLING_ATM) */
     he_book_option book[HE_BOOK_MAX];
     double reserved[7];
 } he_config;

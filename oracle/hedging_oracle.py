@@ -28,8 +28,9 @@ Generate mode (the north-star extension) produces the same market data the
 reference would replay from an NPZ written by a GBM generator: S in f64
 (advanced with Philox4x32-10 normals, counter layout in `philox_normals`),
 variance constant, C/P = f64 Black-Scholes at K=round(S_t) (rolling ATM,
-rbergomi_sim.py:418,437-446) -- then runs the identical env logic on the f32
-casts (hedging_env_v2.py:38-41).
+rbergomi_sim.py:418,437-446; gen["mark"] = "fixed_european": the fixed-strike
+European of option_price_assignment.py:10-21,33-49, K = round(S0), T = 1 - t/252) --
+then runs the identical env logic on the f32 casts (hedging_env_v2.py:38-41).
 
 Pinned by: tests/golden/*.npz, recorded from the reference itself by
 oracle/make_golden.py (see tests/test_oracle_golden.py).
@@ -38,6 +39,8 @@ import json
 
 import numpy as np
 from scipy.special import ndtr
+
+from oracle.analytics_oracle import black_scholes_vectorized
 
 LOSS_CODES = {"mse": 0, "abs": 1, "cvar": 2}  # anything else -> 3 ("other", |x| branch)
 
@@ -334,6 +337,9 @@ class OracleVecEnv:
             self.S64 = np.zeros(self.n, np.float64)
             self.V64 = np.zeros(self.n, np.float64)
             self.book = list(g.get("book", None) or ())
+            self.mark = g.get("mark", "rolling_atm")
+            if self.mark not in ("rolling_atm", "fixed_european"):
+                raise ValueError(self.mark)
             self.runmax = np.zeros(self.n, np.float64)
         else:
             raise ValueError(mode)
@@ -355,7 +361,17 @@ class OracleVecEnv:
         self.pv_prev = z.astype(np.float64)
 
     # ------------------------------------------------------------------ market
-    def _gbm_marks(self, S64, V64=None):
+    def _gbm_marks(self, S64, V64, t):
+        """C, P (f64) of the generated market at episode step t (int array)."""
+        if self.mark == "fixed_european":
+            # option_price_assignment.py:33-49: strike np.round(paths[:, 0]), expiry one year
+            # after the episode start, T = np.clip(1 - t / 252, 0, None); the market's own
+            # volatility in place of the realized one (GBM sqrt(v), Heston sqrt(max(v_t, 0)))
+            K = np.round(np.full(len(S64), self.g_s0))
+            T = np.clip(1 - np.asarray(t, np.int64) / 252, 0, None)
+            v = V64 if self.mode == "heston" else np.full(len(S64), self.g_v)
+            sig = np.sqrt(np.maximum(v, 0.0))
+            return black_scholes_vectorized(S64, K, T, self.r, sig)
         K = np.round(S64)
         if self.mode == "heston":
             sig = np.sqrt(np.maximum(V64, 0.0))
@@ -463,7 +479,7 @@ class OracleVecEnv:
             self.V64[ids] = self.g_v
             S = self.S64[ids].astype(np.float32)
             v = np.full(len(ids), self.g_v).astype(np.float32)
-            Cd, Pd = self._gbm_marks(self.S64[ids], self.V64[ids])
+            Cd, Pd = self._gbm_marks(self.S64[ids], self.V64[ids], np.zeros(len(ids), np.int64))
             C = Cd.astype(np.float32)
             P = Pd.astype(np.float32)
         self.t[ids] = 0
@@ -591,7 +607,7 @@ class OracleVecEnv:
             self.S = self.S64.astype(np.float32)
             if self.mode == "heston":
                 self.v = self.V64.astype(np.float32)
-            Cd, Pd = self._gbm_marks(self.S64, self.V64)
+            Cd, Pd = self._gbm_marks(self.S64, self.V64, self.t)
             self.C = np.where(term, self.C, Cd.astype(np.float32))
             self.P = np.where(term, self.P, Pd.astype(np.float32))
             if self.book:

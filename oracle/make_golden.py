@@ -15,6 +15,8 @@ Outputs `tests/golden/*.npz` (inputs + expected outputs only; no reference
 source).  Re-run:  python oracle/make_golden.py
 G12 (generate mode closed loop, the oracle's GBM market replayed through the
 reference env):  python oracle/make_golden.py --closed-loop
+G13 (the same with fixed-strike European marks made by the reference's own
+black_scholes_vectorized):  python oracle/make_golden.py --closed-loop-fe
 """
 import os
 import sys
@@ -141,7 +143,7 @@ def run_scenario(name, variant, data, env_kwargs, n_envs, n_steps, seed_base, ac
           f"resets={int(term.sum())} nan_rewards={int(np.isnan(rew).sum())}")
 
 
-def closed_loop(n_envs=16, episodes=2, seed=42):
+def closed_loop(n_envs=16, episodes=2, seed=42, mark="rolling_atm"):
     """G12: generate mode pinned to the reference env itself.
 
     The GBM market of generate mode, as the oracle restates it (Philox4x32-10 normals
@@ -157,6 +159,8 @@ def closed_loop(n_envs=16, episodes=2, seed=42):
     from oracle.hedging_oracle import OracleVecEnv
     T = 252
     gen = dict(s0=496.48001098632812, variance=0.029028, mu=0.04, dt=1 / 252, episode_length=T)
+    if mark != "rolling_atm":
+        gen["mark"] = mark
     train = dict(loss_type="abs", pnl_penalty_weight=0.001, lambda_cost=0.0001,
                  theta_weight=0.0002, slippage_bps=1.0, record_metrics=True)  # train_ppo_v2.py:74-80
     orc = OracleVecEnv(n_envs, mode="gbm", gen=dict(gen, seed=seed, env_offset=0),
@@ -172,9 +176,26 @@ def closed_loop(n_envs=16, episodes=2, seed=42):
             orc.t[:] = t
             orc._gbm_advance(np.ones(n_envs, bool))
             S[:, e, t + 1] = orc.S64
-    C, P = orc._gbm_marks(S[..., :T].reshape(-1), None)
-    C = C.reshape(n_envs, E, T)
-    P = P.reshape(n_envs, E, T)
+    if mark == "fixed_european":
+        # the reference's own black_scholes_vectorized (option_price_assignment.py:10-21) over
+        # columns t = 0..T-1 as process_price_paths does (:33-49): K = np.round(S0),
+        # T = np.clip(1 - t / 252, 0, None), sigma = the GBM's sqrt(v) for the realized vol
+        bsv = importlib.import_module("src.sim.option_price_assignment").black_scholes_vectorized
+        Sf = S.reshape(n_envs * E, T + 1)
+        K = np.round(Sf[:, 0])
+        Tg = np.clip(1 - np.arange(T + 1) / 252, 0, None)
+        sig = np.full(n_envs * E, np.sqrt(gen["variance"]))
+        C = np.zeros((n_envs * E, T))
+        P = np.zeros((n_envs * E, T))
+        for t in range(T):
+            C[:, t], P[:, t] = bsv(Sf[:, t], K, Tg[t], 0.04, sig)
+        C = C.reshape(n_envs, E, T)
+        P = P.reshape(n_envs, E, T)
+    else:
+        tt = np.broadcast_to(np.arange(T), (n_envs, E, T)).reshape(-1)
+        C, P = orc._gbm_marks(S[..., :T].reshape(-1), None, tt)
+        C = C.reshape(n_envs, E, T)
+        P = P.reshape(n_envs, E, T)
     V = np.full((n_envs, E, T + 1), gen["variance"])
     cls = _ref_modules()[2]
     rng = np.random.default_rng(20251016)
@@ -225,13 +246,17 @@ def closed_loop(n_envs=16, episodes=2, seed=42):
         actions=actions, reset_obs=reset_obs, obs=obs, terminal_obs=term_obs, reward=rew, terminated=term)
     for k in INFO_KEYS:
         out["info_" + k] = info[k]
-    np.savez_compressed(os.path.join(OUT, "g12_closed_loop.npz"), **out)
-    print(f"g12_closed_loop: envs={n_envs} steps={n_steps} resets={int(term.sum())}")
+    name = "g12_closed_loop" if mark == "rolling_atm" else "g13_closed_loop_fixed_european"
+    np.savez_compressed(os.path.join(OUT, name + ".npz"), **out)
+    print(f"{name}: envs={n_envs} steps={n_steps} resets={int(term.sum())}")
 
 
 def main():
     if "--closed-loop" in sys.argv:
         closed_loop()
+        return
+    if "--closed-loop-fe" in sys.argv:
+        closed_loop(mark="fixed_european")
         return
     os.makedirs(OUT, exist_ok=True)
     rng = np.random.default_rng(20250629)

@@ -18,7 +18,7 @@ def pytest_configure(config):
 def golden_files(prefix="g"):
     return sorted(f for f in os.listdir(GOLDEN)
                   if f.startswith(prefix) and f.endswith(".npz")
-                  and not f.startswith(("g7_", "g9_", "g10_", "g11_", "g12_")))
+                  and not f.startswith(("g7_", "g9_", "g10_", "g11_", "g12_", "g13_")))
 
 
 @pytest.fixture(scope="session")

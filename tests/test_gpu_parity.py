@@ -300,6 +300,44 @@ def test_heston_matches_oracle():
     assert stats["pnl_exact"] == stats["pnl_total"], stats  # bit for bit, as for GBM
 
 
+@pytest.mark.parametrize("mode", ["gbm", "heston"])
+def test_fixed_european_marks_match_oracle(mode, greeks_site):
+    """he_config.mark = HE_MARK_FIXED_EUROPEAN (option_price_assignment.py:10-21,33-49):
+    C/P of the episode's option struck at round(S0), T = max(1 - t/252, 0), at the
+    market's volatility.  Episodes of 260 steps cross t = 252, where T reaches 0 and the
+    marks turn intrinsic (K e^{-r 0}).  Market info, P&L and rewards bit for bit."""
+    cfg = dict(loss_type="abs", pnl_penalty_weight=0.001, lambda_cost=0.0001, theta_weight=0.0002,
+               slippage_bps=1.0)
+    gen = dict(s0=496.48001098632812, variance=0.029028, mu=0.04, dt=1 / 252, episode_length=260,
+               mark="fixed_european")
+    if mode == "heston":
+        gen.update(heston_kappa=1.5, heston_theta=0.035, heston_xi=0.6, heston_rho=-0.7)
+    stats = run_gbm_pair(128, 300, 19, cfg, gen, mode=mode)
+    assert stats["pnl_exact"] == stats["pnl_total"], stats
+
+
+def test_fixed_european_reset_marks_and_config_errors():
+    """The reset obs carries the t = 0 fixed-European marks (T = 1 year), and the mark is
+    refused where it has no meaning (replay tables) or is not an he_mark."""
+    from cantorrl_amd.vec_env import HedgingVecEnv
+    from oracle.analytics_oracle import black_scholes_vectorized
+    s0 = 496.48001098632812
+    env = HedgingVecEnv(4, mode="gbm", generate=dict(mark="fixed_european"), return_numpy=False, info_keys=())
+    obs = env.reset_tensors().cpu().numpy()
+    c, p = black_scholes_vectorized(np.array([s0]), np.array([np.round(s0)]), np.array([1.0]), 0.04,
+                                    np.array([np.sqrt(0.029028)]))
+    s0s = np.float32(s0)
+    assert_same(obs[:, 1], np.full(4, np.float32(c[0]) / s0s, np.float32), "obs C/S0")
+    assert_same(obs[:, 2], np.full(4, np.float32(p[0]) / s0s, np.float32), "obs P/S0")
+    env.close()
+    with pytest.raises(ValueError):
+        HedgingVecEnv(4, mode="gbm", generate=dict(mark="asian"), return_numpy=False)
+    z = np.zeros((2, 3), np.float32) + 100
+    with pytest.raises(ValueError):
+        HedgingVecEnv(4, tables=(z, z, z[:, :2], z[:, :2]), generate=dict(mark="fixed_european"),
+                      return_numpy=False)
+
+
 def test_partial_reset_keeps_other_envs_on_their_paths():
     """he_reset(env_ids) mid-block rewinds the market of the untouched envs: their
     trajectories equal a run without the partial reset."""
@@ -588,6 +626,15 @@ LDS_CASES = {
                               dict(loss_type="mse", record_metrics=False), (5, 64, 13, 71)),
     "heston_hot_xi": (257, dict(episode_length=25, heston_kappa=0.5, heston_theta=0.09, heston_xi=2.5,
                                 heston_rho=0.3, variance=0.04), {}, (1, 5, 12, 13, 11, 37, 64, 3)),
+    # fixed-strike European marks (generic producers; T past 252: intrinsic marks)
+    "fixed_european": (1000, dict(episode_length=40, mark="fixed_european"),
+                       dict(loss_type="abs", pnl_penalty_weight=0.001, lambda_cost=0.0001, theta_weight=0.0002,
+                            slippage_bps=1.0), (64, 37, 100, 9)),
+    "fixed_european_long_T1": (257, dict(episode_length=255, mark="fixed_european"), {}, (300, 1, 213)),
+    "fixed_european_T1": (70, dict(episode_length=1, mark="fixed_european"), {}, (7, 12)),
+    "heston_fixed_european_book": (333, dict(episode_length=29, mark="fixed_european", **HESTON_GEN,
+                                             book=[dict(type="put", strike=480.0, expiry=20, quantity=-10.0)]),
+                                   {}, (5, 64, 13, 71)),
 }
 
 
@@ -734,19 +781,25 @@ def test_episode_summaries_match_oracle(path, monkeypatch):
     venv.close()
 
 
+CLOSED_LOOPS = {"rolling_atm": "g12_closed_loop.npz", "fixed_european": "g13_closed_loop_fixed_european.npz"}
+
+
+@pytest.mark.parametrize("mark", sorted(CLOSED_LOOPS))
 @pytest.mark.parametrize("api", ["step", "rollout_lds", "rollout_tile"])
-def test_generate_mode_matches_reference_closed_loop(api, monkeypatch):
-    """G12 (tests/golden/g12_closed_loop.npz): GPU generate mode against the UNMODIFIED
-    reference env replaying the generate-mode market (oracle/make_golden.py
-    --closed-loop; 16 envs x 2 episodes of 252 steps, seed 42, SURVEY 8(d) inputs).
-    he_step with every info field, and he_rollout through lds_rollout_kernel and through
-    the tile kernels: obs columns, done flags, integer fields bit-exact, greeks at
-    OBS_RTOL, rewards and the f64 P&L fields at PNL_RTOL."""
+def test_generate_mode_matches_reference_closed_loop(api, mark, monkeypatch):
+    """G12 / G13 (tests/golden/g12_closed_loop.npz, g13_closed_loop_fixed_european.npz): GPU
+    generate mode against the UNMODIFIED reference env replaying the generate-mode market
+    (oracle/make_golden.py --closed-loop / --closed-loop-fe; 16 envs x 2 episodes of 252
+    steps, seed 42, SURVEY 8(d) inputs; G13's marks made by the reference's own
+    black_scholes_vectorized).  he_step with every info field, and he_rollout through
+    lds_rollout_kernel and through the tile kernels: obs columns, done flags, integer
+    fields bit-exact, greeks at OBS_RTOL, rewards and the f64 P&L fields at PNL_RTOL."""
     import json
     from cantorrl_amd.vec_env import HedgingVecEnv
-    z = np.load(os.path.join(GOLDEN, "g12_closed_loop.npz"), allow_pickle=False)
+    z = np.load(os.path.join(GOLDEN, CLOSED_LOOPS[mark]), allow_pickle=False)
     d = {k: z[k] for k in z.files}
     gen, cfg = json.loads(str(d["gen_json"])), json.loads(str(d["config_json"]))
+    assert gen.get("mark", "rolling_atm") == mark
     n, steps = int(d["n_envs"]), int(d["n_steps"])
     monkeypatch.setenv("HE_LDS_ROLLOUT", "0" if api == "rollout_tile" else "1")
     env = HedgingVecEnv(n, mode="gbm", generate=gen, seed=int(d["seed"]), return_numpy=False,

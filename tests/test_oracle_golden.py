@@ -87,19 +87,26 @@ def test_bs_price_matches_option_calculator():
     assert_same(v, z["vega"], "vega", rtol=1e-12)
 
 
-def load_closed_loop():
+CLOSED_LOOPS = {"rolling_atm": "g12_closed_loop.npz", "fixed_european": "g13_closed_loop_fixed_european.npz"}
+
+
+def load_closed_loop(mark="rolling_atm"):
     import json
-    z = np.load(os.path.join(GOLDEN, "g12_closed_loop.npz"), allow_pickle=False)
+    z = np.load(os.path.join(GOLDEN, CLOSED_LOOPS[mark]), allow_pickle=False)
     d = {k: z[k] for k in z.files}
     return json.loads(str(d["gen_json"])), json.loads(str(d["config_json"])), d
 
 
-def test_oracle_generate_mode_matches_reference_closed_loop():
-    """G12: the oracle's generate mode (its own GBM market, made inside the env) equals
-    the unmodified reference env replaying that market (oracle/make_golden.py
-    --closed-loop): every obs, reward, done flag, terminal obs and info field, bit for
-    bit, over 2 episodes x 16 envs."""
-    gen, cfg, d = load_closed_loop()
+@pytest.mark.parametrize("mark", sorted(CLOSED_LOOPS))
+def test_oracle_generate_mode_matches_reference_closed_loop(mark):
+    """G12 / G13: the oracle's generate mode (its own GBM market, made inside the env)
+    equals the unmodified reference env replaying that market (oracle/make_golden.py
+    --closed-loop / --closed-loop-fe): every obs, reward, done flag, terminal obs and info
+    field, bit for bit, over 2 episodes x 16 envs.  G13's fixed-strike European marks were
+    made by the reference's own black_scholes_vectorized (option_price_assignment.py:10-21),
+    so it pins the oracle's mark function as well as the env mechanics."""
+    gen, cfg, d = load_closed_loop(mark)
+    assert gen.get("mark", "rolling_atm") == mark
     n, seed = int(d["n_envs"]), int(d["seed"])
     env = OracleVecEnv(n, mode="gbm", gen=dict(gen, seed=seed, env_offset=0), **cfg)
     env.seed_envs_at(np.arange(n), [seed] * n)
