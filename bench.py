@@ -63,7 +63,15 @@ LDS_STEP_B, LDS_STATE_B = 65, 80
 # he_rollout step_kernel (K steps): per step action 8 + tile post slots 24 | 12 | 32 + obs
 #   52 + reward 4 + terminated 1; per launch state 32 + pre slot 12 | 12 | 16
 GREEKS_IN_STEP_MIN_ENVS = 262144  # hedge_env.hip kGreeksInStepMinEnvs
-STEP_BYTES_PER_ENV = {"gbm": 134, "gbm_step": 122, "heston": 146}
+STEP_BYTES_PER_ENV = {"gbm": 134, "gbm_step": 122, "heston": 146,
+                      # replay he_step: state 16 + path 4 + S0 4 + action 8 + table rows (pre {S,v,C,P}
+                      # 16, post 16, post greeks 16) + obs 52 + reward 4 + flags 2 + state written 16
+                      "replay": 154}
+# Replay rollouts (step_kernel, K fused steps): per env-step action 8 + the path row's
+# {S, v, C, P} 16 and {greeks, lag} 16 + obs 52 + reward 4 + terminated 1; per launch the
+# state (t, pos, cash) read + written 32, path + S0 read 8, the pre-step row 16.  SURVEY 8(d)
+# prices replay at its generate-mode figure + the 16-B gather of S, v, C, P at t + 1.
+REPLAY_ROLLOUT_B, REPLAY_STATE_B, SURVEY_REPLAY_GATHER_B = 97, 56, 16
 ROLLOUT_BYTES_PER_ENV = {"gbm": 89, "gbm_step": 77, "heston": 97}
 ROLLOUT_STATE_BYTES = {"gbm": 44, "gbm_step": 44, "heston": 48}
 # market_kernel per env-step: tile records written; per env and block: the block-start
@@ -84,14 +92,16 @@ def fused_market():
 
 
 def tile_layout(mode, n):
-    if mode == "heston":
-        return "heston"
+    if mode in ("heston", "replay"):
+        return mode
     thr = int(os.environ.get("HE_GREEKS_IN_STEP_MIN_ENVS") or GREEKS_IN_STEP_MIN_ENVS)
     return "gbm_step" if n >= thr else "gbm"
 
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
-MIN_TIMED_STEPS = 512  # >= 2 episodes of 252 steps
+# >= 2 episodes of 252 steps; 2,560 = 10 launches of the K = 256 rollout, so the
+# timed region's per-launch device time averages over 10 dispatches
+MIN_TIMED_STEPS = 2560
 M_BLOCK = 64           # market block (he_config.market_block)
 
 TRAIN_KW = dict(loss_type="abs", pnl_penalty_weight=0.001, lambda_cost=0.0001, theta_weight=0.0002,
@@ -120,7 +130,52 @@ CONFIGS = {
             kw=TRAIN_KW,
             workload="configs[4]: Heston full-truncation Euler (rho=-0.7) + up-and-out barrier call book, "
                      "131,072 envs/GPU (1M over 8 GPUs)"),
+    # the agents' own workload: train_ppo_v2.py:40 replays paths_rbergomi_options_100k.npz (100,000
+    # paths x 253 columns, 405 MB as f32 {S, v, C, P}, past the 256 MB Infinity Cache) through
+    # hedging_env_v2.py:223-231; a synthetic table of that shape in the reference NPZ layout
+    6: dict(envs=65536, mode="replay", gen=GEN, kw=TRAIN_KW, table=dict(paths=100000, cols=253),
+            workload="replay (train_ppo_v2.py:40): 65,536 envs/GPU replaying a synthetic 100,000 x 253 path table "
+                     "in the reference NPZ layout (paths, volatilities, call/put_prices_atm), v2 env, "
+                     "train_ppo_v2 reward"),
 }
+
+_TABLES = {}
+
+
+def replay_tables(paths, cols, seed=2025):
+    """A synthetic table in the reference NPZ layout (rbergomi_sim.py:528 keys, f32 as
+    hedging_env_v2.py:36-41 loads them): S = a GBM-like path from S0 = 496.48 with a
+    lognormal variance v, C / P = Black-Scholes rolling-ATM marks (30-day tenor, r = 0.04)
+    at K = round(S_t) and sigma = sqrt(v_t), columns 0 .. cols - 2."""
+    key = (paths, cols, seed)
+    if key in _TABLES:
+        return _TABLES[key]
+    from scipy.special import ndtr
+    rng = np.random.default_rng(seed)
+    T = cols - 1
+    dt, r, tenor = 1 / 252, 0.04, 30 / 252
+    xi = 0.029028
+    S = np.empty((paths, cols), np.float32)
+    v = np.empty((paths, cols), np.float32)
+    C = np.empty((paths, T), np.float32)
+    P = np.empty((paths, T), np.float32)
+    for a in range(0, paths, 12500):  # bounded f64 temporaries
+        b = min(paths, a + 12500)
+        m = b - a
+        wv = np.cumsum(rng.standard_normal((m, cols)) * np.sqrt(dt), axis=1)
+        vv = xi * np.exp(1.5 * wv - 0.5 * 1.5 ** 2 * np.arange(cols) * dt)
+        z = rng.standard_normal((m, T))
+        lr = (r - 0.5 * vv[:, :-1]) * dt + np.sqrt(vv[:, :-1] * dt) * z
+        SS = 496.48 * np.exp(np.concatenate([np.zeros((m, 1)), np.cumsum(lr, axis=1)], axis=1))
+        S[a:b], v[a:b] = SS, vv
+        s, K, sig = SS[:, :-1], np.round(SS[:, :-1]), np.sqrt(vv[:, :-1])
+        d1 = (np.log(s / K) + (r + 0.5 * sig * sig) * tenor) / (sig * np.sqrt(tenor))
+        d2 = d1 - sig * np.sqrt(tenor)
+        Kd = K * np.exp(-r * tenor)
+        C[a:b] = s * ndtr(d1) - Kd * ndtr(d2)
+        P[a:b] = Kd * ndtr(-d2) - s * ndtr(-d1)
+    _TABLES[key] = (S, v, C, P)
+    return _TABLES[key]
 
 
 def parse(argv=None):
@@ -136,7 +191,7 @@ def parse(argv=None):
                          "train_ppo_v2.py:48, on the LDS path; 64 on the tile path)")
     ap.add_argument("--no-step-api", action="store_true", help="skip the secondary graph-mode he_step run")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-seconds", type=float, default=6.0, help="seconds per CPU-baseline leg (4 legs)")
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC traffic pass")
     ap.add_argument("--probe", action="store_true", help=argparse.SUPPRESS)
@@ -148,23 +203,23 @@ def parse(argv=None):
     return ap.parse_args(argv)
 
 
-def _cpu_sample(seconds, seed=42, barrier=None):
-    """One host core: the oracle (NumPy restatement of the reference env) on 256 envs."""
+def _cpu_sample(seconds, seed=42, barrier=None, n=256, offset=0):
+    """One host core: the oracle (NumPy restatement of the reference env) on n envs
+    (global env ids offset .. offset + n - 1 of the GBM workload)."""
     from oracle.hedging_oracle import OracleVecEnv
-    n = 256
-    env = OracleVecEnv(n, mode="gbm", gen=dict(GEN, seed=seed), **TRAIN_KW)
+    env = OracleVecEnv(n, mode="gbm", gen=dict(GEN, seed=seed, env_offset=offset), **TRAIN_KW)
     env.seed_envs_at(np.arange(n), [seed] * n)
     env.reset()
-    rng = np.random.default_rng(seed)
-    acts = rng.uniform(-1, 1, size=(64, n, 2)).astype(np.float32)
-    for k in range(8):
+    rng = np.random.default_rng(seed + offset)
+    acts = rng.uniform(-1, 1, size=(8, n, 2)).astype(np.float32)
+    for k in range(2):
         env.step(acts[k])
     if barrier is not None:
         barrier.wait()
     steps = 0
     t0 = time.perf_counter()
     while True:
-        env.step(acts[steps % 64])
+        env.step(acts[steps % 8])
         steps += 1
         el = time.perf_counter() - t0
         if el >= seconds:
@@ -181,32 +236,48 @@ def _pool_init(b):
 
 
 def _pool_task(a):
-    return _cpu_sample(a[0], a[1], _BARRIER)
+    return _cpu_sample(a[0], a[1], _BARRIER, n=a[2], offset=a[3])
+
+
+def _cpu_all_cores(seconds, procs, n_per, shard):
+    """procs forked processes, one thread each, started together (a barrier)."""
+    import multiprocessing as mp
+    ctx = mp.get_context("fork")
+    b = ctx.Barrier(procs)
+    with ctx.Pool(procs, initializer=_pool_init, initargs=(b,)) as pool:
+        res = pool.map(_pool_task, [(seconds, 42 if shard else 42 + i, n_per, i * n_per if shard else 0)
+                                    for i in range(procs)])
+    return sum(s / e for s, e in res)
 
 
 def cpu_baseline(seconds):
-    """the oracle at N=256 on the host, 1 thread and one process per core.
+    """SURVEY 8(d) / BASELINE.md section 2: the oracle on the host at N = 65,536 (the
+    headline workload) and N = 256 (config 1), one process with one thread, then all
+    granted cores (one process per core; at 65,536 each process steps its 65,536 / P
+    shard of the global env ids).  `value` is the 65,536-env all-cores rate.
 
-    Must run before anything initialises the GPU: the all-core leg forks worker processes.
+    Must run before anything initialises the GPU: the all-core legs fork worker processes.
     """
-    import multiprocessing as mp
-    steps1, el1 = _cpu_sample(seconds)
-    v1 = steps1 / el1
+    N = CONFIGS[2]["envs"]
     try:
         avail = len(os.sched_getaffinity(0))
     except AttributeError:
         avail = os.cpu_count() or 1
     procs = max(1, min(avail, 16))   # the GPU box grants 16 host cores per GPU
-    ctx = mp.get_context("fork")
-    b = ctx.Barrier(procs)
-    with ctx.Pool(procs, initializer=_pool_init, initargs=(b,)) as pool:
-        res = pool.map(_pool_task, [(seconds, 42 + i) for i in range(procs)])
-    vp = sum(s / e for s, e in res)
-    return dict(value=vp, unit="env-steps/s", cores=procs, kind="port",
-                sample=f"oracle/hedging_oracle.py OracleVecEnv GBM, 256 envs per process, {procs} processes "
-                       f"x {seconds:.0f} s (NumPy, 1 thread each; {avail} cores in affinity mask)",
-                single_core_value=v1,
-                single_core_sample=f"256 envs x {steps1 // 256} steps ({el1:.1f} s, 1 thread)",
+    s1, e1 = _cpu_sample(seconds, n=N)
+    vN = _cpu_all_cores(seconds, procs, N // procs, shard=True)
+    s256, e256 = _cpu_sample(seconds)
+    v256 = _cpu_all_cores(seconds, procs, 256, shard=False)
+    return dict(value=vN, unit="env-steps/s", cores=procs, kind="port",
+                sample=f"oracle/hedging_oracle.py OracleVecEnv GBM (the headline workload), {N} envs as {procs} "
+                       f"processes x {N // procs} envs x {seconds:.0f} s (NumPy, 1 thread each; {avail} cores in "
+                       f"affinity mask)",
+                single_core_value=s1 / e1,
+                single_core_sample=f"{N} envs x {s1 // N} steps in one process ({e1:.1f} s, 1 thread)",
+                n256_value=v256,
+                n256_sample=f"256 envs per process, {procs} processes x {seconds:.0f} s (BASELINE config 1)",
+                n256_single_core_value=s256 / e256,
+                n256_single_core_sample=f"256 envs x {s256 // 256} steps ({e256:.1f} s, 1 thread)",
                 **REFERENCE_CPU)
 
 
@@ -223,6 +294,14 @@ REFERENCE_CPU = dict(
 def make_env(args, dev, rank=0, prefetch="auto"):
     from cantorrl_amd.vec_env import HedgingVecEnv
     cfg = CONFIGS[args.config]
+    if cfg["mode"] == "replay":
+        # env i of rank r draws its episodes from PCG64(SeedSequence(seed + r * envs + i)),
+        # the reference's per-env reset(seed) streams (hedging_env_v2.py:146-150)
+        env = HedgingVecEnv(args.envs, tables=replay_tables(**cfg["table"]), seed=args.seed,
+                            global_env_offset=rank * args.envs, device=dev, return_numpy=False, info_keys=(),
+                            **cfg["kw"])
+        env.reset_tensors()
+        return env
     env = HedgingVecEnv(args.envs, mode=cfg["mode"], generate=cfg["gen"], seed=args.seed,
                         global_env_offset=rank * args.envs, device=dev, return_numpy=False, info_keys=(),
                         market_prefetch=prefetch, **cfg["kw"])
@@ -563,7 +642,12 @@ def roofline(mode, n, kern_ms, rk, book=False, market="gbm", lds=False):
     overhead = 0
     if mode == "rollout":
         survey = n * (rk * SURVEY_ROLLOUT_B + SURVEY_ROLLOUT_STATE_B)
-        if lds:
+        if market == "replay":
+            survey = n * (rk * (SURVEY_ROLLOUT_B + SURVEY_REPLAY_GATHER_B) + SURVEY_ROLLOUT_STATE_B)
+            own = n * (rk * REPLAY_ROLLOUT_B + REPLAY_STATE_B)
+            kname = ("step_kernel (he_rollout, replay, K=%d fused steps; each env gathers its path row from "
+                     "the table)" % rk)
+        elif lds:
             # + the book's running max, + Heston's f64 variance (each read + written)
             own = n * (rk * LDS_STEP_B + LDS_STATE_B + (16 if book else 0) + (16 if market == "heston" else 0))
             kname = ("lds_rollout_kernel (he_rollout, K=%d fused steps; the market made in LDS by "
@@ -578,7 +662,7 @@ def roofline(mode, n, kern_ms, rk, book=False, market="gbm", lds=False):
                 kname = ("step_market_kernel (he_rollout, K=%d fused steps + the next block's market "
                          "tile in the same grid)" % rk)
     else:
-        survey = n * SURVEY_STEP_B
+        survey = n * (SURVEY_STEP_B + (SURVEY_REPLAY_GATHER_B if market == "replay" else 0))
         own = n * (STEP_BYTES_PER_ENV[market] + (16 if book else 0))
         kname = "step1_kernel (he_step, K=1)"
     achieved = survey / (kern_ms * 1e-3) / 1e9
@@ -797,7 +881,7 @@ def main(argv=None):
             args.envs = CONFIGS[args.config]["envs"]
         if args.rollout_k is None and args.workload == "env":
             lds0 = args.mode == "rollout" and lds_rollout(CONFIGS[args.config])
-            args.rollout_k = 256 if lds0 else M_BLOCK
+            args.rollout_k = 256 if (lds0 or CONFIGS[args.config]["mode"] == "replay") else M_BLOCK
         sys.exit(launch(args, argv))
     if args.workload == "rbergomi":
         rbergomi_main(args)
@@ -805,9 +889,10 @@ def main(argv=None):
     if args.envs is None:
         args.envs = CONFIGS[args.config]["envs"]
     lds = args.mode == "rollout" and lds_rollout(CONFIGS[args.config])
+    replay = CONFIGS[args.config]["mode"] == "replay"  # one step_kernel dispatch per he_rollout, any K
     if args.rollout_k is None:
-        args.rollout_k = 256 if lds else M_BLOCK
-    if args.mode == "rollout" and (args.rollout_k < 1 or (not lds and args.rollout_k > M_BLOCK)):
+        args.rollout_k = 256 if (lds or replay) else M_BLOCK
+    if args.mode == "rollout" and (args.rollout_k < 1 or (not (lds or replay) and args.rollout_k > M_BLOCK)):
         raise SystemExit("--rollout-k must be >= 1 (<= 64 on the tile path: one dispatch per call is timed)")
     if args.probe:
         probe(args)
@@ -862,11 +947,24 @@ def main(argv=None):
                        bytes_per_rank=n * 16, gathers=runner.gathers)
         payload.update(summarize_payload(runner.gathered))
     hev = HipEvents()
-    kern_ms = kernel_time_ms(hev, runner, 64 if args.mode == "rollout" else 256)
+    probe_ms = kernel_time_ms(hev, runner, 64 if args.mode == "rollout" else 256)
     env.close()
+    # The dominant kernel's average launch duration.  On the LDS path one he_rollout is one
+    # lds_rollout_kernel dispatch, so the HIP events around the timed region on the
+    # launching stream, over its launches, are that average (the task's definition; at one
+    # rank nothing else runs on the stream).  Elsewhere (tile path: market + step kernels
+    # per call; ranks > 1: the gathers ride on the stream) the per-dispatch probe
+    # (he_time_next_step: hipExtLaunchKernelGGL events around exactly the step kernel).
+    launches = K // runner.chunk
+    region = (lds or (replay and args.mode == "rollout")) and world == 1
+    kern_ms = dev_ms / launches if region else probe_ms
 
     roof = roofline(args.mode, n, kern_ms, args.rollout_k, has_book, tile_layout(cfg["mode"], n), lds)
-    if not lds:  # the tile path: market_kernel makes the HBM market tile
+    roof["kernel_us_source"] = ("HIP events around the timed region / %d launches" % launches if region else
+                                "he_time_next_step probe: HIP events around single dispatches")
+    roof["kernel_us_probe"] = round(probe_ms * 1e3, 3)
+    roof["kernel_us_timed_region"] = round(dev_ms / launches * 1e3, 3)
+    if not lds and not replay:  # the tile path: market_kernel makes the HBM market tile
         roof["tile_layout"] = tile_layout(cfg["mode"], n)
         mkt_ms = market_time_ms(hev, args, dev, acts, stream)
         roof["market_kernel_us_per_64_steps"] = round(mkt_ms * 1e3, 3)
@@ -893,6 +991,17 @@ def main(argv=None):
         roof["traffic_counters_kb"] = {k: round(v, 1) for k, v in pmc[1].items()}
     else:
         roof["traffic_note"] = pmc[1]
+    if (has_book or cfg["mode"] == "heston") and roof.get("valu") and roof["valu"]["kernel"] == "lds_rollout_kernel":
+        # configs 4 / 5: the producers' f64 market work (8 Black-Scholes prices per env-step,
+        # or the Heston chain + barrier pricer) bounds the kernel, not HBM.  The roofline is
+        # the VALU issue rate against the issue bound of the kernel's own f64 / other mix (a
+        # wave64 instruction every 2 cycles per SIMD, f64 every 4); the HBM side stays under "hbm".
+        v = roof["valu"]
+        hbm = {k: roof.pop(k) for k in ("achieved", "peak", "unit", "frac")}
+        hbm["bound_note"] = "not the bound of this configuration (see valu)"
+        roof = dict(bound="valu", achieved=v["issue_per_simd_cycle"], peak=v["issue_bound_per_simd_cycle"],
+                    unit="VALU wave-instructions per SIMD-cycle", frac=v["valu_issue_frac"],
+                    traffic=roof.pop("traffic", None), hbm=hbm, **{k: x for k, x in roof.items() if k != "bound"})
 
     step_api = None
     if world == 1 and args.mode != "graph" and not args.no_step_api:
@@ -916,14 +1025,21 @@ def main(argv=None):
             "n_gpus": world,
             "steps": K,
             "warmup": W,
+            # the command's --steps / --warmup: raised to the timed floor (MIN_TIMED_STEPS, >= 2
+            # episodes and 10 launches) and to whole launches of the rollout chunk
+            "requested_steps": args.steps,
+            "requested_warmup": args.warmup,
             "ms_per_step": round(wall * 1e3 / K, 6),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f64+f32",
-            "data": "synthetic (GBM paths from Philox4x32-10, U(-1,1) actions pre-generated on device)",
+            "data": ("synthetic (a 100,000 x 253 GBM / lognormal-variance table with rolling-ATM BS marks in "
+                     "the reference NPZ layout, U(-1,1) actions pre-generated on device)" if replay else
+                     "synthetic (GBM paths from Philox4x32-10, U(-1,1) actions pre-generated on device)"),
             "config": {"workload": cfg["workload"], "config_index": args.config, "envs_per_gpu": n,
-                       "episode_length": cfg["gen"]["episode_length"], "mode": args.mode,
+                       "episode_length": (cfg["table"]["cols"] - 1) if replay else cfg["gen"]["episode_length"],
+                       "mode": args.mode,
                        "rollout_k": args.rollout_k if args.mode == "rollout" else None,
                        "parallelism": f"env-shard x{world}"},
             "device_ms_per_step": round(dev_ms / K, 6),

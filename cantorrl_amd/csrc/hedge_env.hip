@@ -1472,6 +1472,63 @@ __device__ __forceinline__ void step_body(const Params& pk, int64_t n_envs, cons
                 flush_part(k);
             }
         }
+    } else if (REPLAY && !SINGLE && p.T > kRolloutPrefetch) {
+        // replay rollout (train_ppo_v2.py:40's workload): the same D-deep ring, the rows of
+        // step k+D issued before step k's stores.  Step kk's row is the env's path at its t
+        // then (hedging_env_v2.py:223-231): from the state before step k, t_k + (kk - k) + 1
+        // while no episode ends in between (t_k + (kk - k) < T); past an end the new path is
+        // not drawn yet, so that slot is loaded from the old path and re-issued once the
+        // reset has drawn it (every ring slot of a lane that just reset: its step k + m
+        // reads row m of the new path) -- a wave-uniform branch once per episode.
+        constexpr int D = kRolloutPrefetch;
+        const int32_t T = p.T;
+        const int64_t icl = wrow0 + (lane % kEpw);
+        const int64_t ic = icl < N ? icl : N - 1;
+        float2 ra[D];
+        float4 rA[D], rB[D];
+        ra[0] = a;
+        rA[0] = postA;
+        rB[0] = postB;
+        auto row_of = [&](int gap) {   // the post-step row of the step `gap` ahead of the current one
+            const uint32_t tb = (live ? e.t : 0u) + (uint32_t)gap;
+            const uint32_t tn = tb < (uint32_t)T ? tb + 1u : (uint32_t)T;
+            return (live ? (int64_t)e.path : 0) * (T + 1) + tn;
+        };
+        auto load = [&](int d, int kk, int gap) {
+            kk = kk < k_steps ? kk : k_steps - 1;
+            if (!POL) ra[d] = ld2(gact, (int64_t)kk * N + ic);
+            const int64_t r = row_of(gap);
+            rA[d] = ld4(mA, r);
+            rB[d] = ld4(mB, r);
+        };
+#pragma unroll
+        for (int d = 1; d < D; ++d) load(d, d, d);
+        for (int kb = 0; kb < k_steps; kb += D) {
+#pragma unroll
+            for (int d = 0; d < D; ++d) {
+                const int k = kb + d;
+                if (k >= k_steps) break;
+                const Mkt post = as_mkt(rA[d]);
+                const float4 g = rB[d];
+                const float2 ak = ra[d];
+                load(d, k + D, D);
+                step_part(k, post, g, ak);
+                // a lane that just reset (t back to 0 on a new path): its slots for steps
+                // k + 1 .. k + D were issued from the old path
+                if (__ballot(live && e.t == 0u) != 0ull) {
+                    if (live && e.t == 0u) {
+#pragma unroll
+                        for (int m = 1; m <= D; ++m) {
+                            const int sl = (d + m) % D;
+                            const int64_t r = (int64_t)e.path * (T + 1) + m;
+                            rA[sl] = ld4(mA, r);
+                            rB[sl] = ld4(mB, r);
+                        }
+                    }
+                }
+                flush_part(k);
+            }
+        }
     } else {
         for (int k = 0; k < k_steps; ++k) {
             Mkt post = as_mkt(postA);
@@ -3598,11 +3655,17 @@ he_status he_step(he_env* env, const float* actions, float* obs, float* reward, 
         const void* const* f = reinterpret_cast<const void* const*>(info);
         for (size_t k = 0; k < sizeof(he_info) / sizeof(void*); ++k) want_info |= f[k] != nullptr;
     }
-    if (env->vn_on && (!obs || !reward))
+    // he_vecnorm_attach arms THIS step only (one-shot): steps nobody armed -- the inner env
+    // stepped directly, another wrapper's -- never touch a wrapper's returns or partials
+    const bool vn = env->vn_on;
+    if (vn && (!obs || !reward)) {
+        env->vn_on = false;
         return fail(env, HE_EINVAL, "he_vecnorm_attach: he_step needs the obs and reward buffers");
+    }
     env->vn_fused = false;
     he_status s = launch_steps(env, io, want_info, 1, stream);
-    if (s != HE_OK || !env->vn_on || env->vn_fused) return s;
+    env->vn_on = false;
+    if (s != HE_OK || !vn || env->vn_fused) return s;
     // VecNormalize attached, and this step took another kernel: the moments after it
     vn::MomentsArgs vm = env->vn;
     vm.obs = obs;

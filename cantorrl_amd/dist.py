@@ -25,11 +25,12 @@ def shard_offset(n_per_rank, rank):
     return n_per_rank * rank
 
 
-def init(backend=None):
-    """Initialise the default process group for this process's device."""
+def init(backend=None, force=False):
+    """Initialise the default process group for this process's device (at world size 1
+    only with force=True: a one-rank group, e.g. to exercise RCCL on a one-GPU box)."""
     import torch.distributed as dist
     rank, local, world = world_info()
-    if world == 1 or dist.is_initialized():
+    if dist.is_initialized() or (world == 1 and not force):
         return rank, local, world
     if backend is None:
         backend = "nccl" if torch.cuda.is_available() else "gloo"
@@ -45,7 +46,7 @@ def gather_rollout(t, group=None):
     """All-gather a per-env tensor [N, ...] from every rank -> [world*N, ...] in
     global-id order (rank-major, matching shard_offset)."""
     import torch.distributed as dist
-    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+    if not dist.is_initialized():
         return t
     w = dist.get_world_size(group)
     out = torch.empty((w * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)

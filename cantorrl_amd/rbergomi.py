@@ -22,7 +22,8 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "librbergomi.so")
+# CANTORRL_RBERGOMI_LIB: an alternative build (e.g. the host-ASan build of tools/asan/run.sh)
+LIB_PATH = os.environ.get("CANTORRL_RBERGOMI_LIB") or os.path.join(HERE, "lib", "librbergomi.so")
 RB_ABI_VERSION = 1
 RB_OK, RB_EINVAL, RB_EHIP = 0, 1, 3
 OPTION_TYPES = {"call": 0, "put": 1}

@@ -59,7 +59,6 @@ class DeviceVecNormalize:
         # (he_vecnorm_attach; up to 65,536 envs), then he_vecnorm_apply; else he_vecnorm_step
         self._fusable = (getattr(venv, "_h", None) is not None and n <= 65536
                          and os.environ.get("CANTORRL_VN_FUSED", "1") != "0")
-        self._attached = None
         self._actions_pending = None
         self._t_start = time.time()
 
@@ -171,8 +170,13 @@ class DeviceVecNormalize:
         """(normalized obs, normalized reward, terminated, truncated) device tensors;
         the normalized terminal obs of done envs are in `terminal_obs_tensor`."""
         p = self._params()
-        fused = self._attach(p)
-        obs, rew, term, trunc = self.venv.step_tensors(actions)
+        fused = self._arm(p)
+        try:
+            obs, rew, term, trunc = self.venv.step_tensors(actions)
+        except BaseException:
+            if fused:  # the armed he_step did not run: nothing may keep this object's buffers
+                self.lib.he_vecnorm_attach(self.venv._h, None, None, None, None)
+            raise
         fn = self.lib.he_vecnorm_apply if fused else self.lib.he_vecnorm_step
         st = fn(ctypes.byref(p), self.num_envs, self._p(obs), self._p(rew),
                                       self._p(term), self._p(self.venv._tobs), self._p(self._returns),
@@ -183,39 +187,22 @@ class DeviceVecNormalize:
         self._check(st, "he_vecnorm_apply" if fused else "he_vecnorm_step")
         return self._obs_out, self._rew_out, term, trunc
 
-    def _attach(self, p):
-        """Attach (or detach) the statistics to the env's he_step for this step's
-        parameters; returns whether he_step now runs the moments."""
-        want = self._fusable and bool(p.training)
-        key = (p.training, p.norm_obs, p.gamma) if want else None
-        if key != self._attached:
-            h = self.venv._h
-            st = self.lib.he_vecnorm_attach(h, ctypes.byref(p) if want else None, self._p(self._returns),
-                                            self._p(self._stats), self._p(self._scratch))
-            if st != _lib.HE_OK and want:  # a build without the fused path: two launches
-                self._fusable, want, key = False, False, None
-            else:
-                self._check(st, "he_vecnorm_attach")
-            self._attached = key
-        return want
-
-    def _detach(self):
-        """The env handle keeps device pointers into this object's buffers while attached:
-        drop them before the buffers go (close, garbage collection)."""
-        h = getattr(self.venv, "_h", None)
-        if getattr(self, "_attached", None) is not None and h is not None and h.value:
-            self.lib.he_vecnorm_attach(h, None, None, None, None)
-        self._attached = None
+    def _arm(self, p):
+        """Arm the env's next he_step (one-shot, he_vecnorm_attach) to run the moments half
+        into this object's buffers; returns whether it will.  Armed per step, so another
+        wrapper on the same env, or the inner env stepped directly, never reads or advances
+        these buffers, and the handle holds no pointer into them after the step."""
+        if not (self._fusable and p.training):
+            return False
+        st = self.lib.he_vecnorm_attach(self.venv._h, ctypes.byref(p), self._p(self._returns),
+                                        self._p(self._stats), self._p(self._scratch))
+        if st != _lib.HE_OK:  # a build without the fused path: two launches
+            self._fusable = False
+            return False
+        return True
 
     def close(self):
-        self._detach()
         self.venv.close()
-
-    def __del__(self):
-        try:
-            self._detach()
-        except Exception:  # noqa: BLE001 -- interpreter shutdown
-            pass
 
     @property
     def terminal_obs_tensor(self):

@@ -370,14 +370,15 @@ he_status he_vecnorm_step(const he_vecnorm_params* p, int64_t n, const float* ob
                           int32_t* ep_length_done, void* stream);
 
 /* The same step split in two, for n <= 65,536 (one moments partial per he_step
- * workgroup): he_vecnorm_attach(env, p, returns, stats, scratch) makes every later
- * he_step on `env` also run the first half -- the batch moments of the obs and reward it
- * writes, and returns = returns * gamma + reward -- in its own launch (no effect unless
- * p->training; p = NULL detaches); he_vecnorm_apply, with the arguments of
- * he_vecnorm_step and the same buffers, is then the second half alone: the statistics
- * update and the normalization.  Replaces he_vecnorm_step's moments launch.  Call
- * he_vecnorm_apply once after each he_step on the attached env, and detach before the
- * returns / stats / scratch buffers are freed (the handle keeps their pointers). */
+ * workgroup): he_vecnorm_attach(env, p, returns, stats, scratch) arms the NEXT he_step on
+ * `env` (one-shot, consumed by that call whatever its status) to also run the first half
+ * -- the batch moments of the obs and reward it writes, and returns = returns * gamma +
+ * reward -- in its own launch (no effect unless p->training; p = NULL disarms);
+ * he_vecnorm_apply, with the arguments of he_vecnorm_step and the same buffers, is then
+ * the second half alone: the statistics update and the normalization.  Replaces
+ * he_vecnorm_step's moments launch.  Arm right before each he_step whose output the
+ * apply consumes: steps nobody armed (the inner env stepped directly, another wrapper's
+ * step) leave the buffers alone, and the handle holds no pointer past the armed step. */
 he_status he_vecnorm_attach(he_env* env, const he_vecnorm_params* p, double* returns, double* stats, void* scratch);
 he_status he_vecnorm_apply(const he_vecnorm_params* p, int64_t n, const float* obs, const float* reward,
                            const uint8_t* done, const float* terminal_obs, double* returns, double* stats,

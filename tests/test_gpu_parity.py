@@ -244,6 +244,25 @@ def test_state_checkpoint_roundtrip(greeks_site):
     assert torch.equal(o1, o2) and torch.equal(r1, r2)
 
 
+def test_set_state_refuses_other_formats():
+    """the checkpoint header carries its format; a blob of another format (an
+    older build's) is refused by name, not by a bare size mismatch."""
+    from cantorrl_amd import _lib
+    from cantorrl_amd.vec_env import HedgingVecEnv
+    env = HedgingVecEnv(64, mode="gbm", seed=1, return_numpy=False, info_keys=())
+    env.reset_tensors()
+    blob = env.get_state()
+    assert int(blob[:8].view(np.uint64)[0]) >> 8 == 3
+    old = blob.copy()
+    old[:8] = np.array([1 | (2 << 8)], np.uint64).view(np.uint8)
+    with pytest.raises(_lib.HedgeEnvError, match="checkpoint format 2 != 3"):
+        env.set_state(old)
+    with pytest.raises(_lib.HedgeEnvError, match="state buffer size"):
+        env.set_state(blob[:-4])
+    env.set_state(blob)
+    env.close()
+
+
 @pytest.mark.parametrize("path", ["lds", "fused", "side"])
 def test_set_state_into_a_stepped_env(path, monkeypatch):
     """Restoring a checkpoint into an env that has stepped on (the fused grid leaves the
@@ -667,13 +686,17 @@ def test_lds_rollout_equals_tile_rollout(case, monkeypatch):
         assert torch.equal(a, b), (case, i)
 
 
-def _bench_configs():
+def _bench_module():
     import importlib.util
     spec = importlib.util.spec_from_file_location(
         "bench_cfg", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "bench.py"))
     mod = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(mod)
-    return mod.CONFIGS
+    return mod
+
+
+def _bench_configs():
+    return _bench_module().CONFIGS
 
 
 @pytest.mark.parametrize("config", [2, 3, 4, 5])
@@ -712,6 +735,44 @@ def test_full_size_slice_matches_oracle(config):
             compare_obs(obs_sl[k], oo, f"obs[{s}]")
             terms += int(oterm.sum())
     assert terms == m  # every env finished its first episode at t = 252
+    venv.close()
+
+
+def test_full_size_replay_slice_matches_oracle():
+    """bench.py config 6, the agents' own workload (train_ppo_v2.py:40): 65,536 envs replaying
+    a 100,000 x 253 table through he_rollout (K = 256 and a ragged 64), 320 steps across the
+    t = 252 autoreset, whose new episode rows come from each env's PCG64(SeedSequence(42 +
+    global id)) stream: the last 192 envs against the oracle replaying the same table with
+    those seeds -- episode rows, done flags and obs bit-exact (greeks at OBS_RTOL), rewards
+    bit-exact (replay P&L is the reference's own f64 chain)."""
+    from cantorrl_amd.vec_env import HedgingVecEnv
+    bench = _bench_module()
+    c = bench.CONFIGS[6]
+    S, v, C, P = bench.replay_tables(**c["table"])
+    n, seed, m = c["envs"], 42, 192
+    lo = n - m
+    venv = HedgingVecEnv(n, tables=(S, v, C, P), seed=seed, info_keys=(), return_numpy=False, **c["kw"])
+    orc = OracleVecEnv(m, mode="replay", data=(S, v, C, P), **c["kw"])
+    o_obs = orc.reset(seeds=[seed + lo + i for i in range(m)])
+    compare_obs(venv.reset_tensors()[lo:].cpu().numpy(), o_obs, "reset_obs")
+    g = torch.Generator(device="cuda")
+    g.manual_seed(9)
+    terms = 0
+    s = 0
+    for chunk in (256, 64):
+        acts = torch.rand((chunk, n, 2), device="cuda", generator=g) * 2.2 - 1.1
+        obs, rew, term = venv.rollout(acts)
+        torch.cuda.synchronize()
+        a_sl = acts[:, lo:].cpu().numpy()
+        obs_sl, rew_sl, term_sl = obs[:, lo:].cpu().numpy(), rew[:, lo:].cpu().numpy(), term[:, lo:].cpu().numpy()
+        for k in range(chunk):
+            oo, orew, oterm, _, _ = orc.step(a_sl[k])
+            assert_same(term_sl[k].astype(bool), oterm, f"terminated[{s}]")
+            assert_same(rew_sl[k], orew.astype(np.float32), f"reward[{s}]")
+            compare_obs(obs_sl[k], oo, f"obs[{s}]")
+            terms += int(oterm.sum())
+            s += 1
+    assert terms == m
     venv.close()
 
 

@@ -57,6 +57,22 @@ def test_create_rejects_bad_config_without_gpu():
     lib.he_destroy(h)
 
 
+def test_create_rejects_bad_mark_without_gpu():
+    """he_config.mark (ABI v3): an he_mark, and generate modes only (replay reads its marks
+    from the table)."""
+    lib = _lib.load()
+    for mode, mark, msg in ((_lib.HE_MODE_GBM, 7, b"bad mark"),
+                            (_lib.HE_MODE_REPLAY, _lib.HE_MARK_FIXED_EUROPEAN, b"replay mode")):
+        c = _lib.HeConfig()
+        lib.he_config_init(c, 2)
+        assert c.mark == _lib.HE_MARK_ROLLING_ATM and c.abi_version == _lib.HE_ABI_VERSION == 3
+        c.mode, c.mark = mode, mark
+        h = _lib.ctypes.c_void_p()
+        assert lib.he_create(c, _lib.ctypes.byref(h)) == _lib.HE_EINVAL
+        assert msg in lib.he_last_error(h)
+        lib.he_destroy(h)
+
+
 @pytest.mark.parametrize("seed", [0, 1, 7, 42, 12345, 2 ** 32 - 1, 2 ** 32, 2 ** 40 + 3, 2 ** 63 + 11])
 def test_pcg64_seed_state_matches_numpy(seed):
     st = np.random.PCG64(np.random.SeedSequence(seed)).state["state"]

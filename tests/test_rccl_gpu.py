@@ -1,0 +1,77 @@
+"""RCCL at the rollout-buffer boundary, on the GPU (the device-tensor branch
+had only ever run over gloo).  One process, world size 1: `torch.distributed` with
+backend "nccl" (RCCL on ROCm) initialised by the bench's own init_dist and by
+cantorrl_amd.dist.init, then the per-env episode summaries he_episode_summaries writes
+({return, sum P&L, sum cost, length} of each env's last finished episode,
+train_ppo_v2.py:48,119) pushed through bench.gather_summaries and
+cantorrl_amd.dist.gather_rollout as device tensors -- all_gather_into_tensor on the
+launching stream, no host sync -- and compared with the summaries themselves."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.fixture
+def rccl_group(monkeypatch):
+    import torch.distributed as dist
+    for k, v in dict(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), RANK="0", WORLD_SIZE="1",
+                     LOCAL_RANK="0").items():
+        monkeypatch.setenv(k, v)
+    monkeypatch.delenv("BENCH_DIST_BACKEND", raising=False)
+    yield dist
+    if dist.is_initialized():
+        dist.destroy_process_group()
+
+
+def test_rccl_gather_of_episode_summaries(rccl_group):
+    import bench
+    from cantorrl_amd import dist as hd
+    from cantorrl_amd.vec_env import HedgingVecEnv
+    dist = rccl_group
+    d, backend = bench.init_dist(0)
+    assert backend == "nccl" and dist.get_backend() == "nccl" and dist.get_world_size() == 1
+    assert hd.init(backend="nccl", force=True) == (0, 0, 1)  # already initialised: a no-op
+    n, T = 65536, 20
+    env = HedgingVecEnv(n, mode="gbm", generate=dict(episode_length=T), seed=42, return_numpy=False, info_keys=(),
+                        **bench.TRAIN_KW)
+    env.reset_tensors()
+    stream = torch.cuda.Stream()
+    g = torch.Generator(device="cuda")
+    g.manual_seed(3)
+    acts = torch.rand((64, n, 2), device="cuda", generator=g) * 2 - 1
+    summ = torch.zeros((n, 4), dtype=torch.float32, device="cuda")
+    gathered = torch.empty((n, 4), dtype=torch.float32, device="cuda")
+    with torch.cuda.stream(stream):
+        env.rollout(acts)                                   # 3 finished episodes per env
+        env.episode_summaries(summ)                         # he_episode_summaries on the stream
+        bench.gather_summaries(dist, summ, gathered)        # RCCL, stream-ordered behind it
+        via_dist = hd.gather_rollout(summ)
+    torch.cuda.synchronize()
+    ref = env.episode_summaries().cpu().numpy()
+    assert (ref[:, 3] == T).all()
+    np.testing.assert_array_equal(gathered.cpu().numpy(), ref)
+    np.testing.assert_array_equal(via_dist.cpu().numpy(), ref)
+    # the boundary's cost: summaries + gather per 256-step rollout, device time on the stream
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    with torch.cuda.stream(stream):
+        ev[0].record(stream)
+        for _ in range(20):
+            env.episode_summaries(summ)
+            bench.gather_summaries(dist, summ, gathered)
+        ev[1].record(stream)
+    torch.cuda.synchronize()
+    per_us = ev[0].elapsed_time(ev[1]) * 1e3 / 20
+    print(f"he_episode_summaries + RCCL all_gather of [{n}, 4] f32 (world 1): {per_us:.1f} us per boundary")
+    assert per_us < 2000.0
+    env.close()

@@ -204,3 +204,55 @@ def test_fused_moments_equal_separate_launch(info, monkeypatch):
     np.testing.assert_allclose(ra.var, rb.var, rtol=1e-10, atol=1e-16)
     np.testing.assert_allclose(qa.var, qb.var, rtol=1e-10)
     np.testing.assert_array_equal(ta, tb)
+
+
+def test_two_wrappers_on_one_env_and_inner_steps():
+    """the fused moments are armed per step (he_vecnorm_attach is one-shot).
+    Two DeviceVecNormalize on one env, the first dropped after the second has stepped, and
+    the inner env stepped directly in between: each wrapper's returns and statistics equal
+    a wrapper that alone saw exactly its own steps (the separate-launch path)."""
+    import gc
+    from cantorrl_amd.vec_normalize import DeviceVecNormalize
+    n = 2000
+    g = torch.Generator(device=DEV)
+    g.manual_seed(5)
+    acts = [torch.rand((n, 2), device=DEV, generator=g) * 2 - 1 for _ in range(12)]
+
+    def drive(env, wrappers, plan):
+        # plan: ("a" | "b" | "inner", action index); returns the last normalized outputs per wrapper
+        for who, k in plan:
+            if who == "inner":
+                env.step_tensors(acts[k])
+            else:
+                wrappers[who].step_tensors(acts[k])
+        torch.cuda.synchronize()
+
+    plan = [("a", 0), ("b", 1), ("inner", 2), ("a", 3), ("b", 4), ("b", 5), ("inner", 6), ("b", 7)]
+    env = _env(n)
+    a, b = DeviceVecNormalize(env, gamma=0.9), DeviceVecNormalize(env, gamma=0.8)
+    a.reset_tensors()
+    b._returns.zero_()
+    drive(env, {"a": a, "b": b}, plan[:5])
+    ra = a.returns.copy()
+    del a
+    gc.collect()
+    drive(env, {"b": b}, plan[5:])
+    rb, sb = b.returns.copy(), b.obs_rms
+    env.close()
+    # the same env trajectory with separate-launch wrappers (nothing fused, nothing shared)
+    import os
+    os.environ["CANTORRL_VN_FUSED"] = "0"
+    try:
+        env2 = _env(n)
+        a2, b2 = DeviceVecNormalize(env2, gamma=0.9), DeviceVecNormalize(env2, gamma=0.8)
+        a2.reset_tensors()
+        b2._returns.zero_()
+        drive(env2, {"a": a2, "b": b2}, plan)
+        np.testing.assert_allclose(ra, a2.returns, rtol=1e-12, atol=1e-15)  # a stepped at 0 and 3 only
+        np.testing.assert_allclose(rb, b2.returns, rtol=1e-12, atol=1e-15)
+        np.testing.assert_allclose(sb.mean, b2.obs_rms.mean, rtol=1e-12, atol=1e-14)
+        np.testing.assert_allclose(sb.var, b2.obs_rms.var, rtol=1e-10, atol=1e-16)
+        assert abs(sb.count - b2.obs_rms.count) < 1e-9
+        env2.close()
+    finally:
+        del os.environ["CANTORRL_VN_FUSED"]
