@@ -604,13 +604,38 @@ def market_time_ms(hev, args, dev, acts, stream):
     return float(np.median(d2[M_BLOCK::M_BLOCK])) - float(np.median(np.delete(d2, np.arange(0, 4 * M_BLOCK, M_BLOCK))))
 
 
+# The GPU's clocks ramp up under sustained load: back-to-back 65,536-env launches measured
+# 395-404 us each in the first ~10 ms after idle and 320 us from ~30 ms on
+# (tools/launch_timing.py, r03s2).  The warm-up therefore runs for at least this long
+# (whole chunks; the line reports the warm-up steps actually run beside the requested ones).
+MIN_WARMUP_SECONDS = 0.5
+
+
 def timed(runner, K, W, dist):
-    """W untimed warm-up steps, then exactly K timed steps between barriers; returns
+    """W untimed warm-up steps (extended to MIN_WARMUP_SECONDS of work; the count run is left
+    in runner.warmup_steps), then exactly K timed steps between barriers; returns
     (max-over-ranks wall seconds, device ms on the stream)."""
     stream = runner.stream
+    t_w = time.perf_counter()
+    d_saved, runner.dist = runner.dist, None  # no gathers while warming: ranks' counts may differ
     with torch.cuda.stream(stream):
         runner.run(W)
     torch.cuda.synchronize()
+    while time.perf_counter() - t_w < MIN_WARMUP_SECONDS:
+        with torch.cuda.stream(stream):
+            runner.run(runner.chunk * 4)
+        torch.cuda.synchronize()
+        W += runner.chunk * 4
+    if dist is not None:  # every rank warms for the longest rank's count of steps
+        w = torch.tensor([W], dtype=torch.int64,
+                         device="cpu" if dist.get_backend() == "gloo" else torch.device("cuda", torch.cuda.current_device()))
+        dist.all_reduce(w, op=dist.ReduceOp.MAX)
+        if int(w.item()) > W:
+            with torch.cuda.stream(stream):
+                runner.run(int(w.item()) - W)
+            torch.cuda.synchronize()
+            W = int(w.item())
+    runner.dist = d_saved
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
@@ -626,6 +651,7 @@ def timed(runner, K, W, dist):
         dist.barrier()
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
+    runner.warmup_steps = W
     host = dist is not None and dist.get_backend() == "gloo"
     t = torch.tensor([wall], dtype=torch.float64,
                      device="cpu" if host else torch.device("cuda", torch.cuda.current_device()))
@@ -1024,7 +1050,7 @@ def main(argv=None):
             "unit": "env-steps/s",
             "n_gpus": world,
             "steps": K,
-            "warmup": W,
+            "warmup": runner.warmup_steps,
             # the command's --steps / --warmup: raised to the timed floor (MIN_TIMED_STEPS, >= 2
             # episodes and 10 launches) and to whole launches of the rollout chunk
             "requested_steps": args.steps,

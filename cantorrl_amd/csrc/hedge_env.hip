@@ -2367,9 +2367,12 @@ __device__ __forceinline__ void lds_producer(const Params& p, int k_steps, const
 // atomic per workgroup) and its waves take role = (SIMD id + ticket) mod 4 -- a bijection
 // over its 4 distinct SIMDs, and across the 4 workgroups resident on a CU (consecutive
 // tickets) every SIMD hosts one wave of each role.  Wave-to-SIMD placement not
-// one-per-SIMD (never seen) falls back to role = wave index.
+// one-per-SIMD (never seen) falls back to role = wave index.  Same-box A/B (r03s1, two
+// runs each): configs 4 / 5 (producer-bound) 11.25 -> 10.54 ms and 2.49 -> 2.25 ms per
+// launch; config 2 unchanged (its placement is already one role per SIMD on 230 of 256
+// CUs, tools/lds_hwid.py).
 #ifndef HE_LDS_BALANCE
-#define HE_LDS_BALANCE 0
+#define HE_LDS_BALANCE 1
 #endif
 #if HE_LDS_BALANCE || defined(HE_LDS_HWID)
 __device__ uint32_t g_cu_ticket[4096];
