@@ -441,6 +441,219 @@ HE_HD void bs_vectorized(double S, double K, double T, double r, double sigma, d
     *put = p;
 }
 
+// ---------------------------------------------------------------- lockstep forms
+// The same functions over NN independent arguments at once, element for element the
+// scalar version's operations in the scalar version's order (so the same bits), but with
+// the loop over polynomial coefficients outside the loop over elements: a wave gets NN
+// independent FMA chains to interleave instead of one dependent chain, and each f64
+// constant is materialised in SGPRs once per coefficient for NN FMAs instead of once per
+// FMA.  Used by the LDS producers, which evaluate several market slots per lane.
+template <int NN>
+HE_HD void exp_k_n(const double* x, double* out) {
+    double k[NN], r[NN], q[NN];
+#pragma unroll
+    for (int h = 0; h < NN; ++h) {
+        const double xs = (fabs(x[h]) < 700.0) ? x[h] : 0.0;   // |x| >= 700 / NaN: library exp below
+        k[h] = rint(xs * 1.4426950408889634074);
+        const double rh = fma_kb(-k[h], 6.93147180369123816490e-01, xs);
+        r[h] = fma_kb(-k[h], 1.90821492927058770002e-10, rh);
+        q[h] = 1.0 / 355687428096000.0;
+    }
+    constexpr double C[16] = {1.0 / 20922789888000.0, 1.0 / 1307674368000.0, 1.0 / 87178291200.0,
+                              1.0 / 6227020800.0,     1.0 / 479001600.0,     1.0 / 39916800.0,
+                              1.0 / 3628800.0,        1.0 / 362880.0,        1.0 / 40320.0,
+                              1.0 / 5040.0,           1.0 / 720.0,           1.0 / 120.0,
+                              1.0 / 24.0,             1.0 / 6.0,             0.5,
+                              0.0};
+#pragma unroll
+    for (int c = 0; c < 15; ++c)
+#pragma unroll
+        for (int h = 0; h < NN; ++h) q[h] = fma_k(q[h], r[h], C[c]);
+#pragma unroll
+    for (int h = 0; h < NN; ++h) {
+        const double s1 = 1.0 + r[h];
+        const double e1 = (1.0 - s1) + r[h];
+        const double v = ldexp(s1 + fma(r[h] * r[h], q[h], e1), (int)k[h]);
+        out[h] = (fabs(x[h]) < 700.0) ? v : exp(x[h]);
+    }
+}
+
+template <int NN>
+HE_HD void philox4x32_10_n(u32x4* c, uint32_t k0, uint32_t k1) {
+    const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
+    const uint32_t W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
+#pragma unroll
+    for (int rd = 0; rd < 10; ++rd) {
+        if (rd) { k0 += W0; k1 += W1; }
+#pragma unroll
+        for (int h = 0; h < NN; ++h) {
+            const uint64_t p0 = (uint64_t)M0 * c[h].x, p1 = (uint64_t)M1 * c[h].z;
+            u32x4 o;
+            o.x = (uint32_t)(p1 >> 32) ^ c[h].y ^ k0;
+            o.y = (uint32_t)p1;
+            o.z = (uint32_t)(p0 >> 32) ^ c[h].w ^ k1;
+            o.w = (uint32_t)p0;
+            c[h] = o;
+        }
+    }
+}
+
+template <int NN>
+HE_HD void box_muller_n(const double* u1, const double* u2, double* z1, double* z2) {
+    double s[NN], s2[NN], p[NN], ed[NN];
+#pragma unroll
+    for (int h = 0; h < NN; ++h) {
+        int e;
+        double m = frexp(u1[h], &e);
+        const bool lo = m < 0.70710678118654752;
+        m = lo ? m + m : m;
+        ed[h] = (double)(lo ? e - 1 : e);
+        s[h] = (m - 1.0) / (m + 1.0);
+        s2[h] = s[h] * s[h];
+        p[h] = 1.0 / 19.0;
+    }
+    constexpr double PL[8] = {1.0 / 17.0, 1.0 / 15.0, 1.0 / 13.0, 1.0 / 11.0, 1.0 / 9.0, 1.0 / 7.0, 1.0 / 5.0, 1.0 / 3.0};
+#pragma unroll
+    for (int c = 0; c < 8; ++c)
+#pragma unroll
+        for (int h = 0; h < NN; ++h) p[h] = fma_k(p[h], s2[h], PL[c]);
+    double rad[NN], r[NN], rr[NN], sp[NN], cp[NN];
+    int qi[NN];
+#pragma unroll
+    for (int h = 0; h < NN; ++h) {
+        const double lm = (2.0 * s[h]) + (2.0 * s[h]) * (s2[h] * p[h]);
+        const double lg = fma(ed[h], 6.93147180369123816490e-01, fma(ed[h], 1.90821492927058770002e-10, lm));
+        rad[h] = sqrt(-2.0 * lg);
+        const double x = 4.0 * u2[h];
+        const double q = rint(x);
+        r[h] = x - q;
+        rr[h] = r[h] * r[h];
+        qi[h] = (int)q & 3;
+        sp[h] = 6.066935731106192e-12;
+        cp[h] = 6.565963114979468e-11;
+    }
+    constexpr double SP[8] = {-6.688035109811464e-10, 5.692172921967924e-08, -3.598843235212084e-06,
+                              0.00016044118478735975, -0.004681754135318687, 0.07969262624616703,
+                              -0.6459640975062462,    1.5707963267948966};
+    constexpr double CP[8] = {-6.386603083791849e-09, 4.710874778818169e-07, -2.5202042373060596e-05,
+                              0.0009192602748394263,  -0.020863480763352957, 0.253669507901048,
+                              -1.2337005501361697,    1.0};
+#pragma unroll
+    for (int c = 0; c < 8; ++c)
+#pragma unroll
+        for (int h = 0; h < NN; ++h) {
+            sp[h] = fma_k(sp[h], rr[h], SP[c]);
+            cp[h] = fma_k(cp[h], rr[h], CP[c]);
+        }
+#pragma unroll
+    for (int h = 0; h < NN; ++h) {
+        const double sn = r[h] * sp[h];
+        const double cs = cp[h];
+        const bool swp = (qi[h] & 1) != 0;
+        const double s_ = swp ? cs : sn, c_ = swp ? sn : cs;
+        const double sinv = (qi[h] & 2) ? -s_ : s_;
+        const double cosv = ((qi[h] + 1) & 2) ? -c_ : c_;
+        z1[h] = rad[h] * cosv;
+        z2[h] = rad[h] * sinv;
+    }
+}
+
+// ndtr_pair over NN arguments: the |x| < 1/4 series lockstep when every argument of the
+// lane is there (rolling-ATM marks always are), else each through ndtr_pair.
+template <int NN>
+HE_HD void ndtr_pair_n(const double* a, double* pos, double* neg) {
+    const double SQRT1_2 = 0.70710678118654752440;
+    double x[NN], z[NN], p[NN];
+    bool easy = true;
+#pragma unroll
+    for (int h = 0; h < NN; ++h) {
+        x[h] = a[h] * SQRT1_2;
+        easy = easy && (fabs(x[h]) < 0.25);   // NaN: false
+        z[h] = x[h] * x[h];
+        p[h] = 0.000001646211436588924740161296;
+    }
+    if (!easy) {
+#pragma unroll
+        for (int h = 0; h < NN; ++h) ndtr_pair(a[h], pos + h, neg + h);
+        return;
+    }
+    constexpr double E[8] = {-0.00001492565035840625097746242, 0.0001205533298178966425102734,
+                             -0.0008548327023450852832546658,  0.005223977625442187842111847,
+                             -0.02686617064513125175943235,    0.1128379167095512573896159,
+                             -0.376126389031837524632053,      1.128379167095512573896159};
+#pragma unroll
+    for (int c = 0; c < 8; ++c)
+#pragma unroll
+        for (int h = 0; h < NN; ++h) p[h] = fma_k(p[h], z[h], E[c]);
+#pragma unroll
+    for (int h = 0; h < NN; ++h) {
+        const double e = x[h] * p[h];
+        pos[h] = 0.5 + 0.5 * e;
+        neg[h] = 0.5 + 0.5 * (-e);
+    }
+}
+
+// log_ratio over NN (S, K) pairs: the log1p series lockstep when every quotient of the
+// lane is within 2^-7 of 1 (S >= 64), else each through log_ratio.
+template <int NN>
+HE_HD void log_ratio_n(const double* S, const double* K, double* out) {
+    double y[NN], p[NN];
+    bool easy = true;
+#pragma unroll
+    for (int h = 0; h < NN; ++h) {
+#if defined(HE_LOGRATIO_RCP) && defined(__HIP_DEVICE_COMPILE__)
+        double r = __builtin_amdgcn_rcp(K[h]);   // log_ratio's A/B form, the same operations
+        r = fma(fma(-K[h], r, 1.0), r, r);
+        r = fma(fma(-K[h], r, 1.0), r, r);
+        y[h] = (S[h] - K[h]) * r;
+#else
+        const double q = S[h] / K[h];
+        y[h] = q - 1.0;
+#endif
+        easy = easy && (fabs(y[h]) < 0.0078125);
+        p[h] = 1.0 / 9.0;
+    }
+    if (!easy) {
+#pragma unroll
+        for (int h = 0; h < NN; ++h) out[h] = log_ratio(S[h], K[h]);
+        return;
+    }
+    constexpr double L[8] = {-1.0 / 8.0, 1.0 / 7.0, -1.0 / 6.0, 1.0 / 5.0, -1.0 / 4.0, 1.0 / 3.0, -0.5, 1.0};
+#pragma unroll
+    for (int c = 0; c < 8; ++c)
+#pragma unroll
+        for (int h = 0; h < NN; ++h) p[h] = fma_k(p[h], y[h], L[c]);
+#pragma unroll
+    for (int h = 0; h < NN; ++h) out[h] = y[h] * p[h];
+}
+
+// bs_call_put over NN spots S with strikes K at the constant-sigma BSConst c.
+template <int NN>
+HE_HD void bs_call_put_n(const double* S, const double* K, const BSConst& c, double* call, double* put) {
+    if (c.intrinsic) {
+#pragma unroll
+        for (int h = 0; h < NN; ++h) bs_call_put(S[h], K[h], c, call + h, put + h);
+        return;
+    }
+    double lr[NN], d[2 * NN], nd[2 * NN], md[2 * NN];
+    log_ratio_n<NN>(S, K, lr);
+#pragma unroll
+    for (int h = 0; h < NN; ++h) {
+        d[h] = (lr[h] + c.a) * c.inv_b;
+        d[NN + h] = d[h] - c.b;
+    }
+    ndtr_pair_n<NN>(d, nd, md);             // two groups of NN chains: 2 NN would spill
+    ndtr_pair_n<NN>(d + NN, nd + NN, md + NN);
+#pragma unroll
+    for (int h = 0; h < NN; ++h) {
+        const double Kd = K[h] * c.disc;
+        const double cv = S[h] * nd[h] - Kd * nd[NN + h];
+        const double pv = Kd * md[NN + h] - S[h] * md[h];
+        call[h] = (cv < 0.0) ? 0.0 : cv;
+        put[h] = (pv < 0.0) ? 0.0 : pv;
+    }
+}
+
 // ---------------------------------------------------------------- PCG64 (numpy)
 // numpy/random/src/pcg64: 128-bit LCG, XSL-RR output; next32 keeps the high
 // half of a 64-bit draw buffered (has_uint32/uinteger).

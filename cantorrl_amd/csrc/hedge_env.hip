@@ -658,6 +658,31 @@ __device__ __forceinline__ void normals(const Params& p, int64_t gid, uint64_t n
     box_muller(u01(x.x, x.y), u01(x.z, x.w), z1, z2);
 }
 
+// The Box-Muller pairs of Philox blocks m0 .. m0 + B - 1 of env gid into z[2B] (cos, sin,
+// cos, ...): normals() for B blocks in lockstep, the same bits.
+template <int B>
+__device__ __forceinline__ void philox_normals_n(const Params& p, int64_t gid, uint64_t m0, double* z) {
+    u32x4 c[B];
+    double u1[B], u2[B], z1[B], z2[B];
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+        const uint64_t m = m0 + (uint64_t)b;
+        c[b] = u32x4{(uint32_t)m, (uint32_t)(m >> 32), (uint32_t)gid, (uint32_t)((uint64_t)gid >> 32)};
+    }
+    philox4x32_10_n<B>(c, p.key0, p.key1);
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+        u1[b] = u01(c[b].x, c[b].y);
+        u2[b] = u01(c[b].z, c[b].w);
+    }
+    box_muller_n<B>(u1, u2, z1, z2);
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+        z[2 * b] = z1[b];
+        z[2 * b + 1] = z2[b];
+    }
+}
+
 // ------------------------------------------------------------------ market kernel
 // One workgroup = 64 envs x 4 slot-lanes.  Slot j (1..M) is the market after the
 // j-th step from the block start; slot 0 is the block start itself.  With
@@ -1712,6 +1737,12 @@ __global__ __launch_bounds__(kBlock, HE_FUSED_WAVES) void step_market_kernel(Par
 #ifndef HE_LDS_M
 #define HE_LDS_M 8
 #endif
+#ifndef HE_LDS_PROD_FULL
+#define HE_LDS_PROD_FULL 0  // A/B: producers specialised for whole blocks (straight-line slots)
+#endif
+#ifndef HE_LDS_PROD_LOCK
+#define HE_LDS_PROD_LOCK 1  // with HE_LDS_PROD_FULL: the lean GBM producers' slots in lockstep
+#endif
 #ifndef HE_LDS_BOOK_OPTS
 #define HE_LDS_BOOK_OPTS 1  // the book's options read from an LDS copy (config 4: 10.38 -> 8.98 ms per launch; 0: from the scalar cache)
 #endif
@@ -2171,12 +2202,54 @@ __device__ __forceinline__ void lds_producer(const Params& p, int k_steps, const
         if (bp < nb) {
             const int kb = bp * kLdsM;
             const int len = (k_steps - kb) < kLdsM ? (k_steps - kb) : kLdsM;
+            // FULL: a whole kLdsM-slot block (every block of the launch but a ragged last
+            // one): the per-slot `len` tests are compile-time true, so each stage's slots
+            // are straight-line code -- independent chains the wave can interleave, and
+            // one materialisation of each polynomial constant per stage instead of per slot
+            auto block = [&](auto full) {
+                constexpr bool FULL = decltype(full)::value;
+                // LOCK: the lean GBM producers of a whole block evaluate their kLdsH slots in
+                // lockstep (he_math.h *_n forms: the same operations per slot, so the same
+                // bits, as kLdsH interleaved chains with shared constants)
+                constexpr bool LOCK = FULL && LEAN && !HESTON && HE_LDS_PROD_LOCK;
+
             const uint64_t nf = a0 + (uint64_t)(kb + sl0);
             const uint32_t tpf = (tpb + (uint32_t)sl0) % T;
             double ex[kLdsH];   // own slots' growth factors S_j / S_{j-1} (before the clamp)
             double Vx[kLdsH];   // Heston: own slots' v after the step
             double Vin = Vbs;   // Heston: v before the lane's first slot
-            if constexpr (!HESTON) {
+            if constexpr (LOCK) {
+                // slot h's normal is the (nf + h - 2 m0)-th of the Box-Muller pairs of the
+                // Philox blocks m0 = nf / 2, m0 + 1 (and m0 + 2 when nf is odd): cos, sin, ...
+                const uint64_t m0 = nf >> 1;
+                const bool odd = (nf & 1) != 0;
+                double zs[kLdsH];
+                if (__ballot(odd) == 0ull) {   // every lane even: blocks m0 .. m0 + kLdsH / 2 - 1
+                    double zz[kLdsH];
+                    philox_normals_n<kLdsH / 2>(p, gid, m0, zz);
+#pragma unroll
+                    for (int h = 0; h < kLdsH; ++h) zs[h] = zz[h];
+                } else {
+                    double zz[kLdsH + 2];
+                    philox_normals_n<kLdsH / 2 + 1>(p, gid, m0, zz);
+#pragma unroll
+                    for (int h = 0; h < kLdsH; ++h) {
+                        // both candidates pinned in registers: left alone, the select becomes
+                        // zz[h + odd], a dynamically indexed array in scratch memory
+                        double a = zz[h], b = zz[h + 1];
+                        asm volatile("" : "+v"(a), "+v"(b));
+                        zs[h] = odd ? b : a;
+                    }
+                }
+                double arg[kLdsH];
+#pragma unroll
+                for (int h = 0; h < kLdsH; ++h) {
+                    Vx[h] = 0.0;
+                    const double dW = p.sqrt_dt * zs[h];
+                    arg[h] = p.drift + p.sqrt_var * dW;   // rbergomi_sim.py:459-463
+                }
+                exp_k_n<kLdsH>(arg, ex);
+            } else if constexpr (!HESTON) {
                 // (1) the random part of every slot: Philox block m = n / 2 gives the
                 // Box-Muller pair of steps 2m (cos) and 2m + 1 (sin)
                 double zc = 0.0;
@@ -2184,7 +2257,7 @@ __device__ __forceinline__ void lds_producer(const Params& p, int k_steps, const
                 for (int h = 0; h < kLdsH; ++h) {
                     ex[h] = 1.0;
                     Vx[h] = 0.0;
-                    if (sl0 + h < len) {
+                    if (FULL || sl0 + h < len) {
                         const uint64_t n = nf + (uint64_t)h;
                         double z;
                         if (h == 0 || (n & 1) == 0) {
@@ -2221,7 +2294,7 @@ __device__ __forceinline__ void lds_producer(const Params& p, int k_steps, const
                 for (int h = 0; h < kLdsH; ++h) {
                     w1[h] = 0.0;
                     ws[h] = 0.0;
-                    if (sl0 + h < len) {
+                    if (FULL || sl0 + h < len) {
                         double z1, z2;
                         normals(p, gid, nf + (uint64_t)h, &z1, &z2);
                         const double dw1 = p.sqrt_dt * z1, dw2 = p.sqrt_dt * z2;
@@ -2245,7 +2318,7 @@ __device__ __forceinline__ void lds_producer(const Params& p, int k_steps, const
                 for (int j = 0; j < kLdsM; ++j) {
                     if (j == sl0) Vin = v;
                     double vp = 0.0, sq = 0.0;
-                    if (j < len) {
+                    if (FULL || j < len) {
                         if (tq == 0) v = p.var;  // autoreset: a new episode starts from v0
                         vp = v < 0.0 ? 0.0 : v;  // full truncation
                         sq = sqrt(vp);
@@ -2265,7 +2338,7 @@ __device__ __forceinline__ void lds_producer(const Params& p, int k_steps, const
                 for (int h = 0; h < kLdsH; ++h) {
                     const double drift = (p.mu - 0.5 * vpx[h]) * p.dt;
                     const double diff = sqx[h] * ws[h];
-                    ex[h] = (sl0 + h < len) ? HE_HESTON_EXP(drift + diff) : 1.0;
+                    ex[h] = (FULL || sl0 + h < len) ? HE_HESTON_EXP(drift + diff) : 1.0;
                 }
             }
             // (2) the f64 price chain: the block's growth factors gathered from the env's
@@ -2288,7 +2361,7 @@ __device__ __forceinline__ void lds_producer(const Params& p, int k_steps, const
 #pragma unroll
                 for (int j = 0; j < kLdsM; ++j) {
                     if (j == sl0) Sin = S;
-                    if (j < len) {
+                    if (FULL || j < len) {
                         if (tp == 0) {  // autoreset: a new episode starts from S0
                             S = p.s0;
                             if (BOOK) Mr = p.s0;
@@ -2312,9 +2385,23 @@ __device__ __forceinline__ void lds_producer(const Params& p, int k_steps, const
             // the position before it (hedging_env_v2.py:229-231)
             uint32_t tp = tpf;
             const int wb = bp & 1;
+            double lkC[kLdsH], lkP[kLdsH];   // LOCK: the slots' marks, in lockstep
+            if constexpr (LOCK) {
+                double Sm[kLdsH], Km[kLdsH];
+                uint32_t tq = tpf;
+#pragma unroll
+                for (int h = 0; h < kLdsH; ++h) {
+                    const bool last = tq + 1 == T;
+                    const double Sprev = (h == 0) ? Sin : Sx[h - 1];
+                    Sm[h] = last ? ((tq == 0) ? p.s0 : Sprev) : Sx[h];
+                    Km[h] = rint(Sm[h]);   // marks<GBM>: the rolling-ATM strike K = round(S)
+                    tq = (tq + 1 == T) ? 0u : tq + 1;
+                }
+                bs_call_put_n<kLdsH>(Sm, Km, p.bs, lkC, lkP);
+            }
 #pragma unroll
             for (int h = 0; h < kLdsH; ++h) {
-                if (sl0 + h < len) {
+                if (FULL || sl0 + h < len) {
                     const bool last = tp + 1 == T;
                     const double Sprev = (h == 0) ? Sin : Sx[h - 1];
                     const double Sm = last ? ((tp == 0) ? p.s0 : Sprev) : Sx[h];
@@ -2324,8 +2411,13 @@ __device__ __forceinline__ void lds_producer(const Params& p, int k_steps, const
 #if defined(HE_LDS_SKIP) && (HE_LDS_SKIP & 2)
                     C = (float)Sm * 0.02f; P = (float)Sm * 0.018f;  // diagnostic build: no marks
 #else
-                    // the episode step of the marks: the slot's (tp + 1), or tp for the lagged ones
-                    marks<MODE, !LEAN>(p, Sm, Vm, last ? tp : tp + 1u, &C, &P);
+                    if constexpr (LOCK) {
+                        C = (float)lkC[h];
+                        P = (float)lkP[h];
+                    } else {
+                        // the episode step of the marks: the slot's (tp + 1), or tp for the lagged ones
+                        marks<MODE, !LEAN>(p, Sm, Vm, last ? tp : tp + 1u, &C, &P);
+                    }
 #endif
                     const int sl = sl0 + h;
                     W.sc[wb][sl][le] = make_float2((float)Sx[h], C);
@@ -2352,6 +2444,13 @@ __device__ __forceinline__ void lds_producer(const Params& p, int k_steps, const
                     tp = (tp + 1 == T) ? 0u : tp + 1;
                 }
             }
+            };
+#if HE_LDS_PROD_FULL
+            if (len == kLdsM) block(std::true_type{});
+            else block(std::false_type{});
+#else
+            block(std::false_type{});
+#endif
             tpb = (uint32_t)(((uint64_t)tpb + kLdsM) % T);
         }
         LDS_BAR();  // block bp handed to the steppers
@@ -2461,10 +2560,60 @@ __global__ void device_rng_kernel(uint32_t k0, uint32_t k1, const uint64_t* gid,
     if (normals) box_muller(u01(x.x, x.y), u01(x.z, x.w), normals + 2 * k, normals + 2 * k + 1);
 }
 
-__global__ void device_math_kernel(int32_t op, const double* x, int64_t count, double* out) {
-    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= count) return;
-    out[k] = (op == 0) ? exp_k(x[k]) : x[k];
+// he_device_math / he_host_math: group g = elements [4g, 4g + 4) (ops 4 / 5: two (u1, u2)
+// pairs), padded with `pad` past count.  Ops 1, 3, 5 are the lockstep forms the LDS
+// producers run, ops 0, 2, 4 the scalar ones the tile kernels run: equal bit for bit.
+HE_HD void math_group(int32_t op, const double* x, int64_t count, double* out, int64_t g, const BSConst& bs) {
+    const double pad = (op == 4 || op == 5) ? 0.5 : ((op == 2 || op == 3) ? 500.0 : 0.0);
+    double a[4], r[4], q[4];
+    for (int h = 0; h < 4; ++h) a[h] = (4 * g + h < count) ? x[4 * g + h] : pad;
+    switch (op) {
+        case 0:
+            for (int h = 0; h < 4; ++h) r[h] = exp_k(a[h]);
+            break;
+        case 1:
+            exp_k_n<4>(a, r);
+            break;
+        case 2:   // the rolling-ATM call mark at S = a (marks<GBM>)
+            for (int h = 0; h < 4; ++h) bs_call_put(a[h], rint(a[h]), bs, r + h, q + h);
+            break;
+        case 3: {
+            double K[4];
+            for (int h = 0; h < 4; ++h) K[h] = rint(a[h]);
+            bs_call_put_n<4>(a, K, bs, r, q);
+            break;
+        }
+        case 4:
+            box_muller(a[0], a[1], r, r + 1);
+            box_muller(a[2], a[3], r + 2, r + 3);
+            break;
+        default: {  // 5
+            const double u1[2] = {a[0], a[2]}, u2[2] = {a[1], a[3]};
+            double z1[2], z2[2];
+            box_muller_n<2>(u1, u2, z1, z2);
+            r[0] = z1[0], r[1] = z2[0], r[2] = z1[1], r[3] = z2[1];
+        }
+    }
+    for (int h = 0; h < 4; ++h)
+        if (4 * g + h < count) out[4 * g + h] = r[h];
+}
+
+__global__ void device_math_kernel(int32_t op, const double* x, int64_t count, double* out, BSConst bs) {
+    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (4 * g >= count) return;
+    math_group(op, x, count, out, g, bs);
+}
+
+// the constant-sigma BS constants of the default GBM handle (fill_params' expressions)
+static BSConst default_bs() {
+    BSConst c;
+    const double sig = sqrt(0.029028), T = 30.0 / 252.0, r = 0.04;
+    c.intrinsic = 0;
+    c.a = (r + 0.5 * pow(sig, 2.0)) * T;
+    c.b = sig * sqrt(T);
+    c.inv_b = 1.0 / c.b;
+    c.disc = exp(-r * T);
+    return c;
 }
 
 // Explicit reset of envs `ids` (NULL: all).  Generate: the market position of a
@@ -3536,16 +3685,18 @@ he_status he_device_rng(uint64_t seed, const uint64_t* env_ids, const uint64_t* 
 }
 
 he_status he_device_math(int32_t op, const double* x, int64_t count, double* out, void* stream) {
-    if (op != 0 || count < 0 || (count > 0 && (!x || !out))) return HE_EINVAL;
+    if (op < 0 || op > 5 || count < 0 || (count > 0 && (!x || !out))) return HE_EINVAL;
     if (count == 0) return HE_OK;
-    hipLaunchKernelGGL(device_math_kernel, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
-                       op, x, count, out);
+    const int64_t groups = (count + 3) / 4;
+    hipLaunchKernelGGL(device_math_kernel, dim3((unsigned)((groups + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       op, x, count, out, default_bs());
     return hipGetLastError() == hipSuccess ? HE_OK : HE_EHIP;
 }
 
 he_status he_host_math(int32_t op, const double* x, int64_t count, double* out) {
-    if (op != 0 || count < 0 || (count > 0 && (!x || !out))) return HE_EINVAL;
-    for (int64_t k = 0; k < count; ++k) out[k] = exp_k(x[k]);
+    if (op < 0 || op > 5 || count < 0 || (count > 0 && (!x || !out))) return HE_EINVAL;
+    const BSConst bs = default_bs();
+    for (int64_t g = 0; 4 * g < count; ++g) math_group(op, x, count, out, g, bs);
     return HE_OK;
 }
 

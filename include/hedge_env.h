@@ -321,8 +321,11 @@ he_status he_host_div_byf(const float* a, int64_t count, float b, float* out);
  * generate modes draw from them into normals[2k..2k+1]; either output may be NULL. */
 he_status he_device_rng(uint64_t seed, const uint64_t* env_ids, const uint64_t* step_index, int64_t count,
                         uint32_t* words, double* normals, void* stream);
-/* op 0: the generate-mode price-advance exp (he_math.h exp_k), on the device (DEVICE
- * pointers) and on the host (HOST pointers), for bit-identity and accuracy tests. */
+/* Generate-mode math on the device (DEVICE pointers) and on the host (HOST pointers), for
+ * bit-identity and accuracy tests: op 0 the price-advance exp (he_math.h exp_k), op 2 the
+ * rolling-ATM call mark of the default GBM handle at S = x (bs_call_put, K = round(S)),
+ * op 4 Box-Muller on (u1, u2) pairs of x; ops 1, 3, 5 the same through the lockstep forms
+ * the LDS producers run (exp_k_n, bs_call_put_n, box_muller_n; groups of 4 elements). */
 he_status he_device_math(int32_t op, const double* x, int64_t count, double* out, void* stream);
 he_status he_host_math(int32_t op, const double* x, int64_t count, double* out);
 

@@ -61,3 +61,30 @@ def test_device_exp_equals_host_build():
     torch.cuda.synchronize()
     assert np.array_equal(out.cpu().numpy().view(np.int64)[:-6], host.view(np.int64)[:-6])
     assert np.allclose(out.cpu().numpy()[-6:], host[-6:], rtol=1e-15)
+
+
+@pytest.mark.parametrize("op", [1, 3, 5])
+def test_device_lockstep_math_equals_scalar(op):
+    """On the device, the lockstep forms the LDS producers run (op 1 exp_k_n, 3
+    bs_call_put_n, 5 box_muller_n) give the scalar forms' bits (ops 0, 2, 4: the tile
+    kernels' functions); exp and Box-Muller also equal the host build (he_device_math)."""
+    from cantorrl_amd import _lib
+    lib = _lib.load()
+    rng = np.random.default_rng(op)
+    if op == 1:
+        x = np.concatenate([rng.normal(0, 0.02, 100_001), rng.uniform(-699, 699, 1000)])
+    elif op == 3:
+        x = np.concatenate([496.48 * np.exp(rng.normal(0, 0.2, 100_001)), rng.uniform(0.01, 80, 1000)])
+    else:
+        x = rng.random(2 * 50_001)
+    xd = _dev(x)
+    st = torch.cuda.current_stream().cuda_stream
+    lock, scal = torch.empty_like(xd), torch.empty_like(xd)
+    assert lib.he_device_math(op, xd.data_ptr(), x.size, lock.data_ptr(), st) == 0
+    assert lib.he_device_math(op - 1, xd.data_ptr(), x.size, scal.data_ptr(), st) == 0
+    torch.cuda.synchronize()
+    assert np.array_equal(lock.cpu().numpy().view(np.int64), scal.cpu().numpy().view(np.int64))
+    if op != 3:  # exp_k and Box-Muller use no library transcendental: host == device
+        host = np.empty_like(x)
+        assert lib.he_host_math(op - 1, x.ctypes.data, x.size, host.ctypes.data) == 0
+        assert np.array_equal(lock.cpu().numpy().view(np.int64), host.view(np.int64))

@@ -201,3 +201,32 @@ def test_exp_k_within_one_ulp():
     assert lib.he_host_math(0, x.ctypes.data, x.size, out.ctypes.data) == 0
     assert np.array_equal(out[:2], [1.0, 1.0])
     assert np.allclose(out[2:5], np.exp(x[2:5]), rtol=1e-15) and out[5] == np.inf and out[6] == 0.0
+
+
+def test_lockstep_math_equals_scalar_forms():
+    """he_math.h's lockstep forms (exp_k_n, bs_call_put_n, box_muller_n: what the LDS
+    producers evaluate for 4 market slots at once) give the scalar functions' bits (what the
+    tile kernels and the host run), including the arguments that leave the fast paths:
+    |x| >= 700 and NaN for exp, S < 64 (log ratio outside the series) and NaN for the
+    marks, u at the quadrant and octave edges for Box-Muller."""
+    lib = _lib.load()
+    rng = np.random.default_rng(11)
+
+    def run(op, x):
+        x = np.ascontiguousarray(x, np.float64)
+        out = np.empty_like(x)
+        assert lib.he_host_math(op, x.ctypes.data, x.size, out.ctypes.data) == 0
+        return out
+
+    xe = np.concatenate([rng.normal(0, 0.02, 40001), rng.uniform(-720, 720, 4000),
+                         [700.0, -700.0, 699.999, np.nan, np.inf, -np.inf, 0.0, -0.0]])
+    assert np.array_equal(run(1, xe).view(np.int64), run(0, xe).view(np.int64))
+    S = np.concatenate([496.48 * np.exp(rng.normal(0, 0.2, 40001)), rng.uniform(0.01, 80, 4000),
+                        [63.5, 64.0, 64.4, 500.5, 499.5, 1e-8, 1e6, np.nan]])
+    a, b = run(3, S), run(2, S)
+    assert np.array_equal(np.isnan(a), np.isnan(b))
+    ok = ~np.isnan(b)
+    assert np.array_equal(a[ok].view(np.int64), b[ok].view(np.int64))
+    u = rng.random(2 * 30001)
+    u[:8] = [0.125, 0.25, 0.5, 0.75, 1 - 2 ** -53, 2 ** -53, 0.70710678118654752, 0.5 + 2 ** -40]
+    assert np.array_equal(run(5, u).view(np.int64), run(4, u).view(np.int64))
