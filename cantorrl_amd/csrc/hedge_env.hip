@@ -94,6 +94,12 @@ constexpr int kMaxBlock = 64;    // max market block length M
 #define HE_ROLLOUT_PREFETCH 4
 #endif
 constexpr int kRolloutPrefetch = HE_ROLLOUT_PREFETCH;  // rollout: steps of inputs in flight
+#ifndef HE_REPLAY_PREFETCH
+#define HE_REPLAY_PREFETCH 8
+#endif
+// replay rollouts: steps of path rows in flight (config 6, same box: D = 4 585 us per 256-step
+// launch, D = 8 574-576 us, r03s4)
+constexpr int kReplayPrefetch = HE_REPLAY_PREFETCH;
 #ifndef HE_MKT_WAVES
 #define HE_MKT_WAVES 2  // market_kernel: min waves per SIMD (3 is faster alone, slower beside rollouts)
 #endif
@@ -642,6 +648,108 @@ __device__ __forceinline__ double book_value(const Params& p, double S, double v
 }
 __device__ __forceinline__ double book_value(const Params& p, double S, double var, int32_t t, double runmax) {
     return book_value(p, S, var, t, runmax, p.book_tab);
+}
+
+// mills over NN arguments in lockstep (the same operations per element: the same bits).
+template <int NN>
+__device__ __forceinline__ void mills_n(const double* a, double* out) {
+    double u[NN], r[NN];
+#pragma unroll
+    for (int h = 0; h < NN; ++h) {
+        const double d = a[h] + kMillsC;
+        double y = __builtin_amdgcn_rcp(d);
+        y = fma(fma(-d, y, 1.0), y, y);
+        y = fma(fma(-d, y, 1.0), y, y);
+        u[h] = fma(-kMillsB, y, kMillsA);
+        r[h] = -4.4206737983570504e-10;
+    }
+    constexpr double MC[20] = {-3.8907837965992227e-09, -1.6735307803068382e-09, 3.5462265542512339e-08,
+                               6.1229321472110077e-08,  -1.4934329903924975e-07, -5.8954452073183568e-07,
+                               1.6391429736383158e-07,  4.1122801372346195e-06,  3.4217038844164288e-06,
+                               -2.7074245209317019e-05, -4.4835109354094885e-05, 0.00021086542652290141,
+                               0.00039784937176197925,  -0.002353960594219441,   -0.0013327285592737549,
+                               0.034655415072285041,    -0.13151258275835945,    0.29927575053510824,
+                               -0.48122354789588401,    0.30783718216692846};
+#pragma unroll
+    for (int c = 0; c < 20; ++c)
+#pragma unroll
+        for (int h = 0; h < NN; ++h) r[h] = fma_k(r[h], u[h], MC[c]);
+#pragma unroll
+    for (int h = 0; h < NN; ++h) out[h] = r[h];
+}
+
+// book_value<true> (the handle's constant variance) of NN market slots in lockstep: per
+// option (in book order, the same accumulation) the Europeans' d1 / d2, phi and the two
+// Mills ratios of every slot as interleaved chains; an up-and-out call takes book_option
+// per slot.  The same operations per slot as book_value: the same bits.
+template <int NN>
+__device__ __forceinline__ void book_value_n(const Params& p, const double* S, const int32_t* t, const double* runmax,
+                                             const double* tab, const BookOpt* opts, double* out) {
+    BookEnv b[NN];
+    double lnS[NN];
+#pragma unroll
+    for (int h = 0; h < NN; ++h) lnS[h] = log(S[h]);
+#pragma unroll
+    for (int h = 0; h < NN; ++h) {
+        b[h].S = S[h];
+        b[h].lnS = lnS[h];
+        b[h].sig = p.bk_sig;
+        b[h].isig = p.bk_isig;
+        b[h].s2 = p.bk_s2;
+        b[h].lam = p.bk_lam;
+        out[h] = 0.0;
+    }
+    const double r = p.r_d;
+    for (int k = 0; k < p.book_n; ++k) {
+        BookOpt o = opts[k];
+        o.type = __builtin_amdgcn_readfirstlane(o.type);
+        o.expiry = __builtin_amdgcn_readfirstlane(o.expiry);
+        if (o.type == HE_BOOK_UO_CALL) {
+#pragma unroll
+            for (int h = 0; h < NN; ++h) out[h] = out[h] + o.q100 * book_option(p, o, b[h], o.expiry - t[h], runmax[h], tab);
+            continue;
+        }
+        double d1[NN], d2[NN], Kd[NN], SoKd[NN], ea[2 * NN], ph[NN], ml[2 * NN];
+        bool live[NN];
+#pragma unroll
+        for (int h = 0; h < NN; ++h) {
+            const int32_t m = o.expiry - t[h];
+            live[h] = m > 0 && b[h].sig > 0.0;
+            const int32_t mc = live[h] ? m : 1;
+            const double tau = (double)mc * p.dt;
+            const double* e = tab + 4 * mc;
+            const double sst = b[h].sig * e[0];
+            const double isst = b[h].isig * e[1];
+            d1[h] = ((b[h].lnS - o.lnK) + (r + 0.5 * b[h].s2) * tau) * isst;
+            d2[h] = d1[h] - sst;
+            Kd[h] = o.K * e[2];
+            SoKd[h] = S[h] * (o.invK * e[3]);
+            ea[h] = tail_arg(d1[h]);
+            ea[NN + h] = tail_arg(d2[h]);
+            ph[h] = -0.5 * (ea[h] * ea[h]);   // phi_of's argument
+        }
+        exp_k_n<NN>(ph, ph);
+        mills_n<2 * NN>(ea, ml);
+#pragma unroll
+        for (int h = 0; h < NN; ++h) {
+            const double ph1 = ph[h] * kInvSqrt2Pi;
+            const double q1 = ph1 * ml[h], q2 = (ph1 * SoKd[h]) * ml[NN + h];
+            double n1, m1, n2, m2;
+            ncdf_from_tail(d1[h], q1, &n1, &m1);
+            ncdf_from_tail(d2[h], q2, &n2, &m2);
+            double v;
+            if (o.type == HE_BOOK_PUT) {
+                v = Kd[h] * m2 - S[h] * m1;
+                const double ip = o.K - S[h];
+                v = live[h] ? v : ((ip < 0.0) ? 0.0 : ip);
+            } else {
+                v = S[h] * n1 - Kd[h] * n2;
+                const double ic = S[h] - o.K;
+                v = live[h] ? v : ((ic < 0.0) ? 0.0 : ic);
+            }
+            out[h] = out[h] + o.q100 * ((v < 0.0) ? 0.0 : v);
+        }
+    }
 }
 
 // The Heston price advance's exp (market_body and the LDS producers, the same function):
@@ -1497,7 +1605,7 @@ __device__ __forceinline__ void step_body(const Params& pk, int64_t n_envs, cons
                 flush_part(k);
             }
         }
-    } else if (REPLAY && !SINGLE && p.T > kRolloutPrefetch) {
+    } else if (REPLAY && !SINGLE && p.T > kReplayPrefetch) {
         // replay rollout (train_ppo_v2.py:40's workload): the same D-deep ring, the rows of
         // step k+D issued before step k's stores.  Step kk's row is the env's path at its t
         // then (hedging_env_v2.py:223-231): from the state before step k, t_k + (kk - k) + 1
@@ -1505,7 +1613,7 @@ __device__ __forceinline__ void step_body(const Params& pk, int64_t n_envs, cons
         // not drawn yet, so that slot is loaded from the old path and re-issued once the
         // reset has drawn it (every ring slot of a lane that just reset: its step k + m
         // reads row m of the new path) -- a wave-uniform branch once per episode.
-        constexpr int D = kRolloutPrefetch;
+        constexpr int D = kReplayPrefetch;
         const int32_t T = p.T;
         const int64_t icl = wrow0 + (lane % kEpw);
         const int64_t ic = icl < N ? icl : N - 1;
@@ -1737,8 +1845,18 @@ __global__ __launch_bounds__(kBlock, HE_FUSED_WAVES) void step_market_kernel(Par
 #ifndef HE_LDS_M
 #define HE_LDS_M 8
 #endif
+// Producers specialised for whole blocks (straight-line slots, and with LOCK the lean GBM
+// slots in lockstep).  Same-box A/B (r03s4, two runs each, with 4 waves per SIMD for the
+// 122 VGPRs the lockstep slots hold): config 2 308 / 310 -> 302 / 306 us per launch, config
+// 4 9.03 / 9.05 -> 8.75 / 8.74 ms.
+#ifndef HE_LDS_BALANCE
+#define HE_LDS_BALANCE 1  // SIMD-balanced wave roles (lds_role, below)
+#endif
 #ifndef HE_LDS_PROD_FULL
-#define HE_LDS_PROD_FULL 0  // A/B: producers specialised for whole blocks (straight-line slots)
+#define HE_LDS_PROD_FULL 1
+#endif
+#ifndef HE_LDS_BOOK_LOCK
+#define HE_LDS_BOOK_LOCK 0  // A/B: the GBM book's slots priced in lockstep too (book_value_n)
 #endif
 #ifndef HE_LDS_PROD_LOCK
 #define HE_LDS_PROD_LOCK 1  // with HE_LDS_PROD_FULL: the lean GBM producers' slots in lockstep
@@ -1794,7 +1912,12 @@ struct LdsGeom {
 #ifdef HE_LDS_MINWAVES
     static constexpr int minwaves = (BOOK || HESTON) ? HE_LDS_MINWAVES_BOOK : HE_LDS_MINWAVES;
 #else
-    static constexpr int minwaves = (BOOK || HESTON) ? HE_LDS_MINWAVES_BOOK : (4 * (2 + prod) + 3) / 4 + 1;
+    // the balanced placement (HE_LDS_BALANCE) puts exactly one wave of each of a CU's 4
+    // workgroups on every SIMD: 4 waves per SIMD, 128 VGPRs (the lockstep producers hold
+    // 122); the unbalanced build keeps a spare wave for an uneven placement
+    static constexpr int minwaves = (BOOK || HESTON) ? HE_LDS_MINWAVES_BOOK
+                                                     : ((HE_LDS_PROD_FULL && HE_LDS_BALANCE) ? 4
+                                                                                             : (4 * (2 + prod) + 3) / 4 + 1);
 #endif
     static_assert(H * lanes == kLdsM && penvs * lanes == kLdsEnvs, "producer lane layout");
 };
@@ -2385,9 +2508,10 @@ __device__ __forceinline__ void lds_producer(const Params& p, int k_steps, const
             // the position before it (hedging_env_v2.py:229-231)
             uint32_t tp = tpf;
             const int wb = bp & 1;
-            double lkC[kLdsH], lkP[kLdsH];   // LOCK: the slots' marks, in lockstep
+            double lkC[kLdsH], lkP[kLdsH], lkB[kLdsH];   // LOCK: the slots' marks (+ book), in lockstep
             if constexpr (LOCK) {
                 double Sm[kLdsH], Km[kLdsH];
+                int32_t tb[kLdsH];
                 uint32_t tq = tpf;
 #pragma unroll
                 for (int h = 0; h < kLdsH; ++h) {
@@ -2395,9 +2519,17 @@ __device__ __forceinline__ void lds_producer(const Params& p, int k_steps, const
                     const double Sprev = (h == 0) ? Sin : Sx[h - 1];
                     Sm[h] = last ? ((tq == 0) ? p.s0 : Sprev) : Sx[h];
                     Km[h] = rint(Sm[h]);   // marks<GBM>: the rolling-ATM strike K = round(S)
+                    tb[h] = (int32_t)(tq + 1);
                     tq = (tq + 1 == T) ? 0u : tq + 1;
                 }
                 bs_call_put_n<kLdsH>(Sm, Km, p.bs, lkC, lkP);
+#if HE_LDS_BOOK_OPTS && HE_LDS_BOOK_LOCK
+                if constexpr (BOOK) {   // two slots at a time: four at once spill (760 B of scratch)
+#pragma unroll
+                    for (int h = 0; h < kLdsH; h += 2)
+                        book_value_n<2>(p, Sx + h, tb + h, Mx + h, &W.btab[0][0], &W.bopt[0], lkB + h);
+                }
+#endif
             }
 #pragma unroll
             for (int h = 0; h < kLdsH; ++h) {
@@ -2426,8 +2558,9 @@ __device__ __forceinline__ void lds_producer(const Params& p, int k_steps, const
                     // the book after the step into slot sl (episode step tp + 1, the new S,
                     // not lagged): market_body's tileC
 #if HE_LDS_BOOK_OPTS
-                    if (BOOK) W.bk[wb][sl][le] = book_value<!HESTON>(p, Sx[h], Vh, (int32_t)(tp + 1), Mx[h], &W.btab[0][0],
-                                                                     &W.bopt[0]);
+                    if constexpr (BOOK && LOCK && HE_LDS_BOOK_LOCK) W.bk[wb][sl][le] = lkB[h];
+                    else if (BOOK) W.bk[wb][sl][le] = book_value<!HESTON>(p, Sx[h], Vh, (int32_t)(tp + 1), Mx[h],
+                                                                          &W.btab[0][0], &W.bopt[0]);
 #else
                     if (BOOK) W.bk[wb][sl][le] = book_value<!HESTON>(p, Sx[h], Vh, (int32_t)(tp + 1), Mx[h], &W.btab[0][0]);
 #endif
@@ -2470,9 +2603,6 @@ __device__ __forceinline__ void lds_producer(const Params& p, int k_steps, const
 // runs each): configs 4 / 5 (producer-bound) 11.25 -> 10.54 ms and 2.49 -> 2.25 ms per
 // launch; config 2 unchanged (its placement is already one role per SIMD on 230 of 256
 // CUs, tools/lds_hwid.py).
-#ifndef HE_LDS_BALANCE
-#define HE_LDS_BALANCE 1
-#endif
 #if HE_LDS_BALANCE || defined(HE_LDS_HWID)
 __device__ uint32_t g_cu_ticket[4096];
 #endif
