@@ -378,6 +378,38 @@ __device__ __forceinline__ float4 greeks_lean(float S, float num_drift, float in
     return make_float4(cd, gam, pd, 0.0f);
 }
 
+// greeks_lean of NN prices as interleaved chains: each stage over all NN elements before
+// the next (ILP across the elements), the per-element operations of greeks_lean, so the
+// same bits.
+template <int NN>
+__device__ __forceinline__ void greeks_lean_n(const float* S, float num_drift, float inv_sst_f, float sstf,
+                                              float* cd, float* gam, float* pd) {
+    float K[NN], d1[NN], x[NN], tail[NN];
+#pragma unroll
+    for (int j = 0; j < NN; ++j) {
+        K[j] = rintf(S[j]);
+        d1[j] = (logf(S[j] / np_maxf(K[j], 1e-6f)) + num_drift) * inv_sst_f;
+    }
+#pragma unroll
+    for (int j = 0; j < NN; ++j) {
+        x[j] = d1[j] * 0.70710678118654752f;
+        tail[j] = 0.5f * erfcf(fabsf(x[j]));
+    }
+#pragma unroll
+    for (int j = 0; j < NN; ++j) {
+        const float gd = S[j] * sstf;
+        const float gm = (fabsf(gd) < 1e-9f)
+                             ? 0.0f
+                             : (expf(-0.5f * (d1[j] * d1[j])) * 0.398942280401432678f) * __builtin_amdgcn_rcpf(gd);
+        const bool tiny = S[j] <= 1e-6f;
+        const float c = (x[j] >= 0.0f) ? 1.0f - tail[j] : tail[j];
+        const float q = (x[j] >= 0.0f) ? -tail[j] : tail[j] - 1.0f;
+        cd[j] = tiny ? ((K[j] == 0.0f) ? 0.5f : ((K[j] > 0.0f) ? 0.0f : 1.0f)) : c;
+        pd[j] = tiny ? ((K[j] == 0.0f) ? -0.5f : ((K[j] < 0.0f) ? 0.0f : -1.0f)) : q;
+        gam[j] = tiny ? 0.0f : gm;
+    }
+}
+
 // ------------------------------------------------------------------ observation
 // S_t / S_{t-1} - 1 clipped to +-1, 0 when S_{t-1} == 0 (hedging_env_v2.py:129-136):
 // a function of the market alone, so it is computed where the market is (market_kernel
@@ -1858,6 +1890,9 @@ __global__ __launch_bounds__(kBlock, HE_FUSED_WAVES) void step_market_kernel(Par
 #ifndef HE_LDS_BOOK_LOCK
 #define HE_LDS_BOOK_LOCK 0  // A/B: the GBM book's slots priced in lockstep too (book_value_n)
 #endif
+#ifndef HE_LDS_OBS_LOCK
+#define HE_LDS_OBS_LOCK 0  // the lean obs stepper's greeks of a full block in lockstep (A/B)
+#endif
 #ifndef HE_LDS_PROD_LOCK
 #define HE_LDS_PROD_LOCK 1  // with HE_LDS_PROD_FULL: the lean GBM producers' slots in lockstep
 #endif
@@ -2079,8 +2114,9 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
 #pragma unroll
     for (int d = 0; d < D; ++d) ra[d] = ld2(gact, (int64_t)(d < k_steps ? d : k_steps - 1) * N + i);
 
-    // ---- the block loop over a step function step(buf, sl, k, action)
-    auto run = [&](auto&& step) {
+    // ---- the block loop over a step function step(buf, sl, k, action, in_full_block), with
+    // blk(buf) called once per full block after its barrier (a block-wide prologue)
+    auto run_blk = [&](auto&& blk, auto&& step) {
         LDS_BAR();  // block 0 produced
         for (int b = 0; b < nfull; ++b) {
 #if defined(HE_LDS_DIAG) && HE_LDS_DIAG == 2
@@ -2088,13 +2124,14 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
             continue;
 #endif
             const int buf = b & 1;
+            blk(buf);
 #pragma unroll
             for (int sl = 0; sl < kLdsM; ++sl) {
                 const int k = b * kLdsM + sl;
                 const float2 ak = ra[sl % D];
                 const int kn = k + D;
                 ra[sl % D] = ld2(gact, (int64_t)(kn < k_steps ? kn : k_steps - 1) * N + i);
-                step(buf, sl, k, ak);
+                step(buf, sl, k, ak, std::true_type{});
             }
             LDS_BAR();  // buffer b & 1 handed back, block b + 1 produced
         }
@@ -2103,11 +2140,14 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
             const int buf = nfull & 1;
             for (int sl = 0; sl < tail; ++sl) {
                 const int k = nfull * kLdsM + sl;
-                step(buf, sl, k, ld2(gact, (int64_t)k * N + i));
+                step(buf, sl, k, ld2(gact, (int64_t)k * N + i), std::false_type{});
             }
 #endif
             LDS_BAR();
         }
+    };
+    auto run = [&](auto&& step) {
+        run_blk([](int) {}, [&](int buf, int sl, int k, float2 ak, auto) { step(buf, sl, k, ak); });
     };
 
     if constexpr (LEAN) {
@@ -2132,11 +2172,24 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
 #endif
             float preS = pre.S;
             if (e.t != 0) preS = (float)cur.S[i];
-            auto obs_step = [&](int buf, int sl, int k, float2 ak, auto full) {
+            // HE_LDS_OBS_LOCK: a full block's 8 greeks evaluated up front as interleaved chains
+            // (greeks_lean_n, the same bits), held in registers for the block's 8 steps
+            float lkc[kLdsM], lkg[kLdsM], lkp[kLdsM];
+            auto obs_blk = [&](int buf) {
+#if HE_LDS_OBS_LOCK
+                float Sb[kLdsM];
+#pragma unroll
+                for (int sl = 0; sl < kLdsM; ++sl) Sb[sl] = L.sc[buf][sl][lane].x;
+                greeks_lean_n<kLdsM>(Sb, gnd, gis, gsf, lkc, lkg, lkp);
+#endif
+            };
+            auto obs_step = [&](int buf, int sl, int k, float2 ak, auto full, auto fb) {
                 const float2 r0 = L.sc[buf][sl][lane];
                 const float rP = L.pp[buf][sl][lane];
                 // the obs greeks: greeks_fast of the market price, as market_kernel makes them
-                const float4 g = greeks_lean(r0.x, gnd, gis, gsf);
+                float4 g;
+                if constexpr (decltype(fb)::value && HE_LDS_OBS_LOCK) g = make_float4(lkc[sl], lkg[sl], lkp[sl], 0.0f);
+                else g = greeks_lean(r0.x, gnd, gis, gsf);
                 // (i)-(ii) of step_env: the integer trade logic (:181-200)
                 const int32_t nc = e.call + trade_round(ak.x * mt_f, mt);
                 const int32_t nq = e.put + trade_round(ak.y * mt_f, mt);
@@ -2174,9 +2227,13 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
                 preS = term ? rst.S : r0.x;
             };
             if (wrows == kLdsEnvs)
-                run([&](int buf, int sl, int k, float2 ak) { obs_step(buf, sl, k, ak, std::true_type{}); });
+                run_blk(obs_blk, [&](int buf, int sl, int k, float2 ak, auto fb) {
+                    obs_step(buf, sl, k, ak, std::true_type{}, fb);
+                });
             else
-                run([&](int buf, int sl, int k, float2 ak) { obs_step(buf, sl, k, ak, std::false_type{}); });
+                run_blk(obs_blk, [&](int buf, int sl, int k, float2 ak, auto fb) {
+                    obs_step(buf, sl, k, ak, std::false_type{}, fb);
+                });
         } else {
             const double tcpc = p.tcpc, slip_frac = p.slip_frac, lam = p.lam, w = p.w, theta = p.theta;
             const double shares_d = p.shares_d, inv_shares = p.inv_shares, den = p.den, inv_den = p.inv_den;

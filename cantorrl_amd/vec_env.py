@@ -13,6 +13,7 @@ them.  `step_tensors` is the zero-copy path for GPU-resident learners.
 """
 import os
 import time
+import weakref
 
 import numpy as np
 import torch
@@ -199,6 +200,7 @@ class HedgingVecEnv:
         self.return_numpy = bool(return_numpy)
         self.monitor_keywords = tuple(monitor_keywords) if monitor_keywords else None
         self._pending_seeds = None
+        self._live_view = None  # weakref to the newest InfoView (see InfoView)
         self._actions_pending = None
         self._ep_ret = np.zeros(n, np.float64)
         self._ep_len = np.zeros(n, np.int64)
@@ -247,23 +249,34 @@ class HedgingVecEnv:
         """SB3 semantics: env i gets seed + i, applied at the next reset()."""
         if seed is None:
             seed = int(np.random.randint(0, 2 ** 31 - 1))
-        self._pending_seeds = [int(seed) + i for i in range(self.num_envs)]
-        return self._pending_seeds
+        seeds = [int(seed) + i for i in range(self.num_envs)]
+        # generate modes key every env's Philox stream by (seed, global id): one seed
+        self._pending_seeds = seeds if self.mode == "replay" else seeds[:1]
+        return seeds
 
     def seed_envs(self, seeds, env_ids=None):
         """Per-env reset(seed=...) re-seeding (replay).  Generate modes have one Philox
-        key per handle: seeds[0] becomes it (env i's stream is keyed by its global id),
-        and env_ids are refused (he_seed: HE_EINVAL)."""
+        key per handle (env i's stream is keyed by its global id): exactly one seed, and
+        env_ids are refused (he_seed: HE_EINVAL)."""
         seeds = np.ascontiguousarray(np.asarray(seeds, dtype=np.uint64)).reshape(-1)
-        if self.mode != "replay" and env_ids is None:
-            seeds = seeds[:1]
+        if self.mode != "replay" and len(seeds) != 1:
+            raise ValueError(f"{self.mode} mode takes one seed per handle (env i's Philox stream is "
+                             f"keyed by the seed and its global id), got {len(seeds)}")
         ids = None if env_ids is None else np.ascontiguousarray(np.asarray(env_ids, dtype=np.int64))
         st = self.lib.he_seed(self._h, None if ids is None else ids.ctypes.data, seeds.ctypes.data,
                               len(seeds))
         _lib.check(self.lib, self._h, st, "he_seed")
 
     # ------------------------------------------------------------------ reset
+    def _retire_view(self):
+        """Freeze the newest InfoView (if still alive) before its buffers are overwritten."""
+        r, self._live_view = self._live_view, None
+        v = r() if r is not None else None
+        if v is not None:
+            v._freeze()
+
     def reset_tensors(self, env_ids=None):
+        self._retire_view()
         if self._pending_seeds is not None:
             self.seed_envs(self._pending_seeds)
             self._pending_seeds = None
@@ -295,6 +308,7 @@ class HedgingVecEnv:
             a = torch.as_tensor(actions, dtype=torch.float32)
             self._act.copy_(a.reshape(self.num_envs, 2), non_blocking=True)
             act = self._act
+        self._retire_view()
         st = self.lib.he_step(self._h, act.data_ptr(), self._obs.data_ptr(), self._rew.data_ptr(),
                               self._term.data_ptr(), self._trunc.data_ptr(),
                               self._tobs.data_ptr() if terminal_obs else None,
@@ -447,26 +461,36 @@ class HedgingVecEnv:
 class InfoView:
     """Lazy list[dict] of per-env infos (SB3 contract) over the device info SoA.
 
-    The step's info buffers (and terminal obs) are snapshotted on the device when the view
-    is made -- the next step overwrites the env's own buffers -- and copied to the host on
-    the first access, so a view read after later steps still shows its own step."""
+    The view reads the env's live info buffers, copied to the host on the first access.
+    It is the env's newest view until the env's next step or reset, which first freezes
+    it (a device copy of the info buffers, only when the view is still alive and has not
+    been read): a view read after later steps still shows its own step, and a view that is
+    dropped or read before the next step costs no copy.  Done rows (terminal obs, Monitor
+    episode) are materialized by step_wait right away, from the live buffers."""
 
     def __init__(self, venv, done):
         self._v = venv
         self._done = done
         self._cache = {}
         self._host = None
-        self._snap = {k: t.clone() for k, t in venv._info_t.items()}
-        self._tobs_snap = venv._tobs.clone()
+        self._snap = None
+        venv._retire_view()
+        venv._live_view = weakref.ref(self)
+
+    def _freeze(self):
+        if self._host is None and self._snap is None:
+            self._snap = {k: t.clone() for k, t in self._v._info_t.items()}
 
     def _host_info(self):
         if self._host is None:
-            self._host = {k: t.cpu().numpy() for k, t in self._snap.items()}
+            src = self._snap if self._snap is not None else self._v._info_t
+            self._host = {k: t.cpu().numpy() for k, t in src.items()}
+            self._snap = None
         return self._host
 
     def _materialize_done(self, done):
         v = self._v
-        tobs = self._tobs_snap.cpu().numpy()
+        tobs = v._tobs.cpu().numpy()  # called by step_wait before any later step
         h = self._host_info()
         for i in np.nonzero(done)[0]:
             d = self[i]

@@ -275,16 +275,14 @@ class _NormInfoView(InfoView):
     def __init__(self, wrapper, done):
         super().__init__(wrapper.venv, done)
         self._w = wrapper
-        # this step's normalized terminal obs and Monitor sums (the next step overwrites them)
-        self._ntobs = wrapper._tobs_out.clone()
-        self._er = wrapper._ep_ret_done.clone()
-        self._el = wrapper._ep_len_done.clone()
 
     def _materialize_done(self, done):
+        # called by step_wait right after the step: this step's normalized terminal obs and
+        # Monitor sums are still in the wrapper's buffers
         w, v = self._w, self._w.venv
-        tobs = self._ntobs.cpu().numpy()
-        er = self._er.cpu().numpy()
-        el = self._el.cpu().numpy()
+        tobs = w._tobs_out.cpu().numpy()
+        er = w._ep_ret_done.cpu().numpy()
+        el = w._ep_len_done.cpu().numpy()
         h = self._host_info()
         for i in np.nonzero(done)[0]:
             d = self[i]

@@ -139,6 +139,37 @@ def test_stats_assignment_pkl_path_and_stale_infos(tmp_path):
         e.close()
 
 
+def test_info_views_freeze_lazily_and_generate_seeding_takes_one_seed():
+    """a device-path info view costs no copy when it is read (or dropped)
+    before the next step, and is frozen (still showing its own step) when it is not; in
+    generate modes seed_envs takes exactly one seed instead of silently keeping seeds[0]."""
+    from cantorrl_amd.vec_env import HedgingVecEnv
+    from cantorrl_amd.vec_normalize import DeviceVecNormalize
+    for wrap in (False, True):
+        env = HedgingVecEnv(32, mode="gbm", generate=dict(episode_length=6), seed=3, device=DEV,
+                            return_numpy=False, info_keys=("call_contracts",), **KW)
+        e = DeviceVecNormalize(env) if wrap else env
+        e.reset()
+        one = torch.full((32, 2), 1.0, device=DEV)
+        e.step_async(one)
+        ra = e.step_wait()[3]
+        assert ra[4]["call_contracts"] == 15 and ra._snap is None  # read live, no copy
+        e.step_async(one)
+        ka = e.step_wait()[3]           # kept, unread, across the next steps
+        e.step_async(one)
+        kb = e.step_wait()[3]
+        assert ka._snap is not None and kb._snap is None
+        e.step_async(one)
+        e.step_wait()
+        assert ka[4]["call_contracts"] == 30 and kb[4]["call_contracts"] == 45
+        with pytest.raises(ValueError, match="one seed"):
+            env.seed_envs([1, 2, 3])
+        env.seed_envs([5])
+        assert len(env.seed(11)) == 32 and env._pending_seeds == [11]
+        env.reset()
+        e.close()
+
+
 def test_nonfinite_counter():
     """check_finite: he_count_nonfinite after each step counts non-finite obs/reward
     values on the device.  Replay tables with a NaN mark column (as the shipped
