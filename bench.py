@@ -671,8 +671,12 @@ def roofline(mode, n, kern_ms, rk, book=False, market="gbm", lds=False):
         if market == "replay":
             survey = n * (rk * (SURVEY_ROLLOUT_B + SURVEY_REPLAY_GATHER_B) + SURVEY_ROLLOUT_STATE_B)
             own = n * (rk * REPLAY_ROLLOUT_B + REPLAY_STATE_B)
-            kname = ("step_kernel (he_rollout, replay, K=%d fused steps; each env gathers its path row from "
-                     "the table)" % rk)
+            if os.environ.get("HE_LDS_ROLLOUT", "1") != "0":
+                kname = ("lds_replay_kernel (he_rollout, replay, K=%d fused steps; a loader wave stages each "
+                         "env's path rows in LDS one block ahead of the steppers)" % rk)
+            else:
+                kname = ("step_kernel (he_rollout, replay, K=%d fused steps; each env gathers its path row from "
+                         "the table)" % rk)
         elif lds:
             # + the book's running max, + Heston's f64 variance (each read + written)
             own = n * (rk * LDS_STEP_B + LDS_STATE_B + (16 if book else 0) + (16 if market == "heston" else 0))

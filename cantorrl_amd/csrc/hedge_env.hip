@@ -243,7 +243,27 @@ struct Env {
     int32_t path;
     float s0;          // initial_S0_for_episode as f32 (1.0 when substituted)
     bool s0_small;
+    // replay LDS steppers (EP): the episode's quotient constants (replay_episode_consts)
+    double s0s_d, inv_s0s_d;  // max(S0, 25) of the obs prices (inf as DBL_MAX) and RN(1/.)
+    double den, inv_den;      // the reward denominator and RN(1/.)
 };
+
+// The per-episode divisors of a replay env (hedging_env_v2.py:120-122 obs prices,
+// :243-256 reward), computed once at the episode's reset so the steps take the
+// correctly rounded Markstein quotients (div_f32_by, div_by) instead of true
+// divisions: the same values as make_obs's / step_env's quotients.  An infinite
+// max(S0, 25) is held as DBL_MAX: div_f32_by then gives a·0 = ±0 like a / inf.
+__device__ __forceinline__ void replay_episode_consts(const Params& p, Env& e) {
+    const float f = np_maxf(e.s0, 25.0f);
+    const double fd = (double)f;
+    e.s0s_d = (fd == __builtin_inf()) ? 1.7976931348623157e308 : fd;
+    e.inv_s0s_d = 1.0 / fd;
+    double den;
+    if (p.loss == HE_LOSS_MSE) den = e.s0_small ? (625.0 + 1e-9) : (double)(f * f + 1e-9f);
+    else den = e.s0_small ? (25.0 + 1e-9) : (double)(f + 1e-9f);
+    e.den = den;
+    e.inv_den = 1.0 / den;
+}
 
 __device__ __forceinline__ int32_t unpack_lo(uint32_t p) { return (int32_t)(int16_t)(p & 0xFFFFu); }
 __device__ __forceinline__ int32_t unpack_hi(uint32_t p) { return (int32_t)(int16_t)(p >> 16); }
@@ -423,13 +443,17 @@ __device__ __forceinline__ float lag_return(float S, float Sp) {
 // constants use div_byf (correctly rounded, 3 instructions).
 // FAST: the hot configuration is known at compile time (see fast_config()):
 // generate mode, record_metrics, max_contracts_held > 0, T > 0.
-template <bool FAST = false>
+template <bool FAST = false, bool EP = false>
 __device__ __forceinline__ void make_obs(const Params& p, const Env& e, const Mkt& m, float4 g, float Sp,
                                          float vp, float* o) {
     if (FAST || p.s0s_const) {
         o[0] = div_f32_by(m.S, p.s0s_d, p.inv_s0s_d);
         o[1] = div_f32_by(m.C, p.s0s_d, p.inv_s0s_d);
         o[2] = div_f32_by(m.P, p.s0s_d, p.inv_s0s_d);
+    } else if (EP) {  // the episode's max(S0, 25) (replay_episode_consts)
+        o[0] = div_f32_by(m.S, e.s0s_d, e.inv_s0s_d);
+        o[1] = div_f32_by(m.C, e.s0s_d, e.inv_s0s_d);
+        o[2] = div_f32_by(m.P, e.s0s_d, e.inv_s0s_d);
     } else {
         float s0s = np_maxf(e.s0, 25.0f);
         o[0] = m.S / s0s;
@@ -1132,7 +1156,7 @@ __device__ __forceinline__ double portfolio_value(const Params& p, const Env& e,
 // FAST: variant 2, loss != mse, shares_to_hedge != 0, generate mode (constant reward
 // denominator) -- the branches on those flags compiled out (fast_config()).
 // pv_last = portfolio_value(pre-step state), carried in registers across fused steps.
-template <bool BOOK, bool FAST = false>
+template <bool BOOK, bool FAST = false, bool EP = false>
 __device__ __forceinline__ void step_env(const Params& p, Env& e, const Mkt& pre, const Mkt& post, float a0,
                                          float a1, double pv_last, StepOut& o) {
     double pv_prev;
@@ -1179,6 +1203,8 @@ __device__ __forceinline__ void step_env(const Params& p, Env& e, const Mkt& pre
     const double num = (!FAST && p.loss == HE_LOSS_MSE) ? ps * ps : fabs(ps);
     if (FAST || p.den_const) {
         term_v = div_by(num, p.den, p.inv_den);
+    } else if (EP) {  // the episode's denominator (replay_episode_consts): num / den
+        term_v = div_by(num, e.den, e.inv_den);
     } else {
         float f = np_maxf(e.s0, 25.0f);
         double den;
@@ -1903,7 +1929,15 @@ __global__ __launch_bounds__(kBlock, HE_FUSED_WAVES) void step_market_kernel(Par
 #define HE_LDS_HOIST 0  // A/B: obs-wave constants forced into VGPRs (1: greeks, 2: reset obs)
 #endif
 #ifndef HE_LDS_PRIO_REW
-#define HE_LDS_PRIO_REW 0
+// the reward stepper above the obs stepper, GBM without a book (same-box A/B r03s9, config 2,
+// two runs each: priority 0 312 / 300 us per launch, 1 319 / 313, 2 314 / 302, 3 305 / 296)
+#define HE_LDS_PRIO_REW 3
+#endif
+#ifndef HE_LDS_PRIO_REW_BOOK
+#define HE_LDS_PRIO_REW_BOOK 0  // with a book or Heston (producer-bound)
+#endif
+#ifndef HE_REPLAY_PRIO_REW
+#define HE_REPLAY_PRIO_REW 0
 #endif
 #ifndef HE_LDS_PRIO_OBS
 #define HE_LDS_PRIO_OBS 2  // the obs wave is the workgroup's critical chain: it wins issue
@@ -2052,7 +2086,7 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
     GLOBAL float* const grew = (GLOBAL float*)io.rew;
     GLOBAL uint8_t* const gterm = (GLOBAL uint8_t*)io.term;
     if (OBS) __builtin_amdgcn_s_setprio(HE_LDS_PRIO_OBS);
-    else __builtin_amdgcn_s_setprio(HE_LDS_PRIO_REW);
+    else __builtin_amdgcn_s_setprio((BOOK || HESTON) ? HE_LDS_PRIO_REW_BOOK : HE_LDS_PRIO_REW);
     LDS_T0();
     Env e{};
     Mkt pre = rst;
@@ -2727,6 +2761,338 @@ __global__ __launch_bounds__((LdsGeom<MODE, BOOK>::threads), (LdsGeom<MODE, BOOK
     if (wave == 0) lds_stepper<MODE, BOOK, LEAN, false>(p, s, io, k_steps, cur, lm, base);
     else if (wave == 1) lds_stepper<MODE, BOOK, LEAN, true>(p, s, io, k_steps, cur, lm, base);
     else lds_producer<MODE, BOOK, LEAN>(p, k_steps, cur, lm, base, wave - 2);
+}
+
+// ------------------------------------------------------------------ replay rollouts in LDS
+// he_rollout in replay mode (train_ppo_v2.py:40's workload: the envs replay rows of a
+// paths table through hedging_env_v2.py:223-231, bench config 6) on the LDS kernel's
+// layout: a workgroup of 64 envs, a reward stepper and an obs stepper wave, and two LOADER
+// waves in place of the producers.  The rows an env reads do not depend on its actions
+// (episodes end at t = T whatever the agent does, and the next episode's row is the env's
+// own PCG64 draw), so the loaders walk every env's (path, t) and PCG64 stream ahead of the
+// steppers: for block b + 1 each issues its half of the M post-step rows {S, v, C, P} of
+// every env (one lane per env; an env's rows of a block are contiguous in the table) a
+// whole block before they go to LDS, evaluates their obs greeks there (HE_REPLAY_LGREEKS:
+// the row's own greeks(), so the 16-B recg record is not read per step), and for an env
+// whose episode ends in the block draws the new path (replay_reset's pcg64_integers) and
+// loads its row 0 -- the reset obs and the next episode's starting market.  Needs T >= M
+// (at most one episode end per env and block) and autoreset.
+//
+// The steppers' arithmetic is step_env / make_obs (generic configuration: any variant,
+// loss, costs, record_metrics) with the episode's divisors held per env
+// (replay_episode_consts), so the outputs are the tile kernels' bits
+// (test_lds_replay_equals_tile_replay).
+struct LdsReplay {
+    float4 mk[2][kLdsM][kLdsEnvs];   // post-step row {S, v, C, P} of every slot
+    float2 gd[2][kLdsM][kLdsEnvs];   // its {call_delta, put_delta}
+    float gg[2][kLdsM][kLdsEnvs];    // its gamma
+    float4 rk[2][kLdsEnvs];          // the new episode of an env ending in the block: row 0 {S0, v0, C0, P0}
+    float4 rg[2][kLdsEnvs];          // and its greeks {call_delta, gamma, put_delta, -}
+    float stage[2][kLdsEnvs * kObs]; // obs row staging, by step parity
+};
+static_assert(kLdsM > 8 || sizeof(LdsReplay) <= 40 * 1024 - 64, "4 workgroups per CU");
+
+#ifndef HE_REPLAY_LGREEKS
+#define HE_REPLAY_LGREEKS 1  // the loaders evaluate the rows' obs greeks (table_greeks_kernel's greeks()) instead of reading recg
+#endif
+// Loader wave `part` (0, 1) stages slots [part * H, part * H + H) of every block, H = M / 2; both
+// walk the whole block's positions and PCG64 draws (the same values), part 0 also the
+// new-episode records and the state write-back.
+__device__ __forceinline__ void lds_replay_loader(const Params& p, State s, int k_steps, LdsReplay& L,
+                                                  int64_t base, int part) {
+    constexpr int H = kLdsM / 2;
+    const int lane = threadIdx.x & 63;
+    const int64_t N = p.n;
+    const int64_t i0 = base + lane;
+    const int64_t i = i0 < N ? i0 : N - 1;   // lanes past N mirror env N-1
+    const uint32_t T = (uint32_t)p.T;
+    const int64_t W = (int64_t)T + 1;        // a path's row stride
+    const GLOBAL v4f* rec = (const GLOBAL v4f*)p.rec;
+    const GLOBAL v4f* recg = (const GLOBAL v4f*)p.recg;
+    const int sl0 = part * H;
+    __builtin_amdgcn_s_setprio(HE_LDS_PRIO_PROD);
+    LDS_T0();
+    int32_t path = s.path[i];
+    uint32_t t = s.t[i];                     // episode step before the next slot (< T: autoreset)
+    Pcg64 g;
+    g.sh = s.pcg[i];
+    g.sl = s.pcg[N + i];
+    g.ih = s.pcg[2 * N + i];
+    g.il = s.pcg[3 * N + i];
+    g.has32 = s.pcgb[i];
+    g.buf32 = s.pcgb[N + i];
+    float s0enc = s.s0[i];
+    const int nb = (k_steps + kLdsM - 1) / kLdsM;
+    float4 A[H], B[H], R0, G0;
+    int rsl = kLdsM;  // slot of the episode end in the issued block (kLdsM: none)
+    // the loads of block bp from the position (path, t) before it; the position advanced past it
+    auto issue = [&](int bp) {
+        const int kb = bp * kLdsM;
+        const int len = (k_steps - kb) < kLdsM ? (k_steps - kb) : kLdsM;
+        // the step from t = T - 1 ends the episode (hedging_env_v2.py:217-219): slot T - 1 - t
+        const uint32_t te = T - 1u - t;
+        rsl = te < (uint32_t)len ? (int)te : kLdsM;
+        int32_t np = path;
+        if (rsl < kLdsM) np = (int32_t)pcg64_integers(g, (uint64_t)p.n_paths);  // replay_reset's draw
+        const int64_t ro = (int64_t)path * W + (int64_t)t + 1, rn = (int64_t)np * W;
+#pragma unroll
+        for (int h = 0; h < H; ++h) {
+            // slots up to the end read the old path's rows t + 1 + sl (row T holds the lagged
+            // marks), the slots after it the new path's rows 1, 2, ...
+            const int sl = sl0 + h;
+            const int64_t r = (sl <= rsl) ? ro + sl : rn + (sl - rsl);
+#if defined(HE_REPLAY_DIAG) && HE_REPLAY_DIAG == 1
+            A[h] = make_float4(100.0f + (float)sl, 0.04f, 3.0f, 2.5f);  // diagnostic build: no table reads
+            B[h] = make_float4(0.5f, 0.01f, -0.5f, 0.0f);
+#else
+            A[h] = ld4(rec, r);
+            if (!HE_REPLAY_LGREEKS) B[h] = ld4(recg, r);
+#endif
+        }
+        if (part == 0) {
+            R0 = ld4(rec, rn);
+            G0 = ld4(recg, rn);
+        }
+        if (rsl < kLdsM) {
+            path = np;
+            t = (uint32_t)(len - 1 - rsl);
+        } else {
+            t += (uint32_t)len;
+        }
+    };
+    if (nb > 0) issue(0);
+    for (int bp = 0; bp <= nb; ++bp) {
+        if (bp < nb) {
+            const int kb = bp * kLdsM;
+            const int len = (k_steps - kb) < kLdsM ? (k_steps - kb) : kLdsM;
+            const int wb = bp & 1;
+#pragma unroll
+            for (int h = 0; h < H; ++h) {
+                const int sl = sl0 + h;
+                if (sl < len) {
+#if HE_REPLAY_LGREEKS && !(defined(HE_REPLAY_DIAG) && HE_REPLAY_DIAG == 1)
+                    // table_greeks_kernel's record, here from the row itself
+                    B[h] = p.record_metrics ? greeks<false>(p, A[h].x, A[h].y) : make_float4(0.f, 0.f, 0.f, 0.f);
+#endif
+                    L.mk[wb][sl][lane] = A[h];
+                    L.gd[wb][sl][lane] = make_float2(B[h].x, B[h].z);
+                    L.gg[wb][sl][lane] = B[h].y;
+                }
+            }
+            if (part == 0) {
+                L.rk[wb][lane] = R0;
+                L.rg[wb][lane] = G0;
+                if (rsl < kLdsM) s0enc = (R0.x < 1e-6f) ? -1.0f : R0.x;  // replay_reset's S0 (-1: python 1.0)
+            }
+            if (bp + 1 < nb) issue(bp + 1);  // in flight while the steppers run block bp
+        }
+        LDS_BAR();  // block bp handed to the steppers
+    }
+    LDS_T1(2 + part);
+    if (part == 0 && i0 < N) {
+        int64_t j = i;
+        asm volatile("" : "+v"(j));
+        s.path[j] = path;
+        s.s0[j] = s0enc;
+        s.pcg[j] = g.sh;
+        s.pcg[N + j] = g.sl;
+        s.pcgb[j] = g.has32;
+        s.pcgb[N + j] = g.buf32;
+    }
+}
+
+// OBS = false: the reward wave (owns the env state); OBS = true: the obs wave.
+template <bool OBS>
+__device__ __forceinline__ void lds_replay_stepper(const Params& p, State s, const Io& io, int k_steps,
+                                                   LdsReplay& L, int64_t base) {
+    constexpr int D = kLdsPrefetch;
+    const int lane = threadIdx.x & 63;
+    const int64_t N = p.n;
+    const int nfull = k_steps / kLdsM;
+    const int tail = k_steps - nfull * kLdsM;
+    const int64_t i0 = base + lane;
+    const int64_t i = i0 < N ? i0 : N - 1;
+    const int wrows = (int)((N - base) < kLdsEnvs ? (N - base) : kLdsEnvs);
+    const int32_t T = p.T;
+    const GLOBAL v2f* gact = (const GLOBAL v2f*)io.act;
+    GLOBAL float* const grew = (GLOBAL float*)io.rew;
+    GLOBAL uint8_t* const gterm = (GLOBAL uint8_t*)io.term;
+    __builtin_amdgcn_s_setprio(OBS ? HE_LDS_PRIO_OBS : HE_REPLAY_PRIO_REW);
+    LDS_T0();
+    Env e{};
+    e.t = s.t[i];
+    {
+        const uint32_t pk = s.pos[i];
+        e.call = unpack_lo(pk);
+        e.put = unpack_hi(pk);
+    }
+    e.path = -1;
+    const float s0enc = s.s0[i];
+    e.s0_small = (s0enc == -1.0f);
+    e.s0 = e.s0_small ? 1.0f : s0enc;
+    replay_episode_consts(p, e);
+    // the row the env stands at (step_body's replay prologue)
+    const uint32_t tt = e.t > (uint32_t)T ? (uint32_t)T : e.t;
+    Mkt pre = as_mkt(ld4((const GLOBAL v4f*)p.rec, (int64_t)s.path[i] * (T + 1) + tt));
+    pre.B = 0.0;
+    double pv_last = 0.0;
+    double sm0 = 0.0, sm1 = 0.0, sm2 = 0.0;
+    uint32_t slen = 0;
+    float last0 = 0.f, last1 = 0.f, last2 = 0.f, last3 = 0.f;
+    if (!OBS) {
+        e.cash = s.cash[i];
+        pv_last = portfolio_value<false>(p, e, pre);
+        sm0 = s.sum[i];
+        sm1 = s.sum[N + i];
+        sm2 = s.sum[2 * N + i];
+        slen = s.sum_len[i];
+        last0 = s.last[i];
+        last1 = s.last[N + i];
+        last2 = s.last[2 * N + i];
+        last3 = s.last[3 * N + i];
+    }
+    float2 ra[D];
+#pragma unroll
+    for (int d = 0; d < D; ++d) ra[d] = ld2(gact, (int64_t)(d < k_steps ? d : k_steps - 1) * N + i);
+
+    // a new episode for the envs ending at this step (wave-uniform branch, taken in a block
+    // where some lane's episode ends): env_reset_common + the new path's S0 and divisors,
+    // the market of row 0; OBS: the reset obs (make_obs of row 0 at t = 0)
+    auto new_episode = [&](int buf, bool term, float* o) {
+        if (__ballot(term) != 0ull) {
+            const float4 r0 = L.rk[buf][lane];
+            Env n = e;
+            env_reset_common(p, n);
+            n.cash = p.initial_cash;
+            n.s0_small = r0.x < 1e-6f;
+            n.s0 = n.s0_small ? 1.0f : r0.x;
+            replay_episode_consts(p, n);
+            const Mkt m0 = as_mkt(r0);
+            if (OBS) {
+                const float4 g0 = L.rg[buf][lane];
+                float ro[kObs];
+                make_obs<false, true>(p, n, m0, g0, m0.S, m0.v, ro);
+#pragma unroll
+                for (int c = 0; c < kObs; ++c) o[c] = term ? ro[c] : o[c];
+            }
+            e.t = term ? n.t : e.t;
+            e.call = term ? n.call : e.call;
+            e.put = term ? n.put : e.put;
+            e.cash = term ? n.cash : e.cash;
+            e.s0 = term ? n.s0 : e.s0;
+            e.s0_small = term ? n.s0_small : e.s0_small;
+            e.s0s_d = term ? n.s0s_d : e.s0s_d;
+            e.inv_s0s_d = term ? n.inv_s0s_d : e.inv_s0s_d;
+            e.den = term ? n.den : e.den;
+            e.inv_den = term ? n.inv_den : e.inv_den;
+            pre.S = term ? m0.S : pre.S;
+            pre.v = term ? m0.v : pre.v;
+            pre.C = term ? m0.C : pre.C;
+            pre.P = term ? m0.P : pre.P;
+        }
+    };
+    auto step = [&](int buf, int sl, int k, float2 ak, auto full) {
+        const int64_t koff = (int64_t)k * N;
+        Mkt post = as_mkt(L.mk[buf][sl][lane]);
+        post.B = 0.0;
+        if (OBS) {
+            const float2 gd = L.gd[buf][sl][lane];
+            const float4 g = make_float4(gd.x, L.gg[buf][sl][lane], gd.y, lag_return(post.S, pre.S));
+            // (i)-(ii) of step_env: the integer trade logic (:181-200)
+            const int32_t nc = e.call + trade_round(ak.x * p.mt_f, p.mt);
+            const int32_t nq = e.put + trade_round(ak.y * p.mt_f, p.mt);
+            e.call = nc < -p.maxh ? -p.maxh : (nc > p.maxh ? p.maxh : nc);
+            e.put = nq < -p.maxh ? -p.maxh : (nq > p.maxh ? p.maxh : nq);
+            e.t = e.t + 1;
+            const bool term = (int32_t)e.t >= T;
+            float o[kObs];
+            make_obs<false, true>(p, e, post, g, pre.S, pre.v, o);
+            pre = post;
+            new_episode(buf, term, o);  // SB3 autoreset: the reset obs
+            float* const tile = L.stage[k & 1];
+#pragma unroll
+            for (int c = 0; c < kObs; ++c) tile[lane * kObs + c] = o[c];
+            float* out = io.obs + koff * kObs;
+            if constexpr (decltype(full)::value) flush_obs_full(tile, out, base, lane);
+            else flush_obs_wave(tile, out, base, wrows, lane);
+        } else {
+            StepOut so;
+            step_env<false, false, true>(p, e, pre, post, ak.x, ak.y, pv_last, so);
+            pv_last = so.pv;
+            grew[koff + i] = (float)so.reward;
+            gterm[koff + i] = so.term ? 1 : 0;
+            const double a0 = sm0 + so.reward, a1 = sm1 + so.pnl, a2 = sm2 + so.tc;
+            const uint32_t n1 = slen + 1u;
+            float f0 = (float)a0, f1 = (float)a1, f2 = (float)a2, f3 = (float)n1;
+            asm volatile("" : "+v"(f0), "+v"(f1), "+v"(f2), "+v"(f3));
+            last0 = so.term ? f0 : last0;
+            last1 = so.term ? f1 : last1;
+            last2 = so.term ? f2 : last2;
+            last3 = so.term ? f3 : last3;
+            sm0 = so.term ? 0.0 : a0;
+            sm1 = so.term ? 0.0 : a1;
+            sm2 = so.term ? 0.0 : a2;
+            slen = so.term ? 0u : n1;
+            pre = post;
+            new_episode(buf, so.term, nullptr);
+        }
+    };
+    auto run = [&](auto full) {
+        LDS_BAR();  // block 0 loaded
+        for (int b = 0; b < nfull; ++b) {
+#if defined(HE_REPLAY_DIAG) && HE_REPLAY_DIAG == 2
+            LDS_BAR();  // diagnostic build: the steppers only keep the barrier count
+            continue;
+#endif
+            const int buf = b & 1;
+#pragma unroll
+            for (int sl = 0; sl < kLdsM; ++sl) {
+                const int k = b * kLdsM + sl;
+                const float2 ak = ra[sl % D];
+                const int kn = k + D;
+                ra[sl % D] = ld2(gact, (int64_t)(kn < k_steps ? kn : k_steps - 1) * N + i);
+                step(buf, sl, k, ak, full);
+            }
+            LDS_BAR();  // buffer b & 1 handed back, block b + 1 loaded
+        }
+        if (tail) {
+            const int buf = nfull & 1;
+            for (int sl = 0; sl < tail; ++sl) {
+                const int k = nfull * kLdsM + sl;
+                step(buf, sl, k, ld2(gact, (int64_t)k * N + i), std::false_type{});
+            }
+            LDS_BAR();
+        }
+    };
+    if (wrows == kLdsEnvs) run(std::true_type{});
+    else run(std::false_type{});
+    LDS_T1(OBS ? 1 : 0);
+    if (!OBS && i0 < N) {
+        int64_t j = i;
+        asm volatile("" : "+v"(j));
+        s.t[j] = e.t;
+        s.pos[j] = pack_pos(e.call, e.put);
+        s.cash[j] = e.cash;
+        s.sum[j] = sm0;
+        s.sum[N + j] = sm1;
+        s.sum[2 * N + j] = sm2;
+        s.sum_len[j] = slen;
+        s.last[j] = last0;
+        s.last[N + j] = last1;
+        s.last[2 * N + j] = last2;
+        s.last[3 * N + j] = last3;
+    }
+}
+
+__global__ __launch_bounds__(256, 4) __attribute__((amdgpu_num_sgpr(96))) void lds_replay_kernel(
+    const Params* __restrict__ pc, State s, Io io, int k_steps) {
+    __shared__ __attribute__((aligned(16))) LdsReplay lm;
+    const Params& p = *pc;
+    const int wave = lds_role<4>(__builtin_amdgcn_readfirstlane(threadIdx.x >> 6));
+    const int64_t base = (int64_t)blockIdx.x * kLdsEnvs;
+    if (wave == 0) lds_replay_stepper<false>(p, s, io, k_steps, lm, base);
+    else if (wave == 1) lds_replay_stepper<true>(p, s, io, k_steps, lm, base);
+    else lds_replay_loader(p, s, k_steps, lm, base, wave - 2);
 }
 
 // Test hooks (he_device_rng / he_device_math): the device build of the generate-mode
@@ -3459,6 +3825,29 @@ static he_status launch_lds_rollout(he_env* env, const Io& io, int k_total, hipS
     return HE_OK;
 }
 
+// he_rollout in replay mode through lds_replay_kernel (HE_LDS_ROLLOUT=0: step_kernel): every
+// output buffer given, episodes of at least one LDS block (at most one episode end per env
+// and block), autoreset (he_rollout's precondition).
+static bool lds_replay_eligible(const he_env* env, const Io& io) {
+    return env->lds_rollout && env->cfg.autoreset && env->p.T >= kLdsM && env->n_paths > 0 && io.obs && io.rew &&
+           io.term;
+}
+
+static he_status launch_lds_replay(he_env* env, const Io& io, int k_total, hipStream_t st) {
+    const int64_t blocks = (env->cfg.n_envs + kLdsEnvs - 1) / kLdsEnvs;
+    const Params* pc = env->dparams;
+    if (env->ev_start) {  // one-shot: bracket exactly this dispatch
+        hipEvent_t a = (hipEvent_t)env->ev_start, b = (hipEvent_t)env->ev_stop;
+        env->ev_start = env->ev_stop = nullptr;
+        hipExtLaunchKernelGGL(lds_replay_kernel, dim3((unsigned)blocks), dim3(256), 0, st, a, b, 0, pc, env->s, io,
+                              k_total);
+    } else {
+        hipLaunchKernelGGL(lds_replay_kernel, dim3((unsigned)blocks), dim3(256), 0, st, pc, env->s, io, k_total);
+    }
+    HE_HIP(env, hipGetLastError());
+    return HE_OK;
+}
+
 static he_status launch_steps(he_env* env, Io io, bool info, int k_total, void* stream, bool rollout = false) {
     const he_config& c = env->cfg;
     if (c.mode == HE_MODE_REPLAY && !env->rec) return fail(env, HE_ESTATE, "no paths loaded (he_load_paths)");
@@ -3467,6 +3856,7 @@ static he_status launch_steps(he_env* env, Io io, bool info, int k_total, void* 
     hipStream_t st = (hipStream_t)stream;
     io.sums = rollout && !io.pol_on;
     if (c.mode == HE_MODE_REPLAY) {
+        if (rollout && !info && !io.pol_on && lds_replay_eligible(env, io)) return launch_lds_replay(env, io, k_total, st);
         launch_step<HE_MODE_REPLAY, false, false>(env, env->p, io, info, k_total, 0, st);
         HE_HIP(env, hipGetLastError());
         return HE_OK;

@@ -776,6 +776,74 @@ def test_full_size_replay_slice_matches_oracle():
     venv.close()
 
 
+def _edge_tables(paths, cols, seed=3):
+    """A replay table in the reference NPZ layout with the edge rows of the g5 goldens
+    spread over its paths: S0 < 25, S0 = 0 (python 1.0 substitution, zero lag), prices
+    <= 1e-6, a NaN mark column (paths_options.npz's t = 1), v <= 0, S0 = 25 and x.5 prices,
+    an infinite S0 (obs prices and reward denominator by inf)."""
+    S, v, C, P = (a[:paths, :cols].copy() for a in _bench_module().replay_tables(paths=max(paths, 64), cols=253,
+                                                                                 seed=seed))
+    C, P = C[:, :cols - 1].copy(), P[:, :cols - 1].copy()
+    S[0] *= np.float32(10.0 / 496.48)
+    S[1, 0] = 0.0
+    S[2, 1:6] = 1e-7
+    C[3, 1] = np.nan
+    P[3, 1] = np.nan
+    v[4, 2:7] = -0.01
+    v[4, 7] = 0.0
+    S[5] = np.round(S[5] * 2) / 2
+    S[5, 0] = 25.0
+    S[6, 0] = np.inf
+    return S, v, C, P
+
+
+REPLAY_LDS_CASES = {
+    # name: (n_envs, n_paths, T, variant, env kwargs, rollout lengths)
+    "train": (1000, 300, 40, 2, dict(loss_type="abs", pnl_penalty_weight=0.001, lambda_cost=0.0001,
+                                     theta_weight=0.0002, slippage_bps=1.0), (64, 64, 30, 100)),
+    "odd_T_ragged": (257, 40, 25, 2, {}, (1, 5, 12, 13, 11, 37, 64, 3)),
+    "T8_edges": (200, 12, 8, 2, dict(slippage_bps=5.0), (7, 12, 1, 20, 16, 9)),
+    "mse_nometrics_cash": (333, 12, 29, 2, dict(loss_type="mse", record_metrics=False, initial_cash=1000.0),
+                           (5, 64, 13, 71)),
+    "v1_edges": (130, 12, 17, 1, {}, (9, 24, 40)),
+    "long_K": (3000, 500, 252, 2, dict(slippage_bps=5.0), (300, 257)),
+}
+
+
+def _bits(t):
+    return t.view(torch.int32) if t.dtype == torch.float32 else t
+
+
+@pytest.mark.parametrize("case", sorted(REPLAY_LDS_CASES))
+def test_lds_replay_equals_tile_replay(case, monkeypatch):
+    """lds_replay_kernel (a loader wave walks every env's rows and PCG64 episode draws one
+    LDS block ahead of the steppers) gives step_kernel's replay rollouts bit for bit: obs,
+    rewards, done flags and the checkpointed state (t, positions, cash, path, S0, PCG64
+    words, episode sums) after every call -- T = 8 (the shortest eligible episode), odd T,
+    ragged K, env counts off the 64-env workgroup, v1, mse / record_metrics off, and the
+    edge rows (S0 < 25, S0 = 0, tiny prices, NaN marks, v <= 0, S0 = inf) drawn often."""
+    from cantorrl_amd.vec_env import HedgingVecEnv
+    n, paths, T, variant, kw, ks = REPLAY_LDS_CASES[case]
+    tables = _edge_tables(paths, T + 1)
+    g = torch.Generator(device="cuda")
+    g.manual_seed(23)
+    acts = torch.rand((sum(ks), n, 2), device="cuda", generator=g) * 2.2 - 1.1
+    runs = []
+    for lds in ("1", "0"):
+        monkeypatch.setenv("HE_LDS_ROLLOUT", lds)
+        env = HedgingVecEnv(n, tables=tables, variant=variant, seed=77, return_numpy=False, info_keys=(), **kw)
+        got = [env.reset_tensors().clone()]
+        a0 = 0
+        for k in ks:
+            o, r, t = env.rollout(acts[a0:a0 + k].contiguous())
+            got += [o.clone(), r.clone(), t.clone(), torch.from_numpy(env.get_state().copy())]
+            a0 += k
+        env.close()
+        runs.append(got)
+    for i, (a, b) in enumerate(zip(*runs)):
+        assert torch.equal(_bits(a), _bits(b)), (case, i)
+
+
 @pytest.mark.parametrize("path", ["lds", "tile", "book", "book_tile"])
 def test_episode_summaries_match_oracle(path, monkeypatch):
     """he_episode_summaries (the per-env payload ranks all-gather): the
