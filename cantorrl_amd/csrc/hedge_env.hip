@@ -245,25 +245,32 @@ struct Env {
     bool s0_small;
     // replay LDS steppers (EP): the episode's quotient constants (replay_episode_consts)
     double s0s_d, inv_s0s_d;  // max(S0, 25) of the obs prices (inf as DBL_MAX) and RN(1/.)
-    double den, inv_den;      // the reward denominator and RN(1/.)
+    double den;               // the reward denominator
 };
 
 // The per-episode divisors of a replay env (hedging_env_v2.py:120-122 obs prices,
-// :243-256 reward), computed once at the episode's reset so the steps take the
-// correctly rounded Markstein quotients (div_f32_by, div_by) instead of true
-// divisions: the same values as make_obs's / step_env's quotients.  An infinite
-// max(S0, 25) is held as DBL_MAX: div_f32_by then gives a·0 = ±0 like a / inf.
+// :243-256 reward), computed at the episode's reset: max(S0, 25) of the obs prices with
+// its RN reciprocal, so the obs take the correctly rounded Markstein quotient
+// (div_f32_by, make_obs's value; an infinite max(S0, 25) is held as DBL_MAX, so
+// div_f32_by gives a·0 = ±0 like a / inf), and step_env's reward denominator (FAST:
+// loss != mse, a select-only expression).
+template <bool FAST>
+__device__ __forceinline__ double replay_den(const Params& p, float s0, bool small) {
+    const float f = np_maxf(s0, 25.0f);
+    const double da = small ? (25.0 + 1e-9) : (double)(f + 1e-9f);
+    if (FAST) return da;
+    const double dm = small ? (625.0 + 1e-9) : (double)(f * f + 1e-9f);
+    return (p.loss == HE_LOSS_MSE) ? dm : da;
+}
+template <bool FAST = false>
 __device__ __forceinline__ void replay_episode_consts(const Params& p, Env& e) {
     const float f = np_maxf(e.s0, 25.0f);
     const double fd = (double)f;
     e.s0s_d = (fd == __builtin_inf()) ? 1.7976931348623157e308 : fd;
     e.inv_s0s_d = 1.0 / fd;
-    double den;
-    if (p.loss == HE_LOSS_MSE) den = e.s0_small ? (625.0 + 1e-9) : (double)(f * f + 1e-9f);
-    else den = e.s0_small ? (25.0 + 1e-9) : (double)(f + 1e-9f);
-    e.den = den;
-    e.inv_den = 1.0 / den;
+    e.den = replay_den<FAST>(p, e.s0, e.s0_small);
 }
+
 
 __device__ __forceinline__ int32_t unpack_lo(uint32_t p) { return (int32_t)(int16_t)(p & 0xFFFFu); }
 __device__ __forceinline__ int32_t unpack_hi(uint32_t p) { return (int32_t)(int16_t)(p >> 16); }
@@ -446,14 +453,14 @@ __device__ __forceinline__ float lag_return(float S, float Sp) {
 template <bool FAST = false, bool EP = false>
 __device__ __forceinline__ void make_obs(const Params& p, const Env& e, const Mkt& m, float4 g, float Sp,
                                          float vp, float* o) {
-    if (FAST || p.s0s_const) {
-        o[0] = div_f32_by(m.S, p.s0s_d, p.inv_s0s_d);
-        o[1] = div_f32_by(m.C, p.s0s_d, p.inv_s0s_d);
-        o[2] = div_f32_by(m.P, p.s0s_d, p.inv_s0s_d);
-    } else if (EP) {  // the episode's max(S0, 25) (replay_episode_consts)
+    if (EP) {  // the episode's max(S0, 25) (replay_episode_consts)
         o[0] = div_f32_by(m.S, e.s0s_d, e.inv_s0s_d);
         o[1] = div_f32_by(m.C, e.s0s_d, e.inv_s0s_d);
         o[2] = div_f32_by(m.P, e.s0s_d, e.inv_s0s_d);
+    } else if (FAST || p.s0s_const) {
+        o[0] = div_f32_by(m.S, p.s0s_d, p.inv_s0s_d);
+        o[1] = div_f32_by(m.C, p.s0s_d, p.inv_s0s_d);
+        o[2] = div_f32_by(m.P, p.s0s_d, p.inv_s0s_d);
     } else {
         float s0s = np_maxf(e.s0, 25.0f);
         o[0] = m.S / s0s;
@@ -1160,7 +1167,10 @@ template <bool BOOK, bool FAST = false, bool EP = false>
 __device__ __forceinline__ void step_env(const Params& p, Env& e, const Mkt& pre, const Mkt& post, float a0,
                                          float a1, double pv_last, StepOut& o) {
     double pv_prev;
-    if (e.t == 0) {
+    if (EP) {  // the replay LDS steppers: a select, no branch
+        const float pv0 = (p.shares_f * pre.S + 0.0f) + p.init_cash_f;  // f32 (:167-168)
+        pv_prev = (e.t == 0) ? (double)pv0 : pv_last;
+    } else if (e.t == 0) {
         float pv0 = (p.shares_f * pre.S + 0.0f) + p.init_cash_f;  // f32 (:167-168)
         pv_prev = (double)pv0;
         if (BOOK) pv_prev = pv_prev + pre.B;
@@ -1197,14 +1207,16 @@ __device__ __forceinline__ void step_env(const Params& p, Env& e, const Mkt& pre
     // (vi) mark-to-market (:233-238)
     double pv = portfolio_value<BOOK>(p, e, post);
     double pnl = pv - pv_prev;
-    double ps = (!FAST && p.shares_zero) ? pnl : div_by(pnl, p.shares_d, p.inv_shares);
+    // EP (the replay LDS steppers): the IEEE division, straight-line -- div_by's value without
+    // its guard branch, so the unrolled steps of a block stay one basic block
+    double ps = (!FAST && p.shares_zero) ? pnl : (EP ? pnl / p.shares_d : div_by(pnl, p.shares_d, p.inv_shares));
     // (vii) reward (:243-262)
     double term_v;
     const double num = (!FAST && p.loss == HE_LOSS_MSE) ? ps * ps : fabs(ps);
-    if (FAST || p.den_const) {
+    if (EP) {  // the episode's denominator (replay_episode_consts)
+        term_v = num / e.den;
+    } else if (FAST || p.den_const) {
         term_v = div_by(num, p.den, p.inv_den);
-    } else if (EP) {  // the episode's denominator (replay_episode_consts): num / den
-        term_v = div_by(num, e.den, e.inv_den);
     } else {
         float f = np_maxf(e.s0, 25.0f);
         double den;
@@ -1355,10 +1367,17 @@ __device__ __forceinline__ void env_reset_common(const Params& p, Env& e) {
 // SINGLE: the he_step instance (k_steps == 1 at compile time, straight-line code).
 // tA/tB: the market source, tile buffer {S,v,C,P} / greeks (generate) or the
 // replay table rec / recg.
+// step1_vn_kernel's view of a he_step: the workgroup's obs rows in LDS after the step and
+// this thread's reward, for the fused VecNormalize moments.
+struct VnHook {
+    const float* tile;
+    float rew;
+};
+
 template <int MODE, bool INFO, bool SINGLE, bool BOOK, bool FAST, bool POL, bool GS>
 __device__ __forceinline__ void step_body(const Params& pk, int64_t n_envs, const float4* tA, const float4* tB,
                                           const double* tC, State s, Io io, int k_steps_arg, int slot0,
-                                          int64_t bid) {
+                                          int64_t bid, VnHook* hook = nullptr) {
     constexpr bool REPLAY = (MODE == HE_MODE_REPLAY);
     constexpr bool CT = (MODE == HE_MODE_GBM);  // 12-B tile records (see ld3A)
     const int k_steps = SINGLE ? 1 : k_steps_arg;
@@ -1368,6 +1387,7 @@ __device__ __forceinline__ void step_body(const Params& pk, int64_t n_envs, cons
     // market_kernel waves that share the SIMDs (they run at the default priority 0)
     __builtin_amdgcn_s_setprio(3);
     __shared__ __attribute__((aligned(16))) float tile[kEpb * kObs];
+    if (hook) hook->tile = tile;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int64_t wrow0 = bid * kEpb + wave * kEpw;  // first env of this wave
     const int64_t i = wrow0 + lane;
@@ -1524,6 +1544,7 @@ __device__ __forceinline__ void step_body(const Params& pk, int64_t n_envs, cons
             StepOut so;
             step_env<BOOK, FAST>(p, e, pre, post, ak.x, ak.y, pv_last, so);
             pv_last = so.pv;
+            if (hook) hook->rew = (float)so.reward;
             if (POL) {  // the reference evaluation loops' sums, in step order
                 acc[0] = acc[0] + so.reward;
                 acc[1] = acc[1] + so.pnl;
@@ -1802,9 +1823,9 @@ __global__ __launch_bounds__(kBlock) void step1_kernel(const Params* __restrict_
 }
 
 // he_step with VecNormalize attached (he_vecnorm_attach): step1_kernel, then the first half
-// of the VecNormalize step (vn_moments.h) over the rows this workgroup has just written --
-// read back from L2 after the barrier -- instead of a separate moments launch; the
-// caller's he_vecnorm_apply is then the second half alone.
+// of the VecNormalize step (vn_moments.h) over the rows this workgroup has just made --
+// from its LDS obs staging tile and the rewards in registers, with no read back -- instead
+// of a separate moments launch; the caller's he_vecnorm_apply is then the second half alone.
 static_assert(kBlock == vn::kVnThreads && kEpb <= vn::kVnChunk, "one step workgroup = one moments partial");
 template <int MODE, bool BOOK, bool FAST, bool GS>
 __global__ __launch_bounds__(kBlock) void step1_vn_kernel(const Params* __restrict__ pc, int64_t n, const float4* tA,
@@ -1820,9 +1841,17 @@ __global__ __launch_bounds__(kBlock) void step1_vn_kernel(const Params* __restri
     io.info = he_info{};
     io.pol_on = false;
     io.sums = false;
-    step_body<MODE, false, true, BOOK, FAST, false, GS>(*pc, n, tA, tB, tC, s, io, 1, slot0, blockIdx.x);
-    __syncthreads();  // the workgroup's obs / reward rows are visible to all its threads
-    vn::moments_body(vm, blockIdx.x);
+    // this thread's env (kEpw == 64: env = workgroup base + threadIdx.x): its running return
+    // is loaded before the step, so the moments need no further memory round trip
+    static_assert(kEpw == 64 && kEpb == kBlock, "one env per thread");
+    const int64_t r = (int64_t)blockIdx.x * kEpb + threadIdx.x;
+    const double ret_prev = (vm.upd_ret && r < n) ? vm.returns[r] : 0.0;
+    double sft[vn::kD + 1];
+    vn::load_mean_shifts(vm, sft);
+    VnHook hk{nullptr, 0.0f};
+    step_body<MODE, false, true, BOOK, FAST, false, GS>(*pc, n, tA, tB, tC, s, io, 1, slot0, blockIdx.x, &hk);
+    __syncthreads();  // the workgroup's obs rows (LDS, the final ones incl. reset obs) visible to all its threads
+    vn::moments_from_rows(vm, blockIdx.x, hk.tile, hk.rew, ret_prev, sft);
 }
 
 // The same moments after any other he_step launch (info requested, a fused market block).
@@ -1999,11 +2028,28 @@ struct LdsGeom {
 // tile kernels (lds_rollout_eligible).  The producers' per-option table reads are then LDS
 // reads instead of L1/L2 gathers on their critical chain.
 constexpr int kLdsBookRows = 256;
-template <int MODE, bool BOOK>
+#ifndef HE_LDS_OBS_LAG
+// A/B: the lean GBM kernel's obs stepper one block behind, its greeks by the reward stepper.
+// Same-box A/B (r03s12, config 2, two runs each): 309.8 / 324.6 us per launch against 307.1 /
+// 320.1 without -- the obs stepper leaves the critical path (busy 2065 -> 1372 cycles per step)
+// but the second producer wave takes it (1952), so the step stays at ~2200 cycles.
+#define HE_LDS_OBS_LAG 0
+#endif
+// The lean GBM kernel (no book) with HE_LDS_OBS_LAG: the obs greeks of block b are evaluated by
+// the reward stepper while it steps block b (greeks_lean_n, the obs stepper's own bits) into
+// gk, and the obs stepper steps block b one block later -- so the market is triple-buffered.
+template <int MODE, bool BOOK, bool LEAN>
+constexpr bool lds_lag() {
+    return LEAN && !BOOK && MODE == HE_MODE_GBM && HE_LDS_OBS_LAG;
+}
+template <int MODE, bool BOOK, bool LEAN = false>
 struct LdsMarketT {
-    float2 sc[2][kLdsM][kLdsEnvs];
-    float pp[2][kLdsM][kLdsEnvs];
+    static constexpr bool LAG = lds_lag<MODE, BOOK, LEAN>();
+    static constexpr int NB = LAG ? 3 : 2;                             // market buffers
+    float2 sc[NB][kLdsM][kLdsEnvs];
+    float pp[NB][kLdsM][kLdsEnvs];
     float stage[2][kLdsEnvs * kObs];                                   // obs row staging, by step parity
+    float gk[LAG ? 2 : 1][3][LAG ? kLdsM : 1][kLdsEnvs];               // LAG: {call_delta, gamma, put_delta} by block parity
     double bk[BOOK ? 2 : 1][BOOK ? kLdsM : 1][kLdsEnvs];                // book value of every slot
     float vv[MODE == HE_MODE_HESTON ? 2 : 1][MODE == HE_MODE_HESTON ? kLdsM : 1][kLdsEnvs];  // Heston: f32 v_t
     double btab[BOOK ? kLdsBookRows : 1][4];  // the book's tau table (p.book_tab), copied at launch start
@@ -2012,6 +2058,7 @@ struct LdsMarketT {
 #endif
 };
 static_assert(kLdsM > 8 || sizeof(LdsMarketT<HE_MODE_GBM, false>) <= 40 * 1024, "4 workgroups per CU");
+static_assert(kLdsM > 8 || sizeof(LdsMarketT<HE_MODE_GBM, false, true>) <= 40 * 1024 - 64, "4 workgroups per CU");
 static_assert(kLdsM > 8 || sizeof(LdsMarketT<HE_MODE_HESTON, true>) <= 40 * 1024, "4 workgroups per CU");
 
 #ifdef HE_LDS_TIMING
@@ -2070,7 +2117,7 @@ __device__ __forceinline__ void flush_obs_full(const float* img, float* out, int
 // vmcnt(0): every store of the wave drained.)  A partial last block takes a generic loop.
 template <int MODE, bool BOOK, bool LEAN, bool OBS>
 __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& io, int k_steps, const Market& cur,
-                                            LdsMarketT<MODE, BOOK>& L, int64_t base) {
+                                            LdsMarketT<MODE, BOOK, LEAN>& L, int64_t base) {
     constexpr int D = kLdsPrefetch;
     constexpr bool HESTON = MODE == HE_MODE_HESTON;
     static_assert(!(LEAN && HESTON), "the lean steppers take the constant GBM variance");
@@ -2149,16 +2196,22 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
     for (int d = 0; d < D; ++d) ra[d] = ld2(gact, (int64_t)(d < k_steps ? d : k_steps - 1) * N + i);
 
     // ---- the block loop over a step function step(buf, sl, k, action, in_full_block), with
-    // blk(buf) called once per full block after its barrier (a block-wide prologue)
+    // blk(buf, b, len) called once per block after its barrier (a block-wide prologue).
+    // LAG (lds_lag): the obs stepper runs one block behind the reward stepper (an extra
+    // barrier first), the reward stepper's blk evaluates the block's obs greeks for it (an
+    // extra barrier last), so both make nb + 2 barriers like the producers.
+    constexpr bool LAG = LdsMarketT<MODE, BOOK, LEAN>::LAG;
+    constexpr int NB = LdsMarketT<MODE, BOOK, LEAN>::NB;
     auto run_blk = [&](auto&& blk, auto&& step) {
+        if (LAG && OBS) LDS_BAR();  // one block behind
         LDS_BAR();  // block 0 produced
         for (int b = 0; b < nfull; ++b) {
 #if defined(HE_LDS_DIAG) && HE_LDS_DIAG == 2
             LDS_BAR();  // diagnostic build: the steppers only keep the barrier count
             continue;
 #endif
-            const int buf = b & 1;
-            blk(buf);
+            const int buf = b % NB;
+            blk(buf, b, kLdsM);
 #pragma unroll
             for (int sl = 0; sl < kLdsM; ++sl) {
                 const int k = b * kLdsM + sl;
@@ -2171,7 +2224,8 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
         }
         if (tail) {
 #if !(defined(HE_LDS_DIAG) && HE_LDS_DIAG == 2)
-            const int buf = nfull & 1;
+            const int buf = nfull % NB;
+            blk(buf, nfull, tail);
             for (int sl = 0; sl < tail; ++sl) {
                 const int k = nfull * kLdsM + sl;
                 step(buf, sl, k, ld2(gact, (int64_t)k * N + i), std::false_type{});
@@ -2179,9 +2233,10 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
 #endif
             LDS_BAR();
         }
+        if (LAG && !OBS) LDS_BAR();  // the obs stepper's last block
     };
     auto run = [&](auto&& step) {
-        run_blk([](int) {}, [&](int buf, int sl, int k, float2 ak, auto) { step(buf, sl, k, ak); });
+        run_blk([](int, int, int) {}, [&](int buf, int sl, int k, float2 ak, auto) { step(buf, sl, k, ak); });
     };
 
     if constexpr (LEAN) {
@@ -2209,8 +2264,9 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
             // HE_LDS_OBS_LOCK: a full block's 8 greeks evaluated up front as interleaved chains
             // (greeks_lean_n, the same bits), held in registers for the block's 8 steps
             float lkc[kLdsM], lkg[kLdsM], lkp[kLdsM];
-            auto obs_blk = [&](int buf) {
+            auto obs_blk = [&](int buf, int, int) {
 #if HE_LDS_OBS_LOCK
+                if constexpr (LAG) return;
                 float Sb[kLdsM];
 #pragma unroll
                 for (int sl = 0; sl < kLdsM; ++sl) Sb[sl] = L.sc[buf][sl][lane].x;
@@ -2222,8 +2278,14 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
                 const float rP = L.pp[buf][sl][lane];
                 // the obs greeks: greeks_fast of the market price, as market_kernel makes them
                 float4 g;
-                if constexpr (decltype(fb)::value && HE_LDS_OBS_LOCK) g = make_float4(lkc[sl], lkg[sl], lkp[sl], 0.0f);
-                else g = greeks_lean(r0.x, gnd, gis, gsf);
+                if constexpr (LAG) {  // the reward stepper's, one block ago
+                    const int gb = (k / kLdsM) & 1;
+                    g = make_float4(L.gk[gb][0][sl][lane], L.gk[gb][1][sl][lane], L.gk[gb][2][sl][lane], 0.0f);
+                } else if constexpr (decltype(fb)::value && HE_LDS_OBS_LOCK) {
+                    g = make_float4(lkc[sl], lkg[sl], lkp[sl], 0.0f);
+                } else {
+                    g = greeks_lean(r0.x, gnd, gis, gsf);
+                }
                 // (i)-(ii) of step_env: the integer trade logic (:181-200)
                 const int32_t nc = e.call + trade_round(ak.x * mt_f, mt);
                 const int32_t nq = e.put + trade_round(ak.y * mt_f, mt);
@@ -2277,7 +2339,34 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
             // reset market's book)
             double pv0 = (double)((shares_f * rst.S + 0.0f) + p.init_cash_f);
             if (BOOK) pv0 = pv0 + rst.B;
-            run([&](int buf, int sl, int k, float2 ak) {
+            // LAG: the obs greeks of the block (greeks_lean_n: greeks_lean's bits) for the obs
+            // stepper, which steps this block one block later
+            const float gnd = p.g_num_drift, gis = p.g_inv_sst_f, gsf = p.g_sst_f;
+            auto rew_blk = [&](int buf, int b, int len) {
+                if constexpr (LAG) {
+                    const int gb = b & 1;
+                    if (len == kLdsM) {
+                        float Sb[kLdsM], gc[kLdsM], gg[kLdsM], gp[kLdsM];
+#pragma unroll
+                        for (int sl = 0; sl < kLdsM; ++sl) Sb[sl] = L.sc[buf][sl][lane].x;
+                        greeks_lean_n<kLdsM>(Sb, gnd, gis, gsf, gc, gg, gp);
+#pragma unroll
+                        for (int sl = 0; sl < kLdsM; ++sl) {
+                            L.gk[gb][0][sl][lane] = gc[sl];
+                            L.gk[gb][1][sl][lane] = gg[sl];
+                            L.gk[gb][2][sl][lane] = gp[sl];
+                        }
+                    } else {
+                        for (int sl = 0; sl < len; ++sl) {
+                            const float4 g = greeks_lean(L.sc[buf][sl][lane].x, gnd, gis, gsf);
+                            L.gk[gb][0][sl][lane] = g.x;
+                            L.gk[gb][1][sl][lane] = g.y;
+                            L.gk[gb][2][sl][lane] = g.z;
+                        }
+                    }
+                }
+            };
+            run_blk(rew_blk, [&](int buf, int sl, int k, float2 ak, auto) {
                 const int64_t koff = (int64_t)k * N;
                 const float2 sc = L.sc[buf][sl][lane];
                 const float pP = L.pp[buf][sl][lane];
@@ -2385,19 +2474,28 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
 // env mirror env N-1 like the steppers' (identical values, identical addresses).
 template <int MODE, bool BOOK, bool LEAN>
 __device__ __forceinline__ void lds_producer(const Params& p, int k_steps, const Market& cur,
-                                             LdsMarketT<MODE, BOOK>& W, int64_t base, int pw) {
+                                             LdsMarketT<MODE, BOOK, LEAN>& W, int64_t base, int pw) {
     using G = LdsGeom<MODE, BOOK>;
     constexpr bool HESTON = G::HESTON;
     constexpr int kLdsLanes = G::lanes, kLdsPEnvs = G::penvs, kLdsH = G::H;
     const int lane = threadIdx.x & 63;
     const int sub = lane / kLdsPEnvs;
+#ifdef HE_LDS_PW_SWAP
+    const int le = (kLdsLanes - 1 - pw) * kLdsPEnvs + (lane % kLdsPEnvs);  // A/B: the producer waves' env halves swapped
+#else
     const int le = pw * kLdsPEnvs + (lane % kLdsPEnvs);  // local env of this lane
+#endif
     const int64_t N = p.n;
     const int nb = (k_steps + kLdsM - 1) / kLdsM;
     const uint32_t T = (uint32_t)p.T;
     const int64_t pi = (base + le) < N ? base + le : N - 1;
     const int64_t gid = p.goff + pi;
+#ifdef HE_LDS_PRIO_PROD1
+    if (pw == 1) __builtin_amdgcn_s_setprio(HE_LDS_PRIO_PROD1);  // A/B: the second producer wave's own priority
+    else __builtin_amdgcn_s_setprio(HE_LDS_PRIO_PROD);
+#else
     __builtin_amdgcn_s_setprio(HE_LDS_PRIO_PROD);
+#endif
     const uint32_t ep0 = cur.ep[pi];
     const uint32_t t0 = cur.t[pi];
     double Sbs = cur.S[pi];                          // f64 price before slot 0 of block bp
@@ -2598,7 +2696,7 @@ __device__ __forceinline__ void lds_producer(const Params& p, int k_steps, const
             // (3) marks + obs greeks of every slot; the terminal step replays the marks of
             // the position before it (hedging_env_v2.py:229-231)
             uint32_t tp = tpf;
-            const int wb = bp & 1;
+            const int wb = bp % LdsMarketT<MODE, BOOK, LEAN>::NB;
             double lkC[kLdsH], lkP[kLdsH], lkB[kLdsH];   // LOCK: the slots' marks (+ book), in lockstep
             if constexpr (LOCK) {
                 double Sm[kLdsH], Km[kLdsH];
@@ -2679,6 +2777,7 @@ __device__ __forceinline__ void lds_producer(const Params& p, int k_steps, const
         }
         LDS_BAR();  // block bp handed to the steppers
     }
+    if (LdsMarketT<MODE, BOOK, LEAN>::LAG) LDS_BAR();  // the lagged obs stepper's last block
     LDS_T1(2 + (pw < 2 ? pw : 1));
 }
 
@@ -2746,7 +2845,7 @@ template <int MODE, bool BOOK, bool LEAN>
 __global__ __launch_bounds__((LdsGeom<MODE, BOOK>::threads), (LdsGeom<MODE, BOOK>::minwaves))
     __attribute__((amdgpu_num_sgpr(96))) void lds_rollout_kernel(const Params* __restrict__ pc, State s, Io io,
                                                                  int k_steps, Market cur) {
-    __shared__ __attribute__((aligned(16))) LdsMarketT<MODE, BOOK> lm;
+    __shared__ __attribute__((aligned(16))) LdsMarketT<MODE, BOOK, LEAN> lm;
     const Params& p = *pc;  // read through the scalar cache (a by-value copy spills)
     const int wave = lds_role<LdsGeom<MODE, BOOK>::threads / 64>(__builtin_amdgcn_readfirstlane(threadIdx.x >> 6));
     const int64_t base = (int64_t)blockIdx.x * kLdsEnvs;
@@ -2901,11 +3000,17 @@ __device__ __forceinline__ void lds_replay_loader(const Params& p, State s, int 
     }
 }
 
-// OBS = false: the reward wave (owns the env state); OBS = true: the obs wave.
-template <bool OBS>
+// OBS = false: the reward wave (owns the env state); OBS = true: the obs wave.  FAST: the
+// configuration of fast_replay_config (v2, loss != mse, shares_to_hedge != 0, record_metrics,
+// max_contracts_held > 0) with its uniform branches compiled out.
+#ifndef HE_REPLAY_LDS_PREFETCH
+#define HE_REPLAY_LDS_PREFETCH kLdsPrefetch
+#endif
+template <bool OBS, bool FAST>
 __device__ __forceinline__ void lds_replay_stepper(const Params& p, State s, const Io& io, int k_steps,
                                                    LdsReplay& L, int64_t base) {
-    constexpr int D = kLdsPrefetch;
+    constexpr int D = HE_REPLAY_LDS_PREFETCH;  // steps of actions in flight
+    static_assert(kLdsM % D == 0, "the action ring index is the slot mod D");
     const int lane = threadIdx.x & 63;
     const int64_t N = p.n;
     const int nfull = k_steps / kLdsM;
@@ -2930,7 +3035,7 @@ __device__ __forceinline__ void lds_replay_stepper(const Params& p, State s, con
     const float s0enc = s.s0[i];
     e.s0_small = (s0enc == -1.0f);
     e.s0 = e.s0_small ? 1.0f : s0enc;
-    replay_episode_consts(p, e);
+    replay_episode_consts<FAST>(p, e);
     // the row the env stands at (step_body's replay prologue)
     const uint32_t tt = e.t > (uint32_t)T ? (uint32_t)T : e.t;
     Mkt pre = as_mkt(ld4((const GLOBAL v4f*)p.rec, (int64_t)s.path[i] * (T + 1) + tt));
@@ -2955,40 +3060,32 @@ __device__ __forceinline__ void lds_replay_stepper(const Params& p, State s, con
 #pragma unroll
     for (int d = 0; d < D; ++d) ra[d] = ld2(gact, (int64_t)(d < k_steps ? d : k_steps - 1) * N + i);
 
-    // a new episode for the envs ending at this step (wave-uniform branch, taken in a block
-    // where some lane's episode ends): env_reset_common + the new path's S0 and divisors,
-    // the market of row 0; OBS: the reset obs (make_obs of row 0 at t = 0)
-    auto new_episode = [&](int buf, bool term, float* o) {
+    // the obs stepper's new episode for the envs ending at this step (a wave-uniform branch,
+    // taken in a block where some lane's episode ends): env_reset_common + the new path's S0
+    // and divisors, the market of row 0 and the reset obs (make_obs of row 0 at t = 0)
+    auto new_episode_obs = [&](int buf, bool term, float* o) {
         if (__ballot(term) != 0ull) {
             const float4 r0 = L.rk[buf][lane];
             Env n = e;
             env_reset_common(p, n);
-            n.cash = p.initial_cash;
             n.s0_small = r0.x < 1e-6f;
             n.s0 = n.s0_small ? 1.0f : r0.x;
-            replay_episode_consts(p, n);
+            replay_episode_consts<FAST>(p, n);
             const Mkt m0 = as_mkt(r0);
-            if (OBS) {
-                const float4 g0 = L.rg[buf][lane];
-                float ro[kObs];
-                make_obs<false, true>(p, n, m0, g0, m0.S, m0.v, ro);
+            const float4 g0 = L.rg[buf][lane];
+            float ro[kObs];
+            make_obs<FAST, true>(p, n, m0, g0, m0.S, m0.v, ro);
 #pragma unroll
-                for (int c = 0; c < kObs; ++c) o[c] = term ? ro[c] : o[c];
-            }
+            for (int c = 0; c < kObs; ++c) o[c] = term ? ro[c] : o[c];
             e.t = term ? n.t : e.t;
             e.call = term ? n.call : e.call;
             e.put = term ? n.put : e.put;
-            e.cash = term ? n.cash : e.cash;
             e.s0 = term ? n.s0 : e.s0;
             e.s0_small = term ? n.s0_small : e.s0_small;
             e.s0s_d = term ? n.s0s_d : e.s0s_d;
             e.inv_s0s_d = term ? n.inv_s0s_d : e.inv_s0s_d;
-            e.den = term ? n.den : e.den;
-            e.inv_den = term ? n.inv_den : e.inv_den;
             pre.S = term ? m0.S : pre.S;
             pre.v = term ? m0.v : pre.v;
-            pre.C = term ? m0.C : pre.C;
-            pre.P = term ? m0.P : pre.P;
         }
     };
     auto step = [&](int buf, int sl, int k, float2 ak, auto full) {
@@ -3006,9 +3103,9 @@ __device__ __forceinline__ void lds_replay_stepper(const Params& p, State s, con
             e.t = e.t + 1;
             const bool term = (int32_t)e.t >= T;
             float o[kObs];
-            make_obs<false, true>(p, e, post, g, pre.S, pre.v, o);
+            make_obs<FAST, true>(p, e, post, g, pre.S, pre.v, o);
             pre = post;
-            new_episode(buf, term, o);  // SB3 autoreset: the reset obs
+            new_episode_obs(buf, term, o);  // SB3 autoreset: the reset obs
             float* const tile = L.stage[k & 1];
 #pragma unroll
             for (int c = 0; c < kObs; ++c) tile[lane * kObs + c] = o[c];
@@ -3017,7 +3114,7 @@ __device__ __forceinline__ void lds_replay_stepper(const Params& p, State s, con
             else flush_obs_wave(tile, out, base, wrows, lane);
         } else {
             StepOut so;
-            step_env<false, false, true>(p, e, pre, post, ak.x, ak.y, pv_last, so);
+            step_env<false, FAST, true>(p, e, pre, post, ak.x, ak.y, pv_last, so);
             pv_last = so.pv;
             grew[koff + i] = (float)so.reward;
             gterm[koff + i] = so.term ? 1 : 0;
@@ -3033,8 +3130,21 @@ __device__ __forceinline__ void lds_replay_stepper(const Params& p, State s, con
             sm1 = so.term ? 0.0 : a1;
             sm2 = so.term ? 0.0 : a2;
             slen = so.term ? 0u : n1;
-            pre = post;
-            new_episode(buf, so.term, nullptr);
+            // SB3 autoreset, branch-free (the block's steps stay one basic block): the new
+            // episode's row 0 is read every step, its denominator and the reset state selected
+            const float4 r0 = L.rk[buf][lane];
+            const bool small = r0.x < 1e-6f;
+            const double den0 = replay_den<FAST>(p, small ? 1.0f : r0.x, small);
+            const bool tm = so.term;
+            e.t = tm ? 0u : e.t;
+            e.call = tm ? 0 : e.call;
+            e.put = tm ? 0 : e.put;
+            e.cash = tm ? p.initial_cash : e.cash;
+            e.den = tm ? den0 : e.den;
+            pre.S = tm ? r0.x : post.S;
+            pre.v = tm ? r0.y : post.v;
+            pre.C = tm ? r0.z : post.C;
+            pre.P = tm ? r0.w : post.P;
         }
     };
     auto run = [&](auto full) {
@@ -3084,14 +3194,15 @@ __device__ __forceinline__ void lds_replay_stepper(const Params& p, State s, con
     }
 }
 
+template <bool FAST>
 __global__ __launch_bounds__(256, 4) __attribute__((amdgpu_num_sgpr(96))) void lds_replay_kernel(
     const Params* __restrict__ pc, State s, Io io, int k_steps) {
     __shared__ __attribute__((aligned(16))) LdsReplay lm;
     const Params& p = *pc;
     const int wave = lds_role<4>(__builtin_amdgcn_readfirstlane(threadIdx.x >> 6));
     const int64_t base = (int64_t)blockIdx.x * kLdsEnvs;
-    if (wave == 0) lds_replay_stepper<false>(p, s, io, k_steps, lm, base);
-    else if (wave == 1) lds_replay_stepper<true>(p, s, io, k_steps, lm, base);
+    if (wave == 0) lds_replay_stepper<false, FAST>(p, s, io, k_steps, lm, base);
+    else if (wave == 1) lds_replay_stepper<true, FAST>(p, s, io, k_steps, lm, base);
     else lds_replay_loader(p, s, k_steps, lm, base, wave - 2);
 }
 
@@ -3833,16 +3944,29 @@ static bool lds_replay_eligible(const he_env* env, const Io& io) {
            io.term;
 }
 
+// The configuration the FAST replay steppers are specialised for (step_env / make_obs with
+// the uniform branches on these flags compiled out).
+static bool fast_replay_config(const he_env* env) {
+    const he_config& c = env->cfg;
+    return c.mode == HE_MODE_REPLAY && c.variant == 2 && c.loss_type != HE_LOSS_MSE && c.shares_to_hedge != 0 &&
+           c.record_metrics && c.max_contracts_held_per_type > 0 && env->p.T > 0;
+}
+
 static he_status launch_lds_replay(he_env* env, const Io& io, int k_total, hipStream_t st) {
     const int64_t blocks = (env->cfg.n_envs + kLdsEnvs - 1) / kLdsEnvs;
     const Params* pc = env->dparams;
+#ifdef HE_REPLAY_FORCE_GENERIC
+    void (*kern)(const Params*, State, Io, int) = lds_replay_kernel<false>;  // A/B: the generic steppers
+#else
+    void (*kern)(const Params*, State, Io, int) = fast_replay_config(env) ? lds_replay_kernel<true>
+                                                                          : lds_replay_kernel<false>;
+#endif
     if (env->ev_start) {  // one-shot: bracket exactly this dispatch
         hipEvent_t a = (hipEvent_t)env->ev_start, b = (hipEvent_t)env->ev_stop;
         env->ev_start = env->ev_stop = nullptr;
-        hipExtLaunchKernelGGL(lds_replay_kernel, dim3((unsigned)blocks), dim3(256), 0, st, a, b, 0, pc, env->s, io,
-                              k_total);
+        hipExtLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), 0, st, a, b, 0, pc, env->s, io, k_total);
     } else {
-        hipLaunchKernelGGL(lds_replay_kernel, dim3((unsigned)blocks), dim3(256), 0, st, pc, env->s, io, k_total);
+        hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), 0, st, pc, env->s, io, k_total);
     }
     HE_HIP(env, hipGetLastError());
     return HE_OK;

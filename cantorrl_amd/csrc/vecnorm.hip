@@ -112,6 +112,22 @@ __global__ void __launch_bounds__(kVnThreads) vn_moments_kernel(VnArgs a) {
     vn::moments_body(moments_args(a), blockIdx.x);
 }
 
+// A row's inputs besides its obs: reward, done flag, Monitor running sums.
+struct RowIn {
+    float rw;
+    bool dn;
+    double er;
+    int32_t el;
+};
+__device__ __forceinline__ RowIn row_in(const VnArgs& a, int64_t r) {
+    RowIn in;
+    in.rw = a.reward[r];
+    in.dn = a.done ? a.done[r] != 0 : false;
+    in.er = a.ep_ret ? a.ep_ret[r] : 0.0;
+    in.el = a.ep_ret ? a.ep_len[r] : 0;
+    return in;
+}
+
 // Launch 2: every workgroup merges all the partials itself (one block reduction in a
 // fixed order, so the same statistics everywhere; workgroup 0 stores them), then
 // normalizes its rows: obs / reward / terminal obs, returns[done] = 0, Monitor sums.
@@ -125,7 +141,8 @@ __global__ void __launch_bounds__(kVnThreads) vn_apply_kernel(VnArgs a) {
     const bool upd_ret = a.training && !a.reset;
     const int t = threadIdx.x;
     const bool resident = w.r1 - w.r0 <= kVnChunk;
-    // the rows' loads first: they are in flight while the partials are merged
+    // the rows' loads first -- obs, and the row's reward, done flag and Monitor sums: they
+    // are all in flight while the partials are merged (one memory round trip per launch)
     float xr[kD];
     const int nres = resident ? (int)(w.r1 - w.r0) * kD : 0;
     const float* src = a.obs + w.r0 * kD;
@@ -134,6 +151,9 @@ __global__ void __launch_bounds__(kVnThreads) vn_apply_kernel(VnArgs a) {
         const int k = t + q * kVnThreads;
         xr[q] = k < nres ? src[k] : 0.0f;
     }
+    RowIn pin = {};
+    const bool prow = resident && !a.reset && t < (int)(w.r1 - w.r0);
+    if (prow) pin = row_in(a, w.r0 + t);
     if (a.upd_obs || upd_ret) {
         const double* P = a.part + t;
         const bool has = t < a.blocks;
@@ -179,13 +199,13 @@ __global__ void __launch_bounds__(kVnThreads) vn_apply_kernel(VnArgs a) {
         __syncthreads();
     }
     // the rows' own work (reward, returns, terminal obs, Monitor): thread t, row r0 + t
-    auto row_work = [&](int64_t r) {
+    auto row_work = [&](int64_t r, const RowIn& in) {
         if (a.reset) {
             a.returns[r] = 0.0;
             return;
         }
-        const bool dn = a.done ? a.done[r] != 0 : false;
-        const float rw = a.reward[r];
+        const bool dn = in.dn;
+        const float rw = in.rw;
         a.rew_out[r] = a.norm_reward ? (float)clipd((double)rw * srinv, -a.clip_rew, a.clip_rew) : rw;
         if (dn && a.tobs && a.tobs_out) {   // rare: per-row accesses
 #pragma unroll
@@ -197,8 +217,8 @@ __global__ void __launch_bounds__(kVnThreads) vn_apply_kernel(VnArgs a) {
         }
         if (dn) a.returns[r] = 0.0;   // self.returns[dones] = 0
         if (a.ep_ret) {                 // Monitor: sum(rewards), len(rewards)
-            const double er = a.ep_ret[r] + (double)rw;
-            const int32_t el = a.ep_len[r] + 1;
+            const double er = in.er + (double)rw;
+            const int32_t el = in.el + 1;
             if (dn) {
                 a.ep_ret_done[r] = er;
                 a.ep_len_done[r] = el;
@@ -220,7 +240,7 @@ __global__ void __launch_bounds__(kVnThreads) vn_apply_kernel(VnArgs a) {
                                     : xr[q];
             }
         }
-        if (t < (int)(w.r1 - w.r0)) row_work(w.r0 + t);
+        if (t < (int)(w.r1 - w.r0)) row_work(w.r0 + t, pin);
         return;
     }
     for (int64_t c0 = w.r0; c0 < w.r1; c0 += kVnChunk) {
@@ -235,7 +255,7 @@ __global__ void __launch_bounds__(kVnThreads) vn_apply_kernel(VnArgs a) {
                     tile[t * kD + c] = (float)clipd(((double)x - snorm[c][0]) * snorm[c][1], -a.clip_obs, a.clip_obs);
                 }
             }
-            row_work(c0 + t);
+            row_work(c0 + t, a.reset ? RowIn{} : row_in(a, c0 + t));
         }
         __syncthreads();
         float* dst = a.obs_out + c0 * kD;

@@ -76,10 +76,24 @@ __device__ __forceinline__ void load_tile(float* tile, const float* obs, int64_t
     __syncthreads();
 }
 
-// The moments of workgroup `bid`'s rows (blockDim.x == kVnThreads).
-__device__ __forceinline__ void moments_body(const MomentsArgs& a, int bid) {
+// The block sum of a workgroup's moments v, stored as its partial (+ workgroup 0: the
+// snapshot of the old statistics and of the shifts).
+__device__ __forceinline__ void store_partial(const MomentsArgs& a, int bid, const double* v, const double* sft,
+                                             int64_t rows) {
     __shared__ double sh[kVnThreads * (kPart + 1)];
     __shared__ double ssum[kPart];
+    const int t = threadIdx.x;
+    block_sum<kPart - 1>(v, sh, ssum);
+    double* part = a.part + bid;
+    if (t < kPart - 1) part[(1 + t) * kVnMaxBlocks] = ssum[t];
+    if (t == 0) part[0] = (double)rows;
+    double* snap = a.part + kVnMaxBlocks * kPart;
+    if (bid == 0 && t < 2 * kD + 4) snap[t] = a.stats[t];
+    if (bid == 0 && t <= kD) snap[2 * kD + 4 + t] = sft[t];
+}
+
+// The moments of workgroup `bid`'s rows (blockDim.x == kVnThreads).
+__device__ __forceinline__ void moments_body(const MomentsArgs& a, int bid) {
     __shared__ float tile[kVnChunk * kD];
     const int64_t r0 = (int64_t)bid * a.rows_per_block;
     const int64_t r1 = (r0 + a.rows_per_block < a.n) ? r0 + a.rows_per_block : a.n;
@@ -114,13 +128,47 @@ __device__ __forceinline__ void moments_body(const MomentsArgs& a, int bid) {
         }
         __syncthreads();
     }
-    block_sum<kPart - 1>(v, sh, ssum);
-    double* part = a.part + bid;
-    if (t < kPart - 1) part[(1 + t) * kVnMaxBlocks] = ssum[t];
-    if (t == 0) part[0] = (double)(r1 > r0 ? r1 - r0 : 0);
-    double* snap = a.part + kVnMaxBlocks * kPart;
-    if (bid == 0 && t < 2 * kD + 4) snap[t] = a.stats[t];
-    if (bid == 0 && t <= kD) snap[2 * kD + 4 + t] = sft[t];
+    store_partial(a, bid, v, sft, r1 > r0 ? r1 - r0 : 0);
+}
+
+// The same moments from rows already in LDS (step1_vn_kernel: the he_step workgroup's obs
+// staging tile, row t at tile + t * kD, after a workgroup barrier), the thread's reward
+// `rew` (its row r0 + t) and its running return before the update `ret_prev`: the same
+// operations on the same values as moments_body, with no global round trip.  Obs shift:
+// the old running mean (a.shift_mean).
+// sft: the shifts (the old running means of the obs columns and of the returns), loaded by
+// the caller before its step so they are not a round trip here.
+__device__ __forceinline__ void load_mean_shifts(const MomentsArgs& a, double* sft) {
+#pragma unroll
+    for (int c = 0; c < kD; ++c) sft[c] = a.stats[c];
+    sft[kD] = a.stats[2 * kD + 1];
+}
+__device__ __forceinline__ void moments_from_rows(const MomentsArgs& a, int bid, const float* tile, float rew,
+                                                  double ret_prev, const double* sft) {
+    const int64_t r0 = (int64_t)bid * a.rows_per_block;
+    const int64_t r1 = (r0 + a.rows_per_block < a.n) ? r0 + a.rows_per_block : a.n;
+    const int t = threadIdx.x;
+    double v[kPart - 1];
+#pragma unroll
+    for (int c = 0; c < kPart - 1; ++c) v[c] = 0.0;
+    if (t < (int)(r1 - r0)) {
+        if (a.upd_obs) {
+#pragma unroll
+            for (int c = 0; c < kD; ++c) {
+                const double d = (double)tile[t * kD + c] - sft[c];
+                v[c] += d;
+                v[kD + 1 + c] += d * d;
+            }
+        }
+        if (a.upd_ret) {
+            const double ret = ret_prev * a.gamma + (double)rew;   // VecNormalize._update_reward
+            a.returns[r0 + t] = ret;
+            const double d = ret - sft[kD];
+            v[kD] += d;
+            v[2 * kD + 1] += d * d;
+        }
+    }
+    store_partial(a, bid, v, sft, r1 > r0 ? r1 - r0 : 0);
 }
 
 }  // namespace vn

@@ -3,7 +3,7 @@
 
     CANTORRL_HEDGEENV_LIB=tools/abt/timing.so python tools/lds_timing.py [n_envs] [K] [bench config]
 
-Roles: 0 reward stepper, 1 obs stepper, 2-3 producers.  For each: mean cycles from the
+Roles: 0 reward stepper, 1 obs stepper, 2-3 producers (replay, config 6: the loaders).  For each: mean cycles from the
 first barrier to the end and the share of them spent waiting in barriers (s_memtime).
 """
 import ctypes
@@ -20,7 +20,12 @@ from cantorrl_amd.vec_env import HedgingVecEnv  # noqa: E402
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
 K = int(sys.argv[2]) if len(sys.argv) > 2 else 256
 cfg = bench.CONFIGS[int(sys.argv[3]) if len(sys.argv) > 3 else 2]
-env = HedgingVecEnv(n, mode=cfg["mode"], generate=cfg["gen"], seed=42, return_numpy=False, info_keys=(), **cfg["kw"])
+if cfg["mode"] == "replay":  # lds_replay_kernel: roles 2-3 are the loader waves
+    env = HedgingVecEnv(n, tables=bench.replay_tables(**cfg["table"]), seed=42, return_numpy=False, info_keys=(),
+                        **cfg["kw"])
+else:
+    env = HedgingVecEnv(n, mode=cfg["mode"], generate=cfg["gen"], seed=42, return_numpy=False, info_keys=(),
+                        **cfg["kw"])
 env.reset_tensors()
 acts = torch.rand((K, n, 2), device="cuda") * 2 - 1
 for _ in range(4):
