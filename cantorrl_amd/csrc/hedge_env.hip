@@ -2115,6 +2115,40 @@ __device__ __forceinline__ void flush_obs_full(const float* img, float* out, int
 // different outstanding memory ops.  (A copy of a pending load's register at a merge,
 // e.g. the action ring at a loop back-edge behind a `break`, costs an s_waitcnt
 // vmcnt(0): every store of the wave drained.)  A partial last block takes a generic loop.
+#ifndef HE_LDS_PIN
+// A/B: the generic steppers' and the Heston / book producers' hot Params fields pinned in SGPRs
+// (scalar loads in the config 5 kernel 406 -> 75, SGPR spills to VGPR lanes 173 -> 1,066).
+// Same-box A/B (r03s16, two runs each): config 5 2,041 / 2,053 -> 2,126 / 2,128 us per launch,
+// config 4 8,863 / 8,878 -> 8,770 / 8,833: the reloads were not what holds those kernels back.
+#define HE_LDS_PIN 0
+#endif
+// Opaque copies of the Params fields a step / a market block reads in its loop (see HE_LDS_PIN).
+__device__ __forceinline__ void pin_step_consts(Params& q, bool obs) {
+    asm volatile("" : "+s"(q.mt_f), "+s"(q.mt), "+s"(q.maxh), "+s"(q.T), "+s"(q.var_f));
+    if (obs) {
+        asm volatile("" : "+s"(q.maxh_f), "+s"(q.inv_maxh_f), "+s"(q.T_f), "+s"(q.inv_T_f), "+s"(q.s0s_d),
+                     "+s"(q.inv_s0s_d));
+#pragma unroll
+        for (int c = 0; c < 4 + kObs; ++c) asm volatile("" : "+s"(q.rstv[c]));
+    } else {
+        asm volatile("" : "+s"(q.tcpc), "+s"(q.slip_frac), "+s"(q.shares_f), "+s"(q.shares_d), "+s"(q.inv_shares),
+                     "+s"(q.den), "+s"(q.inv_den));
+        asm volatile("" : "+s"(q.w), "+s"(q.lam), "+s"(q.theta), "+s"(q.inv_252), "+s"(q.initial_cash),
+                     "+s"(q.init_cash_f));
+    }
+}
+__device__ __forceinline__ void pin_market_consts(Params& q, bool heston, bool book) {
+    asm volatile("" : "+s"(q.key0), "+s"(q.key1), "+s"(q.sqrt_dt), "+s"(q.s0), "+s"(q.var), "+s"(q.r_d));
+    asm volatile("" : "+s"(q.sqrt_tenor), "+s"(q.tenor_d), "+s"(q.bs.disc));
+    if (heston) {
+        asm volatile("" : "+s"(q.h_rho), "+s"(q.h_sqrt1mrho2), "+s"(q.h_kappa), "+s"(q.h_theta), "+s"(q.h_xi),
+                     "+s"(q.mu), "+s"(q.dt));
+    } else {
+        asm volatile("" : "+s"(q.drift), "+s"(q.sqrt_var));
+    }
+    if (book) asm volatile("" : "+s"(q.dt), "+s"(q.book_n));
+}
+
 template <int MODE, bool BOOK, bool LEAN, bool OBS>
 __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& io, int k_steps, const Market& cur,
                                             LdsMarketT<MODE, BOOK, LEAN>& L, int64_t base) {
@@ -2411,6 +2445,15 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
             });
         }
     } else {
+#if HE_LDS_PIN
+        // the generic steps' per-handle constants, copied once and pinned in SGPRs (opaque):
+        // the kernel is built without MachineLICM, so left to the Params reads every step
+        // re-loads them from the scalar cache, each load's lgkmcnt(0) wait draining the step's
+        // LDS reads too (config 5: 406 scalar loads in the kernel's code)
+        Params pq = p;
+        pin_step_consts(pq, OBS);
+        const Params& p = pq;
+#endif
         if (OBS && e.t != 0) pre = Mkt{(float)cur.S[i], HESTON ? (float)cur.v[i] : p.var_f, cur.C[i], cur.P[i], 0.0};
         auto step = [&](int buf, int sl, int k, float2 ak) {
             const int64_t koff = (int64_t)k * N;
@@ -2473,10 +2516,18 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
 // block bp - 1.  pw = producer wave index (kLdsPEnvs envs each).  Lanes past the last
 // env mirror env N-1 like the steppers' (identical values, identical addresses).
 template <int MODE, bool BOOK, bool LEAN>
-__device__ __forceinline__ void lds_producer(const Params& p, int k_steps, const Market& cur,
+__device__ __forceinline__ void lds_producer(const Params& pp, int k_steps, const Market& cur,
                                              LdsMarketT<MODE, BOOK, LEAN>& W, int64_t base, int pw) {
     using G = LdsGeom<MODE, BOOK>;
     constexpr bool HESTON = G::HESTON;
+#if HE_LDS_PIN
+    // Heston / a book (the producer-bound kernels): the market constants pinned (HE_LDS_PIN)
+    Params pq = pp;
+    if constexpr (HESTON || BOOK) pin_market_consts(pq, HESTON, BOOK);
+    const Params& p = (HESTON || BOOK) ? pq : pp;
+#else
+    const Params& p = pp;
+#endif
     constexpr int kLdsLanes = G::lanes, kLdsPEnvs = G::penvs, kLdsH = G::H;
     const int lane = threadIdx.x & 63;
     const int sub = lane / kLdsPEnvs;
@@ -2841,9 +2892,12 @@ __device__ __forceinline__ int lds_role(int wave) {
 // fewer than the occupancy API and the compiler report (MI355X_MICROARCH.md, Residency),
 // and at 106 the 4 x 6 waves of 4 workgroups no longer fit a CU -- at 65,536 envs the
 // launch ran in two rounds of workgroups (536 vs ~270 us).  The spills go to VGPR lanes.
+#ifndef HE_LDS_NUM_SGPR
+#define HE_LDS_NUM_SGPR 96
+#endif
 template <int MODE, bool BOOK, bool LEAN>
 __global__ __launch_bounds__((LdsGeom<MODE, BOOK>::threads), (LdsGeom<MODE, BOOK>::minwaves))
-    __attribute__((amdgpu_num_sgpr(96))) void lds_rollout_kernel(const Params* __restrict__ pc, State s, Io io,
+    __attribute__((amdgpu_num_sgpr(HE_LDS_NUM_SGPR))) void lds_rollout_kernel(const Params* __restrict__ pc, State s, Io io,
                                                                  int k_steps, Market cur) {
     __shared__ __attribute__((aligned(16))) LdsMarketT<MODE, BOOK, LEAN> lm;
     const Params& p = *pc;  // read through the scalar cache (a by-value copy spills)
@@ -3059,6 +3113,23 @@ __device__ __forceinline__ void lds_replay_stepper(const Params& p, State s, con
     float2 ra[D];
 #pragma unroll
     for (int d = 0; d < D; ++d) ra[d] = ld2(gact, (int64_t)(d < k_steps ? d : k_steps - 1) * N + i);
+    // FAST: the per-handle constants of the step held in VGPRs (opaque).  Left to step_env's
+    // Params reads, the SGPR-capped kernel re-loads them from the scalar cache inside every
+    // step, and each such load's lgkmcnt(0) wait also drains the step's LDS reads.
+    float c_mt_f = p.mt_f, c_shares_f = p.shares_f, c_init_cash_f = p.init_cash_f;
+    float c_maxh_f = p.maxh_f, c_inv_maxh_f = p.inv_maxh_f, c_T_f = p.T_f, c_inv_T_f = p.inv_T_f;
+    int32_t c_mt = p.mt, c_maxh = p.maxh;
+    double c_tcpc = p.tcpc, c_slip = p.slip_frac, c_lam = p.lam, c_w = p.w, c_theta = p.theta;
+    double c_shares_d = p.shares_d, c_inv_252 = p.inv_252, c_init_cash = p.initial_cash;
+    if (FAST) {
+        asm volatile("" : "+v"(c_mt_f), "+v"(c_mt), "+v"(c_maxh));
+        if (OBS) {
+            asm volatile("" : "+v"(c_maxh_f), "+v"(c_inv_maxh_f), "+v"(c_T_f), "+v"(c_inv_T_f));
+        } else {
+            asm volatile("" : "+v"(c_shares_f), "+v"(c_init_cash_f), "+v"(c_tcpc), "+v"(c_slip), "+v"(c_lam));
+            asm volatile("" : "+v"(c_w), "+v"(c_theta), "+v"(c_shares_d), "+v"(c_inv_252), "+v"(c_init_cash));
+        }
+    }
 
     // the obs stepper's new episode for the envs ending at this step (a wave-uniform branch,
     // taken in a block where some lane's episode ends): env_reset_common + the new path's S0
@@ -3096,14 +3167,30 @@ __device__ __forceinline__ void lds_replay_stepper(const Params& p, State s, con
             const float2 gd = L.gd[buf][sl][lane];
             const float4 g = make_float4(gd.x, L.gg[buf][sl][lane], gd.y, lag_return(post.S, pre.S));
             // (i)-(ii) of step_env: the integer trade logic (:181-200)
-            const int32_t nc = e.call + trade_round(ak.x * p.mt_f, p.mt);
-            const int32_t nq = e.put + trade_round(ak.y * p.mt_f, p.mt);
-            e.call = nc < -p.maxh ? -p.maxh : (nc > p.maxh ? p.maxh : nc);
-            e.put = nq < -p.maxh ? -p.maxh : (nq > p.maxh ? p.maxh : nq);
+            const int32_t nc = e.call + trade_round(ak.x * c_mt_f, c_mt);
+            const int32_t nq = e.put + trade_round(ak.y * c_mt_f, c_mt);
+            e.call = nc < -c_maxh ? -c_maxh : (nc > c_maxh ? c_maxh : nc);
+            e.put = nq < -c_maxh ? -c_maxh : (nq > c_maxh ? c_maxh : nq);
             e.t = e.t + 1;
             const bool term = (int32_t)e.t >= T;
             float o[kObs];
-            make_obs<FAST, true>(p, e, post, g, pre.S, pre.v, o);
+            if (FAST) {  // make_obs<true, true> on the pinned constants (hedging_env_v2.py:109-143)
+                o[0] = div_f32_by(post.S, e.s0s_d, e.inv_s0s_d);
+                o[1] = div_f32_by(post.C, e.s0s_d, e.inv_s0s_d);
+                o[2] = div_f32_by(post.P, e.s0s_d, e.inv_s0s_d);
+                o[3] = div_int_byf((float)e.call, c_maxh_f, c_inv_maxh_f);
+                o[4] = div_int_byf((float)e.put, c_maxh_f, c_inv_maxh_f);
+                o[5] = post.v;
+                o[6] = div_int_byf((float)(T - (int32_t)e.t), c_T_f, c_inv_T_f);
+                o[7] = g.x;
+                o[8] = g.y;
+                o[9] = g.z;
+                o[10] = g.y;
+                o[11] = g.w;  // e.t >= 1 after a step
+                o[12] = (pre.S == 0.0f) ? 0.0f : np_clipf(post.v - pre.v, -1.0f, 1.0f);
+            } else {
+                make_obs<FAST, true>(p, e, post, g, pre.S, pre.v, o);
+            }
             pre = post;
             new_episode_obs(buf, term, o);  // SB3 autoreset: the reset obs
             float* const tile = L.stage[k & 1];
@@ -3114,10 +3201,45 @@ __device__ __forceinline__ void lds_replay_stepper(const Params& p, State s, con
             else flush_obs_wave(tile, out, base, wrows, lane);
         } else {
             StepOut so;
-            step_env<false, FAST, true>(p, e, pre, post, ak.x, ak.y, pv_last, so);
+            if (FAST) {  // step_env<false, true, true> on the pinned constants (hedging_env_v2.py:175-262)
+                const float pv0 = (c_shares_f * pre.S + 0.0f) + c_init_cash_f;  // f32 (:167-168)
+                const double pv_prev = (e.t == 0) ? (double)pv0 : pv_last;
+                const int32_t nc = e.call + trade_round(ak.x * c_mt_f, c_mt);
+                const int32_t nq = e.put + trade_round(ak.y * c_mt_f, c_mt);
+                const int32_t cc = nc < -c_maxh ? -c_maxh : (nc > c_maxh ? c_maxh : nc);
+                const int32_t qq = nq < -c_maxh ? -c_maxh : (nq > c_maxh ? c_maxh : nq);
+                const int32_t dc = cc - e.call, dp = qq - e.put;
+                const int32_t adc = dc < 0 ? -dc : dc, adp = dp < 0 ? -dp : dp;
+                const double commission = (double)(adc + adp) * c_tcpc;
+                const double slc = (((double)adc * (double)pre.C) * 100.0) * c_slip;
+                const double slp = (((double)adp * (double)pre.P) * 100.0) * c_slip;
+                so.tc = commission + (slc + slp);
+                e.cash = e.cash - so.tc;
+                e.call = cc;
+                e.put = qq;
+                e.t = e.t + 1;
+                so.term = (int32_t)e.t >= T;
+                const double optv = ((double)cc * (double)post.C) * 100.0 + ((double)qq * (double)post.P) * 100.0;
+                so.pv = ((double)(c_shares_f * post.S) + optv) + e.cash;
+                so.pnl = so.pv - pv_prev;
+#if defined(HE_REPLAY_DIAG) && HE_REPLAY_DIAG == 4  // diagnostic build: reciprocal multiplies, not divisions
+                const double ps = so.pnl * c_inv_252;
+                const double rpc = (-c_w) * (fabs(ps) * c_inv_252);
+#else
+                const double ps = so.pnl / c_shares_d;
+                const double rpc = (-c_w) * (fabs(ps) / e.den);
+#endif
+                const double tcp = c_lam * so.tc;
+                const double thp = c_theta * div_int_by((double)(T - (int32_t)e.t), 252.0, c_inv_252);
+                so.reward = (rpc - tcp) - thp;
+            } else {
+                step_env<false, FAST, true>(p, e, pre, post, ak.x, ak.y, pv_last, so);
+            }
             pv_last = so.pv;
+#if !(defined(HE_REPLAY_DIAG) && HE_REPLAY_DIAG == 3)  // diagnostic build: no reward / done stores
             grew[koff + i] = (float)so.reward;
             gterm[koff + i] = so.term ? 1 : 0;
+#endif
             const double a0 = sm0 + so.reward, a1 = sm1 + so.pnl, a2 = sm2 + so.tc;
             const uint32_t n1 = slen + 1u;
             float f0 = (float)a0, f1 = (float)a1, f2 = (float)a2, f3 = (float)n1;
@@ -3139,7 +3261,7 @@ __device__ __forceinline__ void lds_replay_stepper(const Params& p, State s, con
             e.t = tm ? 0u : e.t;
             e.call = tm ? 0 : e.call;
             e.put = tm ? 0 : e.put;
-            e.cash = tm ? p.initial_cash : e.cash;
+            e.cash = tm ? c_init_cash : e.cash;
             e.den = tm ? den0 : e.den;
             pre.S = tm ? r0.x : post.S;
             pre.v = tm ? r0.y : post.v;
@@ -3158,9 +3280,13 @@ __device__ __forceinline__ void lds_replay_stepper(const Params& p, State s, con
 #pragma unroll
             for (int sl = 0; sl < kLdsM; ++sl) {
                 const int k = b * kLdsM + sl;
+#if defined(HE_REPLAY_DIAG) && HE_REPLAY_DIAG == 5  // diagnostic build: no action loads
+                const float2 ak = make_float2(0.3f * (float)(sl - 4), -0.2f);
+#else
                 const float2 ak = ra[sl % D];
                 const int kn = k + D;
                 ra[sl % D] = ld2(gact, (int64_t)(kn < k_steps ? kn : k_steps - 1) * N + i);
+#endif
                 step(buf, sl, k, ak, full);
             }
             LDS_BAR();  // buffer b & 1 handed back, block b + 1 loaded
@@ -3195,7 +3321,7 @@ __device__ __forceinline__ void lds_replay_stepper(const Params& p, State s, con
 }
 
 template <bool FAST>
-__global__ __launch_bounds__(256, 4) __attribute__((amdgpu_num_sgpr(96))) void lds_replay_kernel(
+__global__ __launch_bounds__(256, 4) __attribute__((amdgpu_num_sgpr(HE_LDS_NUM_SGPR))) void lds_replay_kernel(
     const Params* __restrict__ pc, State s, Io io, int k_steps) {
     __shared__ __attribute__((aligned(16))) LdsReplay lm;
     const Params& p = *pc;

@@ -36,4 +36,9 @@ for t in timing timing_pwswap timing_lagp1; do
   CANTORRL_HEDGEENV_LIB=$R/tools/abt/$t.so timeout -k 10 120 python tools/lds_timing.py 65536 256 > $O/role2_$t.log 2>&1 || { tail -5 $O/role2_$t.log; exit 1; }
   grep -v amdgpu.ids $O/role2_$t.log
 done
+echo "[$(date +%T)] kernarg preload build: parity + Gym-API A/B"
+CANTORRL_HEDGEENV_LIB=$R/tools/ab/kpre.so timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_single_env.py -m gpu -x -q -k "replay_matches or gbm_matches or single_env or closed_loop" --timeout 200 --timeout-method thread > $O/pytest_kpre.log 2>&1 \
+  || { echo "kpre parity failed"; grep -E "FAIL|Error|assert" $O/pytest_kpre.log | head -30; tail -40 $O/pytest_kpre.log; exit 1; }
+tail -1 $O/pytest_kpre.log
+bash tools/gpu/ab_graph.sh $TAG kpre || exit 1
 echo "[$(date +%T)] done"
