@@ -72,6 +72,10 @@ STEP_BYTES_PER_ENV = {"gbm": 134, "gbm_step": 122, "heston": 146,
 # state (t, pos, cash) read + written 32, path + S0 read 8, the pre-step row 16.  SURVEY 8(d)
 # prices replay at its generate-mode figure + the 16-B gather of S, v, C, P at t + 1.
 REPLAY_ROLLOUT_B, REPLAY_STATE_B, SURVEY_REPLAY_GATHER_B = 97, 56, 16
+# lds_replay_kernel: per env-step action 8 + the row's {S, v, C, P} 16 (its greeks are evaluated
+# on chip) + obs 52 + reward 4 + terminated 1; per launch the state above + the episode sums
+# (44 r+w) + the loaders' PCG64 words (40 r+w) and path / S0 written
+LDS_REPLAY_STEP_B, LDS_REPLAY_STATE_B = 81, 56 + 88 + 80 + 8
 ROLLOUT_BYTES_PER_ENV = {"gbm": 89, "gbm_step": 77, "heston": 97}
 ROLLOUT_STATE_BYTES = {"gbm": 44, "gbm_step": 44, "heston": 48}
 # market_kernel per env-step: tile records written; per env and block: the block-start
@@ -447,7 +451,7 @@ def probe(args):
     env.close()
 
 
-STEP_KERNELS = r"step1?_kernel|step_market_kernel|lds_rollout_kernel"
+STEP_KERNELS = r"step1?_kernel|step_market_kernel|lds_rollout_kernel|lds_replay_kernel"
 
 
 def pmc_pass(args, counters, kernels=STEP_KERNELS):
@@ -672,6 +676,7 @@ def roofline(mode, n, kern_ms, rk, book=False, market="gbm", lds=False):
             survey = n * (rk * (SURVEY_ROLLOUT_B + SURVEY_REPLAY_GATHER_B) + SURVEY_ROLLOUT_STATE_B)
             own = n * (rk * REPLAY_ROLLOUT_B + REPLAY_STATE_B)
             if os.environ.get("HE_LDS_ROLLOUT", "1") != "0":
+                own = n * (rk * LDS_REPLAY_STEP_B + LDS_REPLAY_STATE_B)
                 kname = ("lds_replay_kernel (he_rollout, replay, K=%d fused steps; a loader wave stages each "
                          "env's path rows in LDS one block ahead of the steppers)" % rk)
             else:
@@ -1008,7 +1013,7 @@ def main(argv=None):
         # rate against the bound of its f64 mix, and its f64 FLOP rate at the live duration
         dom = max(valu[0], key=lambda k: valu[0][k]["cycles_profiled"])
         v = dict(valu[0][dom])
-        if dom == "lds_rollout_kernel" or (dom.startswith("step") and "market" not in dom):
+        if dom in ("lds_rollout_kernel", "lds_replay_kernel") or (dom.startswith("step") and "market" not in dom):
             v["f64_tflops"] = round(v["f64_flop"] / (kern_ms * 1e-3) / 1e12, 3)
             v["f64_frac_of_vector_peak"] = round(v["f64_tflops"] / FP64_VECTOR_PEAK_TFLOPS, 4)
         roof["valu"] = dict(kernel=dom, peak_f64_tflops=FP64_VECTOR_PEAK_TFLOPS, **v)

@@ -331,7 +331,7 @@ __device__ __forceinline__ float4 greeks(const Params& p, float S, float v) {
 // taken as -N(-d1) (no cancellation), 1/(S sigma sqrt T) through v_rcp_f32.  Within
 // 4 f32 ulp of the reference's f64 values (tests: OBS_RTOL 1e-6 on columns 7-10) at
 // about a third of the cost of the f64 chain (measured: greeks were 32% of
-// market_kernel).  Replay tables and the reset obs keep greeks().
+// market_kernel).  Replay tables and the reset obs keep greeks() (replay_greeks).
 template <bool CONST_VAR>
 __device__ __forceinline__ float4 greeks_fast(const Params& p, float S, float v) {
     float cd, gam, pd;
@@ -386,6 +386,22 @@ __device__ __forceinline__ float4 greeks_fast(const Params& p, float S, float v)
 // normal (lds_lean_config), so the uniform branches are gone, and the S <= 1e-6 case is
 // a select over the main path's result (which it computes for every lane) instead of a
 // divergent if/else.  Same operations and operands, so the same bits as greeks_fast<true>.
+// The obs greeks of a replay row (table_greeks_kernel at load, the replay LDS loaders per
+// row): greeks(), the reference's f64 chain.  HE_REPLAY_GREEKS_FAST=1 (A/B): greeks_fast at
+// the row's own variance, as Heston's generate mode (within 4 f32 ulp, parity green) --
+// the loaders' busy cycles drop (1,650 -> 1,580 per step) but config 6 does not move (418 /
+// 420 against 416 / 418 us per launch, r03s18): the loaders are not its critical wave.
+#ifndef HE_REPLAY_GREEKS_FAST
+#define HE_REPLAY_GREEKS_FAST 0
+#endif
+__device__ __forceinline__ float4 replay_greeks(const Params& p, float S, float v) {
+#if HE_REPLAY_GREEKS_FAST
+    return greeks_fast<false>(p, S, v);
+#else
+    return greeks<false>(p, S, v);
+#endif
+}
+
 __device__ __forceinline__ float4 greeks_lean(float S, float num_drift, float inv_sst_f, float sstf) {
     const float K = rintf(S);
     const float Kc = np_maxf(K, 1e-6f);
@@ -1090,7 +1106,7 @@ __global__ __launch_bounds__(kBlock) void table_greeks_kernel(Params p, float4* 
     int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (k >= count) return;
     float4 r = p.rec[k];
-    float4 g = p.record_metrics ? greeks<false>(p, r.x, r.y) : make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 g = p.record_metrics ? replay_greeks(p, r.x, r.y) : make_float4(0.f, 0.f, 0.f, 0.f);
     // row t >= 1 is stepped into from row t-1 of the same path; row 0 is only a reset obs
     const int64_t t = k % (int64_t)(p.T + 1);
     g.w = (t == 0) ? 0.0f : lag_return(r.x, p.rec[k - 1].x);
@@ -3025,7 +3041,7 @@ __device__ __forceinline__ void lds_replay_loader(const Params& p, State s, int 
                 if (sl < len) {
 #if HE_REPLAY_LGREEKS && !(defined(HE_REPLAY_DIAG) && HE_REPLAY_DIAG == 1)
                     // table_greeks_kernel's record, here from the row itself
-                    B[h] = p.record_metrics ? greeks<false>(p, A[h].x, A[h].y) : make_float4(0.f, 0.f, 0.f, 0.f);
+                    B[h] = p.record_metrics ? replay_greeks(p, A[h].x, A[h].y) : make_float4(0.f, 0.f, 0.f, 0.f);
 #endif
                     L.mk[wb][sl][lane] = A[h];
                     L.gd[wb][sl][lane] = make_float2(B[h].x, B[h].z);

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round measurements.  Phase "tests": the whole -m gpu suite + smoke().  Phase "bench":
 # the headline bench line (PMC traffic + CPU baseline + step API), the same command under
-# rocprofv3 --kernel-trace --stats, configs 3-5, and the 2-rank rehearsal of the --gpus N
+# rocprofv3 --kernel-trace --stats (and config 6's), configs 3-6, and the 2-rank rehearsal of the --gpus N
 # launcher (gloo collectives, both ranks on this box's one GPU).
 #   gpurun --timeout 1200 -- bash tools/gpu/round.sh <tag> tests|bench
 set -o pipefail
@@ -25,9 +25,15 @@ cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 $R/bench.py --no-pmc --no-cpu-baseline --no-step-api > $O/bench_rocprof.log 2>&1 || { tail -20 $O/bench_rocprof.log; exit 1; }
 cd $R
 grep "^{" $O/bench_rocprof.log > $O/bench_under_rocprof.jsonl
-for c in 3 4 5; do
+python3 tools/kstats.py $O/prof | head -4
+echo "[$(date +%T)] config 6 under rocprofv3 --kernel-trace --stats"
+cd /tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof6 -o run -- python3 $R/bench.py --config 6 --no-pmc --no-cpu-baseline --no-step-api > $O/bench6_rocprof.log 2>&1 || { tail -20 $O/bench6_rocprof.log; exit 1; }
+cd $R
+python3 tools/kstats.py $O/prof6 | head -4
+for c in 3 4 5 6; do
   echo "[$(date +%T)] bench config $c"
-  # configs 4 and 5 (book / Heston: producer-bound) with the PMC passes: traffic + VALU issue
+  # configs 4, 5 (book / Heston: producer-bound) and 6 (replay) with the PMC passes: traffic + VALU issue
   pmc=--no-pmc; [ $c != 3 ] && pmc=""
   timeout -k 10 400 python -u bench.py --config $c $pmc --no-cpu-baseline --no-step-api > $O/b_cfg$c.log 2>&1 || { tail -20 $O/b_cfg$c.log; exit 1; }
   grep "^{" $O/b_cfg$c.log >> $O/bench_cfg345.jsonl
