@@ -2578,6 +2578,13 @@ __device__ __forceinline__ void lds_producer(const Params& pp, int k_steps, cons
         LDS_BAR();  // diagnostic build: the producers only keep the barrier count
         continue;
 #endif
+#ifdef HE_LDS_PROD_ALT
+        // A/B: the producer waves alternate between priority 1 and 2 by block, so the SIMD's
+        // arbitration between two producers of different workgroups (the older one wins a
+        // tie) does not favour the same wave every block
+        if (((bp + pw) & 1) != 0) __builtin_amdgcn_s_setprio(HE_LDS_PRIO_PROD);
+        else __builtin_amdgcn_s_setprio(HE_LDS_PRIO_PROD + 1);
+#endif
         if (bp < nb) {
             const int kb = bp * kLdsM;
             const int len = (k_steps - kb) < kLdsM ? (k_steps - kb) : kLdsM;
@@ -2992,7 +2999,8 @@ __device__ __forceinline__ void lds_replay_loader(const Params& p, State s, int 
     g.buf32 = s.pcgb[N + i];
     float s0enc = s.s0[i];
     const int nb = (k_steps + kLdsM - 1) / kLdsM;
-    float4 A[H], B[H], R0, G0;
+    float4 A[H], B[H];
+    float4 R0 = make_float4(0.f, 0.f, 0.f, 0.f), G0 = R0;  // the new episode's row 0 (lanes ending in the block)
     int rsl = kLdsM;  // slot of the episode end in the issued block (kLdsM: none)
     // the loads of block bp from the position (path, t) before it; the position advanced past it
     auto issue = [&](int bp) {
@@ -3018,9 +3026,9 @@ __device__ __forceinline__ void lds_replay_loader(const Params& p, State s, int 
             if (!HE_REPLAY_LGREEKS) B[h] = ld4(recg, r);
 #endif
         }
-        if (part == 0) {
-            R0 = ld4(rec, rn);
-            G0 = ld4(recg, rn);
+        if (part == 0 && rsl < kLdsM) {  // lanes whose episode ends in the block (exec-masked:
+            R0 = ld4(rec, rn);           // the others fetch nothing -- loaded for every env, these
+            G0 = ld4(recg, rn);          // two 16-B records cost 2 lines per env and block)
         }
         if (rsl < kLdsM) {
             path = np;
