@@ -844,6 +844,49 @@ def test_lds_replay_equals_tile_replay(case, monkeypatch):
         assert torch.equal(_bits(a), _bits(b)), (case, i)
 
 
+def test_lds_replay_mixed_with_steps_resets_and_checkpoints(monkeypatch):
+    """Replay rollouts through lds_replay_kernel interleaved with he_step calls (the tile
+    step kernel continues from the state the loader and reward waves wrote: t, positions,
+    cash, path, S0, PCG64 words), a partial reset and a checkpoint restored into a fresh env
+    give exactly what the tile kernels give on the same sequence."""
+    from cantorrl_amd.vec_env import HedgingVecEnv
+    n, T = 700, 25
+    tables = _edge_tables(40, T + 1)
+    g = torch.Generator(device="cuda")
+    g.manual_seed(29)
+    acts = torch.rand((400, n, 2), device="cuda", generator=g) * 2.2 - 1.1
+    outs = []
+    for lds in ("1", "0"):
+        monkeypatch.setenv("HE_LDS_ROLLOUT", lds)
+        env = HedgingVecEnv(n, tables=tables, seed=13, return_numpy=False, info_keys=(), slippage_bps=2.0)
+        got = [env.reset_tensors().clone()]
+        a0 = 0
+        for kind, k in (("r", 64), ("r", 30), ("s", 5), ("r", 93), ("reset", 0), ("r", 17), ("ckpt", 0),
+                        ("r", 64), ("s", 2), ("r", 70)):
+            if kind == "r":
+                o, r, t = env.rollout(acts[a0:a0 + k].contiguous())
+                got += [o.clone(), r.clone(), t.clone()]
+                a0 += k
+            elif kind == "s":
+                for _ in range(k):
+                    o, r, t, _ = env.step_tensors(acts[a0], terminal_obs=False)
+                    got += [o.clone(), r.clone(), t.clone()]
+                    a0 += 1
+            elif kind == "reset":
+                got.append(env.reset_tensors(env_ids=[0, 5, 350, 699]).clone())
+            else:
+                blob = env.get_state()
+                env.close()
+                env = HedgingVecEnv(n, tables=tables, seed=13, return_numpy=False, info_keys=(), slippage_bps=2.0)
+                env.set_state(blob)
+        got.append(torch.from_numpy(env.get_state().copy()))
+        env.close()
+        outs.append(got)
+    assert len(outs[0]) == len(outs[1])
+    for i, (a, b) in enumerate(zip(*outs)):
+        assert torch.equal(_bits(a), _bits(b)), i
+
+
 @pytest.mark.parametrize("path", ["lds", "tile", "book", "book_tile"])
 def test_episode_summaries_match_oracle(path, monkeypatch):
     """he_episode_summaries (the per-env payload ranks all-gather): the
