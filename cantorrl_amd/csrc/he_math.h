@@ -448,6 +448,16 @@ HE_HD void bs_vectorized(double S, double K, double T, double r, double sigma, d
 // independent FMA chains to interleave instead of one dependent chain, and each f64
 // constant is materialised in SGPRs once per coefficient for NN FMAs instead of once per
 // FMA.  Used by the LDS producers, which evaluate several market slots per lane.
+// Whether any lane of the wave holds `c` (device; the host build is one lane).  The lockstep
+// fast paths below branch on it, so their common case is one straight-line block for the
+// whole wave instead of an exec-mask branch per lane group (the general path gives the same
+// bits for every lane, so which lanes take it does not matter).
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(HE_LOCK_LANEWISE)
+__device__ __forceinline__ bool he_any_lane(bool c) { return __ballot(c) != 0ull; }
+#else
+HE_HD bool he_any_lane(bool c) { return c; }
+#endif
+
 template <int NN>
 HE_HD void exp_k_n(const double* x, double* out) {
     double k[NN], r[NN], q[NN];
@@ -473,8 +483,14 @@ HE_HD void exp_k_n(const double* x, double* out) {
     for (int h = 0; h < NN; ++h) {
         const double s1 = 1.0 + r[h];
         const double e1 = (1.0 - s1) + r[h];
-        const double v = ldexp(s1 + fma(r[h] * r[h], q[h], e1), (int)k[h]);
-        out[h] = (fabs(x[h]) < 700.0) ? v : exp(x[h]);
+        out[h] = ldexp(s1 + fma(r[h] * r[h], q[h], e1), (int)k[h]);
+    }
+    bool big = false;
+#pragma unroll
+    for (int h = 0; h < NN; ++h) big = big || !(fabs(x[h]) < 700.0);
+    if (he_any_lane(big)) {   // |x| >= 700 / NaN somewhere in the wave: the library exp there
+#pragma unroll
+        for (int h = 0; h < NN; ++h) out[h] = (fabs(x[h]) < 700.0) ? out[h] : exp(x[h]);
     }
 }
 
@@ -559,7 +575,7 @@ HE_HD void box_muller_n(const double* u1, const double* u2, double* z1, double* 
 }
 
 // ndtr_pair over NN arguments: the |x| < 1/4 series lockstep when every argument of the
-// lane is there (rolling-ATM marks always are), else each through ndtr_pair.
+// wave is there (rolling-ATM marks always are), else each through ndtr_pair.
 template <int NN>
 HE_HD void ndtr_pair_n(const double* a, double* pos, double* neg) {
     const double SQRT1_2 = 0.70710678118654752440;
@@ -572,7 +588,7 @@ HE_HD void ndtr_pair_n(const double* a, double* pos, double* neg) {
         z[h] = x[h] * x[h];
         p[h] = 0.000001646211436588924740161296;
     }
-    if (!easy) {
+    if (he_any_lane(!easy)) {   // device: wave-uniform (a scalar branch; the lockstep path stays straight-line)
 #pragma unroll
         for (int h = 0; h < NN; ++h) ndtr_pair(a[h], pos + h, neg + h);
         return;
@@ -613,7 +629,7 @@ HE_HD void log_ratio_n(const double* S, const double* K, double* out) {
         easy = easy && (fabs(y[h]) < 0.0078125);
         p[h] = 1.0 / 9.0;
     }
-    if (!easy) {
+    if (he_any_lane(!easy)) {
 #pragma unroll
         for (int h = 0; h < NN; ++h) out[h] = log_ratio(S[h], K[h]);
         return;

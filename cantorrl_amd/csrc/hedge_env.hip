@@ -45,6 +45,24 @@ using namespace he;
 namespace {
 
 #define GLOBAL __attribute__((address_space(1)))
+// HE_OPAQUE_SEL (default): values a select picks from are pinned in VGPRs first, so the
+// backend keeps the select instead of a divergent branch around their computation.
+#ifndef HE_OPAQUE_SEL
+#define HE_OPAQUE_SEL 1
+#endif
+#ifndef HE_OBS_PIN
+#define HE_OBS_PIN(a) asm volatile("" : "+v"(a))
+#endif
+#ifndef HE_OPAQUE_ASM
+#define HE_OPAQUE_ASM asm volatile
+#endif
+#if HE_OPAQUE_SEL
+#define HE_OPAQUE1(a) HE_OPAQUE_ASM("" : "+v"(a))
+#define HE_OPAQUE3(a, b, c) HE_OPAQUE_ASM("" : "+v"(a), "+v"(b), "+v"(c))
+#else
+#define HE_OPAQUE1(a) do {} while (0)
+#define HE_OPAQUE3(a, b, c) do {} while (0)
+#endif
 typedef float v2f __attribute__((ext_vector_type(2)));
 typedef float v4f __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ float4 ld4(const GLOBAL v4f* p, int64_t k) {
@@ -382,10 +400,6 @@ __device__ __forceinline__ float4 greeks_fast(const Params& p, float S, float v)
     return make_float4(cd, gam, pd, 0.0f);
 }
 
-// greeks_fast<true> for the lean LDS obs stepper: the handle's sigma, tenor and sst are
-// normal (lds_lean_config), so the uniform branches are gone, and the S <= 1e-6 case is
-// a select over the main path's result (which it computes for every lane) instead of a
-// divergent if/else.  Same operations and operands, so the same bits as greeks_fast<true>.
 // The obs greeks of a replay row (table_greeks_kernel at load, the replay LDS loaders per
 // row): greeks(), the reference's f64 chain.  HE_REPLAY_GREEKS_FAST=1 (A/B): greeks_fast at
 // the row's own variance, as Heston's generate mode (within 4 f32 ulp, parity green) --
@@ -402,6 +416,13 @@ __device__ __forceinline__ float4 replay_greeks(const Params& p, float S, float 
 #endif
 }
 
+// greeks_fast<true> for the lean LDS obs stepper: the handle's sigma, tenor and sst are
+// normal (lds_lean_config), so the uniform branches are gone, and the S <= 1e-6 case is
+// a select over the main path's result (which it computes for every lane) instead of a
+// divergent if/else.  Same operations and operands, so the same bits as greeks_fast<true>.
+// The select operands are made opaque (asm): left alone, the backend turns the nested
+// constant selects and the gamma quotient into exec-mask branches -- five per step in the
+// obs stepper's block, which split the unrolled steps into separate basic blocks.
 __device__ __forceinline__ float4 greeks_lean(float S, float num_drift, float inv_sst_f, float sstf) {
     const float K = rintf(S);
     const float Kc = np_maxf(K, 1e-6f);
@@ -412,11 +433,14 @@ __device__ __forceinline__ float4 greeks_lean(float S, float num_drift, float in
     float cd = (x >= 0.0f) ? 1.0f - tail : tail;
     float pd = (x >= 0.0f) ? -tail : tail - 1.0f;
     const float gd = S * sstf;
-    float gam = (fabsf(gd) < 1e-9f) ? 0.0f
-                                    : (expf(-0.5f * (d1 * d1)) * 0.398942280401432678f) * __builtin_amdgcn_rcpf(gd);
+    float ge = (expf(-0.5f * (d1 * d1)) * 0.398942280401432678f) * __builtin_amdgcn_rcpf(gd);
+    float ct = (K == 0.0f) ? 0.5f : ((K > 0.0f) ? 0.0f : 1.0f);
+    float pt = (K == 0.0f) ? -0.5f : ((K < 0.0f) ? 0.0f : -1.0f);
+    HE_OPAQUE3(ge, ct, pt);
+    float gam = (fabsf(gd) < 1e-9f) ? 0.0f : ge;
     const bool tiny = S <= 1e-6f;  // weak python 1e-6 compares as float32(1e-6)
-    cd = tiny ? ((K == 0.0f) ? 0.5f : ((K > 0.0f) ? 0.0f : 1.0f)) : cd;
-    pd = tiny ? ((K == 0.0f) ? -0.5f : ((K < 0.0f) ? 0.0f : -1.0f)) : pd;
+    cd = tiny ? ct : cd;
+    pd = tiny ? pt : pd;
     gam = tiny ? 0.0f : gam;
     return make_float4(cd, gam, pd, 0.0f);
 }
@@ -441,14 +465,17 @@ __device__ __forceinline__ void greeks_lean_n(const float* S, float num_drift, f
 #pragma unroll
     for (int j = 0; j < NN; ++j) {
         const float gd = S[j] * sstf;
-        const float gm = (fabsf(gd) < 1e-9f)
-                             ? 0.0f
-                             : (expf(-0.5f * (d1[j] * d1[j])) * 0.398942280401432678f) * __builtin_amdgcn_rcpf(gd);
+        float ge = (expf(-0.5f * (d1[j] * d1[j])) * 0.398942280401432678f) * __builtin_amdgcn_rcpf(gd);
+        HE_OPAQUE1(ge);
+        const float gm = (fabsf(gd) < 1e-9f) ? 0.0f : ge;
         const bool tiny = S[j] <= 1e-6f;
         const float c = (x[j] >= 0.0f) ? 1.0f - tail[j] : tail[j];
         const float q = (x[j] >= 0.0f) ? -tail[j] : tail[j] - 1.0f;
-        cd[j] = tiny ? ((K[j] == 0.0f) ? 0.5f : ((K[j] > 0.0f) ? 0.0f : 1.0f)) : c;
-        pd[j] = tiny ? ((K[j] == 0.0f) ? -0.5f : ((K[j] < 0.0f) ? 0.0f : -1.0f)) : q;
+        float ct = (K[j] == 0.0f) ? 0.5f : ((K[j] > 0.0f) ? 0.0f : 1.0f);
+        float pt = (K[j] == 0.0f) ? -0.5f : ((K[j] < 0.0f) ? 0.0f : -1.0f);
+        HE_OPAQUE3(ct, pt, ge);
+        cd[j] = tiny ? ct : c;
+        pd[j] = tiny ? pt : q;
         gam[j] = tiny ? 0.0f : gm;
     }
 }
@@ -458,7 +485,9 @@ __device__ __forceinline__ void greeks_lean_n(const float* S, float num_drift, f
 // a function of the market alone, so it is computed where the market is (market_kernel
 // slots, replay table load) and travels in the .w lane of the greeks record.
 __device__ __forceinline__ float lag_return(float S, float Sp) {
-    return (Sp == 0.0f) ? 0.0f : np_clipf((S - Sp) / Sp, -1.0f, 1.0f);
+    float q = (S - Sp) / Sp;  // for every lane (opaque): a select, not a branch around the division
+    HE_OPAQUE1(q);
+    return (Sp == 0.0f) ? 0.0f : np_clipf(q, -1.0f, 1.0f);
 }
 
 // hedging_env_v2.py:109-143.  m = market after the step, g = its greeks and, in g.w,
@@ -2105,15 +2134,28 @@ __device__ uint64_t g_lds_tim[4][4096][3];
 
 // Store one workgroup's 64 obs rows (the image, 832 floats) as 3 x 16 B + 4 B per lane:
 // every lane active, no branch.
+#ifndef HE_OBS_SC1
+#define HE_OBS_SC1 0  // A/B: the obs rows stored write-through (sc1: the lines leave the XCD's L2)
+#endif
 __device__ __forceinline__ void flush_obs_full(const float* img, float* out, int64_t row0, int lane) {
     asm volatile("" ::: "memory");
     GLOBAL float* dst = (GLOBAL float*)out + row0 * kObs;
+#if HE_OBS_SC1
+    typedef int v4i __attribute__((ext_vector_type(4)));
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)dst, 0, kLdsEnvs * kObs * 4, 0x00020000);
+    const v4i* s4 = reinterpret_cast<const v4i*>(img);
+    __builtin_amdgcn_raw_buffer_store_b128(s4[lane], rs, lane * 16, 0, 16);
+    __builtin_amdgcn_raw_buffer_store_b128(s4[lane + 64], rs, (lane + 64) * 16, 0, 16);
+    __builtin_amdgcn_raw_buffer_store_b128(s4[lane + 128], rs, (lane + 128) * 16, 0, 16);
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(int, img[768 + lane]), rs, (768 + lane) * 4, 0, 16);
+#else
     GLOBAL v4f* d4 = (GLOBAL v4f*)dst;
     const v4f* s4 = reinterpret_cast<const v4f*>(img);
     d4[lane] = s4[lane];
     d4[lane + 64] = s4[lane + 64];
     d4[lane + 128] = s4[lane + 128];
     dst[768 + lane] = img[768 + lane];
+#endif
     asm volatile("" ::: "memory");
 }
 
@@ -2362,6 +2404,14 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
                 // staged in LDS (two tiles, alternating by step: the next step's row writes
                 // do not wait behind this step's read-back) and stored as whole 16-B lines
                 float* const tile = L.stage[k & 1];
+#ifdef HE_OBS_ROW_OPAQUE
+                // A/B: the obs row made for every lane (opaque) before the autoreset select, so
+                // the backend keeps 13 selects instead of an if/else around the obs computation
+                // (one exec-mask branch per step).  With asm volatile the 13 pins are scheduling
+                // barriers: config 2 299 / 307 -> 320 / 322 us per launch (r03s24).
+#pragma unroll
+                for (int c = 0; c < kObs; ++c) HE_OBS_PIN(o[c]);
+#endif
 #pragma unroll
                 for (int c = 0; c < kObs; ++c) tile[lane * kObs + c] = term ? ro[c] : o[c];
                 float* out = io.obs + (int64_t)k * N * kObs;
