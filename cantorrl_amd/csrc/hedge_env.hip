@@ -1867,6 +1867,162 @@ __global__ __launch_bounds__(kBlock) void step1_kernel(const Params* __restrict_
     step_body<MODE, false, true, BOOK, FAST, false, GS>(*pc, n, tA, tB, tC, s, io, 1, slot0, blockIdx.x);
 }
 
+// Opaque copies of the Params fields a step / a market block reads in its loop (see HE_LDS_PIN).
+__device__ __forceinline__ void pin_step_consts(Params& q, bool obs) {
+    asm volatile("" : "+s"(q.mt_f), "+s"(q.mt), "+s"(q.maxh), "+s"(q.T), "+s"(q.var_f));
+    if (obs) {
+        asm volatile("" : "+s"(q.maxh_f), "+s"(q.inv_maxh_f), "+s"(q.T_f), "+s"(q.inv_T_f), "+s"(q.s0s_d),
+                     "+s"(q.inv_s0s_d));
+#pragma unroll
+        for (int c = 0; c < 4 + kObs; ++c) asm volatile("" : "+s"(q.rstv[c]));
+    } else {
+        asm volatile("" : "+s"(q.tcpc), "+s"(q.slip_frac), "+s"(q.shares_f), "+s"(q.shares_d), "+s"(q.inv_shares),
+                     "+s"(q.den), "+s"(q.inv_den));
+        asm volatile("" : "+s"(q.w), "+s"(q.lam), "+s"(q.theta), "+s"(q.inv_252), "+s"(q.initial_cash),
+                     "+s"(q.init_cash_f));
+    }
+}
+// he_step split by role (GBM, the FAST configuration, market greeks from the tile, no book,
+// no info): at 65,536 envs step1_kernel is one wave per SIMD, so each env's whole chain --
+// loads, the f64 P&L, the obs row -- is exposed latency.  Here a workgroup of 8
+// waves steps 256 envs: waves 0-3 the reward chain of step_env (trades, costs, P&L, reward,
+// the state), waves 4-7 the obs of the same envs (the trade logic again, make_obs, the
+// SB3 terminal / reset obs) -- two independent chains per env on different waves.  The
+// same device functions on the same operands as step_body, so the same bits.  One
+// workgroup barrier: the obs waves arrive once their loads have returned, the reward
+// waves before their stores (the state the obs waves read).
+// Opt-in (HE_STEP_SPLIT=1 in the environment at he_create), parity-tested
+// (test_split_step_equals_step1): same-box graph-mode A/B (r03s28, 3 runs each) 1.29-1.33e10
+// env-steps/s against step1_kernel's 1.34-1.37e10 -- twice the waves to dispatch and the
+// second role's duplicate loads cost more than the overlap of the two chains gains.
+#ifndef HE_STEP_SPLIT
+#define HE_STEP_SPLIT 1
+#endif
+#ifndef HE_SPLIT_PIN
+#define HE_SPLIT_PIN 1  // the role's Params fields loaded up front (not lazily mid-chain)
+#endif
+#ifndef HE_SPLIT_EARLY_BAR
+#define HE_SPLIT_EARLY_BAR 1
+#endif
+__global__ __launch_bounds__(2 * kBlock) void step1_split_kernel(const Params* __restrict__ pc, int64_t n,
+                                                                 const float4* tA, const float4* tB, State s,
+                                                                 StepIo sio, int slot0) {
+    static_assert(kEpw == 64 && kEpb == kBlock, "one env per thread and role");
+    __builtin_amdgcn_s_setprio(3);
+    __shared__ __attribute__((aligned(16))) float tile[kEpb * kObs];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const bool obs_role = wave >= 4;
+    const int w = wave & 3;
+    const int64_t wrow0 = (int64_t)blockIdx.x * kEpb + w * 64;
+    const int64_t i = wrow0 + lane;
+    const int64_t N = n;
+    const bool live = i < N;
+    const int64_t ic = live ? i : (N - 1);  // dead lanes load a live env's addresses
+    const int wrows = (int)((N - wrow0) < 64 ? (N - wrow0 > 0 ? N - wrow0 : 0) : 64);
+    auto mA = (const GLOBAL v4f*)tA;
+    auto mB = (const GLOBAL v4f*)tB;
+    // every load of the step issued first, by both roles (one memory round trip; the
+    // second role's loads of the same lines hit L2), and pinned there: otherwise the
+    // backend sinks some into the role branches, a second dependent round trip
+    // (row bases in SGPRs, 32-bit env index: plain base + index * size addresses)
+    const uint32_t iu = (uint32_t)ic;
+    const GLOBAL v4f* rowA0 = (const GLOBAL v4f*)((const GLOBAL f3*)mA + (int64_t)slot0 * N);
+    const GLOBAL v4f* rowA1 = (const GLOBAL v4f*)((const GLOBAL f3*)mA + (int64_t)(slot0 + 1) * N);
+    const GLOBAL v4f* rowB1 = (const GLOBAL v4f*)((const GLOBAL f3*)mB + (int64_t)(slot0 + 1) * N);
+    uint32_t t0 = s.t[iu];
+    uint32_t pk = s.pos[iu];
+    float2 a = ld2((const GLOBAL v2f*)sio.act, iu);
+    float4 g = ld3B(rowB1, iu);
+    float4 postA = ld3B(rowA1, iu);  // {S, C, P}: v is the handle's constant (ld3A)
+    float4 preA = ld3B(rowA0, iu);
+    double cash = s.cash[iu];
+    // the Params loads after these (scalar loads return out of order: a scalar load issued
+    // before the address operands of the vector loads would hold them back)
+    asm volatile("" ::: "memory");
+#if HE_SPLIT_PIN
+    Params pq = *pc;
+    const Params& p = pq;
+#else
+    const Params& p = *pc;
+#endif
+#if HE_SPLIT_PIN
+    // while the loads are in flight: every Params field the role reads, in SGPRs (one
+    // scalar round trip instead of one per first use along the chain)
+    if (obs_role) {
+        pin_step_consts(pq, true);
+    } else {
+        pin_step_consts(pq, false);
+        asm volatile("" : "+s"(pq.autoreset));
+    }
+#endif
+    asm volatile("" : "+v"(t0), "+v"(pk), "+v"(a.x), "+v"(a.y), "+v"(postA.x), "+v"(postA.y), "+v"(postA.z),
+                 "+v"(preA.x), "+v"(preA.y), "+v"(preA.z), "+v"(cash), "+v"(g.x), "+v"(g.y), "+v"(g.z));
+    const float var_f = p.var_f;
+    postA = make_float4(postA.x, var_f, postA.y, postA.z);
+    preA = make_float4(preA.x, var_f, preA.y, preA.z);
+    const Mkt rst{p.rstv[0], p.rstv[1], p.rstv[2], p.rstv[3], 0.0};
+    Env e;
+    e.t = t0;
+    e.call = unpack_lo(pk);
+    e.put = unpack_hi(pk);
+    e.path = -1;
+    e.s0_small = rst.S < 1e-6f;
+    e.s0 = e.s0_small ? 1.0f : rst.S;
+    const Mkt pre = (t0 == 0) ? rst : as_mkt(preA);
+    const Mkt post = as_mkt(postA);
+    if (!obs_role) {
+        // the reward chain (step_env, hedging_env_v2.py:175-262) and the state
+        e.cash = cash;
+        const double pv_last = portfolio_value<false>(p, e, pre);
+        StepOut so;
+        step_env<false, true>(p, e, pre, post, a.x, a.y, pv_last, so);
+        if (so.term && p.autoreset) env_reset_common(p, e);  // SB3 autoreset
+        // every store after the barrier (its fence would wait for stores issued before it)
+        __syncthreads();  // the obs waves have their state inputs
+        if (live) {
+            ((GLOBAL float*)sio.rew)[i] = (float)so.reward;
+            ((GLOBAL uint8_t*)sio.term)[i] = so.term ? 1 : 0;
+            if (sio.trunc) ((GLOBAL uint8_t*)sio.trunc)[i] = 0;
+            s.t[i] = e.t;
+            s.pos[i] = pack_pos(e.call, e.put);
+            s.cash[i] = e.cash;
+        }
+    } else {
+        // the obs (hedging_env_v2.py:109-143) of the post-step state: step_env's trade logic
+        // (:181-200) for the positions, then make_obs; the terminal / reset obs of SB3
+#if HE_SPLIT_EARLY_BAR
+        // the state loads have returned (the pins above): the reward waves may store the
+        // state now, not after this wave's obs stores
+        __syncthreads();
+#endif
+        g.w = lag_return(post.S, (e.t >= (uint32_t)p.T) ? rst.S : pre.S);
+        const int32_t nc = e.call + trade_round(a.x * p.mt_f, p.mt);
+        const int32_t nq = e.put + trade_round(a.y * p.mt_f, p.mt);
+        e.call = nc < -p.maxh ? -p.maxh : (nc > p.maxh ? p.maxh : nc);
+        e.put = nq < -p.maxh ? -p.maxh : (nq > p.maxh ? p.maxh : nq);
+        e.t = e.t + 1;
+        const bool term = (int32_t)e.t >= p.T;
+        float o[kObs];
+        make_obs<true>(p, e, post, g, pre.S, pre.v, o);
+        float* const orow = tile + (w * 64 + lane) * kObs;
+        if (p.autoreset && __ballot(term) != 0ull) {
+            if (term && live && sio.tobs) {
+#pragma unroll
+                for (int c = 0; c < kObs; ++c) sio.tobs[i * kObs + c] = o[c];
+            }
+#pragma unroll
+            for (int c = 0; c < kObs; ++c) o[c] = term ? p.rstv[4 + c] : o[c];
+        }
+#pragma unroll
+        for (int c = 0; c < kObs; ++c) orow[c] = o[c];
+        flush_obs_wave(tile + w * 64 * kObs, sio.obs, wrow0, wrows, lane);
+#if !HE_SPLIT_EARLY_BAR
+        __syncthreads();
+#endif
+    }
+}
+
 // he_step with VecNormalize attached (he_vecnorm_attach): step1_kernel, then the first half
 // of the VecNormalize step (vn_moments.h) over the rows this workgroup has just made --
 // from its LDS obs staging tile and the rewards in registers, with no read back -- instead
@@ -2180,21 +2336,6 @@ __device__ __forceinline__ void flush_obs_full(const float* img, float* out, int
 // config 4 8,863 / 8,878 -> 8,770 / 8,833: the reloads were not what holds those kernels back.
 #define HE_LDS_PIN 0
 #endif
-// Opaque copies of the Params fields a step / a market block reads in its loop (see HE_LDS_PIN).
-__device__ __forceinline__ void pin_step_consts(Params& q, bool obs) {
-    asm volatile("" : "+s"(q.mt_f), "+s"(q.mt), "+s"(q.maxh), "+s"(q.T), "+s"(q.var_f));
-    if (obs) {
-        asm volatile("" : "+s"(q.maxh_f), "+s"(q.inv_maxh_f), "+s"(q.T_f), "+s"(q.inv_T_f), "+s"(q.s0s_d),
-                     "+s"(q.inv_s0s_d));
-#pragma unroll
-        for (int c = 0; c < 4 + kObs; ++c) asm volatile("" : "+s"(q.rstv[c]));
-    } else {
-        asm volatile("" : "+s"(q.tcpc), "+s"(q.slip_frac), "+s"(q.shares_f), "+s"(q.shares_d), "+s"(q.inv_shares),
-                     "+s"(q.den), "+s"(q.inv_den));
-        asm volatile("" : "+s"(q.w), "+s"(q.lam), "+s"(q.theta), "+s"(q.inv_252), "+s"(q.initial_cash),
-                     "+s"(q.init_cash_f));
-    }
-}
 __device__ __forceinline__ void pin_market_consts(Params& q, bool heston, bool book) {
     asm volatile("" : "+s"(q.key0), "+s"(q.key1), "+s"(q.sqrt_dt), "+s"(q.s0), "+s"(q.var), "+s"(q.r_d));
     asm volatile("" : "+s"(q.sqrt_tenor), "+s"(q.tenor_d), "+s"(q.bs.disc));
@@ -3645,6 +3786,7 @@ struct he_env {
     int32_t next_state = 0;   // next block: 0 none, 1 generating on `xs` (ev_next), 2 ready
     bool fuse_market = true;  // rollouts: next block's market in the step grid (HE_FUSED_MARKET=0: side stream)
     bool lds_rollout = true;  // he_rollout (GBM, no book): lds_rollout_kernel (HE_LDS_ROLLOUT=0: tile kernels)
+    bool step_split = false;  // he_step (GBM FAST): step1_split_kernel if HE_STEP_SPLIT=1 at he_create (A/B, slower)
     int32_t prefetch_mode = 0; // 0 auto, 1 never, 2 always: market_kernel(b+1) on `xs` during block b
     hipStream_t xs = nullptr; // library side stream for market prefetch
     hipEvent_t ev_fork = nullptr, ev_next = nullptr;
@@ -3937,6 +4079,21 @@ static void launch_step_gs(he_env* env, const Params& p, const Io& io, bool info
         const float4* tA = REPLAY ? p.rec : p.tileA;
         const float4* tB = REPLAY ? p.recg : p.tileB;
         StepIo sio{io.act, io.obs, io.rew, io.term, io.trunc, io.tobs};
+        if constexpr (MODE == HE_MODE_GBM && FAST && !BOOK && !GS) {
+            if (HE_STEP_SPLIT && env->step_split && !env->vn_on && io.obs && io.rew && io.term) {
+                const unsigned sb = (unsigned)((env->cfg.n_envs + kEpb - 1) / kEpb);
+                if (env->ev_start) {
+                    hipEvent_t a = (hipEvent_t)env->ev_start, b = (hipEvent_t)env->ev_stop;
+                    env->ev_start = env->ev_stop = nullptr;
+                    hipExtLaunchKernelGGL(step1_split_kernel, dim3(sb), dim3(2 * kBlock), 0, st, a, b, 0, pc, p.n, tA, tB,
+                                          env->s, sio, slot0);
+                } else {
+                    hipLaunchKernelGGL(step1_split_kernel, dim3(sb), dim3(2 * kBlock), 0, st, pc, p.n, tA, tB, env->s,
+                                       sio, slot0);
+                }
+                return;
+            }
+        }
         if (env->vn_on) {  // + the VecNormalize moments in the same launch
             vn::MomentsArgs vm = env->vn;
             vm.obs = io.obs;
@@ -4395,6 +4552,8 @@ he_status he_create(const he_config* cfg, he_env** out) {
             env->fuse_market = !(ev && ev[0] == '0');
             const char* el = getenv("HE_LDS_ROLLOUT");
             env->lds_rollout = !(el && el[0] == '0');
+            const char* es = getenv("HE_STEP_SPLIT");
+            env->step_split = es && es[0] == '1';
         }
         HE_HIP(env, hipStreamCreateWithFlags(&env->xs, hipStreamNonBlocking));
         HE_HIP(env, hipEventCreateWithFlags(&env->ev_fork, hipEventDisableTiming));

@@ -1010,3 +1010,33 @@ def test_generate_mode_matches_reference_closed_loop(api, mark, monkeypatch):
         assert_same(summ[:, 2], d["info_transaction_costs_total"][last].sum(0).astype(np.float32), "episode cost",
                     rtol=PNL_RTOL, atol=1e-6)
     env.close()
+
+
+@pytest.mark.parametrize("n,T", [(1, 3), (63, 5), (257, 7), (700, 1), (65536, 6)])
+def test_split_step_equals_step1(n, T, monkeypatch):
+    """he_step's role-split kernel (step1_split_kernel: reward waves and obs waves per 256
+    envs) gives step1_kernel's obs, rewards, done flags, SB3 terminal obs and state bit for
+    bit -- odd env counts (dead lanes), T = 1 (every step terminates), clipped positions."""
+    from cantorrl_amd.vec_env import HedgingVecEnv
+    steps = 3 * T + 4
+    acts = torch.rand((steps, n, 2), device="cuda") * 4.4 - 2.2
+    acts[:, ::3] = torch.tensor([1.0, -1.0], device="cuda")
+    gen = dict(episode_length=T)
+    kw = dict(theta_weight=0.0002, slippage_bps=1.0)
+    outs = []
+    for split in ("1", "0"):
+        monkeypatch.setenv("HE_STEP_SPLIT", split)
+        env = HedgingVecEnv(n, mode="gbm", generate=gen, seed=5, return_numpy=False, info_keys=(), **kw)
+        got = [env.reset_tensors().clone()]
+        for k in range(steps):
+            o, r, t, tr = env.step_tensors(acts[k], terminal_obs=True, info=False)
+            got += [o.clone(), r.clone(), t.clone(), tr.clone()]
+            m = t.bool()
+            got.append(env._tobs[m].clone())
+            if k == T + 1:
+                got.append(env.reset_tensors(env_ids=[0, n - 1]).clone())
+        got.append(torch.as_tensor(env.get_state()))
+        env.close()
+        outs.append(got)
+    for k, (a, b) in enumerate(zip(*outs)):
+        assert torch.equal(_bits(a), _bits(b)), k
