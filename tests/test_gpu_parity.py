@@ -47,10 +47,37 @@ GOLD_INFO = [
 ]
 
 
-def compare_obs(got, exp, name):
+def compare_obs(got, exp, name, gk_atol=0.0):
     cols_exact = [0, 1, 2, 3, 4, 5, 6, 11, 12]
     assert_same(got[..., cols_exact], exp[..., cols_exact], name + "[exact cols]")
-    assert_same(got[..., 7:11], exp[..., 7:11], name + "[greeks]", rtol=OBS_RTOL, atol=OBS_ATOL)
+    assert_same(got[..., 7:11], exp[..., 7:11], name + "[greeks]", rtol=OBS_RTOL, atol=OBS_ATOL + gk_atol)
+
+
+def greeks_log_allowance(S, v, r=0.04, tenor=30 / 252):
+    """Per-env bound on what the f32 log alone can move the obs greeks (columns 7-10).
+    hedging_env_v2.py:95-97 takes log(S / K) in f32, and f32 logs differ by an ulp between
+    platforms: NumPy 2.2's own float32 log is not the correctly rounded value on ~40 % of
+    inputs near 1 (20M samples, this container), ROCm's logf is not either.  The division
+    by sigma*sqrt(T) amplifies that ulp when the variance sits at its 1e-8 floor (Heston's
+    full truncation: seed 8 of the randomised test, v < 0, d1 moved by 1.35e-5 by a
+    one-ulp log):  |dd1| <= 2 ulp(|log q| + |drift|) / (sigma sqrt T),  |dN| <= phi(d1)
+    |dd1|,  |dgamma| <= gamma (|d1| + |dd1|) |dd1|.  At a normal variance this is ~1e-9,
+    far under OBS_ATOL: only the ill-conditioned cases get room.  Returns the [n, 4] atol."""
+    S = np.asarray(S, np.float32).astype(np.float64)
+    v = np.asarray(v, np.float32).astype(np.float64)
+    with np.errstate(all="ignore"):
+        K = np.maximum(np.round(S), 1e-6)
+        sigma = np.sqrt(np.maximum(v, 1e-8))
+        sst = sigma * np.sqrt(tenor)
+        lq = np.log(S / K)
+        drift = (r + 0.5 * sigma ** 2) * tenor
+        dd1 = 2.0 * 2.0 ** -24 * (np.abs(lq) + np.abs(drift)) / sst
+        d1 = (lq + drift) / sst
+        phi = np.exp(-0.5 * d1 ** 2) / np.sqrt(2 * np.pi)
+        dcd = phi * dd1
+        dg = phi / (S * sst) * (np.abs(d1) + dd1) * dd1
+    out = np.stack([dcd, dg, dcd, dg], axis=1)
+    return np.where(np.isfinite(out) & (S[:, None] > 1e-6), out, 0.0)
 
 
 def make_vec(d, cfg):
@@ -89,7 +116,7 @@ def test_replay_matches_reference_golden(fname):
     env.close()
 
 
-def run_gbm_pair(n, steps, seed, cfg, gen, offset=0, mode="gbm", pnl_rtol=0.0):
+def run_gbm_pair(n, steps, seed, cfg, gen, offset=0, mode="gbm", pnl_rtol=0.0, variant=2):
     """GPU generate mode against the oracle, step by step: integers and the market info bit
     for bit, the P&L fields and rewards bit for bit too unless pnl_rtol > 0 (north_star's
     bar, PNL_RTOL: the liability book's own pricer is not the oracle's scipy ndtr), and the
@@ -97,9 +124,9 @@ def run_gbm_pair(n, steps, seed, cfg, gen, offset=0, mode="gbm", pnl_rtol=0.0):
     from cantorrl_amd.vec_env import HedgingVecEnv
     rng = np.random.default_rng(seed)
     acts = rng.uniform(-1.05, 1.05, size=(steps, n, 2)).astype(np.float32)
-    venv = HedgingVecEnv(n, mode=mode, generate=gen, seed=seed, global_env_offset=offset,
+    venv = HedgingVecEnv(n, mode=mode, generate=gen, seed=seed, global_env_offset=offset, variant=variant,
                          info_keys=all_info_keys(), return_numpy=False, **cfg)
-    orc = OracleVecEnv(n, mode=mode, gen=dict(gen, seed=seed, env_offset=offset), **cfg)
+    orc = OracleVecEnv(n, variant=variant, mode=mode, gen=dict(gen, seed=seed, env_offset=offset), **cfg)
     orc.seed_envs_at(np.arange(n), [seed] * n)
     o_obs = orc.reset()
     g_obs = venv.reset_tensors().cpu().numpy()
@@ -128,7 +155,7 @@ def run_gbm_pair(n, steps, seed, cfg, gen, offset=0, mode="gbm", pnl_rtol=0.0):
                 stats["pnl_total"] += got.size
         assert_same(rew.cpu().numpy(), orew.astype(np.float32), f"reward[{s}]",
                     rtol=pnl_rtol, atol=1e-9 if pnl_rtol else 0.0)
-        compare_obs(obs.cpu().numpy(), oo, f"obs[{s}]")
+        compare_obs(obs.cpu().numpy(), oo, f"obs[{s}]", gk_atol=greeks_log_allowance(orc.S, orc.v))
     venv.close()
     return stats
 
@@ -1040,3 +1067,99 @@ def test_split_step_equals_step1(n, T, monkeypatch):
         outs.append(got)
     for k, (a, b) in enumerate(zip(*outs)):
         assert torch.equal(_bits(a), _bits(b)), k
+
+
+def _random_case(seed):
+    """One random generate-mode configuration: market (GBM / Heston, S0 below and above the
+    25 floor, drift, variance, marks, a book of up to 3 options), reward (variant 1 / 2, abs /
+    mse, costs, theta, record_metrics, cash, trade / position limits), env count and a plan
+    of ragged rollouts, single steps, a partial reset and a checkpoint restore."""
+    rng = np.random.default_rng(9000 + seed)
+    mode = "heston" if rng.random() < 0.35 else "gbm"
+    T = int(rng.choice([1, 2, 3, 7, 9, 25, 40, 64, 253]))
+    s0 = float(rng.choice([496.48001098632812, 101.25, 20.0, 1000.5]))
+    gen = dict(episode_length=T, s0=s0, variance=float(rng.choice([0.029028, 0.09, 0.2])),
+               mu=float(rng.choice([0.04, -0.1, 0.0])))
+    if mode == "heston":
+        gen.update(heston_kappa=float(rng.choice([2.0, 0.5])), heston_theta=float(rng.choice([0.029028, 0.09])),
+                   heston_xi=float(rng.choice([0.3, 1.0, 2.5])), heston_rho=float(rng.uniform(-0.9, 0.5)))
+    if rng.random() < 0.25:
+        gen["mark"] = "fixed_european"
+    book = rng.random() < 0.3
+    if book:
+        opts = []
+        for _ in range(int(rng.integers(1, 4))):
+            typ = str(rng.choice(["call", "put", "uo_call"]))
+            k = float(np.round(s0 * rng.uniform(0.9, 1.1)))
+            o = dict(type=typ, strike=k, expiry=int(rng.integers(1, T + 12)), quantity=float(rng.uniform(-50, 10)))
+            if typ == "uo_call":
+                o["barrier"] = float(np.round(max(k, s0) * rng.uniform(1.02, 1.2)))
+            opts.append(o)
+        gen["book"] = opts
+    variant = 1 if rng.random() < 0.15 else 2
+    kw = dict(loss_type="abs" if rng.random() < 0.7 else "mse", pnl_penalty_weight=float(rng.choice([0.01, 0.001])),
+              lambda_cost=float(rng.choice([1.0, 0.0001])), record_metrics=bool(rng.random() < 0.85),
+              initial_cash=float(rng.choice([0.0, 1000.0])), max_trade_per_step=int(rng.choice([15, 3])),
+              max_contracts_held_per_type=int(rng.choice([200, 10])))
+    if variant == 2:
+        kw.update(theta_weight=float(rng.choice([0.0, 0.0002])), slippage_bps=float(rng.choice([0.0, 1.0, 5.0])))
+    n = int(rng.choice([1, 64, 65, 129, 333, 700]))
+    plan = [("r", int(rng.integers(1, 70))), ("s", 0), ("r", int(rng.integers(1, 70))),
+            ("reset", 0), ("r", int(rng.integers(1, 40))), ("ckpt", 0), ("s", 0), ("r", int(rng.integers(1, 70))),
+            ("tail", int(rng.integers(1, 20)))]
+    return mode, gen, kw, variant, n, book, plan
+
+
+@pytest.mark.parametrize("seed", range(16))
+def test_random_configs_paths_agree_and_match_oracle(seed, monkeypatch):
+    """Randomised configurations (_random_case): the LDS rollout kernel, the tile kernels
+    (fused or side-stream market) and he_step alone (the role-split kernel where eligible)
+    give the same obs, rewards, done flags bit for bit over the same plan (he_step alone
+    ends with one rollout, so its state carries on exactly), the two rollout paths the same
+    final state (he_step keeps no episode summaries), and he_step with every info field
+    matches the oracle on the first envs."""
+    from cantorrl_amd.vec_env import HedgingVecEnv
+    mode, gen, kw, variant, n, book, plan = _random_case(seed)
+    steps = sum(k for op, k in plan if op in ("r", "tail")) + sum(1 for op, _ in plan if op == "s")
+    g = torch.Generator(device="cuda")
+    g.manual_seed(seed)
+    acts = torch.rand((steps, n, 2), device="cuda", generator=g) * 4.4 - 2.2
+    ids = sorted({0, n // 2, n - 1})
+    args = dict(mode=mode, generate=gen, seed=77 + seed, global_env_offset=3 * seed, variant=variant,
+                return_numpy=False, info_keys=(), **kw)
+    runs = []
+    for lds, fused, only_steps in (("1", "1", False), ("0", str(seed % 2), False), ("0", "1", True)):
+        monkeypatch.setenv("HE_LDS_ROLLOUT", lds)
+        monkeypatch.setenv("HE_FUSED_MARKET", fused)
+        monkeypatch.setenv("HE_STEP_SPLIT", "1")
+        env = HedgingVecEnv(n, **args)
+        got = [env.reset_tensors().clone()]
+        a0 = 0
+        for op, k in plan:
+            if op == "s" or (op == "r" and only_steps):
+                for _ in range(1 if op == "s" else k):
+                    o, r, t, _ = env.step_tensors(acts[a0], terminal_obs=False, info=False)
+                    got += [o.clone(), r.clone(), t.clone()]
+                    a0 += 1
+            elif op in ("r", "tail"):
+                o, r, t = env.rollout(acts[a0:a0 + k].contiguous())
+                for j in range(k):
+                    got += [o[j].clone(), r[j].clone(), t[j].clone()]
+                a0 += k
+            elif op == "reset":
+                got.append(env.reset_tensors(env_ids=ids)[ids].clone())
+            else:
+                blob = env.get_state()
+                env.close()
+                env = HedgingVecEnv(n, **args)
+                env.set_state(blob)
+        if not only_steps:
+            got.append(torch.from_numpy(env.get_state().copy()))
+        env.close()
+        runs.append(got)
+    for j, other in enumerate(runs[1:]):
+        assert len(other) == len(runs[0]) - j
+        for i, (a, b) in enumerate(zip(runs[0], other)):
+            assert torch.equal(_bits(a), _bits(b)), (seed, j + 1, i)
+    run_gbm_pair(min(n, 48), min(2 * gen["episode_length"] + 3, 80), 77 + seed, kw, gen, offset=3 * seed,
+                 mode=mode, pnl_rtol=PNL_RTOL if book else 0.0, variant=variant)
