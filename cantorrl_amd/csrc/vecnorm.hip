@@ -131,29 +131,45 @@ __device__ __forceinline__ RowIn row_in(const VnArgs& a, int64_t r) {
 // Launch 2: every workgroup merges all the partials itself (one block reduction in a
 // fixed order, so the same statistics everywhere; workgroup 0 stores them), then
 // normalizes its rows: obs / reward / terminal obs, returns[done] = 0, Monitor sums.
+// R > 1 (n <= kVnMaxBlocks * kVnChunk; A/B, HE_VN_APPLY_R): R * 256 rows per workgroup,
+// R per thread, so 1 / R of the workgroups each read the G partials.  Slower: rocprof
+// 7.5 (R = 1) / 10.2 (R = 2) / 15.9 us (R = 4) at 65,536 envs (r03s32) -- the merge's
+// reads are not what the launch waits on; each thread's rows are.
+#ifndef HE_VN_APPLY_R
+#define HE_VN_APPLY_R 1
+#endif
+template <int R>
 __global__ void __launch_bounds__(kVnThreads) vn_apply_kernel(VnArgs a) {
     __shared__ double sh[kVnThreads * (kPart + 1)];
     __shared__ double ssum[kPart];
     __shared__ double snorm[kD][2];   // per obs column: mean, 1 / sqrt(var + eps)
     __shared__ double srinv;
     __shared__ float tile[kVnChunk * kD];
-    const VnRows w = rows_of(a);
+    VnRows w = rows_of(a);
+    if (R > 1) {
+        w.r0 = (int64_t)blockIdx.x * (kVnChunk * R);
+        w.r1 = (w.r0 + kVnChunk * R < a.n) ? w.r0 + kVnChunk * R : a.n;
+    }
     const bool upd_ret = a.training && !a.reset;
     const int t = threadIdx.x;
-    const bool resident = w.r1 - w.r0 <= kVnChunk;
+    const bool resident = w.r1 - w.r0 <= kVnChunk * R;
+    const int nrows = (int)(w.r1 - w.r0);
     // the rows' loads first -- obs, and the row's reward, done flag and Monitor sums: they
     // are all in flight while the partials are merged (one memory round trip per launch)
-    float xr[kD];
-    const int nres = resident ? (int)(w.r1 - w.r0) * kD : 0;
+    float xr[R * kD];
+    const int nres = resident ? nrows * kD : 0;
     const float* src = a.obs + w.r0 * kD;
 #pragma unroll
-    for (int q = 0; q < kD; ++q) {
+    for (int q = 0; q < R * kD; ++q) {
         const int k = t + q * kVnThreads;
         xr[q] = k < nres ? src[k] : 0.0f;
     }
-    RowIn pin = {};
-    const bool prow = resident && !a.reset && t < (int)(w.r1 - w.r0);
-    if (prow) pin = row_in(a, w.r0 + t);
+    RowIn pin[R];
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+        pin[j] = {};
+        if (resident && !a.reset && t + j * kVnThreads < nrows) pin[j] = row_in(a, w.r0 + t + j * kVnThreads);
+    }
     if (a.upd_obs || upd_ret) {
         const double* P = a.part + t;
         const bool has = t < a.blocks;
@@ -232,7 +248,7 @@ __global__ void __launch_bounds__(kVnThreads) vn_apply_kernel(VnArgs a) {
         // k of the slice is column k % 13 (the slice starts at a row boundary)
         float* dst = a.obs_out + w.r0 * kD;
 #pragma unroll
-        for (int q = 0; q < kD; ++q) {
+        for (int q = 0; q < R * kD; ++q) {
             const int k = t + q * kVnThreads;
             if (k < nres) {
                 const int c = k % kD;
@@ -240,7 +256,9 @@ __global__ void __launch_bounds__(kVnThreads) vn_apply_kernel(VnArgs a) {
                                     : xr[q];
             }
         }
-        if (t < (int)(w.r1 - w.r0)) row_work(w.r0 + t, pin);
+#pragma unroll
+        for (int j = 0; j < R; ++j)
+            if (t + j * kVnThreads < nrows) row_work(w.r0 + t + j * kVnThreads, pin[j]);
         return;
     }
     for (int64_t c0 = w.r0; c0 < w.r1; c0 += kVnChunk) {
@@ -293,7 +311,13 @@ he_status launch(VnArgs& a, void* scratch, hipStream_t s, bool moments = true) {
         hipLaunchKernelGGL(vn_moments_kernel, dim3(a.blocks), dim3(kVnThreads), 0, s, a);
         if (hipGetLastError() != hipSuccess) return HE_EHIP;
     }
-    hipLaunchKernelGGL(vn_apply_kernel, dim3(a.blocks), dim3(kVnThreads), 0, s, a);
+    if (HE_VN_APPLY_R > 1 && a.n <= (int64_t)kVnMaxBlocks * kVnChunk) {
+        constexpr int64_t rpb = (int64_t)kVnChunk * HE_VN_APPLY_R;
+        hipLaunchKernelGGL(vn_apply_kernel<HE_VN_APPLY_R>, dim3((unsigned)((a.n + rpb - 1) / rpb)), dim3(kVnThreads),
+                           0, s, a);
+    } else {
+        hipLaunchKernelGGL(vn_apply_kernel<1>, dim3(a.blocks), dim3(kVnThreads), 0, s, a);
+    }
     return hipGetLastError() == hipSuccess ? HE_OK : HE_EHIP;
 }
 
