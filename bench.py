@@ -103,9 +103,10 @@ def tile_layout(mode, n):
 
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
-# >= 2 episodes of 252 steps; 2,560 = 10 launches of the K = 256 rollout, so the
-# timed region's per-launch device time averages over 10 dispatches
-MIN_TIMED_STEPS = 2560
+# >= 2 episodes of 252 steps; 25,600 = 100 launches of the K = 256 rollout, so
+# the timed region's per-launch device time averages over 100 dispatches (~30 ms at config 2:
+# over 10 the same box read 292 and 318 us in two processes, r03s34)
+MIN_TIMED_STEPS = 25600
 M_BLOCK = 64           # market block (he_config.market_block)
 
 TRAIN_KW = dict(loss_type="abs", pnl_penalty_weight=0.001, lambda_cost=0.0001, theta_weight=0.0002,
@@ -185,7 +186,7 @@ def replay_tables(paths, cols, seed=2025):
 def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=2560)
+    ap.add_argument("--steps", type=int, default=MIN_TIMED_STEPS)
     ap.add_argument("--warmup", type=int, default=256)
     ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS), help="BASELINE.json config")
     ap.add_argument("--envs", type=int, default=None, help="envs per GPU (default: the config's)")
@@ -1061,7 +1062,7 @@ def main(argv=None):
             "steps": K,
             "warmup": runner.warmup_steps,
             # the command's --steps / --warmup: raised to the timed floor (MIN_TIMED_STEPS, >= 2
-            # episodes and 10 launches) and to whole launches of the rollout chunk
+            # episodes and 100 launches) and to whole launches of the rollout chunk
             "requested_steps": args.steps,
             "requested_warmup": args.warmup,
             "ms_per_step": round(wall * 1e3 / K, 6),
