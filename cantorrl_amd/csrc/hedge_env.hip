@@ -610,12 +610,37 @@ struct BookEnv {
 constexpr double kMillsA = 1.1813471502590676, kMillsB = 7.6347150259067362, kMillsC = 3.5;
 constexpr double kMillsMax = 37.4;                       // phi(37.4) ~ 1e-304: the tail is 0 past it
 constexpr double kInvSqrt2Pi = 0.39894228040143267794;
+#ifndef HE_MILLS_ESTRIN
+#define HE_MILLS_ESTRIN 0
+#endif
 __device__ __forceinline__ double mills(double a) {
     const double d = a + kMillsC;                        // in [3.5, 41]: no special cases
     double y = __builtin_amdgcn_rcp(d);
     y = fma(fma(-d, y, 1.0), y, y);                      // two Newton steps: 1 / d to the last bits
     y = fma(fma(-d, y, 1.0), y, y);
     const double u = fma(-kMillsB, y, kMillsA);
+#if HE_MILLS_ESTRIN
+    // A/B: the same polynomial by Estrin's scheme (depth 5 instead of 20, ~1.7x the VALU
+    // instructions): whether the producers wait on the Horner chain's latency.  They do
+    // not: config 4 8.71 -> 10.25 ms, config 5 2.04 -> 2.35 ms per launch (r03s36) -- the
+    // book kernels are bound by VALU issue, so only fewer instructions would help.
+    const double u2 = u * u, u4 = u2 * u2, u8 = u4 * u4, u16 = u8 * u8;
+    const double p01 = fma(-0.48122354789588401, u, 0.30783718216692846);
+    const double p23 = fma(-0.13151258275835945, u, 0.29927575053510824);
+    const double p45 = fma(-0.0013327285592737549, u, 0.034655415072285041);
+    const double p67 = fma(0.00039784937176197925, u, -0.002353960594219441);
+    const double p89 = fma(-4.4835109354094885e-05, u, 0.00021086542652290141);
+    const double p1011 = fma(3.4217038844164288e-06, u, -2.7074245209317019e-05);
+    const double p1213 = fma(1.6391429736383158e-07, u, 4.1122801372346195e-06);
+    const double p1415 = fma(-1.4934329903924975e-07, u, -5.8954452073183568e-07);
+    const double p1617 = fma(3.5462265542512339e-08, u, 6.1229321472110077e-08);
+    const double p1819 = fma(-3.8907837965992227e-09, u, -1.6735307803068382e-09);
+    const double p20 = -4.4206737983570504e-10;
+    const double q0 = fma(p23, u2, p01), q1 = fma(p67, u2, p45), q2 = fma(p1011, u2, p89);
+    const double q3 = fma(p1415, u2, p1213), q4 = fma(p1819, u2, p1617);
+    const double g0 = fma(q1, u4, q0), g1 = fma(q3, u4, q2), g2 = fma(p20, u4, q4);
+    return fma(g2, u16, fma(g1, u8, g0));
+#endif
     double r = -4.4206737983570504e-10;
     r = fma_k(r, u, -3.8907837965992227e-09);
     r = fma_k(r, u, -1.6735307803068382e-09);
