@@ -599,15 +599,26 @@ struct BookEnv {
 };
 
 // The normal tail Q(a) = Phi(-a), a >= 0, as phi(a) R(a) with the Mills ratio
-// R(a) = sqrt(pi/2) erfcx(a / sqrt 2) a degree-20 polynomial in u = A - B / (a + c), c = 3.5:
+// R(a) = sqrt(pi/2) erfcx(a / sqrt 2) a degree-16 polynomial in u = A - B / (a + c), c = 5:
 // the Chebyshev fit on a in [0, 38.6] (Q underflows past it) re-expanded in powers of u
-// (coefficients below 0.49 in magnitude, so Horner loses nothing), 2.6e-13 relative on Q
-// against scipy.special.ndtr (tools/mills_fit.py).  Branch-free -- every lane of a wave
+// (coefficients below 0.39 in magnitude, so Horner loses nothing), 1.7e-12 relative on Q
+// against scipy.special.ndtr (tools/mills_fit.py).  The producers of the book kernels are
+// bound by VALU issue, so the degree is what costs: degree 16 against the former 20 at
+// c = 3.5 (2.6e-13, HE_MILLS_DEG16=0): config 4 8.77 -> 8.34 ms, config 5 2.04 -> 2.00 ms
+// per launch (r03s37), the book's P&L still far inside north_star's 1e-5.  Branch-free -- every lane of a wave
 // runs the same instructions whatever its d -- and phi is the caller's: d1 and d2 of a
 // Black-Scholes price share one exp (S phi(d1) = K e^{-r tau} phi(d2)).  Replaces two
 // library erfc per pair, each with its own exp and range branches (the book is an
 // extension without a reference; its bar is the oracle's P&L at 1e-5, test_gpu_parity.py).
+#ifndef HE_MILLS_DEG16
+#define HE_MILLS_DEG16 1
+#endif
+#if HE_MILLS_DEG16
+// degree 16 at c = 5 (tools/mills_fit.py): four FMAs fewer per tail than the former degree 20
+constexpr double kMillsA = 1.2590673575129534, kMillsB = 11.295336787564768, kMillsC = 5.0;
+#else
 constexpr double kMillsA = 1.1813471502590676, kMillsB = 7.6347150259067362, kMillsC = 3.5;
+#endif
 constexpr double kMillsMax = 37.4;                       // phi(37.4) ~ 1e-304: the tail is 0 past it
 constexpr double kInvSqrt2Pi = 0.39894228040143267794;
 #ifndef HE_MILLS_ESTRIN
@@ -641,6 +652,25 @@ __device__ __forceinline__ double mills(double a) {
     const double g0 = fma(q1, u4, q0), g1 = fma(q3, u4, q2), g2 = fma(p20, u4, q4);
     return fma(g2, u16, fma(g1, u8, g0));
 #endif
+#if HE_MILLS_DEG16
+    double r = 2.7428474899566849e-08;
+    r = fma_k(r, u, 1.1082671662043668e-08);
+    r = fma_k(r, u, -3.9869407228616424e-07);
+    r = fma_k(r, u, 5.0477032271454544e-08);
+    r = fma_k(r, u, 4.3841769522583659e-06);
+    r = fma_k(r, u, -5.963304400844242e-06);
+    r = fma_k(r, u, -4.1102680772883148e-05);
+    r = fma_k(r, u, 0.00016913403122505337);
+    r = fma_k(r, u, 4.3092976295952224e-05);
+    r = fma_k(r, u, -0.0026775922346088865);
+    r = fma_k(r, u, 0.013231527706031554);
+    r = fma_k(r, u, -0.041271314376590838);
+    r = fma_k(r, u, 0.097294627097245595);
+    r = fma_k(r, u, -0.18472286873481761);
+    r = fma_k(r, u, 0.29086958400118978);
+    r = fma_k(r, u, -0.38520383404522951);
+    r = fma_k(r, u, 0.23820001819943162);
+#else
     double r = -4.4206737983570504e-10;
     r = fma_k(r, u, -3.8907837965992227e-09);
     r = fma_k(r, u, -1.6735307803068382e-09);
@@ -662,6 +692,7 @@ __device__ __forceinline__ double mills(double a) {
     r = fma_k(r, u, 0.29927575053510824);
     r = fma_k(r, u, -0.48122354789588401);
     r = fma_k(r, u, 0.30783718216692846);
+#endif
     return r;
 }
 
@@ -786,6 +817,11 @@ __device__ __forceinline__ double book_value(const Params& p, double S, double v
 // mills over NN arguments in lockstep (the same operations per element: the same bits).
 template <int NN>
 __device__ __forceinline__ void mills_n(const double* a, double* out) {
+#if HE_MILLS_DEG16
+#pragma unroll
+    for (int h = 0; h < NN; ++h) out[h] = mills(a[h]);
+    return;
+#endif
     double u[NN], r[NN];
 #pragma unroll
     for (int h = 0; h < NN; ++h) {
