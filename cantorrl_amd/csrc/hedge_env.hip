@@ -625,6 +625,9 @@ constexpr double kInvSqrt2Pi = 0.39894228040143267794;
 #define HE_MILLS_ESTRIN 0
 #endif
 __device__ __forceinline__ double mills(double a) {
+#if HE_BOOK_DIAG == 1
+    return a * 0.25;  // diagnostic builds only (tools/gpu): the book without its tails
+#endif
     const double d = a + kMillsC;                        // in [3.5, 41]: no special cases
     double y = __builtin_amdgcn_rcp(d);
     y = fma(fma(-d, y, 1.0), y, y);                      // two Newton steps: 1 / d to the last bits
@@ -701,13 +704,57 @@ __device__ __forceinline__ double tail_arg(double d) {
     const double a = fabs(d);
     return a < kMillsMax ? a : kMillsMax;                // NaN -> kMillsMax (the price is NaN anyway)
 }
-__device__ __forceinline__ double phi_of(double a) { return exp_k(-0.5 * (a * a)) * kInvSqrt2Pi; }
+#ifndef HE_BOOK_EXP_FAST
+#define HE_BOOK_EXP_FAST 1
+#endif
+// exp(x) for the book's phi, x = -a^2 / 2 in [-700, 0] (a <= kMillsMax): exp_k's Cody-Waite
+// reduction, then e^r as its degree-11 Taylor polynomial (truncation < 7e-15 relative on
+// |r| <= ln2 / 2; the book's bar is 1e-5 on P&L) without the Fast2Sum or the range branch:
+// 16 VALU instructions instead of exp_k's 26.
+__device__ __forceinline__ double exp_book(double x) {
+    const double k = rint(x * 1.4426950408889634074);
+    const double rh = fma_kb(-k, 6.93147180369123816490e-01, x);
+    const double r = fma_kb(-k, 1.90821492927058770002e-10, rh);
+    double q = 1.0 / 39916800.0;                  // 1/11!
+    q = fma_k(q, r, 1.0 / 3628800.0);
+    q = fma_k(q, r, 1.0 / 362880.0);
+    q = fma_k(q, r, 1.0 / 40320.0);
+    q = fma_k(q, r, 1.0 / 5040.0);
+    q = fma_k(q, r, 1.0 / 720.0);
+    q = fma_k(q, r, 1.0 / 120.0);
+    q = fma_k(q, r, 1.0 / 24.0);
+    q = fma_k(q, r, 1.0 / 6.0);
+    q = fma_k(q, r, 0.5);
+    q = fma_k(q, r, 1.0);
+    q = fma_k(q, r, 1.0);
+    return ldexp(q, (int)k);
+}
+__device__ __forceinline__ double phi_of(double a) {
+#if HE_BOOK_EXP_FAST
+    return exp_book(-0.5 * (a * a)) * kInvSqrt2Pi;
+#else
+    return exp_k(-0.5 * (a * a)) * kInvSqrt2Pi;
+#endif
+}
 
-// N(d) and N(-d) from the tail q = Q(|d|)
+// N(d) and N(-d) from the tail q = Q(|d|).  HE_BOOK_NCDF_FAST (A/B, off): 0.5 -+ s (0.5 - q)
+// with s = sign(d), three VALU instructions per pair instead of five -- but the small tail
+// comes back as 0.5 - (0.5 - q), an absolute 2^-54 error that the barrier formula's
+// (H/S)^(2 lam) factors amplify past the 1e-5 P&L bar (config 5's full-size slice, r03s40).
+#ifndef HE_BOOK_NCDF_FAST
+#define HE_BOOK_NCDF_FAST 0
+#endif
 __device__ __forceinline__ void ncdf_from_tail(double d, double q, double* pos, double* neg) {
+#if HE_BOOK_NCDF_FAST
+    const double h = 0.5 - q;
+    const double sh = __builtin_copysign(h, d);
+    *pos = 0.5 + sh;
+    *neg = 0.5 - sh;
+#else
     const bool p = d > 0.0;
     *pos = p ? 1.0 - q : q;
     *neg = p ? q : 1.0 - q;
+#endif
 }
 
 // One book option (branch-free in the lane-varying quantities: remaining steps, running max).
@@ -794,6 +841,9 @@ __device__ __forceinline__ double book_value(const Params& p, double S, double v
         b.lam = (p.r_d + 0.5 * b.s2) / b.s2;
     }
     double B = 0.0;
+#if HE_BOOK_DIAG == 2
+    return S * 1e-3;  // diagnostic builds only: no book pricing at all
+#endif
 #ifdef HE_BOOK_UNROLL
 #pragma unroll HE_BOOK_UNROLL
 #endif
