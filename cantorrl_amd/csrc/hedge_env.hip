@@ -707,6 +707,9 @@ __device__ __forceinline__ double tail_arg(double d) {
 #ifndef HE_BOOK_EXP_FAST
 #define HE_BOOK_EXP_FAST 1
 #endif
+#ifndef HE_BOOK_EXP_FAST_UO
+#define HE_BOOK_EXP_FAST_UO 0  // A/B: the barrier formula's powers through exp_book_g too
+#endif
 // exp(x) for the book's phi, x = -a^2 / 2 in [-700, 0] (a <= kMillsMax): exp_k's Cody-Waite
 // reduction, then e^r as its degree-11 Taylor polynomial (truncation < 7e-15 relative on
 // |r| <= ln2 / 2; the book's bar is 1e-5 on P&L) without the Fast2Sum or the range branch:
@@ -728,6 +731,16 @@ __device__ __forceinline__ double exp_book(double x) {
     q = fma_k(q, r, 1.0);
     q = fma_k(q, r, 1.0);
     return ldexp(q, (int)k);
+}
+// exp_book with exp_k's range guard, for the barrier formula's (H/S) powers (any sign,
+// +-inf when S is 0 or inf)
+__device__ __forceinline__ double exp_book_g(double x) {
+#if HE_BOOK_EXP_FAST && HE_BOOK_EXP_FAST_UO
+    if (!(fabs(x) < 700.0)) return exp(x);
+    return exp_book(x);
+#else
+    return exp_k(x);
+#endif
 }
 __device__ __forceinline__ double phi_of(double a) {
 #if HE_BOOK_EXP_FAST
@@ -795,8 +808,8 @@ __device__ __forceinline__ double book_option(const Params& p, const BookOpt& o,
             const double ert = e[3];                             // e^{r tau}
             const double ax = tail_arg(x1), ay = tail_arg(y), ay1 = tail_arg(y1);
             const double px = phi_of(ax), py = phi_of(ay), py1 = phi_of(ay1);
-            const double sh = exp_k(-lhs);                       // S / H
-            const double hs = exp_k(lhs);                        // H / S
+            const double sh = exp_book_g(-lhs);                  // S / H
+            const double hs = exp_book_g(lhs);                   // H / S
             const double ax_ = tail_arg(x1 - sst), ay_ = tail_arg(y - sst), ay1_ = tail_arg(y1 - sst);
             const double qx = px * mills(ax), qx_ = (px * (sh * ert)) * mills(ax_);
             const double qy = py * mills(ay), qy_ = (py * ((hs * hs) * (S * o.invK) * ert)) * mills(ay_);
@@ -808,7 +821,7 @@ __device__ __forceinline__ double book_option(const Params& p, const BookOpt& o,
             ncdf_from_tail(y - sst, qy_, &ny_, &my_);
             ncdf_from_tail(y1, qy1, &ny1, &my1);
             ncdf_from_tail(y1 - sst, qy1_, &ny1_, &my1_);
-            const double p2l = exp_k((2.0 * b.lam) * lhs);       // (H/S)^(2 lam)
+            const double p2l = exp_book_g((2.0 * b.lam) * lhs);  // (H/S)^(2 lam)
             const double p2l2 = p2l * (sh * sh);                 // (H/S)^(2 lam - 2)
             const double cui = S * nx - Kd * nx_ - S * p2l * (my - my1) + Kd * p2l2 * (my_ - my1_);
             v = v - cui;
