@@ -205,6 +205,9 @@ def parse(argv=None):
                     help="env: the hedging-env step (headline); rbergomi: the rough-Bergomi MC mark generator")
     ap.add_argument("--rb-paths", type=int, default=2048, help="rbergomi: paths per GPU (x 252 days x call/put)")
     ap.add_argument("--rb-normals", choices=["f64", "f32"], default="f64")
+    ap.add_argument("--gather-rollout", action="store_true",
+                    help="N > 1: also all-gather each boundary's rollout tensors (obs / reward / terminated of "
+                         "the last he_rollout) in global env order (SURVEY 8(e): small N only)")
     return ap.parse_args(argv)
 
 
@@ -255,25 +258,41 @@ def _cpu_all_cores(seconds, procs, n_per, shard):
     return sum(s / e for s, e in res)
 
 
-def cpu_baseline(seconds):
-    """SURVEY 8(d) / BASELINE.md section 2: the oracle on the host at N = 65,536 (the
-    headline workload) and N = 256 (config 1), one process with one thread, then all
-    granted cores (one process per core; at 65,536 each process steps its 65,536 / P
-    shard of the global env ids).  `value` is the 65,536-env all-cores rate.
+def host_cores():
+    """(cores to use, affinity-mask count, where the first number comes from).
 
-    Must run before anything initialises the GPU: the all-core legs fork worker processes.
-    """
-    N = CONFIGS[2]["envs"]
+    SURVEY 8(d) asks for every host core in the affinity mask.  On the GPU pool the mask
+    shows the whole machine (256 CPUs) while the job's share is the per-GPU grant the pool
+    exports as OMP_NUM_THREADS (16 per GPU; the pool's rules: "size worker pools to the box's
+    CPU share (16 for one GPU): nproc and os.cpu_count() show the whole machine's CPUs") --
+    a pool of 256 workers would run on other jobs' cores.  So: the affinity count, capped by
+    that grant when the environment states one."""
     try:
         avail = len(os.sched_getaffinity(0))
     except AttributeError:
         avail = os.cpu_count() or 1
-    procs = max(1, min(avail, 16))   # the GPU box grants 16 host cores per GPU
+    grant = os.environ.get("OMP_NUM_THREADS", "")
+    if grant.isdigit() and 0 < int(grant) < avail:
+        return int(grant), avail, (f"OMP_NUM_THREADS={grant}: the host cores this job is granted per GPU "
+                                   f"({avail} CPUs in the affinity mask belong to the whole machine)")
+    return avail, avail, f"every core of the affinity mask ({avail})"
+
+
+def cpu_baseline(seconds):
+    """SURVEY 8(d) / BASELINE.md section 2: the oracle on the host at N = 65,536 (the
+    headline workload) and N = 256 (config 1), one process with one thread, then all
+    granted cores (host_cores(): one process per core; at 65,536 each process steps its
+    65,536 / P shard of the global env ids).  `value` is the 65,536-env all-cores rate.
+
+    Must run before anything initialises the GPU: the all-core legs fork worker processes.
+    """
+    N = CONFIGS[2]["envs"]
+    procs, avail, why = host_cores()
     s1, e1 = _cpu_sample(seconds, n=N)
     vN = _cpu_all_cores(seconds, procs, N // procs, shard=True)
     s256, e256 = _cpu_sample(seconds)
     v256 = _cpu_all_cores(seconds, procs, 256, shard=False)
-    return dict(value=vN, unit="env-steps/s", cores=procs, kind="port",
+    return dict(value=vN, unit="env-steps/s", cores=procs, affinity_cores=avail, cores_source=why, kind="port",
                 sample=f"oracle/hedging_oracle.py OracleVecEnv GBM (the headline workload), {N} envs as {procs} "
                        f"processes x {N // procs} envs x {seconds:.0f} s (NumPy, 1 thread each; {avail} cores in "
                        f"affinity mask)",
@@ -322,6 +341,8 @@ class Runner:
         self.dist, self.gathered = dist, gathered
         self.summaries = torch.zeros((args.envs, 4), dtype=torch.float32, device=acts.device)
         self.gathers = 0
+        self.boundary_events = []   # (start, summaries+gather done, rollout tensors gathered) per boundary
+        self.rollout_gathered = None
         self.lib, self.h = env.lib, env._h
         self.ring = acts.shape[0]
         n = args.envs
@@ -386,12 +407,35 @@ class Runner:
 
     def gather(self, cs):
         """The rollout-buffer boundary (train_ppo_v2.py:48, n_steps = 256): every rank's
-        per-env episode summaries, stream-ordered behind the rollouts that made them."""
+        per-env episode summaries, stream-ordered behind the rollouts that made them; with
+        --gather-rollout also the last rollout's obs / reward / terminated tensors
+        [K, N, ...] of every rank, in global env order ([K, world * N, ...]).  Each boundary
+        is bracketed by events on the launching stream (RCCL: the collective's completion
+        is ordered into this stream; gloo: the host copy syncs it)."""
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+        ev[0].record(self.stream)
         st = self.lib.he_episode_summaries(self.h, self.summaries.data_ptr(), cs)
         if st:
             raise RuntimeError(self.lib.he_last_error(self.h).decode())
         gather_summaries(self.dist, self.summaries, self.gathered)
+        ev[1].record(self.stream)
+        if self.args.gather_rollout and self.mode == "rollout":
+            from cantorrl_amd import dist as hd
+            host = self.dist.get_backend() == "gloo"
+            self.rollout_gathered = [hd.gather_rollout(t.cpu() if host else t, env_dim=1)
+                                     for t in (self.ro, self.rr, self.rt)]
+        ev[2].record(self.stream)
+        self.boundary_events.append(ev)
         self.gathers += 1
+
+    def boundary_us(self):
+        """Mean device time per boundary on the stream: (summaries + gather, rollout-tensor
+        gather) in us, over the timed region's boundaries."""
+        if not self.boundary_events:
+            return None, None
+        a = np.array([e[0].elapsed_time(e[1]) for e in self.boundary_events]) * 1e3
+        b = np.array([e[1].elapsed_time(e[2]) for e in self.boundary_events]) * 1e3
+        return float(a.mean()), (float(b.mean()) if self.args.gather_rollout else None)
 
 
 GATHER_EVERY = 256  # train_ppo_v2.py:48 n_steps
@@ -641,6 +685,7 @@ def timed(runner, K, W, dist):
             torch.cuda.synchronize()
             W = int(w.item())
     runner.dist = d_saved
+    runner.boundary_events = []   # the timed region's boundaries only
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
@@ -709,6 +754,53 @@ def roofline(mode, n, kern_ms, rk, book=False, market="gbm", lds=False):
                 kernel_gbs=round(own / (kern_ms * 1e-3) / 1e9, 1))
 
 
+def config_bound(cfg):
+    """The resource that bounds a configuration's dominant kernel, fixed per config (not by
+    whether the counters ran): with a liability book or Heston the producers' f64 market work
+    (8 Black-Scholes prices per env-step, the variance chain + barrier pricer) bounds the LDS
+    kernel -- VALU issue; otherwise the step I/O -- HBM."""
+    return "valu" if (cfg["gen"].get("book") or cfg["mode"] == "heston") else "hbm"
+
+
+def finish_roofline(roof, cfg, valu, pmc, kern_ms):
+    """Attach the PMC results (VALU issue, HBM traffic) to the HBM roofline `roof` and, for a
+    VALU-bound configuration (config_bound), make the VALU issue rate the headline figure: the
+    issue rate against the bound of the kernel's own f64 / other mix (a wave64 instruction
+    every 2 cycles per SIMD, f64 every 4), the HBM side kept under "hbm".  Without the VALU
+    pass such a line still says "valu" and leaves the figure null, with a note."""
+    if valu[0]:
+        # the dominant kernel by profiled cycles
+        dom = max(valu[0], key=lambda k: valu[0][k]["cycles_profiled"])
+        v = dict(valu[0][dom])
+        if dom in ("lds_rollout_kernel", "lds_replay_kernel") or (dom.startswith("step") and "market" not in dom):
+            v["f64_tflops"] = round(v["f64_flop"] / (kern_ms * 1e-3) / 1e12, 3)
+            v["f64_frac_of_vector_peak"] = round(v["f64_tflops"] / FP64_VECTOR_PEAK_TFLOPS, 4)
+        roof["valu"] = dict(kernel=dom, peak_f64_tflops=FP64_VECTOR_PEAK_TFLOPS, **v)
+        roof["valu_by_kernel"] = valu[0]
+    elif valu[1] != "skipped":
+        roof["valu_note"] = valu[1]
+    if pmc[0] is not None:
+        roof["traffic"] = int(pmc[0])
+        roof["traffic_over_bytes"] = round(pmc[0] / roof["bytes_per_launch"], 4)
+        roof["traffic_counters_kb"] = {k: round(v, 1) for k, v in pmc[1].items()}
+    else:
+        roof["traffic_note"] = pmc[1]
+    if config_bound(cfg) != "valu":
+        return roof
+    hbm = {k: roof.pop(k) for k in ("achieved", "peak", "unit", "frac")}
+    hbm["bound_note"] = "not the bound of this configuration (see valu)"
+    v = roof.get("valu")
+    if v is not None and v["kernel"] == "lds_rollout_kernel":
+        head = dict(achieved=v["issue_per_simd_cycle"], peak=v["issue_bound_per_simd_cycle"], frac=v["valu_issue_frac"])
+    else:
+        head = dict(achieved=None, peak=None, frac=None)
+        roof["valu_note"] = ("VALU issue not measured in this run (the PMC pass was %s): the bound is still VALU issue "
+                             "of the LDS producers; see the HBM figure under 'hbm' for the I/O side" %
+                             (valu[1] if valu[1] else "absent"))
+    return dict(bound="valu", unit="VALU wave-instructions per SIMD-cycle", traffic=roof.pop("traffic", None),
+                hbm=hbm, **head, **{k: x for k, x in roof.items() if k != "bound"})
+
+
 # ---------------------------------------------------------------------- rbergomi workload
 RB_MC, RB_DAYS = 5000, 252
 
@@ -744,16 +836,13 @@ def rb_cpu_baseline(seconds, base):
     """1 thread and one process per granted host core (forked before GPU init)."""
     import multiprocessing as mp
     n1, el1 = _rb_cpu_sample(seconds, base)
-    try:
-        avail = len(os.sched_getaffinity(0))
-    except AttributeError:
-        avail = os.cpu_count() or 1
-    procs = max(1, min(avail, 16))
+    procs, avail, why = host_cores()
     ctx = mp.get_context("fork")
     b = ctx.Barrier(procs)
     with ctx.Pool(procs, initializer=_pool_init, initargs=(b,)) as pool:
         res = pool.map(_rb_pool_task, [(seconds, tuple(base), i + 1) for i in range(procs)])
-    return dict(value=sum(n / e for n, e in res), unit="options/s", cores=procs, kind="port",
+    return dict(value=sum(n / e for n, e in res), unit="options/s", cores=procs, affinity_cores=avail,
+                cores_source=why, kind="port",
                 sample=f"oracle/rbergomi_oracle.py price_options (the reference's FFT form), batches of 8 options x "
                        f"{RB_MC} MC paths, {procs} processes x {seconds:.0f} s (NumPy, 1 thread each)",
                 single_core_value=n1 / el1,
@@ -981,7 +1070,18 @@ def main(argv=None):
                             "all-gathered to [world * envs, 4]", backend="rccl" if backend == "nccl" else backend,
                        every_steps=GATHER_EVERY,
                        bytes_per_rank=n * 16, gathers=runner.gathers)
+        if backend != "nccl":
+            payload["sync"] = ("host-synced rehearsal: gather_summaries copies the device summaries to the host "
+                               "(local.to(cpu), a stream sync) and gathers them over gloo; the boundary time "
+                               "measures that host round trip, not RCCL")
         payload.update(summarize_payload(runner.gathered))
+        if args.gather_rollout and runner.rollout_gathered is not None:
+            ro, rr, rt = runner.rollout_gathered
+            payload["rollout_tensors"] = dict(
+                what="the last he_rollout's obs / reward / terminated [K, N, ...] of every rank, gathered along the "
+                     "env dimension into [K, world * N, ...] (global env order, cantorrl_amd.dist.gather_rollout "
+                     "env_dim=1)", shapes=[list(ro.shape), list(rr.shape), list(rt.shape)],
+                bytes_per_rank=int(sum(t.numel() * t.element_size() for t in (ro, rr, rt)) // world))
     hev = HipEvents()
     probe_ms = kernel_time_ms(hev, runner, 64 if args.mode == "rollout" else 256)
     env.close()
@@ -994,6 +1094,25 @@ def main(argv=None):
     launches = K // runner.chunk
     region = (lds or (replay and args.mode == "rollout")) and world == 1
     kern_ms = dev_ms / launches if region else probe_ms
+    per_rank = None
+    if dist is not None:
+        # every rank's own timers, so an N-rank line explains itself: the step kernel's
+        # per-dispatch probe, the device time per launch over the timed region (kernels +
+        # the boundaries riding on the stream), and the boundary's device time
+        b_us, r_us = runner.boundary_us()
+        mine = torch.tensor([rank, probe_ms * 1e3, dev_ms / launches * 1e3,
+                             b_us if b_us is not None else float("nan"), r_us if r_us is not None else float("nan"),
+                             runner.gathers, wall], dtype=torch.float64,
+                            device="cpu" if backend == "gloo" else dev)
+        allv = [torch.empty_like(mine) for _ in range(world)]
+        dist.all_gather(allv, mine)
+        per_rank = []
+        for v in allv:
+            v = v.cpu().tolist()
+            per_rank.append(dict(rank=int(v[0]), kernel_us_probe=round(v[1], 3), device_us_per_launch=round(v[2], 3),
+                                 boundary_us=None if v[3] != v[3] else round(v[3], 2),
+                                 rollout_gather_us=None if v[4] != v[4] else round(v[4], 2),
+                                 boundaries=int(v[5]), wall_s=round(v[6], 6)))
 
     roof = roofline(args.mode, n, kern_ms, args.rollout_k, has_book, tile_layout(cfg["mode"], n), lds)
     roof["kernel_us_source"] = ("HIP events around the timed region / %d launches" % launches if region else
@@ -1009,35 +1128,7 @@ def main(argv=None):
         if mkt_ms / M_BLOCK > kern_ms / steps_per_launch:
             roof["dominant_kernel"] = "market_kernel (the HBM market tile, %.1f us per step vs %.1f for the steps)" % (
                 mkt_ms * 1e3 / M_BLOCK, kern_ms * 1e3 / steps_per_launch)
-    if valu[0]:
-        # the dominant kernel by profiled cycles; with a book it is VALU-bound: its issue
-        # rate against the bound of its f64 mix, and its f64 FLOP rate at the live duration
-        dom = max(valu[0], key=lambda k: valu[0][k]["cycles_profiled"])
-        v = dict(valu[0][dom])
-        if dom in ("lds_rollout_kernel", "lds_replay_kernel") or (dom.startswith("step") and "market" not in dom):
-            v["f64_tflops"] = round(v["f64_flop"] / (kern_ms * 1e-3) / 1e12, 3)
-            v["f64_frac_of_vector_peak"] = round(v["f64_tflops"] / FP64_VECTOR_PEAK_TFLOPS, 4)
-        roof["valu"] = dict(kernel=dom, peak_f64_tflops=FP64_VECTOR_PEAK_TFLOPS, **v)
-        roof["valu_by_kernel"] = valu[0]
-    elif valu[1] != "skipped":
-        roof["valu_note"] = valu[1]
-    if pmc[0] is not None:
-        roof["traffic"] = int(pmc[0])
-        roof["traffic_over_bytes"] = round(pmc[0] / roof["bytes_per_launch"], 4)
-        roof["traffic_counters_kb"] = {k: round(v, 1) for k, v in pmc[1].items()}
-    else:
-        roof["traffic_note"] = pmc[1]
-    if (has_book or cfg["mode"] == "heston") and roof.get("valu") and roof["valu"]["kernel"] == "lds_rollout_kernel":
-        # configs 4 / 5: the producers' f64 market work (8 Black-Scholes prices per env-step,
-        # or the Heston chain + barrier pricer) bounds the kernel, not HBM.  The roofline is
-        # the VALU issue rate against the issue bound of the kernel's own f64 / other mix (a
-        # wave64 instruction every 2 cycles per SIMD, f64 every 4); the HBM side stays under "hbm".
-        v = roof["valu"]
-        hbm = {k: roof.pop(k) for k in ("achieved", "peak", "unit", "frac")}
-        hbm["bound_note"] = "not the bound of this configuration (see valu)"
-        roof = dict(bound="valu", achieved=v["issue_per_simd_cycle"], peak=v["issue_bound_per_simd_cycle"],
-                    unit="VALU wave-instructions per SIMD-cycle", frac=v["valu_issue_frac"],
-                    traffic=roof.pop("traffic", None), hbm=hbm, **{k: x for k, x in roof.items() if k != "bound"})
+    roof = finish_roofline(roof, cfg, valu, pmc, kern_ms)
 
     step_api = None
     if world == 1 and args.mode != "graph" and not args.no_step_api:
@@ -1085,6 +1176,13 @@ def main(argv=None):
         }
         if payload is not None:
             line["gather"] = payload
+            line["per_rank"] = per_rank
+            bu = [r["boundary_us"] for r in per_rank if r["boundary_us"] is not None]
+            if bu:
+                payload["boundary_us_per_256_steps"] = dict(
+                    max=max(bu), mean=round(sum(bu) / len(bu), 2),
+                    what="device time on the launching stream of he_episode_summaries + the all-gather, per "
+                         "rollout-buffer boundary (every %d steps), the timed region's boundaries" % GATHER_EVERY)
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()

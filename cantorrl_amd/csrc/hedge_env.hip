@@ -45,24 +45,10 @@ using namespace he;
 namespace {
 
 #define GLOBAL __attribute__((address_space(1)))
-// HE_OPAQUE_SEL (default): values a select picks from are pinned in VGPRs first, so the
-// backend keeps the select instead of a divergent branch around their computation.
-#ifndef HE_OPAQUE_SEL
-#define HE_OPAQUE_SEL 1
-#endif
-#ifndef HE_OBS_PIN
-#define HE_OBS_PIN(a) asm volatile("" : "+v"(a))
-#endif
-#ifndef HE_OPAQUE_ASM
-#define HE_OPAQUE_ASM asm volatile
-#endif
-#if HE_OPAQUE_SEL
-#define HE_OPAQUE1(a) HE_OPAQUE_ASM("" : "+v"(a))
-#define HE_OPAQUE3(a, b, c) HE_OPAQUE_ASM("" : "+v"(a), "+v"(b), "+v"(c))
-#else
-#define HE_OPAQUE1(a) do {} while (0)
-#define HE_OPAQUE3(a, b, c) do {} while (0)
-#endif
+// Values a select picks from are pinned in VGPRs first (opaque), so the backend keeps the
+// select instead of a divergent branch around their computation.
+#define HE_OPAQUE1(a) asm volatile("" : "+v"(a))
+#define HE_OPAQUE3(a, b, c) asm volatile("" : "+v"(a), "+v"(b), "+v"(c))
 typedef float v2f __attribute__((ext_vector_type(2)));
 typedef float v4f __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ float4 ld4(const GLOBAL v4f* p, int64_t k) {
@@ -99,37 +85,26 @@ __device__ __forceinline__ void st3(float4* p, int64_t k, float x, float y, floa
 }
 
 constexpr int kBlock = 256;      // step kernel: threads per workgroup (4 waves)
-#ifndef HE_STEP_EPW
-#define HE_STEP_EPW 64
-#endif
-constexpr int kEpw = HE_STEP_EPW;          // step kernel: envs per wave (64, or 32 = 2x the waves)
+// step kernel: envs per wave (one per lane; 32 per wave, twice the waves, measured -10 % on the
+// Gym-API path, r02s8)
+constexpr int kEpw = 64;
 constexpr int kEpb = (kBlock / 64) * kEpw; // step kernel: envs per workgroup
 constexpr int kObs = HE_OBS_DIM;
 constexpr int kMktEnvs = 32;     // market kernel: envs per workgroup (half a wave wide)
 constexpr int kMktLanes = 8;     //                slot-lanes per env (4 waves, 16.6 KB LDS)
 constexpr int kMaxBlock = 64;    // max market block length M
-#ifndef HE_ROLLOUT_PREFETCH
-#define HE_ROLLOUT_PREFETCH 4
-#endif
-constexpr int kRolloutPrefetch = HE_ROLLOUT_PREFETCH;  // rollout: steps of inputs in flight
-#ifndef HE_REPLAY_PREFETCH
-#define HE_REPLAY_PREFETCH 8
-#endif
+constexpr int kRolloutPrefetch = 4;  // rollout: steps of inputs in flight
 // replay rollouts: steps of path rows in flight (config 6, same box: D = 4 585 us per 256-step
 // launch, D = 8 574-576 us, r03s4)
-constexpr int kReplayPrefetch = HE_REPLAY_PREFETCH;
-#ifndef HE_MKT_WAVES
-#define HE_MKT_WAVES 2  // market_kernel: min waves per SIMD (3 is faster alone, slower beside rollouts)
-#endif
+constexpr int kReplayPrefetch = 8;
+constexpr int kMktWaves = 2;  // market_kernel: min waves per SIMD (3 is faster alone, slower beside rollouts)
 constexpr int64_t kPrefetchMinEnvs = 131072;  // auto prefetch for single steps from here
 // GBM: obs greeks evaluated by the step kernel (no tileB) from this many envs.  A
 // rollout wave at 65,536 envs (one wave per SIMD) pays the f32 greeks' dependent
 // VALU latency in full (3.19e10 -> 2.88e10 env-steps/s), while at 1,048,576 envs the
 // 12 bytes per env-step saved win (2.95e10 -> 3.68e10; MI355X, he_rollout K=64).
-#ifndef HE_GREEKS_IN_STEP_MIN_ENVS
-#define HE_GREEKS_IN_STEP_MIN_ENVS 262144
-#endif
-constexpr int64_t kGreeksInStepMinEnvs = HE_GREEKS_IN_STEP_MIN_ENVS;
+// (HE_GREEKS_IN_STEP_MIN_ENVS in the environment at he_create overrides it: tests, A/B)
+constexpr int64_t kGreeksInStepMinEnvs = 262144;
 
 // ------------------------------------------------------------------ parameters
 // One option of the liability book (he_book_option), device copy: q100 = quantity*100.
@@ -401,19 +376,10 @@ __device__ __forceinline__ float4 greeks_fast(const Params& p, float S, float v)
 }
 
 // The obs greeks of a replay row (table_greeks_kernel at load, the replay LDS loaders per
-// row): greeks(), the reference's f64 chain.  HE_REPLAY_GREEKS_FAST=1 (A/B): greeks_fast at
-// the row's own variance, as Heston's generate mode (within 4 f32 ulp, parity green) --
-// the loaders' busy cycles drop (1,650 -> 1,580 per step) but config 6 does not move (418 /
-// 420 against 416 / 418 us per launch, r03s18): the loaders are not its critical wave.
-#ifndef HE_REPLAY_GREEKS_FAST
-#define HE_REPLAY_GREEKS_FAST 0
-#endif
+// row): greeks(), the reference's f64 chain.  (greeks_fast at the row's own variance was
+// A/B-tested: the loaders' busy cycles drop, config 6 does not move -- r03s18.)
 __device__ __forceinline__ float4 replay_greeks(const Params& p, float S, float v) {
-#if HE_REPLAY_GREEKS_FAST
-    return greeks_fast<false>(p, S, v);
-#else
     return greeks<false>(p, S, v);
-#endif
 }
 
 // greeks_fast<true> for the lean LDS obs stepper: the handle's sigma, tenor and sst are
@@ -443,41 +409,6 @@ __device__ __forceinline__ float4 greeks_lean(float S, float num_drift, float in
     pd = tiny ? pt : pd;
     gam = tiny ? 0.0f : gam;
     return make_float4(cd, gam, pd, 0.0f);
-}
-
-// greeks_lean of NN prices as interleaved chains: each stage over all NN elements before
-// the next (ILP across the elements), the per-element operations of greeks_lean, so the
-// same bits.
-template <int NN>
-__device__ __forceinline__ void greeks_lean_n(const float* S, float num_drift, float inv_sst_f, float sstf,
-                                              float* cd, float* gam, float* pd) {
-    float K[NN], d1[NN], x[NN], tail[NN];
-#pragma unroll
-    for (int j = 0; j < NN; ++j) {
-        K[j] = rintf(S[j]);
-        d1[j] = (logf(S[j] / np_maxf(K[j], 1e-6f)) + num_drift) * inv_sst_f;
-    }
-#pragma unroll
-    for (int j = 0; j < NN; ++j) {
-        x[j] = d1[j] * 0.70710678118654752f;
-        tail[j] = 0.5f * erfcf(fabsf(x[j]));
-    }
-#pragma unroll
-    for (int j = 0; j < NN; ++j) {
-        const float gd = S[j] * sstf;
-        float ge = (expf(-0.5f * (d1[j] * d1[j])) * 0.398942280401432678f) * __builtin_amdgcn_rcpf(gd);
-        HE_OPAQUE1(ge);
-        const float gm = (fabsf(gd) < 1e-9f) ? 0.0f : ge;
-        const bool tiny = S[j] <= 1e-6f;
-        const float c = (x[j] >= 0.0f) ? 1.0f - tail[j] : tail[j];
-        const float q = (x[j] >= 0.0f) ? -tail[j] : tail[j] - 1.0f;
-        float ct = (K[j] == 0.0f) ? 0.5f : ((K[j] > 0.0f) ? 0.0f : 1.0f);
-        float pt = (K[j] == 0.0f) ? -0.5f : ((K[j] < 0.0f) ? 0.0f : -1.0f);
-        HE_OPAQUE3(ct, pt, ge);
-        cd[j] = tiny ? ct : c;
-        pd[j] = tiny ? pt : q;
-        gam[j] = tiny ? 0.0f : gm;
-    }
 }
 
 // ------------------------------------------------------------------ observation
@@ -604,26 +535,15 @@ struct BookEnv {
 // (coefficients below 0.39 in magnitude, so Horner loses nothing), 1.7e-12 relative on Q
 // against scipy.special.ndtr (tools/mills_fit.py).  The producers of the book kernels are
 // bound by VALU issue, so the degree is what costs: degree 16 against the former 20 at
-// c = 3.5 (2.6e-13, HE_MILLS_DEG16=0): config 4 8.77 -> 8.34 ms, config 5 2.04 -> 2.00 ms
+// c = 3.5 (2.6e-13): config 4 8.77 -> 8.34 ms, config 5 2.04 -> 2.00 ms
 // per launch (r03s37), the book's P&L still far inside north_star's 1e-5.  Branch-free -- every lane of a wave
 // runs the same instructions whatever its d -- and phi is the caller's: d1 and d2 of a
 // Black-Scholes price share one exp (S phi(d1) = K e^{-r tau} phi(d2)).  Replaces two
 // library erfc per pair, each with its own exp and range branches (the book is an
 // extension without a reference; its bar is the oracle's P&L at 1e-5, test_gpu_parity.py).
-#ifndef HE_MILLS_DEG16
-#define HE_MILLS_DEG16 1
-#endif
-#if HE_MILLS_DEG16
-// degree 16 at c = 5 (tools/mills_fit.py): four FMAs fewer per tail than the former degree 20
 constexpr double kMillsA = 1.2590673575129534, kMillsB = 11.295336787564768, kMillsC = 5.0;
-#else
-constexpr double kMillsA = 1.1813471502590676, kMillsB = 7.6347150259067362, kMillsC = 3.5;
-#endif
 constexpr double kMillsMax = 37.4;                       // phi(37.4) ~ 1e-304: the tail is 0 past it
 constexpr double kInvSqrt2Pi = 0.39894228040143267794;
-#ifndef HE_MILLS_ESTRIN
-#define HE_MILLS_ESTRIN 0
-#endif
 __device__ __forceinline__ double mills(double a) {
 #if HE_BOOK_DIAG == 1
     return a * 0.25;  // diagnostic builds only (tools/gpu): the book without its tails
@@ -633,29 +553,6 @@ __device__ __forceinline__ double mills(double a) {
     y = fma(fma(-d, y, 1.0), y, y);                      // two Newton steps: 1 / d to the last bits
     y = fma(fma(-d, y, 1.0), y, y);
     const double u = fma(-kMillsB, y, kMillsA);
-#if HE_MILLS_ESTRIN
-    // A/B: the same polynomial by Estrin's scheme (depth 5 instead of 20, ~1.7x the VALU
-    // instructions): whether the producers wait on the Horner chain's latency.  They do
-    // not: config 4 8.71 -> 10.25 ms, config 5 2.04 -> 2.35 ms per launch (r03s36) -- the
-    // book kernels are bound by VALU issue, so only fewer instructions would help.
-    const double u2 = u * u, u4 = u2 * u2, u8 = u4 * u4, u16 = u8 * u8;
-    const double p01 = fma(-0.48122354789588401, u, 0.30783718216692846);
-    const double p23 = fma(-0.13151258275835945, u, 0.29927575053510824);
-    const double p45 = fma(-0.0013327285592737549, u, 0.034655415072285041);
-    const double p67 = fma(0.00039784937176197925, u, -0.002353960594219441);
-    const double p89 = fma(-4.4835109354094885e-05, u, 0.00021086542652290141);
-    const double p1011 = fma(3.4217038844164288e-06, u, -2.7074245209317019e-05);
-    const double p1213 = fma(1.6391429736383158e-07, u, 4.1122801372346195e-06);
-    const double p1415 = fma(-1.4934329903924975e-07, u, -5.8954452073183568e-07);
-    const double p1617 = fma(3.5462265542512339e-08, u, 6.1229321472110077e-08);
-    const double p1819 = fma(-3.8907837965992227e-09, u, -1.6735307803068382e-09);
-    const double p20 = -4.4206737983570504e-10;
-    const double q0 = fma(p23, u2, p01), q1 = fma(p67, u2, p45), q2 = fma(p1011, u2, p89);
-    const double q3 = fma(p1415, u2, p1213), q4 = fma(p1819, u2, p1617);
-    const double g0 = fma(q1, u4, q0), g1 = fma(q3, u4, q2), g2 = fma(p20, u4, q4);
-    return fma(g2, u16, fma(g1, u8, g0));
-#endif
-#if HE_MILLS_DEG16
     double r = 2.7428474899566849e-08;
     r = fma_k(r, u, 1.1082671662043668e-08);
     r = fma_k(r, u, -3.9869407228616424e-07);
@@ -673,29 +570,6 @@ __device__ __forceinline__ double mills(double a) {
     r = fma_k(r, u, 0.29086958400118978);
     r = fma_k(r, u, -0.38520383404522951);
     r = fma_k(r, u, 0.23820001819943162);
-#else
-    double r = -4.4206737983570504e-10;
-    r = fma_k(r, u, -3.8907837965992227e-09);
-    r = fma_k(r, u, -1.6735307803068382e-09);
-    r = fma_k(r, u, 3.5462265542512339e-08);
-    r = fma_k(r, u, 6.1229321472110077e-08);
-    r = fma_k(r, u, -1.4934329903924975e-07);
-    r = fma_k(r, u, -5.8954452073183568e-07);
-    r = fma_k(r, u, 1.6391429736383158e-07);
-    r = fma_k(r, u, 4.1122801372346195e-06);
-    r = fma_k(r, u, 3.4217038844164288e-06);
-    r = fma_k(r, u, -2.7074245209317019e-05);
-    r = fma_k(r, u, -4.4835109354094885e-05);
-    r = fma_k(r, u, 0.00021086542652290141);
-    r = fma_k(r, u, 0.00039784937176197925);
-    r = fma_k(r, u, -0.002353960594219441);
-    r = fma_k(r, u, -0.0013327285592737549);
-    r = fma_k(r, u, 0.034655415072285041);
-    r = fma_k(r, u, -0.13151258275835945);
-    r = fma_k(r, u, 0.29927575053510824);
-    r = fma_k(r, u, -0.48122354789588401);
-    r = fma_k(r, u, 0.30783718216692846);
-#endif
     return r;
 }
 
@@ -704,12 +578,6 @@ __device__ __forceinline__ double tail_arg(double d) {
     const double a = fabs(d);
     return a < kMillsMax ? a : kMillsMax;                // NaN -> kMillsMax (the price is NaN anyway)
 }
-#ifndef HE_BOOK_EXP_FAST
-#define HE_BOOK_EXP_FAST 1
-#endif
-#ifndef HE_BOOK_EXP_FAST_UO
-#define HE_BOOK_EXP_FAST_UO 1  // the barrier formula's powers too: config 5 1.93 -> 1.89 ms (r03s44)
-#endif
 // exp(x) for the book's phi, x = -a^2 / 2 in [-700, 0] (a <= kMillsMax): exp_k's Cody-Waite
 // reduction, then e^r as its degree-11 Taylor polynomial (truncation < 7e-15 relative on
 // |r| <= ln2 / 2; the book's bar is 1e-5 on P&L) without the Fast2Sum or the range branch:
@@ -733,41 +601,21 @@ __device__ __forceinline__ double exp_book(double x) {
     return ldexp(q, (int)k);
 }
 // exp_book with exp_k's range guard, for the barrier formula's (H/S) powers (any sign,
-// +-inf when S is 0 or inf)
+// +-inf when S is 0 or inf): config 5 1.93 -> 1.89 ms per launch against exp_k (r03s44)
 __device__ __forceinline__ double exp_book_g(double x) {
-#if HE_BOOK_EXP_FAST && HE_BOOK_EXP_FAST_UO
     if (!(fabs(x) < 700.0)) return exp(x);
     return exp_book(x);
-#else
-    return exp_k(x);
-#endif
 }
-__device__ __forceinline__ double phi_of(double a) {
-#if HE_BOOK_EXP_FAST
-    return exp_book(-0.5 * (a * a)) * kInvSqrt2Pi;
-#else
-    return exp_k(-0.5 * (a * a)) * kInvSqrt2Pi;
-#endif
-}
+// phi through exp_book: config 4 8.35 -> 7.74 ms, config 5 2.00 -> 1.94 ms against exp_k (r03s41)
+__device__ __forceinline__ double phi_of(double a) { return exp_book(-0.5 * (a * a)) * kInvSqrt2Pi; }
 
-// N(d) and N(-d) from the tail q = Q(|d|).  HE_BOOK_NCDF_FAST (A/B, off): 0.5 -+ s (0.5 - q)
-// with s = sign(d), three VALU instructions per pair instead of five -- but the small tail
-// comes back as 0.5 - (0.5 - q), an absolute 2^-54 error that the barrier formula's
-// (H/S)^(2 lam) factors amplify past the 1e-5 P&L bar (config 5's full-size slice, r03s40).
-#ifndef HE_BOOK_NCDF_FAST
-#define HE_BOOK_NCDF_FAST 0
-#endif
+// N(d) and N(-d) from the tail q = Q(|d|), as selects.  (0.5 -+ sign(d) (0.5 - q) is two
+// instructions fewer per pair, but returns the small tail as 0.5 - (0.5 - q), an absolute
+// 2^-54 error the barrier formula's (H/S)^(2 lam) factors push past the 1e-5 P&L bar, r03s40.)
 __device__ __forceinline__ void ncdf_from_tail(double d, double q, double* pos, double* neg) {
-#if HE_BOOK_NCDF_FAST
-    const double h = 0.5 - q;
-    const double sh = __builtin_copysign(h, d);
-    *pos = 0.5 + sh;
-    *neg = 0.5 - sh;
-#else
     const bool p = d > 0.0;
     *pos = p ? 1.0 - q : q;
     *neg = p ? q : 1.0 - q;
-#endif
 }
 
 // One book option (branch-free in the lane-varying quantities: remaining steps, running max).
@@ -857,9 +705,6 @@ __device__ __forceinline__ double book_value(const Params& p, double S, double v
 #if HE_BOOK_DIAG == 2
     return S * 1e-3;  // diagnostic builds only: no book pricing at all
 #endif
-#ifdef HE_BOOK_UNROLL
-#pragma unroll HE_BOOK_UNROLL
-#endif
     for (int k = 0; k < p.book_n; ++k) {
         BookOpt o;
         if (opts) {  // an LDS copy: the type and expiry back in SGPRs (uniform branches)
@@ -877,119 +722,9 @@ __device__ __forceinline__ double book_value(const Params& p, double S, double v
     return book_value(p, S, var, t, runmax, p.book_tab);
 }
 
-// mills over NN arguments in lockstep (the same operations per element: the same bits).
-template <int NN>
-__device__ __forceinline__ void mills_n(const double* a, double* out) {
-#if HE_MILLS_DEG16
-#pragma unroll
-    for (int h = 0; h < NN; ++h) out[h] = mills(a[h]);
-    return;
-#endif
-    double u[NN], r[NN];
-#pragma unroll
-    for (int h = 0; h < NN; ++h) {
-        const double d = a[h] + kMillsC;
-        double y = __builtin_amdgcn_rcp(d);
-        y = fma(fma(-d, y, 1.0), y, y);
-        y = fma(fma(-d, y, 1.0), y, y);
-        u[h] = fma(-kMillsB, y, kMillsA);
-        r[h] = -4.4206737983570504e-10;
-    }
-    constexpr double MC[20] = {-3.8907837965992227e-09, -1.6735307803068382e-09, 3.5462265542512339e-08,
-                               6.1229321472110077e-08,  -1.4934329903924975e-07, -5.8954452073183568e-07,
-                               1.6391429736383158e-07,  4.1122801372346195e-06,  3.4217038844164288e-06,
-                               -2.7074245209317019e-05, -4.4835109354094885e-05, 0.00021086542652290141,
-                               0.00039784937176197925,  -0.002353960594219441,   -0.0013327285592737549,
-                               0.034655415072285041,    -0.13151258275835945,    0.29927575053510824,
-                               -0.48122354789588401,    0.30783718216692846};
-#pragma unroll
-    for (int c = 0; c < 20; ++c)
-#pragma unroll
-        for (int h = 0; h < NN; ++h) r[h] = fma_k(r[h], u[h], MC[c]);
-#pragma unroll
-    for (int h = 0; h < NN; ++h) out[h] = r[h];
-}
-
-// book_value<true> (the handle's constant variance) of NN market slots in lockstep: per
-// option (in book order, the same accumulation) the Europeans' d1 / d2, phi and the two
-// Mills ratios of every slot as interleaved chains; an up-and-out call takes book_option
-// per slot.  The same operations per slot as book_value: the same bits.
-template <int NN>
-__device__ __forceinline__ void book_value_n(const Params& p, const double* S, const int32_t* t, const double* runmax,
-                                             const double* tab, const BookOpt* opts, double* out) {
-    BookEnv b[NN];
-    double lnS[NN];
-#pragma unroll
-    for (int h = 0; h < NN; ++h) lnS[h] = log(S[h]);
-#pragma unroll
-    for (int h = 0; h < NN; ++h) {
-        b[h].S = S[h];
-        b[h].lnS = lnS[h];
-        b[h].sig = p.bk_sig;
-        b[h].isig = p.bk_isig;
-        b[h].s2 = p.bk_s2;
-        b[h].lam = p.bk_lam;
-        out[h] = 0.0;
-    }
-    const double r = p.r_d;
-    for (int k = 0; k < p.book_n; ++k) {
-        BookOpt o = opts[k];
-        o.type = __builtin_amdgcn_readfirstlane(o.type);
-        o.expiry = __builtin_amdgcn_readfirstlane(o.expiry);
-        if (o.type == HE_BOOK_UO_CALL) {
-#pragma unroll
-            for (int h = 0; h < NN; ++h) out[h] = out[h] + o.q100 * book_option(p, o, b[h], o.expiry - t[h], runmax[h], tab);
-            continue;
-        }
-        double d1[NN], d2[NN], Kd[NN], SoKd[NN], ea[2 * NN], ph[NN], ml[2 * NN];
-        bool live[NN];
-#pragma unroll
-        for (int h = 0; h < NN; ++h) {
-            const int32_t m = o.expiry - t[h];
-            live[h] = m > 0 && b[h].sig > 0.0;
-            const int32_t mc = live[h] ? m : 1;
-            const double tau = (double)mc * p.dt;
-            const double* e = tab + 4 * mc;
-            const double sst = b[h].sig * e[0];
-            const double isst = b[h].isig * e[1];
-            d1[h] = ((b[h].lnS - o.lnK) + (r + 0.5 * b[h].s2) * tau) * isst;
-            d2[h] = d1[h] - sst;
-            Kd[h] = o.K * e[2];
-            SoKd[h] = S[h] * (o.invK * e[3]);
-            ea[h] = tail_arg(d1[h]);
-            ea[NN + h] = tail_arg(d2[h]);
-            ph[h] = -0.5 * (ea[h] * ea[h]);   // phi_of's argument
-        }
-        exp_k_n<NN>(ph, ph);
-        mills_n<2 * NN>(ea, ml);
-#pragma unroll
-        for (int h = 0; h < NN; ++h) {
-            const double ph1 = ph[h] * kInvSqrt2Pi;
-            const double q1 = ph1 * ml[h], q2 = (ph1 * SoKd[h]) * ml[NN + h];
-            double n1, m1, n2, m2;
-            ncdf_from_tail(d1[h], q1, &n1, &m1);
-            ncdf_from_tail(d2[h], q2, &n2, &m2);
-            double v;
-            if (o.type == HE_BOOK_PUT) {
-                v = Kd[h] * m2 - S[h] * m1;
-                const double ip = o.K - S[h];
-                v = live[h] ? v : ((ip < 0.0) ? 0.0 : ip);
-            } else {
-                v = S[h] * n1 - Kd[h] * n2;
-                const double ic = S[h] - o.K;
-                v = live[h] ? v : ((ic < 0.0) ? 0.0 : ic);
-            }
-            out[h] = out[h] + o.q100 * ((v < 0.0) ? 0.0 : v);
-        }
-    }
-}
-
-// The Heston price advance's exp (market_body and the LDS producers, the same function):
-// the library exp -- its P&L equals the oracle's bit for bit on the parity cases, as
-// exp_k's does (tools/pnl_exact.py), and it is 1 % faster at config 5 (r02 g18).
-#ifndef HE_HESTON_EXP
-#define HE_HESTON_EXP exp
-#endif
+// The Heston price advance's exp (market_body and the LDS producers, the same function) is
+// the library exp: its P&L equals the oracle's bit for bit on the parity cases, as exp_k's
+// does (tools/pnl_exact.py), and it is 1 % faster at config 5 (r02 g18).
 
 // Box-Muller pair of the Philox block of (seed, global env id, env-step index n).
 __device__ __forceinline__ void normals(const Params& p, int64_t gid, uint64_t n, double* z1, double* z2) {
@@ -1078,16 +813,7 @@ __device__ __forceinline__ void market_body(Params p, Market cur, Market bak, in
         for (uint64_t m = m0 + (uint64_t)sub; m <= m1; m += kMktLanes) {
             if (!live) break;
             double z[2];
-#if defined(HE_MKT_SKIP) && (HE_MKT_SKIP & 4)
-            {   // diagnostic build: no Box-Muller (timing A/B only)
-                u32x4 ctr = {(uint32_t)m, (uint32_t)(m >> 32), (uint32_t)gid, (uint32_t)((uint64_t)gid >> 32)};
-                u32x4 x = philox4x32_10(ctr, p.key0, p.key1);
-                z[0] = u01(x.x, x.y) - 0.5;
-                z[1] = u01(x.z, x.w) - 0.5;
-            }
-#else
             normals(p, gid, m, &z[0], &z[1]);
-#endif
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
                 uint64_t n = 2 * m + (uint64_t)h;
@@ -1120,7 +846,7 @@ __device__ __forceinline__ void market_body(Params p, Market cur, Market bak, in
                 double dWS = shS[lane][j], dw1 = shV[lane][j];
                 double drift = (p.mu - 0.5 * vp) * p.dt;
                 double diff = sqrt(vp) * dWS;
-                double Sn = S * HE_HESTON_EXP(drift + diff);
+                double Sn = S * exp(drift + diff);
                 S = (Sn < 1e-8) ? 1e-8 : Sn;
                 v = (v + p.h_kappa * (p.h_theta - vp) * p.dt) + p.h_xi * sqrt(vp) * dw1;
                 shV[lane][j] = v;
@@ -1163,11 +889,7 @@ __device__ __forceinline__ void market_body(Params p, Market cur, Market bak, in
         double v64 = HESTON ? shV[lane][j] : p.var;
         float C, P;
         if (tj < T) {
-#if defined(HE_MKT_SKIP) && (HE_MKT_SKIP & 2)
-            C = (float)S64; P = (float)v64;  // diagnostic build: no marks
-#else
             marks<MODE>(p, S64, v64, tj, &C, &P);
-#endif
         } else if (T == 1u) {  // lagged marks of t = T-1 = 0: the reset marks
             C = p.rstv[2];
             P = p.rstv[3];
@@ -1187,11 +909,7 @@ __device__ __forceinline__ void market_body(Params p, Market cur, Market bak, in
         if (HESTON) p.tileA[(int64_t)j * N + i] = make_float4(S32, v32, C, P);
         else st3(p.tileA, (int64_t)j * N + i, S32, C, P);
         if (HESTON) {
-#if defined(HE_MKT_SKIP) && (HE_MKT_SKIP & 1)
-            float4 g = make_float4(S32, v32, 0.f, 0.f);  // diagnostic build: no greeks
-#else
             float4 g = p.record_metrics ? greeks_fast<false>(p, S32, v32) : make_float4(0.f, 0.f, 0.f, 0.f);
-#endif
             // the step into slot j starts from the reset market (first step of an
             // episode) or from slot j-1
             const float Sp32 = (tj == 1u) ? p.rstv[0] : (float)shS[lane][j - 1];
@@ -1226,7 +944,7 @@ __device__ __forceinline__ void market_body(Params p, Market cur, Market bak, in
 }
 
 template <int MODE, bool BOOK>
-__global__ __launch_bounds__(kMktEnvs * kMktLanes, HE_MKT_WAVES) void market_kernel(Params p, Market cur, Market bak,
+__global__ __launch_bounds__(kMktEnvs * kMktLanes, kMktWaves) void market_kernel(Params p, Market cur, Market bak,
                                                                                      int32_t advance_only) {
     market_body<MODE, BOOK>(p, cur, bak, advance_only, blockIdx.x);
 }
@@ -1991,162 +1709,6 @@ __global__ __launch_bounds__(kBlock) void step1_kernel(const Params* __restrict_
     step_body<MODE, false, true, BOOK, FAST, false, GS>(*pc, n, tA, tB, tC, s, io, 1, slot0, blockIdx.x);
 }
 
-// Opaque copies of the Params fields a step / a market block reads in its loop (see HE_LDS_PIN).
-__device__ __forceinline__ void pin_step_consts(Params& q, bool obs) {
-    asm volatile("" : "+s"(q.mt_f), "+s"(q.mt), "+s"(q.maxh), "+s"(q.T), "+s"(q.var_f));
-    if (obs) {
-        asm volatile("" : "+s"(q.maxh_f), "+s"(q.inv_maxh_f), "+s"(q.T_f), "+s"(q.inv_T_f), "+s"(q.s0s_d),
-                     "+s"(q.inv_s0s_d));
-#pragma unroll
-        for (int c = 0; c < 4 + kObs; ++c) asm volatile("" : "+s"(q.rstv[c]));
-    } else {
-        asm volatile("" : "+s"(q.tcpc), "+s"(q.slip_frac), "+s"(q.shares_f), "+s"(q.shares_d), "+s"(q.inv_shares),
-                     "+s"(q.den), "+s"(q.inv_den));
-        asm volatile("" : "+s"(q.w), "+s"(q.lam), "+s"(q.theta), "+s"(q.inv_252), "+s"(q.initial_cash),
-                     "+s"(q.init_cash_f));
-    }
-}
-// he_step split by role (GBM, the FAST configuration, market greeks from the tile, no book,
-// no info): at 65,536 envs step1_kernel is one wave per SIMD, so each env's whole chain --
-// loads, the f64 P&L, the obs row -- is exposed latency.  Here a workgroup of 8
-// waves steps 256 envs: waves 0-3 the reward chain of step_env (trades, costs, P&L, reward,
-// the state), waves 4-7 the obs of the same envs (the trade logic again, make_obs, the
-// SB3 terminal / reset obs) -- two independent chains per env on different waves.  The
-// same device functions on the same operands as step_body, so the same bits.  One
-// workgroup barrier: the obs waves arrive once their loads have returned, the reward
-// waves before their stores (the state the obs waves read).
-// Opt-in (HE_STEP_SPLIT=1 in the environment at he_create), parity-tested
-// (test_split_step_equals_step1): same-box graph-mode A/B (r03s28, 3 runs each) 1.29-1.33e10
-// env-steps/s against step1_kernel's 1.34-1.37e10 -- twice the waves to dispatch and the
-// second role's duplicate loads cost more than the overlap of the two chains gains.
-#ifndef HE_STEP_SPLIT
-#define HE_STEP_SPLIT 1
-#endif
-#ifndef HE_SPLIT_PIN
-#define HE_SPLIT_PIN 1  // the role's Params fields loaded up front (not lazily mid-chain)
-#endif
-#ifndef HE_SPLIT_EARLY_BAR
-#define HE_SPLIT_EARLY_BAR 1
-#endif
-__global__ __launch_bounds__(2 * kBlock) void step1_split_kernel(const Params* __restrict__ pc, int64_t n,
-                                                                 const float4* tA, const float4* tB, State s,
-                                                                 StepIo sio, int slot0) {
-    static_assert(kEpw == 64 && kEpb == kBlock, "one env per thread and role");
-    __builtin_amdgcn_s_setprio(3);
-    __shared__ __attribute__((aligned(16))) float tile[kEpb * kObs];
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const bool obs_role = wave >= 4;
-    const int w = wave & 3;
-    const int64_t wrow0 = (int64_t)blockIdx.x * kEpb + w * 64;
-    const int64_t i = wrow0 + lane;
-    const int64_t N = n;
-    const bool live = i < N;
-    const int64_t ic = live ? i : (N - 1);  // dead lanes load a live env's addresses
-    const int wrows = (int)((N - wrow0) < 64 ? (N - wrow0 > 0 ? N - wrow0 : 0) : 64);
-    auto mA = (const GLOBAL v4f*)tA;
-    auto mB = (const GLOBAL v4f*)tB;
-    // every load of the step issued first, by both roles (one memory round trip; the
-    // second role's loads of the same lines hit L2), and pinned there: otherwise the
-    // backend sinks some into the role branches, a second dependent round trip
-    // (row bases in SGPRs, 32-bit env index: plain base + index * size addresses)
-    const uint32_t iu = (uint32_t)ic;
-    const GLOBAL v4f* rowA0 = (const GLOBAL v4f*)((const GLOBAL f3*)mA + (int64_t)slot0 * N);
-    const GLOBAL v4f* rowA1 = (const GLOBAL v4f*)((const GLOBAL f3*)mA + (int64_t)(slot0 + 1) * N);
-    const GLOBAL v4f* rowB1 = (const GLOBAL v4f*)((const GLOBAL f3*)mB + (int64_t)(slot0 + 1) * N);
-    uint32_t t0 = s.t[iu];
-    uint32_t pk = s.pos[iu];
-    float2 a = ld2((const GLOBAL v2f*)sio.act, iu);
-    float4 g = ld3B(rowB1, iu);
-    float4 postA = ld3B(rowA1, iu);  // {S, C, P}: v is the handle's constant (ld3A)
-    float4 preA = ld3B(rowA0, iu);
-    double cash = s.cash[iu];
-    // the Params loads after these (scalar loads return out of order: a scalar load issued
-    // before the address operands of the vector loads would hold them back)
-    asm volatile("" ::: "memory");
-#if HE_SPLIT_PIN
-    Params pq = *pc;
-    const Params& p = pq;
-#else
-    const Params& p = *pc;
-#endif
-#if HE_SPLIT_PIN
-    // while the loads are in flight: every Params field the role reads, in SGPRs (one
-    // scalar round trip instead of one per first use along the chain)
-    if (obs_role) {
-        pin_step_consts(pq, true);
-    } else {
-        pin_step_consts(pq, false);
-        asm volatile("" : "+s"(pq.autoreset));
-    }
-#endif
-    asm volatile("" : "+v"(t0), "+v"(pk), "+v"(a.x), "+v"(a.y), "+v"(postA.x), "+v"(postA.y), "+v"(postA.z),
-                 "+v"(preA.x), "+v"(preA.y), "+v"(preA.z), "+v"(cash), "+v"(g.x), "+v"(g.y), "+v"(g.z));
-    const float var_f = p.var_f;
-    postA = make_float4(postA.x, var_f, postA.y, postA.z);
-    preA = make_float4(preA.x, var_f, preA.y, preA.z);
-    const Mkt rst{p.rstv[0], p.rstv[1], p.rstv[2], p.rstv[3], 0.0};
-    Env e;
-    e.t = t0;
-    e.call = unpack_lo(pk);
-    e.put = unpack_hi(pk);
-    e.path = -1;
-    e.s0_small = rst.S < 1e-6f;
-    e.s0 = e.s0_small ? 1.0f : rst.S;
-    const Mkt pre = (t0 == 0) ? rst : as_mkt(preA);
-    const Mkt post = as_mkt(postA);
-    if (!obs_role) {
-        // the reward chain (step_env, hedging_env_v2.py:175-262) and the state
-        e.cash = cash;
-        const double pv_last = portfolio_value<false>(p, e, pre);
-        StepOut so;
-        step_env<false, true>(p, e, pre, post, a.x, a.y, pv_last, so);
-        if (so.term && p.autoreset) env_reset_common(p, e);  // SB3 autoreset
-        // every store after the barrier (its fence would wait for stores issued before it)
-        __syncthreads();  // the obs waves have their state inputs
-        if (live) {
-            ((GLOBAL float*)sio.rew)[i] = (float)so.reward;
-            ((GLOBAL uint8_t*)sio.term)[i] = so.term ? 1 : 0;
-            if (sio.trunc) ((GLOBAL uint8_t*)sio.trunc)[i] = 0;
-            s.t[i] = e.t;
-            s.pos[i] = pack_pos(e.call, e.put);
-            s.cash[i] = e.cash;
-        }
-    } else {
-        // the obs (hedging_env_v2.py:109-143) of the post-step state: step_env's trade logic
-        // (:181-200) for the positions, then make_obs; the terminal / reset obs of SB3
-#if HE_SPLIT_EARLY_BAR
-        // the state loads have returned (the pins above): the reward waves may store the
-        // state now, not after this wave's obs stores
-        __syncthreads();
-#endif
-        g.w = lag_return(post.S, (e.t >= (uint32_t)p.T) ? rst.S : pre.S);
-        const int32_t nc = e.call + trade_round(a.x * p.mt_f, p.mt);
-        const int32_t nq = e.put + trade_round(a.y * p.mt_f, p.mt);
-        e.call = nc < -p.maxh ? -p.maxh : (nc > p.maxh ? p.maxh : nc);
-        e.put = nq < -p.maxh ? -p.maxh : (nq > p.maxh ? p.maxh : nq);
-        e.t = e.t + 1;
-        const bool term = (int32_t)e.t >= p.T;
-        float o[kObs];
-        make_obs<true>(p, e, post, g, pre.S, pre.v, o);
-        float* const orow = tile + (w * 64 + lane) * kObs;
-        if (p.autoreset && __ballot(term) != 0ull) {
-            if (term && live && sio.tobs) {
-#pragma unroll
-                for (int c = 0; c < kObs; ++c) sio.tobs[i * kObs + c] = o[c];
-            }
-#pragma unroll
-            for (int c = 0; c < kObs; ++c) o[c] = term ? p.rstv[4 + c] : o[c];
-        }
-#pragma unroll
-        for (int c = 0; c < kObs; ++c) orow[c] = o[c];
-        flush_obs_wave(tile + w * 64 * kObs, sio.obs, wrow0, wrows, lane);
-#if !HE_SPLIT_EARLY_BAR
-        __syncthreads();
-#endif
-    }
-}
-
 // he_step with VecNormalize attached (he_vecnorm_attach): step1_kernel, then the first half
 // of the VecNormalize step (vn_moments.h) over the rows this workgroup has just made --
 // from its LDS obs staging tile and the rewards in registers, with no read back -- instead
@@ -2191,20 +1753,14 @@ __global__ __launch_bounds__(vn::kVnThreads) void vn_moments_after_step_kernel(v
 // stream alone, with no cross-queue event between them (measured 25 us between the
 // side-stream market's end and the next step dispatch at 65,536 envs).  The step
 // workgroups come first in dispatch order and keep s_setprio 3.
-#ifndef HE_FUSED_DPARAMS
-#define HE_FUSED_DPARAMS 1
-#endif
 // min waves per SIMD of step_market_kernel.  4 (VGPR cap 128: one step + three market
 // workgroups per CU) measured +3.8% at 1,048,576 envs and +0% at 65,536, but spills
 // ~100 B per lane to scratch; kept at the market kernel's 2 (167 VGPRs, 3 per CU)
-#ifndef HE_FUSED_WAVES
-#define HE_FUSED_WAVES HE_MKT_WAVES
-#endif
-#if HE_FUSED_DPARAMS
+constexpr int kFusedWaves = kMktWaves;
 // Params of both tile buffers from the device copies (pc[buf] steps, pc[buf ^ 1] is the
 // market's): a 0.2 KB kernarg segment instead of 2 x Params by value.
 template <int MODE, bool BOOK, bool FAST, bool GS>
-__global__ __launch_bounds__(kBlock, HE_FUSED_WAVES) void step_market_kernel(const Params* __restrict__ pc, int32_t buf,
+__global__ __launch_bounds__(kBlock, kFusedWaves) void step_market_kernel(const Params* __restrict__ pc, int32_t buf,
                                                                            State s, Io io, int k_steps, int slot0,
                                                                            Market cur, Market bak,
                                                                            int32_t step_blocks) {
@@ -2217,19 +1773,6 @@ __global__ __launch_bounds__(kBlock, HE_FUSED_WAVES) void step_market_kernel(con
         market_body<MODE, BOOK>(pc[buf ^ 1], cur, bak, 0, (int64_t)blockIdx.x - step_blocks);
     }
 }
-#else
-template <int MODE, bool BOOK, bool FAST, bool GS>
-__global__ __launch_bounds__(kBlock, HE_FUSED_WAVES) void step_market_kernel(Params pk, State s, Io io, int k_steps,
-                                                                           int slot0, Params pm, Market cur,
-                                                                           Market bak, int32_t step_blocks) {
-    static_assert(kBlock == kMktEnvs * kMktLanes, "one workgroup shape for both roles");
-    if ((int32_t)blockIdx.x < step_blocks)
-        step_body<MODE, false, false, BOOK, FAST, false, GS>(pk, pk.n, pk.tileA, pk.tileB, pk.tileC, s, io, k_steps,
-                                                              slot0, blockIdx.x);
-    else
-        market_body<MODE, BOOK>(pm, cur, bak, 0, (int64_t)blockIdx.x - step_blocks);
-}
-#endif
 
 // ------------------------------------------------------------------ LDS rollout
 // he_rollout, GBM without a book: ONE launch per call, and the market never leaves the
@@ -2251,70 +1794,25 @@ __global__ __launch_bounds__(kBlock, HE_FUSED_WAVES) void step_market_kernel(Par
 // rollouts == tile rollouts == repeated he_step).  HBM traffic is the step I/O of
 // hedging_env_v2.py:175-294 only: actions in, obs / reward / terminated out, and the
 // per-env state + market position once per launch.
-#ifndef HE_LDS_LANES
-#define HE_LDS_LANES 2
-#endif
-#ifndef HE_LDS_M
-#define HE_LDS_M 8
-#endif
-// Producers specialised for whole blocks (straight-line slots, and with LOCK the lean GBM
-// slots in lockstep).  Same-box A/B (r03s4, two runs each, with 4 waves per SIMD for the
-// 122 VGPRs the lockstep slots hold): config 2 308 / 310 -> 302 / 306 us per launch, config
-// 4 9.03 / 9.05 -> 8.75 / 8.74 ms.
+// SIMD-balanced wave roles (lds_role, below); HE_LDS_BALANCE=0 only in the placement
+// diagnostics of tools/lds_hwid.py
 #ifndef HE_LDS_BALANCE
-#define HE_LDS_BALANCE 1  // SIMD-balanced wave roles (lds_role, below)
+#define HE_LDS_BALANCE 1
 #endif
-#ifndef HE_LDS_PROD_FULL
-#define HE_LDS_PROD_FULL 1
-#endif
-#ifndef HE_LDS_BOOK_LOCK
-#define HE_LDS_BOOK_LOCK 0  // A/B: the GBM book's slots priced in lockstep too (book_value_n)
-#endif
-#ifndef HE_LDS_OBS_LOCK
-#define HE_LDS_OBS_LOCK 0  // the lean obs stepper's greeks of a full block in lockstep (A/B)
-#endif
-#ifndef HE_LDS_PROD_LOCK
-#define HE_LDS_PROD_LOCK 1  // with HE_LDS_PROD_FULL: the lean GBM producers' slots in lockstep
-#endif
-#ifndef HE_LDS_BOOK_OPTS
-#define HE_LDS_BOOK_OPTS 1  // the book's options read from an LDS copy (config 4: 10.38 -> 8.98 ms per launch; 0: from the scalar cache)
-#endif
-#ifndef HE_LDS_HOIST
-#define HE_LDS_HOIST 0  // A/B: obs-wave constants forced into VGPRs (1: greeks, 2: reset obs)
-#endif
-#ifndef HE_LDS_PRIO_REW
-// the reward stepper above the obs stepper, GBM without a book (same-box A/B r03s9, config 2,
-// two runs each: priority 0 312 / 300 us per launch, 1 319 / 313, 2 314 / 302, 3 305 / 296)
-#define HE_LDS_PRIO_REW 3
-#endif
-#ifndef HE_LDS_PRIO_REW_BOOK
-#define HE_LDS_PRIO_REW_BOOK 0  // with a book or Heston (producer-bound)
-#endif
-#ifndef HE_REPLAY_PRIO_REW
-#define HE_REPLAY_PRIO_REW 0
-#endif
-#ifndef HE_LDS_PRIO_OBS
-#define HE_LDS_PRIO_OBS 2  // the obs wave is the workgroup's critical chain: it wins issue
-#endif
-#ifndef HE_LDS_PRIO_PROD
-#define HE_LDS_PRIO_PROD 1
-#endif
-#ifndef HE_LDS_LANES_BOOK
-// a liability book or Heston: 2 producer waves (4 waves per workgroup, 4 workgroups per
-// CU at 128 VGPRs) -- same-box A/B against 4 (r02 g2): config 4 1.11e10 -> 1.21e10,
+// Wave priorities (s_setprio).  The reward stepper above the obs stepper, GBM without a book
+// (same-box A/B r03s9, config 2, two runs each: priority 0 312 / 300 us per launch, 1 319 /
+// 313, 2 314 / 302, 3 305 / 296); with a book or Heston (producer-bound) at 0 (3: config 4
+// +4 %, config 5 +3 %).  The obs wave is the GBM workgroup's critical chain: it wins issue
+// over the producers.
+constexpr int kPrioRew = 3, kPrioRewBook = 0, kPrioReplayRew = 0, kPrioObs = 2, kPrioProd = 1;
+// Producer lanes per env: 2 producer waves (4 waves per workgroup, 4 workgroups per CU at 128
+// VGPRs); with a book or Heston same-box A/B against 4 (r02 g2): config 4 1.11e10 -> 1.21e10,
 // config 5 1.19e10 -> 1.25e10 env-steps/s
-#define HE_LDS_LANES_BOOK 2
-#endif
-#ifndef HE_LDS_MINWAVES_BOOK
-#define HE_LDS_MINWAVES_BOOK 4
-#endif
+constexpr int kLdsLanesGbm = 2, kLdsLanesBook = 2, kLdsMinWavesBook = 4;
 constexpr int kLdsEnvs = 64;                         // envs per workgroup = one stepper wave
-constexpr int kLdsM = HE_LDS_M;                      // slots per LDS market block
-#ifdef HE_LDS_PREFETCH
-constexpr int kLdsPrefetch = HE_LDS_PREFETCH;  // A/B builds
-#else
+// slots per LDS market block (same-box A/B r02: M = 16 -12 %, M = 4 -3 %)
+constexpr int kLdsM = 8;
 constexpr int kLdsPrefetch = kLdsM % 6 == 0 ? 6 : (kLdsM % 4 == 0 ? 4 : kLdsM);  // steps of actions in flight
-#endif
 static_assert(kLdsM % kLdsPrefetch == 0, "the action ring index is the slot mod D");
 
 // Workgroup geometry of one market configuration: `lanes` producer lanes per env in
@@ -2327,21 +1825,16 @@ struct LdsGeom {
     static constexpr bool HESTON = MODE == HE_MODE_HESTON;
     // Heston: two normals, a sqrt and a per-step Black-Scholes constant set per slot --
     // producer-bound like a book, so it takes the book's lane count
-    static constexpr int lanes = (BOOK || HESTON) ? HE_LDS_LANES_BOOK : HE_LDS_LANES;
+    static constexpr int lanes = (BOOK || HESTON) ? kLdsLanesBook : kLdsLanesGbm;
     static constexpr int prod = lanes;
     static constexpr int penvs = kLdsEnvs / lanes;
     static constexpr int threads = 64 * (2 + prod);  // + the reward and the obs stepper waves
     static constexpr int H = kLdsM / lanes;
-#ifdef HE_LDS_MINWAVES
-    static constexpr int minwaves = (BOOK || HESTON) ? HE_LDS_MINWAVES_BOOK : HE_LDS_MINWAVES;
-#else
     // the balanced placement (HE_LDS_BALANCE) puts exactly one wave of each of a CU's 4
     // workgroups on every SIMD: 4 waves per SIMD, 128 VGPRs (the lockstep producers hold
     // 122); the unbalanced build keeps a spare wave for an uneven placement
-    static constexpr int minwaves = (BOOK || HESTON) ? HE_LDS_MINWAVES_BOOK
-                                                     : ((HE_LDS_PROD_FULL && HE_LDS_BALANCE) ? 4
-                                                                                             : (4 * (2 + prod) + 3) / 4 + 1);
-#endif
+    static constexpr int minwaves = (BOOK || HESTON) ? kLdsMinWavesBook
+                                                     : (HE_LDS_BALANCE ? 4 : (4 * (2 + prod) + 3) / 4 + 1);
     static_assert(H * lanes == kLdsM && penvs * lanes == kLdsEnvs, "producer lane layout");
 };
 
@@ -2353,34 +1846,18 @@ struct LdsGeom {
 // tile kernels (lds_rollout_eligible).  The producers' per-option table reads are then LDS
 // reads instead of L1/L2 gathers on their critical chain.
 constexpr int kLdsBookRows = 256;
-#ifndef HE_LDS_OBS_LAG
-// A/B: the lean GBM kernel's obs stepper one block behind, its greeks by the reward stepper.
-// Same-box A/B (r03s12, config 2, two runs each): 309.8 / 324.6 us per launch against 307.1 /
-// 320.1 without -- the obs stepper leaves the critical path (busy 2065 -> 1372 cycles per step)
-// but the second producer wave takes it (1952), so the step stays at ~2200 cycles.
-#define HE_LDS_OBS_LAG 0
-#endif
-// The lean GBM kernel (no book) with HE_LDS_OBS_LAG: the obs greeks of block b are evaluated by
-// the reward stepper while it steps block b (greeks_lean_n, the obs stepper's own bits) into
-// gk, and the obs stepper steps block b one block later -- so the market is triple-buffered.
-template <int MODE, bool BOOK, bool LEAN>
-constexpr bool lds_lag() {
-    return LEAN && !BOOK && MODE == HE_MODE_GBM && HE_LDS_OBS_LAG;
-}
 template <int MODE, bool BOOK, bool LEAN = false>
 struct LdsMarketT {
-    static constexpr bool LAG = lds_lag<MODE, BOOK, LEAN>();
-    static constexpr int NB = LAG ? 3 : 2;                             // market buffers
+    static constexpr int NB = 2;                                       // market buffers
     float2 sc[NB][kLdsM][kLdsEnvs];
     float pp[NB][kLdsM][kLdsEnvs];
     float stage[2][kLdsEnvs * kObs];                                   // obs row staging, by step parity
-    float gk[LAG ? 2 : 1][3][LAG ? kLdsM : 1][kLdsEnvs];               // LAG: {call_delta, gamma, put_delta} by block parity
     double bk[BOOK ? 2 : 1][BOOK ? kLdsM : 1][kLdsEnvs];                // book value of every slot
     float vv[MODE == HE_MODE_HESTON ? 2 : 1][MODE == HE_MODE_HESTON ? kLdsM : 1][kLdsEnvs];  // Heston: f32 v_t
     double btab[BOOK ? kLdsBookRows : 1][4];  // the book's tau table (p.book_tab), copied at launch start
-#if HE_LDS_BOOK_OPTS
-    BookOpt bopt[BOOK ? HE_BOOK_MAX : 1];     // the book's options, copied at launch start
-#endif
+    // the book's options, copied at launch start (config 4: 10.38 -> 8.98 ms per launch against
+    // reading them through the scalar cache)
+    BookOpt bopt[BOOK ? HE_BOOK_MAX : 1];
 };
 static_assert(kLdsM > 8 || sizeof(LdsMarketT<HE_MODE_GBM, false>) <= 40 * 1024, "4 workgroups per CU");
 static_assert(kLdsM > 8 || sizeof(LdsMarketT<HE_MODE_GBM, false, true>) <= 40 * 1024 - 64, "4 workgroups per CU");
@@ -2413,29 +1890,16 @@ __device__ uint64_t g_lds_tim[4][4096][3];
 #endif
 
 // Store one workgroup's 64 obs rows (the image, 832 floats) as 3 x 16 B + 4 B per lane:
-// every lane active, no branch.
-#ifndef HE_OBS_SC1
-#define HE_OBS_SC1 0  // A/B: the obs rows stored write-through (sc1: the lines leave the XCD's L2)
-#endif
+// every lane active, no branch.  (Write-through sc1 stores: config 2 +-0, config 6 +1.5 %.)
 __device__ __forceinline__ void flush_obs_full(const float* img, float* out, int64_t row0, int lane) {
     asm volatile("" ::: "memory");
     GLOBAL float* dst = (GLOBAL float*)out + row0 * kObs;
-#if HE_OBS_SC1
-    typedef int v4i __attribute__((ext_vector_type(4)));
-    const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)dst, 0, kLdsEnvs * kObs * 4, 0x00020000);
-    const v4i* s4 = reinterpret_cast<const v4i*>(img);
-    __builtin_amdgcn_raw_buffer_store_b128(s4[lane], rs, lane * 16, 0, 16);
-    __builtin_amdgcn_raw_buffer_store_b128(s4[lane + 64], rs, (lane + 64) * 16, 0, 16);
-    __builtin_amdgcn_raw_buffer_store_b128(s4[lane + 128], rs, (lane + 128) * 16, 0, 16);
-    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(int, img[768 + lane]), rs, (768 + lane) * 4, 0, 16);
-#else
     GLOBAL v4f* d4 = (GLOBAL v4f*)dst;
     const v4f* s4 = reinterpret_cast<const v4f*>(img);
     d4[lane] = s4[lane];
     d4[lane + 64] = s4[lane + 64];
     d4[lane + 128] = s4[lane + 128];
     dst[768 + lane] = img[768 + lane];
-#endif
     asm volatile("" ::: "memory");
 }
 
@@ -2453,25 +1917,6 @@ __device__ __forceinline__ void flush_obs_full(const float* img, float* out, int
 // different outstanding memory ops.  (A copy of a pending load's register at a merge,
 // e.g. the action ring at a loop back-edge behind a `break`, costs an s_waitcnt
 // vmcnt(0): every store of the wave drained.)  A partial last block takes a generic loop.
-#ifndef HE_LDS_PIN
-// A/B: the generic steppers' and the Heston / book producers' hot Params fields pinned in SGPRs
-// (scalar loads in the config 5 kernel 406 -> 75, SGPR spills to VGPR lanes 173 -> 1,066).
-// Same-box A/B (r03s16, two runs each): config 5 2,041 / 2,053 -> 2,126 / 2,128 us per launch,
-// config 4 8,863 / 8,878 -> 8,770 / 8,833: the reloads were not what holds those kernels back.
-#define HE_LDS_PIN 0
-#endif
-__device__ __forceinline__ void pin_market_consts(Params& q, bool heston, bool book) {
-    asm volatile("" : "+s"(q.key0), "+s"(q.key1), "+s"(q.sqrt_dt), "+s"(q.s0), "+s"(q.var), "+s"(q.r_d));
-    asm volatile("" : "+s"(q.sqrt_tenor), "+s"(q.tenor_d), "+s"(q.bs.disc));
-    if (heston) {
-        asm volatile("" : "+s"(q.h_rho), "+s"(q.h_sqrt1mrho2), "+s"(q.h_kappa), "+s"(q.h_theta), "+s"(q.h_xi),
-                     "+s"(q.mu), "+s"(q.dt));
-    } else {
-        asm volatile("" : "+s"(q.drift), "+s"(q.sqrt_var));
-    }
-    if (book) asm volatile("" : "+s"(q.dt), "+s"(q.book_n));
-}
-
 template <int MODE, bool BOOK, bool LEAN, bool OBS>
 __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& io, int k_steps, const Market& cur,
                                             LdsMarketT<MODE, BOOK, LEAN>& L, int64_t base) {
@@ -2489,8 +1934,8 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
     const GLOBAL v2f* gact = (const GLOBAL v2f*)io.act;
     GLOBAL float* const grew = (GLOBAL float*)io.rew;
     GLOBAL uint8_t* const gterm = (GLOBAL uint8_t*)io.term;
-    if (OBS) __builtin_amdgcn_s_setprio(HE_LDS_PRIO_OBS);
-    else __builtin_amdgcn_s_setprio((BOOK || HESTON) ? HE_LDS_PRIO_REW_BOOK : HE_LDS_PRIO_REW);
+    if (OBS) __builtin_amdgcn_s_setprio(kPrioObs);
+    else __builtin_amdgcn_s_setprio((BOOK || HESTON) ? kPrioRewBook : kPrioRew);
     LDS_T0();
     Env e{};
     Mkt pre = rst;
@@ -2552,15 +1997,9 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
 #pragma unroll
     for (int d = 0; d < D; ++d) ra[d] = ld2(gact, (int64_t)(d < k_steps ? d : k_steps - 1) * N + i);
 
-    // ---- the block loop over a step function step(buf, sl, k, action, in_full_block), with
-    // blk(buf, b, len) called once per block after its barrier (a block-wide prologue).
-    // LAG (lds_lag): the obs stepper runs one block behind the reward stepper (an extra
-    // barrier first), the reward stepper's blk evaluates the block's obs greeks for it (an
-    // extra barrier last), so both make nb + 2 barriers like the producers.
-    constexpr bool LAG = LdsMarketT<MODE, BOOK, LEAN>::LAG;
+    // ---- the block loop over a step function step(buf, sl, k, action, in_full_block)
     constexpr int NB = LdsMarketT<MODE, BOOK, LEAN>::NB;
-    auto run_blk = [&](auto&& blk, auto&& step) {
-        if (LAG && OBS) LDS_BAR();  // one block behind
+    auto run_blk = [&](auto&& step) {
         LDS_BAR();  // block 0 produced
         for (int b = 0; b < nfull; ++b) {
 #if defined(HE_LDS_DIAG) && HE_LDS_DIAG == 2
@@ -2568,7 +2007,6 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
             continue;
 #endif
             const int buf = b % NB;
-            blk(buf, b, kLdsM);
 #pragma unroll
             for (int sl = 0; sl < kLdsM; ++sl) {
                 const int k = b * kLdsM + sl;
@@ -2582,7 +2020,6 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
         if (tail) {
 #if !(defined(HE_LDS_DIAG) && HE_LDS_DIAG == 2)
             const int buf = nfull % NB;
-            blk(buf, nfull, tail);
             for (int sl = 0; sl < tail; ++sl) {
                 const int k = nfull * kLdsM + sl;
                 step(buf, sl, k, ld2(gact, (int64_t)k * N + i), std::false_type{});
@@ -2590,11 +2027,8 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
 #endif
             LDS_BAR();
         }
-        if (LAG && !OBS) LDS_BAR();  // the obs stepper's last block
     };
-    auto run = [&](auto&& step) {
-        run_blk([](int, int, int) {}, [&](int buf, int sl, int k, float2 ak, auto) { step(buf, sl, k, ak); });
-    };
+    auto run = [&](auto&& step) { run_blk([&](int buf, int sl, int k, float2 ak, auto) { step(buf, sl, k, ak); }); };
 
     if constexpr (LEAN) {
         // the FAST configuration's constants (fast_config): v2, loss != mse, generate mode
@@ -2605,44 +2039,19 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
             const float T_f = p.T_f, inv_T_f = p.inv_T_f, var_f = p.var_f;
             // the per-step constants held in VGPRs (opaque: the scalar reloads they would
             // otherwise be rematerialized as share lgkmcnt with the LDS traffic)
-            float gnd = p.g_num_drift, gis = p.g_inv_sst_f, gsf = p.g_sst_f;
-#if HE_LDS_HOIST & 1
-            asm volatile("" : "+v"(gnd), "+v"(gis), "+v"(gsf));
-#endif
+            const float gnd = p.g_num_drift, gis = p.g_inv_sst_f, gsf = p.g_sst_f;
             float ro[kObs];
 #pragma unroll
             for (int c = 0; c < kObs; ++c) ro[c] = p.rstv[4 + c];
-#if HE_LDS_HOIST & 2
-#pragma unroll
-            for (int c = 0; c < kObs; ++c) asm volatile("" : "+v"(ro[c]));
-#endif
             float preS = pre.S;
             if (e.t != 0) preS = (float)cur.S[i];
-            // HE_LDS_OBS_LOCK: a full block's 8 greeks evaluated up front as interleaved chains
-            // (greeks_lean_n, the same bits), held in registers for the block's 8 steps
-            float lkc[kLdsM], lkg[kLdsM], lkp[kLdsM];
-            auto obs_blk = [&](int buf, int, int) {
-#if HE_LDS_OBS_LOCK
-                if constexpr (LAG) return;
-                float Sb[kLdsM];
-#pragma unroll
-                for (int sl = 0; sl < kLdsM; ++sl) Sb[sl] = L.sc[buf][sl][lane].x;
-                greeks_lean_n<kLdsM>(Sb, gnd, gis, gsf, lkc, lkg, lkp);
-#endif
-            };
-            auto obs_step = [&](int buf, int sl, int k, float2 ak, auto full, auto fb) {
+            auto obs_step = [&](int buf, int sl, int k, float2 ak, auto full) {
                 const float2 r0 = L.sc[buf][sl][lane];
                 const float rP = L.pp[buf][sl][lane];
                 // the obs greeks: greeks_fast of the market price, as market_kernel makes them
-                float4 g;
-                if constexpr (LAG) {  // the reward stepper's, one block ago
-                    const int gb = (k / kLdsM) & 1;
-                    g = make_float4(L.gk[gb][0][sl][lane], L.gk[gb][1][sl][lane], L.gk[gb][2][sl][lane], 0.0f);
-                } else if constexpr (decltype(fb)::value && HE_LDS_OBS_LOCK) {
-                    g = make_float4(lkc[sl], lkg[sl], lkp[sl], 0.0f);
-                } else {
-                    g = greeks_lean(r0.x, gnd, gis, gsf);
-                }
+                // (the reward stepper making them one block ahead, or a block's 8 evaluated in
+                // lockstep up front, measured +-0: r03s12, r03s24)
+                const float4 g = greeks_lean(r0.x, gnd, gis, gsf);
                 // (i)-(ii) of step_env: the integer trade logic (:181-200)
                 const int32_t nc = e.call + trade_round(ak.x * mt_f, mt);
                 const int32_t nq = e.put + trade_round(ak.y * mt_f, mt);
@@ -2669,14 +2078,6 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
                 // staged in LDS (two tiles, alternating by step: the next step's row writes
                 // do not wait behind this step's read-back) and stored as whole 16-B lines
                 float* const tile = L.stage[k & 1];
-#ifdef HE_OBS_ROW_OPAQUE
-                // A/B: the obs row made for every lane (opaque) before the autoreset select, so
-                // the backend keeps 13 selects instead of an if/else around the obs computation
-                // (one exec-mask branch per step).  With asm volatile the 13 pins are scheduling
-                // barriers: config 2 299 / 307 -> 320 / 322 us per launch (r03s24).
-#pragma unroll
-                for (int c = 0; c < kObs; ++c) HE_OBS_PIN(o[c]);
-#endif
 #pragma unroll
                 for (int c = 0; c < kObs; ++c) tile[lane * kObs + c] = term ? ro[c] : o[c];
                 float* out = io.obs + (int64_t)k * N * kObs;
@@ -2688,13 +2089,9 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
                 preS = term ? rst.S : r0.x;
             };
             if (wrows == kLdsEnvs)
-                run_blk(obs_blk, [&](int buf, int sl, int k, float2 ak, auto fb) {
-                    obs_step(buf, sl, k, ak, std::true_type{}, fb);
-                });
+                run_blk([&](int buf, int sl, int k, float2 ak, auto) { obs_step(buf, sl, k, ak, std::true_type{}); });
             else
-                run_blk(obs_blk, [&](int buf, int sl, int k, float2 ak, auto fb) {
-                    obs_step(buf, sl, k, ak, std::false_type{}, fb);
-                });
+                run_blk([&](int buf, int sl, int k, float2 ak, auto) { obs_step(buf, sl, k, ak, std::false_type{}); });
         } else {
             const double tcpc = p.tcpc, slip_frac = p.slip_frac, lam = p.lam, w = p.w, theta = p.theta;
             const double shares_d = p.shares_d, inv_shares = p.inv_shares, den = p.den, inv_den = p.inv_den;
@@ -2704,34 +2101,7 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
             // reset market's book)
             double pv0 = (double)((shares_f * rst.S + 0.0f) + p.init_cash_f);
             if (BOOK) pv0 = pv0 + rst.B;
-            // LAG: the obs greeks of the block (greeks_lean_n: greeks_lean's bits) for the obs
-            // stepper, which steps this block one block later
-            const float gnd = p.g_num_drift, gis = p.g_inv_sst_f, gsf = p.g_sst_f;
-            auto rew_blk = [&](int buf, int b, int len) {
-                if constexpr (LAG) {
-                    const int gb = b & 1;
-                    if (len == kLdsM) {
-                        float Sb[kLdsM], gc[kLdsM], gg[kLdsM], gp[kLdsM];
-#pragma unroll
-                        for (int sl = 0; sl < kLdsM; ++sl) Sb[sl] = L.sc[buf][sl][lane].x;
-                        greeks_lean_n<kLdsM>(Sb, gnd, gis, gsf, gc, gg, gp);
-#pragma unroll
-                        for (int sl = 0; sl < kLdsM; ++sl) {
-                            L.gk[gb][0][sl][lane] = gc[sl];
-                            L.gk[gb][1][sl][lane] = gg[sl];
-                            L.gk[gb][2][sl][lane] = gp[sl];
-                        }
-                    } else {
-                        for (int sl = 0; sl < len; ++sl) {
-                            const float4 g = greeks_lean(L.sc[buf][sl][lane].x, gnd, gis, gsf);
-                            L.gk[gb][0][sl][lane] = g.x;
-                            L.gk[gb][1][sl][lane] = g.y;
-                            L.gk[gb][2][sl][lane] = g.z;
-                        }
-                    }
-                }
-            };
-            run_blk(rew_blk, [&](int buf, int sl, int k, float2 ak, auto) {
+            run_blk([&](int buf, int sl, int k, float2 ak, auto) {
                 const int64_t koff = (int64_t)k * N;
                 const float2 sc = L.sc[buf][sl][lane];
                 const float pP = L.pp[buf][sl][lane];
@@ -2776,15 +2146,8 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
             });
         }
     } else {
-#if HE_LDS_PIN
-        // the generic steps' per-handle constants, copied once and pinned in SGPRs (opaque):
-        // the kernel is built without MachineLICM, so left to the Params reads every step
-        // re-loads them from the scalar cache, each load's lgkmcnt(0) wait draining the step's
-        // LDS reads too (config 5: 406 scalar loads in the kernel's code)
-        Params pq = p;
-        pin_step_consts(pq, OBS);
-        const Params& p = pq;
-#endif
+        // (the generic steps' Params fields pinned in SGPRs instead of the scalar-cache reloads:
+        // config 5 +4 %, config 4 -1 %, r03s16)
         if (OBS && e.t != 0) pre = Mkt{(float)cur.S[i], HESTON ? (float)cur.v[i] : p.var_f, cur.C[i], cur.P[i], 0.0};
         auto step = [&](int buf, int sl, int k, float2 ak) {
             const int64_t koff = (int64_t)k * N;
@@ -2847,37 +2210,20 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
 // block bp - 1.  pw = producer wave index (kLdsPEnvs envs each).  Lanes past the last
 // env mirror env N-1 like the steppers' (identical values, identical addresses).
 template <int MODE, bool BOOK, bool LEAN>
-__device__ __forceinline__ void lds_producer(const Params& pp, int k_steps, const Market& cur,
+__device__ __forceinline__ void lds_producer(const Params& p, int k_steps, const Market& cur,
                                              LdsMarketT<MODE, BOOK, LEAN>& W, int64_t base, int pw) {
     using G = LdsGeom<MODE, BOOK>;
     constexpr bool HESTON = G::HESTON;
-#if HE_LDS_PIN
-    // Heston / a book (the producer-bound kernels): the market constants pinned (HE_LDS_PIN)
-    Params pq = pp;
-    if constexpr (HESTON || BOOK) pin_market_consts(pq, HESTON, BOOK);
-    const Params& p = (HESTON || BOOK) ? pq : pp;
-#else
-    const Params& p = pp;
-#endif
     constexpr int kLdsLanes = G::lanes, kLdsPEnvs = G::penvs, kLdsH = G::H;
     const int lane = threadIdx.x & 63;
     const int sub = lane / kLdsPEnvs;
-#ifdef HE_LDS_PW_SWAP
-    const int le = (kLdsLanes - 1 - pw) * kLdsPEnvs + (lane % kLdsPEnvs);  // A/B: the producer waves' env halves swapped
-#else
     const int le = pw * kLdsPEnvs + (lane % kLdsPEnvs);  // local env of this lane
-#endif
     const int64_t N = p.n;
     const int nb = (k_steps + kLdsM - 1) / kLdsM;
     const uint32_t T = (uint32_t)p.T;
     const int64_t pi = (base + le) < N ? base + le : N - 1;
     const int64_t gid = p.goff + pi;
-#ifdef HE_LDS_PRIO_PROD1
-    if (pw == 1) __builtin_amdgcn_s_setprio(HE_LDS_PRIO_PROD1);  // A/B: the second producer wave's own priority
-    else __builtin_amdgcn_s_setprio(HE_LDS_PRIO_PROD);
-#else
-    __builtin_amdgcn_s_setprio(HE_LDS_PRIO_PROD);
-#endif
+    __builtin_amdgcn_s_setprio(kPrioProd);
     const uint32_t ep0 = cur.ep[pi];
     const uint32_t t0 = cur.t[pi];
     double Sbs = cur.S[pi];                          // f64 price before slot 0 of block bp
@@ -2893,13 +2239,6 @@ __device__ __forceinline__ void lds_producer(const Params& pp, int k_steps, cons
         LDS_BAR();  // diagnostic build: the producers only keep the barrier count
         continue;
 #endif
-#ifdef HE_LDS_PROD_ALT
-        // A/B: the producer waves alternate between priority 1 and 2 by block, so the SIMD's
-        // arbitration between two producers of different workgroups (the older one wins a
-        // tie) does not favour the same wave every block
-        if (((bp + pw) & 1) != 0) __builtin_amdgcn_s_setprio(HE_LDS_PRIO_PROD);
-        else __builtin_amdgcn_s_setprio(HE_LDS_PRIO_PROD + 1);
-#endif
         if (bp < nb) {
             const int kb = bp * kLdsM;
             const int len = (k_steps - kb) < kLdsM ? (k_steps - kb) : kLdsM;
@@ -2912,7 +2251,7 @@ __device__ __forceinline__ void lds_producer(const Params& pp, int k_steps, cons
                 // LOCK: the lean GBM producers of a whole block evaluate their kLdsH slots in
                 // lockstep (he_math.h *_n forms: the same operations per slot, so the same
                 // bits, as kLdsH interleaved chains with shared constants)
-                constexpr bool LOCK = FULL && LEAN && !HESTON && HE_LDS_PROD_LOCK;
+                constexpr bool LOCK = FULL && LEAN && !HESTON;
 
             const uint64_t nf = a0 + (uint64_t)(kb + sl0);
             const uint32_t tpf = (tpb + (uint32_t)sl0) % T;
@@ -2963,27 +2302,14 @@ __device__ __forceinline__ void lds_producer(const Params& pp, int k_steps, cons
                         double z;
                         if (h == 0 || (n & 1) == 0) {
                             double z1, z2;
-#if defined(HE_LDS_SKIP) && (HE_LDS_SKIP & 1)
-                            {   // diagnostic build: no Box-Muller
-                                u32x4 ctr = {(uint32_t)(n >> 1), (uint32_t)(n >> 33), (uint32_t)gid, (uint32_t)((uint64_t)gid >> 32)};
-                                u32x4 x = philox4x32_10(ctr, p.key0, p.key1);
-                                z1 = u01(x.x, x.y) - 0.5;
-                                z2 = u01(x.z, x.w) - 0.5;
-                            }
-#else
                             normals(p, gid, n >> 1, &z1, &z2);
-#endif
                             z = (n & 1) ? z2 : z1;
                             zc = z2;
                         } else {
                             z = zc;
                         }
                         const double dW = p.sqrt_dt * z;
-#if defined(HE_LDS_SKIP) && (HE_LDS_SKIP & 16)
-                        ex[h] = 1.0 + p.drift + p.sqrt_var * dW;  // diagnostic build: no exp
-#else
                         ex[h] = exp_k(p.drift + p.sqrt_var * dW);  // rbergomi_sim.py:459-463
-#endif
                     }
                 }
             } else {
@@ -3039,7 +2365,7 @@ __device__ __forceinline__ void lds_producer(const Params& pp, int k_steps, cons
                 for (int h = 0; h < kLdsH; ++h) {
                     const double drift = (p.mu - 0.5 * vpx[h]) * p.dt;
                     const double diff = sqx[h] * ws[h];
-                    ex[h] = (FULL || sl0 + h < len) ? HE_HESTON_EXP(drift + diff) : 1.0;
+                    ex[h] = (FULL || sl0 + h < len) ? exp(drift + diff) : 1.0;
                 }
             }
             // (2) the f64 price chain: the block's growth factors gathered from the env's
@@ -3086,10 +2412,9 @@ __device__ __forceinline__ void lds_producer(const Params& pp, int k_steps, cons
             // the position before it (hedging_env_v2.py:229-231)
             uint32_t tp = tpf;
             const int wb = bp % LdsMarketT<MODE, BOOK, LEAN>::NB;
-            double lkC[kLdsH], lkP[kLdsH], lkB[kLdsH];   // LOCK: the slots' marks (+ book), in lockstep
+            double lkC[kLdsH], lkP[kLdsH];   // LOCK: the slots' marks, in lockstep
             if constexpr (LOCK) {
                 double Sm[kLdsH], Km[kLdsH];
-                int32_t tb[kLdsH];
                 uint32_t tq = tpf;
 #pragma unroll
                 for (int h = 0; h < kLdsH; ++h) {
@@ -3097,17 +2422,9 @@ __device__ __forceinline__ void lds_producer(const Params& pp, int k_steps, cons
                     const double Sprev = (h == 0) ? Sin : Sx[h - 1];
                     Sm[h] = last ? ((tq == 0) ? p.s0 : Sprev) : Sx[h];
                     Km[h] = rint(Sm[h]);   // marks<GBM>: the rolling-ATM strike K = round(S)
-                    tb[h] = (int32_t)(tq + 1);
                     tq = (tq + 1 == T) ? 0u : tq + 1;
                 }
                 bs_call_put_n<kLdsH>(Sm, Km, p.bs, lkC, lkP);
-#if HE_LDS_BOOK_OPTS && HE_LDS_BOOK_LOCK
-                if constexpr (BOOK) {   // two slots at a time: four at once spill (760 B of scratch)
-#pragma unroll
-                    for (int h = 0; h < kLdsH; h += 2)
-                        book_value_n<2>(p, Sx + h, tb + h, Mx + h, &W.btab[0][0], &W.bopt[0], lkB + h);
-                }
-#endif
             }
 #pragma unroll
             for (int h = 0; h < kLdsH; ++h) {
@@ -3118,9 +2435,6 @@ __device__ __forceinline__ void lds_producer(const Params& pp, int k_steps, cons
                     const double Vh = HESTON ? Vx[h] : p.var;
                     const double Vm = HESTON ? (last ? ((tp == 0) ? p.var : ((h == 0) ? Vin : Vx[h > 0 ? h - 1 : 0])) : Vh) : p.var;
                     float C, P;
-#if defined(HE_LDS_SKIP) && (HE_LDS_SKIP & 2)
-                    C = (float)Sm * 0.02f; P = (float)Sm * 0.018f;  // diagnostic build: no marks
-#else
                     if constexpr (LOCK) {
                         C = (float)lkC[h];
                         P = (float)lkP[h];
@@ -3128,20 +2442,14 @@ __device__ __forceinline__ void lds_producer(const Params& pp, int k_steps, cons
                         // the episode step of the marks: the slot's (tp + 1), or tp for the lagged ones
                         marks<MODE, !LEAN>(p, Sm, Vm, last ? tp : tp + 1u, &C, &P);
                     }
-#endif
                     const int sl = sl0 + h;
                     W.sc[wb][sl][le] = make_float2((float)Sx[h], C);
                     W.pp[wb][sl][le] = P;
                     if (HESTON) W.vv[HESTON ? wb : 0][HESTON ? sl : 0][le] = (float)Vh;
                     // the book after the step into slot sl (episode step tp + 1, the new S,
                     // not lagged): market_body's tileC
-#if HE_LDS_BOOK_OPTS
-                    if constexpr (BOOK && LOCK && HE_LDS_BOOK_LOCK) W.bk[wb][sl][le] = lkB[h];
-                    else if (BOOK) W.bk[wb][sl][le] = book_value<!HESTON>(p, Sx[h], Vh, (int32_t)(tp + 1), Mx[h],
-                                                                          &W.btab[0][0], &W.bopt[0]);
-#else
-                    if (BOOK) W.bk[wb][sl][le] = book_value<!HESTON>(p, Sx[h], Vh, (int32_t)(tp + 1), Mx[h], &W.btab[0][0]);
-#endif
+                    if (BOOK) W.bk[wb][sl][le] = book_value<!HESTON>(p, Sx[h], Vh, (int32_t)(tp + 1), Mx[h],
+                                                                     &W.btab[0][0], &W.bopt[0]);
                     if (kb + sl == k_steps - 1) {  // the market position after the launch
                         const uint32_t q = off + (uint32_t)(k_steps - 1);
                         cur.ep[pi] = ep0 + q / T;
@@ -3156,17 +2464,12 @@ __device__ __forceinline__ void lds_producer(const Params& pp, int k_steps, cons
                 }
             }
             };
-#if HE_LDS_PROD_FULL
             if (len == kLdsM) block(std::true_type{});
             else block(std::false_type{});
-#else
-            block(std::false_type{});
-#endif
             tpb = (uint32_t)(((uint64_t)tpb + kLdsM) % T);
         }
         LDS_BAR();  // block bp handed to the steppers
     }
-    if (LdsMarketT<MODE, BOOK, LEAN>::LAG) LDS_BAR();  // the lagged obs stepper's last block
     LDS_T1(2 + (pw < 2 ? pw : 1));
 }
 
@@ -3230,12 +2533,10 @@ __device__ __forceinline__ int lds_role(int wave) {
 // fewer than the occupancy API and the compiler report (MI355X_MICROARCH.md, Residency),
 // and at 106 the 4 x 6 waves of 4 workgroups no longer fit a CU -- at 65,536 envs the
 // launch ran in two rounds of workgroups (536 vs ~270 us).  The spills go to VGPR lanes.
-#ifndef HE_LDS_NUM_SGPR
-#define HE_LDS_NUM_SGPR 96
-#endif
+constexpr int kLdsNumSgpr = 96;
 template <int MODE, bool BOOK, bool LEAN>
 __global__ __launch_bounds__((LdsGeom<MODE, BOOK>::threads), (LdsGeom<MODE, BOOK>::minwaves))
-    __attribute__((amdgpu_num_sgpr(HE_LDS_NUM_SGPR))) void lds_rollout_kernel(const Params* __restrict__ pc, State s, Io io,
+    __attribute__((amdgpu_num_sgpr(kLdsNumSgpr))) void lds_rollout_kernel(const Params* __restrict__ pc, State s, Io io,
                                                                  int k_steps, Market cur) {
     __shared__ __attribute__((aligned(16))) LdsMarketT<MODE, BOOK, LEAN> lm;
     const Params& p = *pc;  // read through the scalar cache (a by-value copy spills)
@@ -3244,9 +2545,7 @@ __global__ __launch_bounds__((LdsGeom<MODE, BOOK>::threads), (LdsGeom<MODE, BOOK
     if constexpr (BOOK) {  // the tau table into LDS (rows <= kLdsBookRows: lds_rollout_eligible)
         const int nv = 4 * p.book_rows;
         for (int k = threadIdx.x; k < nv; k += LdsGeom<MODE, BOOK>::threads) (&lm.btab[0][0])[k] = p.book_tab[k];
-#if HE_LDS_BOOK_OPTS
         if ((int)threadIdx.x < p.book_n) lm.bopt[threadIdx.x] = p.book[threadIdx.x];
-#endif
         __syncthreads();
     }
     if (wave == 0) lds_stepper<MODE, BOOK, LEAN, false>(p, s, io, k_steps, cur, lm, base);
@@ -3263,8 +2562,8 @@ __global__ __launch_bounds__((LdsGeom<MODE, BOOK>::threads), (LdsGeom<MODE, BOOK
 // own PCG64 draw), so the loaders walk every env's (path, t) and PCG64 stream ahead of the
 // steppers: for block b + 1 each issues its half of the M post-step rows {S, v, C, P} of
 // every env (one lane per env; an env's rows of a block are contiguous in the table) a
-// whole block before they go to LDS, evaluates their obs greeks there (HE_REPLAY_LGREEKS:
-// the row's own greeks(), so the 16-B recg record is not read per step), and for an env
+// whole block before they go to LDS, evaluates their obs greeks there (the row's own
+// greeks(), so the 16-B recg record is not read per step: 552 -> 425 us per launch, r03s10), and for an env
 // whose episode ends in the block draws the new path (replay_reset's pcg64_integers) and
 // loads its row 0 -- the reset obs and the next episode's starting market.  Needs T >= M
 // (at most one episode end per env and block) and autoreset.
@@ -3283,9 +2582,6 @@ struct LdsReplay {
 };
 static_assert(kLdsM > 8 || sizeof(LdsReplay) <= 40 * 1024 - 64, "4 workgroups per CU");
 
-#ifndef HE_REPLAY_LGREEKS
-#define HE_REPLAY_LGREEKS 1  // the loaders evaluate the rows' obs greeks (table_greeks_kernel's greeks()) instead of reading recg
-#endif
 // Loader wave `part` (0, 1) stages slots [part * H, part * H + H) of every block, H = M / 2; both
 // walk the whole block's positions and PCG64 draws (the same values), part 0 also the
 // new-episode records and the state write-back.
@@ -3301,7 +2597,7 @@ __device__ __forceinline__ void lds_replay_loader(const Params& p, State s, int 
     const GLOBAL v4f* rec = (const GLOBAL v4f*)p.rec;
     const GLOBAL v4f* recg = (const GLOBAL v4f*)p.recg;
     const int sl0 = part * H;
-    __builtin_amdgcn_s_setprio(HE_LDS_PRIO_PROD);
+    __builtin_amdgcn_s_setprio(kPrioProd);
     LDS_T0();
     int32_t path = s.path[i];
     uint32_t t = s.t[i];                     // episode step before the next slot (< T: autoreset)
@@ -3338,7 +2634,6 @@ __device__ __forceinline__ void lds_replay_loader(const Params& p, State s, int 
             B[h] = make_float4(0.5f, 0.01f, -0.5f, 0.0f);
 #else
             A[h] = ld4(rec, r);
-            if (!HE_REPLAY_LGREEKS) B[h] = ld4(recg, r);
 #endif
         }
         if (part == 0 && rsl < kLdsM) {  // lanes whose episode ends in the block (exec-masked:
@@ -3362,7 +2657,7 @@ __device__ __forceinline__ void lds_replay_loader(const Params& p, State s, int 
             for (int h = 0; h < H; ++h) {
                 const int sl = sl0 + h;
                 if (sl < len) {
-#if HE_REPLAY_LGREEKS && !(defined(HE_REPLAY_DIAG) && HE_REPLAY_DIAG == 1)
+#if !(defined(HE_REPLAY_DIAG) && HE_REPLAY_DIAG == 1)
                     // table_greeks_kernel's record, here from the row itself
                     B[h] = p.record_metrics ? replay_greeks(p, A[h].x, A[h].y) : make_float4(0.f, 0.f, 0.f, 0.f);
 #endif
@@ -3396,13 +2691,10 @@ __device__ __forceinline__ void lds_replay_loader(const Params& p, State s, int 
 // OBS = false: the reward wave (owns the env state); OBS = true: the obs wave.  FAST: the
 // configuration of fast_replay_config (v2, loss != mse, shares_to_hedge != 0, record_metrics,
 // max_contracts_held > 0) with its uniform branches compiled out.
-#ifndef HE_REPLAY_LDS_PREFETCH
-#define HE_REPLAY_LDS_PREFETCH kLdsPrefetch
-#endif
 template <bool OBS, bool FAST>
 __device__ __forceinline__ void lds_replay_stepper(const Params& p, State s, const Io& io, int k_steps,
                                                    LdsReplay& L, int64_t base) {
-    constexpr int D = HE_REPLAY_LDS_PREFETCH;  // steps of actions in flight
+    constexpr int D = kLdsPrefetch;  // steps of actions in flight (8: +-0, r03s18)
     static_assert(kLdsM % D == 0, "the action ring index is the slot mod D");
     const int lane = threadIdx.x & 63;
     const int64_t N = p.n;
@@ -3415,7 +2707,7 @@ __device__ __forceinline__ void lds_replay_stepper(const Params& p, State s, con
     const GLOBAL v2f* gact = (const GLOBAL v2f*)io.act;
     GLOBAL float* const grew = (GLOBAL float*)io.rew;
     GLOBAL uint8_t* const gterm = (GLOBAL uint8_t*)io.term;
-    __builtin_amdgcn_s_setprio(OBS ? HE_LDS_PRIO_OBS : HE_REPLAY_PRIO_REW);
+    __builtin_amdgcn_s_setprio(OBS ? kPrioObs : kPrioReplayRew);
     LDS_T0();
     Env e{};
     e.t = s.t[i];
@@ -3660,7 +2952,7 @@ __device__ __forceinline__ void lds_replay_stepper(const Params& p, State s, con
 }
 
 template <bool FAST>
-__global__ __launch_bounds__(256, 4) __attribute__((amdgpu_num_sgpr(HE_LDS_NUM_SGPR))) void lds_replay_kernel(
+__global__ __launch_bounds__(256, 4) __attribute__((amdgpu_num_sgpr(kLdsNumSgpr))) void lds_replay_kernel(
     const Params* __restrict__ pc, State s, Io io, int k_steps) {
     __shared__ __attribute__((aligned(16))) LdsReplay lm;
     const Params& p = *pc;
@@ -3910,7 +3202,6 @@ struct he_env {
     int32_t next_state = 0;   // next block: 0 none, 1 generating on `xs` (ev_next), 2 ready
     bool fuse_market = true;  // rollouts: next block's market in the step grid (HE_FUSED_MARKET=0: side stream)
     bool lds_rollout = true;  // he_rollout (GBM, no book): lds_rollout_kernel (HE_LDS_ROLLOUT=0: tile kernels)
-    bool step_split = false;  // he_step (GBM FAST): step1_split_kernel if HE_STEP_SPLIT=1 at he_create (A/B, slower)
     int32_t prefetch_mode = 0; // 0 auto, 1 never, 2 always: market_kernel(b+1) on `xs` during block b
     hipStream_t xs = nullptr; // library side stream for market prefetch
     hipEvent_t ev_fork = nullptr, ev_next = nullptr;
@@ -4203,21 +3494,6 @@ static void launch_step_gs(he_env* env, const Params& p, const Io& io, bool info
         const float4* tA = REPLAY ? p.rec : p.tileA;
         const float4* tB = REPLAY ? p.recg : p.tileB;
         StepIo sio{io.act, io.obs, io.rew, io.term, io.trunc, io.tobs};
-        if constexpr (MODE == HE_MODE_GBM && FAST && !BOOK && !GS) {
-            if (HE_STEP_SPLIT && env->step_split && !env->vn_on && io.obs && io.rew && io.term) {
-                const unsigned sb = (unsigned)((env->cfg.n_envs + kEpb - 1) / kEpb);
-                if (env->ev_start) {
-                    hipEvent_t a = (hipEvent_t)env->ev_start, b = (hipEvent_t)env->ev_stop;
-                    env->ev_start = env->ev_stop = nullptr;
-                    hipExtLaunchKernelGGL(step1_split_kernel, dim3(sb), dim3(2 * kBlock), 0, st, a, b, 0, pc, p.n, tA, tB,
-                                          env->s, sio, slot0);
-                } else {
-                    hipLaunchKernelGGL(step1_split_kernel, dim3(sb), dim3(2 * kBlock), 0, st, pc, p.n, tA, tB, env->s,
-                                       sio, slot0);
-                }
-                return;
-            }
-        }
         if (env->vn_on) {  // + the VecNormalize moments in the same launch
             vn::MomentsArgs vm = env->vn;
             vm.obs = io.obs;
@@ -4275,24 +3551,12 @@ static void launch_fused_gs(he_env* env, const Params& p, const Io& io, int k, i
     const int nb = env->cur_buf ^ 1;
     const dim3 grid((unsigned)(sblocks + mblocks));
     size_t pad = 0;
-#if defined(HE_FUSED_WG_PER_CU) && HE_FUSED_WG_PER_CU > 0
-    {   // diagnostic: cap the grid's workgroups per CU through dynamic LDS
-        static size_t stat = [] {
-            hipFuncAttributes fa{};
-            (void)hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(step_market_kernel<MODE, BOOK, FAST, GS>));
-            return (size_t)fa.sharedSizeBytes;
-        }();
-        const size_t per = kCuLds / (HE_FUSED_WG_PER_CU + 1) + 1024;
-        pad = per > stat ? per - stat : 0;
-    }
-#endif
     hipEvent_t a = nullptr, b = nullptr;
     if (env->ev_start) {  // one-shot: bracket exactly this dispatch (hipExtLaunchKernelGGL)
         a = (hipEvent_t)env->ev_start;
         b = (hipEvent_t)env->ev_stop;
         env->ev_start = env->ev_stop = nullptr;
     }
-#if HE_FUSED_DPARAMS
     (void)p;
     const Params* pc = env->dparams;
     const int32_t buf = env->cur_buf;
@@ -4302,15 +3566,6 @@ static void launch_fused_gs(he_env* env, const Params& p, const Io& io, int k, i
     else
         hipLaunchKernelGGL((step_market_kernel<MODE, BOOK, FAST, GS>), grid, dim3(kBlock), pad, st, pc, buf, env->s, io,
                            k, slot0, env->cur, env->bak[nb], (int32_t)sblocks);
-#else
-    const Params pm = tile_params(env, nb);
-    if (a)
-        hipExtLaunchKernelGGL((step_market_kernel<MODE, BOOK, FAST, GS>), grid, dim3(kBlock), pad, st, a, b, 0, p,
-                              env->s, io, k, slot0, pm, env->cur, env->bak[nb], (int32_t)sblocks);
-    else
-        hipLaunchKernelGGL((step_market_kernel<MODE, BOOK, FAST, GS>), grid, dim3(kBlock), pad, st, p, env->s, io, k,
-                           slot0, pm, env->cur, env->bak[nb], (int32_t)sblocks);
-#endif
 }
 
 // step the current block (k steps from slot0) and generate the next block into the
@@ -4436,12 +3691,8 @@ static bool fast_replay_config(const he_env* env) {
 static he_status launch_lds_replay(he_env* env, const Io& io, int k_total, hipStream_t st) {
     const int64_t blocks = (env->cfg.n_envs + kLdsEnvs - 1) / kLdsEnvs;
     const Params* pc = env->dparams;
-#ifdef HE_REPLAY_FORCE_GENERIC
-    void (*kern)(const Params*, State, Io, int) = lds_replay_kernel<false>;  // A/B: the generic steppers
-#else
     void (*kern)(const Params*, State, Io, int) = fast_replay_config(env) ? lds_replay_kernel<true>
                                                                           : lds_replay_kernel<false>;
-#endif
     if (env->ev_start) {  // one-shot: bracket exactly this dispatch
         hipEvent_t a = (hipEvent_t)env->ev_start, b = (hipEvent_t)env->ev_stop;
         env->ev_start = env->ev_stop = nullptr;
@@ -4676,8 +3927,6 @@ he_status he_create(const he_config* cfg, he_env** out) {
             env->fuse_market = !(ev && ev[0] == '0');
             const char* el = getenv("HE_LDS_ROLLOUT");
             env->lds_rollout = !(el && el[0] == '0');
-            const char* es = getenv("HE_STEP_SPLIT");
-            env->step_split = es && es[0] == '1';
         }
         HE_HIP(env, hipStreamCreateWithFlags(&env->xs, hipStreamNonBlocking));
         HE_HIP(env, hipEventCreateWithFlags(&env->ev_fork, hipEventDisableTiming));
@@ -5126,8 +4375,11 @@ he_status he_get_config(const he_env* env, he_config* out) {
 }
 
 // Checkpoint blob: an 8-byte header {ready flag, format << 8}, then every state field.
-// The format changes with the field list (3: + the episode summaries of ABI v3).
+// Format 3 added the version byte to the header; the field list is the one round-2 blobs
+// (format 0: a bare ready flag) already carried, so those restore too (same size).  A
+// change to the field list takes a new format number.
 constexpr uint64_t kStateFormat = 3;
+constexpr uint64_t kStateFormatLegacy = 0;
 
 size_t he_state_size(const he_env* env) {
     if (!env) return 0;
@@ -5162,7 +4414,7 @@ he_status he_set_state(he_env* env, const void* host_buf, size_t size) {
     if (size >= 8) {
         uint64_t h0;
         memcpy(&h0, host_buf, 8);
-        if ((h0 >> 8) != kStateFormat)
+        if ((h0 >> 8) != kStateFormat && (h0 >> 8) != kStateFormatLegacy)
             return fail(env, HE_EINVAL, "checkpoint format %llu != %llu: saved by another libhedgeenv version",
                         (unsigned long long)(h0 >> 8), (unsigned long long)kStateFormat);
     }

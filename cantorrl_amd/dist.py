@@ -42,13 +42,27 @@ def init(backend=None, force=False):
     return rank, local, world
 
 
-def gather_rollout(t, group=None):
-    """All-gather a per-env tensor [N, ...] from every rank -> [world*N, ...] in
-    global-id order (rank-major, matching shard_offset)."""
+def gather_rollout(t, group=None, env_dim=0):
+    """All-gather a per-env tensor from every rank in global-id order (rank r's envs are the
+    global ids [r N, (r + 1) N), shard_offset).
+
+    env_dim = 0: [N, ...] -> [world * N, ...] (per-env records: episode summaries).
+    env_dim = 1: [K, N, ...] -> [K, world * N, ...] (he_rollout's obs / reward / terminated,
+    step-major): the collective concatenates the ranks' [K, N, ...] blocks rank-major, so the
+    result is [world, K, N, ...] re-laid out as [K, world, N, ...] (one device copy) --
+    SURVEY 8(e)'s rollout-tensor gather at the buffer boundary (train_ppo_v2.py:48), for
+    small N only (config 4's full tensors are ~9 GB per rank)."""
     import torch.distributed as dist
     if not dist.is_initialized():
         return t
+    if env_dim not in (0, 1) or t.dim() <= env_dim:
+        raise ValueError("env_dim must be 0 or 1 and a dimension of t")
     w = dist.get_world_size(group)
+    t = t.contiguous()
     out = torch.empty((w * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
-    dist.all_gather_into_tensor(out, t.contiguous(), group=group)
-    return out
+    dist.all_gather_into_tensor(out, t, group=group)
+    if env_dim == 0 or w == 1:
+        return out
+    k, n = t.shape[0], t.shape[1]
+    rest = tuple(t.shape[2:])
+    return out.view((w, k, n) + rest).transpose(0, 1).reshape((k, w * n) + rest)

@@ -78,7 +78,7 @@ class HedgingVecEnv:
 
     def __init__(self, n_envs, data_file_path=None, *, tables=None, variant=2, mode=None,
                  generate=None, device=None, seed=None, global_env_offset=0, autoreset=True,
-                 return_numpy=True, info_keys=MONITOR_KEYWORDS, monitor_keywords=None,
+                 return_numpy=True, info_keys=MONITOR_KEYWORDS, monitor_keywords=None, freeze_infos=True,
                  market_block=64, market_prefetch="auto", check_finite=False, **env_kwargs):
         self.lib = _lib.load()
         self.num_envs = int(n_envs)
@@ -191,12 +191,24 @@ class HedgingVecEnv:
         self._info_t = {}
         self._info = _lib.HeInfo()
         known = dict(_lib.INFO_FIELDS)
+        # every info field is a slice of ONE flat buffer (256-B aligned), so freezing a view
+        # (InfoView) is one device copy, not one per key
+        offs, tot = [], 0
         for k in self.info_keys:
             if k not in known:
                 raise KeyError(f"unknown info key {k!r}")
-            t = torch.zeros((n,), dtype=_TORCH_DT[known[k]], device=dev)
+            dt = _TORCH_DT[known[k]]
+            offs.append((k, dt, tot))
+            tot += -(-n * torch.empty((), dtype=dt).element_size() // 256) * 256
+        self._info_flat = torch.zeros(max(tot, 1), dtype=torch.uint8, device=dev)
+        for k, dt, o in offs:
+            t = self._info_flat[o:o + n * torch.empty((), dtype=dt).element_size()].view(dt)
             self._info_t[k] = t
             setattr(self._info, k, t.data_ptr())
+        self._info_offs = offs
+        # InfoView snapshots (see InfoView): freeze_infos=False skips them (a view read after
+        # a later step then shows that step's values)
+        self.freeze_infos = bool(freeze_infos)
         self.return_numpy = bool(return_numpy)
         self.monitor_keywords = tuple(monitor_keywords) if monitor_keywords else None
         self._pending_seeds = None
@@ -272,8 +284,14 @@ class HedgingVecEnv:
         """Freeze the newest InfoView (if still alive) before its buffers are overwritten."""
         r, self._live_view = self._live_view, None
         v = r() if r is not None else None
-        if v is not None:
+        if v is not None and self.freeze_infos:
             v._freeze()
+
+    def _info_snapshot(self):
+        """One device copy of every info field (the flat buffer) -> {key: tensor view}."""
+        flat = self._info_flat.clone()
+        n = self.num_envs
+        return {k: flat[o:o + n * torch.empty((), dtype=dt).element_size()].view(dt) for k, dt, o in self._info_offs}
 
     def reset_tensors(self, env_ids=None):
         self._retire_view()
@@ -463,10 +481,14 @@ class InfoView:
 
     The view reads the env's live info buffers, copied to the host on the first access.
     It is the env's newest view until the env's next step or reset, which first freezes
-    it (a device copy of the info buffers, only when the view is still alive and has not
-    been read): a view read after later steps still shows its own step, and a view that is
-    dropped or read before the next step costs no copy.  Done rows (terminal obs, Monitor
-    episode) are materialized by step_wait right away, from the live buffers."""
+    it when it is still alive and has not been read: a view read after later steps still
+    shows its own step.  In SB3's loop (`obs, r, d, infos = env.step(a)`) the previous
+    `infos` is still referenced while step() runs, so a step usually pays the freeze: ONE
+    device copy of the info fields' flat buffer (N x the keys' bytes: 1.5 MB for the three
+    Monitor keys at 65,536 envs, a few us), not one per key.  freeze_infos=False (env
+    constructor) drops the snapshots for callers that read infos before the next step.
+    Done rows (terminal obs, Monitor episode) are materialized by step_wait right away,
+    from the live buffers."""
 
     def __init__(self, venv, done):
         self._v = venv
@@ -478,8 +500,8 @@ class InfoView:
         venv._live_view = weakref.ref(self)
 
     def _freeze(self):
-        if self._host is None and self._snap is None:
-            self._snap = {k: t.clone() for k, t in self._v._info_t.items()}
+        if self._host is None and self._snap is None and self._v._info_t:
+            self._snap = self._v._info_snapshot()
 
     def _host_info(self):
         if self._host is None:

@@ -196,9 +196,13 @@ class DeviceVecNormalize:
             return False
         st = self.lib.he_vecnorm_attach(self.venv._h, ctypes.byref(p), self._p(self._returns),
                                         self._p(self._stats), self._p(self._scratch))
-        if st != _lib.HE_OK:  # a build without the fused path: two launches
-            self._fusable = False
-            return False
+        # every build has the fused path and __init__ checked the env count, so any failure
+        # here is a real argument error (non-finite gamma, a bad layout): raised, not hidden
+        # behind the two-launch path
+        if st != _lib.HE_OK:
+            msg = self.lib.he_last_error(self.venv._h)
+            raise _lib.HedgeEnvError(f"he_vecnorm_attach failed with status {st}: "
+                                     f"{msg.decode() if msg else ''}")
         return True
 
     def close(self):

@@ -179,7 +179,12 @@ def closed_loop(n_envs=16, episodes=2, seed=42, mark="rolling_atm"):
     if mark == "fixed_european":
         # the reference's own black_scholes_vectorized (option_price_assignment.py:10-21) over
         # columns t = 0..T-1 as process_price_paths does (:33-49): K = np.round(S0),
-        # T = np.clip(1 - t / 252, 0, None), sigma = the GBM's sqrt(v) for the realized vol
+        # T = np.clip(1 - t / 252, 0, None).  DELIBERATE DEVIATION: sigma is the market's own
+        # volatility (the GBM's sqrt(v)), not process_price_paths' expanding-window realized
+        # volatility (calculate_annualized_vol_matrix, :23-31: 0 at t = 0, clamped to 1e-8).
+        # G13 therefore pins the black_scholes_vectorized formula and the env mechanics of
+        # HE_MARK_FIXED_EUROPEAN, not the reference generator's realized-vol marks; those are
+        # the analytics path's (he_fixed_european_marks, pinned by g11 to the reference).
         bsv = importlib.import_module("src.sim.option_price_assignment").black_scholes_vectorized
         Sf = S.reshape(n_envs * E, T + 1)
         K = np.round(Sf[:, 0])

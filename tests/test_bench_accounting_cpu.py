@@ -23,7 +23,7 @@ def bench():
 
 def test_threshold_matches_library(bench):
     src = open(os.path.join(REPO, "cantorrl_amd", "csrc", "hedge_env.hip")).read()
-    assert f"#define HE_GREEKS_IN_STEP_MIN_ENVS {bench.GREEKS_IN_STEP_MIN_ENVS}" in src
+    assert f"constexpr int64_t kGreeksInStepMinEnvs = {bench.GREEKS_IN_STEP_MIN_ENVS};" in src
 
 
 def test_tile_layout(bench, monkeypatch):
@@ -91,3 +91,48 @@ def test_lds_path_selection(bench, monkeypatch):
     assert r5["overhead_bytes_per_launch"] == 0 and r5["kernel"].startswith("lds_rollout_kernel")
     monkeypatch.setenv("HE_LDS_ROLLOUT", "0")
     assert not bench.lds_rollout(bench.CONFIGS[2])
+
+
+def _roof(bench):
+    return bench.roofline("rollout", 65536, 0.3, 256, False, "gbm", lds=True)
+
+
+@pytest.mark.parametrize("config", [2, 3, 4, 5, 6])
+def test_bound_is_fixed_per_config(bench, config):
+    """configs 4 / 5 (a book, Heston) are VALU-bound and say so whether or
+    not the PMC passes ran; the others are HBM-bound.  Without counters a VALU line keeps the
+    figure null with a note, never an HBM fraction in the headline fields."""
+    cfg = bench.CONFIGS[config]
+    want = "valu" if config in (4, 5) else "hbm"
+    assert bench.config_bound(cfg) == want
+    r = bench.finish_roofline(_roof(bench), cfg, (None, "skipped"), (None, "skipped"), 0.3)
+    assert r["bound"] == want
+    if want == "valu":
+        assert r["frac"] is None and r["achieved"] is None and "valu_note" in r
+        assert r["hbm"]["frac"] == _roof(bench)["frac"]
+    else:
+        assert r["frac"] == _roof(bench)["frac"] and r["unit"] == "GB/s"
+    # with the VALU pass: the issue rate is the headline figure
+    valu = {"lds_rollout_kernel": dict(valu_insts=1e9, f64_share=0.5, issue_per_simd_cycle=0.2,
+                                       issue_bound_per_simd_cycle=0.333, valu_issue_frac=0.6, f64_flop=1e12,
+                                       cycles_profiled=1e6)}
+    r = bench.finish_roofline(_roof(bench), cfg, (valu, None), (1.1e9, {"FETCH_SIZE": 1.0, "WRITE_SIZE": 1.0}), 0.3)
+    assert r["bound"] == want and r["traffic"] == int(1.1e9)
+    if want == "valu":
+        assert r["frac"] == 0.6 and r["unit"].startswith("VALU")
+    else:
+        assert r["valu"]["valu_issue_frac"] == 0.6 and r["unit"] == "GB/s"
+
+
+def test_host_cores_follow_the_grant(bench, monkeypatch):
+    """every core of the affinity mask, capped by the per-GPU grant the
+    pool states (OMP_NUM_THREADS), and the line says which."""
+    avail = len(os.sched_getaffinity(0))
+    monkeypatch.delenv("OMP_NUM_THREADS", raising=False)
+    assert bench.host_cores()[:2] == (avail, avail)
+    if avail > 1:
+        monkeypatch.setenv("OMP_NUM_THREADS", "1")
+        c, a, why = bench.host_cores()
+        assert (c, a) == (1, avail) and "OMP_NUM_THREADS=1" in why
+    monkeypatch.setenv("OMP_NUM_THREADS", str(avail + 5))
+    assert bench.host_cores()[0] == avail

@@ -42,8 +42,11 @@ def _worker(rank, world, port, q):
     rew, obs = run_shard(n, off, acts[:, off:off + n])
     g_rew = hd.gather_rollout(torch.from_numpy(rew))
     g_obs = hd.gather_rollout(torch.from_numpy(obs))
+    # he_rollout's step-major layout [K, N, ...] gathered along the env dimension
+    k_rew = hd.gather_rollout(torch.from_numpy(np.ascontiguousarray(rew.T)), env_dim=1)
+    k_obs = hd.gather_rollout(torch.from_numpy(np.ascontiguousarray(obs.transpose(1, 0, 2))), env_dim=1)
     if rank == 0:
-        q.put((g_rew.numpy(), g_obs.numpy()))
+        q.put((g_rew.numpy(), g_obs.numpy(), k_rew.numpy(), k_obs.numpy()))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -61,7 +64,7 @@ def test_two_rank_gloo_shards_equal_single_process():
     procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
-    g_rew, g_obs = q.get(timeout=240)
+    g_rew, g_obs, k_rew, k_obs = q.get(timeout=240)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -69,6 +72,18 @@ def test_two_rank_gloo_shards_equal_single_process():
     rew, obs = run_shard(N_TOTAL, 0, acts)
     assert np.array_equal(g_rew, rew)
     assert np.array_equal(g_obs, obs)
+    # [K, world * N, ...] in global env order: the single process's step-major tensors
+    assert k_rew.shape == (STEPS, N_TOTAL) and k_obs.shape == (STEPS, N_TOTAL, 13)
+    assert np.array_equal(k_rew, rew.T)
+    assert np.array_equal(k_obs, obs.transpose(1, 0, 2))
+
+
+def test_gather_rollout_env_dim_checks():
+    from cantorrl_amd import dist as hd
+    t = torch.zeros(3)
+    assert hd.gather_rollout(t, env_dim=1) is t   # no process group: the local tensor
+    import torch.distributed as dist
+    assert not dist.is_initialized()
 
 
 def test_shard_offset_contract():

@@ -88,6 +88,46 @@ for k in range(64):
 e1.record()
 torch.cuda.synchronize()
 print(f"env he_step alone, eager: {e0.elapsed_time(e1) * 1e3 / 64:.2f} us/step", flush=True)
+
+
+def graph_us(step, label, reps=20):
+    """Device time per step of 64 steps captured into one hipGraph (the bench's graph mode:
+    one market block per graph, so market_kernel is amortised over its 64 steps), replayed
+    `reps` times between two events on the capture stream."""
+    s = torch.cuda.Stream(device=dev)
+    with torch.cuda.stream(s):
+        for k in range(64):   # one eager block: the captured block starts at a block boundary
+            step(k)
+        env.sync_market()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        for k in range(64):
+            step(k)
+        env.sync_market()
+    for _ in range(3):
+        g.replay()
+    torch.cuda.synchronize()
+    a, b = ev(), ev()
+    with torch.cuda.stream(s):
+        a.record(s)
+        for _ in range(reps):
+            g.replay()
+        b.record(s)
+    torch.cuda.synchronize()
+    us = a.elapsed_time(b) * 1e3 / (64 * reps)
+    print(f"graph mode, {label}: {us:.2f} us/step (64 steps per graph incl. the block's market_kernel)", flush=True)
+    return us
+
+
+graph_us(lambda k: env.step_tensors(acts[k]), "he_step alone")
+vn._fusable = True
+graph_us(lambda k: vn.step_tensors(acts[k]), "he_step + VecNormalize, moments fused into he_step")
+vn._fusable = False
+graph_us(lambda k: vn.step_tensors(acts[k]), "he_step + VecNormalize, separate moments launch")
+vn.training = False
+graph_us(lambda k: vn.step_tensors(acts[k]), "he_step + VecNormalize, frozen statistics (eval)")
+vn.training = True
 env.close()
 
 g = torch.Generator(device=dev).manual_seed(0)
