@@ -654,24 +654,40 @@ __device__ __forceinline__ double book_option(const Params& p, const BookOpt& o,
             const double y = (o.lnH2K - b.lnS) * isst + ls;      // log(H^2 / (S K)) / sst + lam sst
             const double y1 = lhs * isst + ls;
             const double ert = e[3];                             // e^{r tau}
-            const double ax = tail_arg(x1), ay = tail_arg(y), ay1 = tail_arg(y1);
-            const double px = phi_of(ax), py = phi_of(ay), py1 = phi_of(ay1);
             const double sh = exp_book_g(-lhs);                  // S / H
             const double hs = exp_book_g(lhs);                   // H / S
-            const double ax_ = tail_arg(x1 - sst), ay_ = tail_arg(y - sst), ay1_ = tail_arg(y1 - sst);
-            const double qx = px * mills(ax), qx_ = (px * (sh * ert)) * mills(ax_);
-            const double qy = py * mills(ay), qy_ = (py * ((hs * hs) * (S * o.invK) * ert)) * mills(ay_);
-            const double qy1 = py1 * mills(ay1), qy1_ = (py1 * (hs * ert)) * mills(ay1_);
-            double nx, mx, nx_, mx_, ny, my, ny_, my_, ny1, my1, ny1_, my1_;
-            ncdf_from_tail(x1, qx, &nx, &mx);
-            ncdf_from_tail(x1 - sst, qx_, &nx_, &mx_);
-            ncdf_from_tail(y, qy, &ny, &my);
-            ncdf_from_tail(y - sst, qy_, &ny_, &my_);
-            ncdf_from_tail(y1, qy1, &ny1, &my1);
-            ncdf_from_tail(y1 - sst, qy1_, &ny1_, &my1_);
             const double p2l = exp_book_g((2.0 * b.lam) * lhs);  // (H/S)^(2 lam)
             const double p2l2 = p2l * (sh * sh);                 // (H/S)^(2 lam - 2)
-            const double cui = S * nx - Kd * nx_ - S * p2l * (my - my1) + Kd * p2l2 * (my_ - my1_);
+            // the three tail pairs one after another (scheduling fences): interleaved, their
+            // six Mills polynomials' live ranges spilled the Heston producers' registers.  The
+            // expression is unchanged (same operations, same order): the same bits.
+            __builtin_amdgcn_sched_barrier(0);
+            double nx, mx, nx_, mx_, ny, my, ny_, my_, ny1, my1, ny1_, my1_;
+            {
+                const double ax = tail_arg(x1), ax_ = tail_arg(x1 - sst);
+                const double px = phi_of(ax);
+                const double qx = px * mills(ax), qx_ = (px * (sh * ert)) * mills(ax_);
+                ncdf_from_tail(x1, qx, &nx, &mx);
+                ncdf_from_tail(x1 - sst, qx_, &nx_, &mx_);
+            }
+            const double t1 = S * nx - Kd * nx_;
+            __builtin_amdgcn_sched_barrier(0);
+            {
+                const double ay = tail_arg(y), ay_ = tail_arg(y - sst);
+                const double py = phi_of(ay);
+                const double qy = py * mills(ay), qy_ = (py * ((hs * hs) * (S * o.invK) * ert)) * mills(ay_);
+                ncdf_from_tail(y, qy, &ny, &my);
+                ncdf_from_tail(y - sst, qy_, &ny_, &my_);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            {
+                const double ay1 = tail_arg(y1), ay1_ = tail_arg(y1 - sst);
+                const double py1 = phi_of(ay1);
+                const double qy1 = py1 * mills(ay1), qy1_ = (py1 * (hs * ert)) * mills(ay1_);
+                ncdf_from_tail(y1, qy1, &ny1, &my1);
+                ncdf_from_tail(y1 - sst, qy1_, &ny1_, &my1_);
+            }
+            const double cui = t1 - S * p2l * (my - my1) + Kd * p2l2 * (my_ - my1_);
             v = v - cui;
             v = (runmax >= o.H || o.H <= K) ? 0.0 : v;          // knocked out / worthless
         }
@@ -2028,7 +2044,6 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
             LDS_BAR();
         }
     };
-    auto run = [&](auto&& step) { run_blk([&](int buf, int sl, int k, float2 ak, auto) { step(buf, sl, k, ak); }); };
 
     if constexpr (LEAN) {
         // the FAST configuration's constants (fast_config): v2, loss != mse, generate mode
@@ -2149,7 +2164,10 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
         // (the generic steps' Params fields pinned in SGPRs instead of the scalar-cache reloads:
         // config 5 +4 %, config 4 -1 %, r03s16)
         if (OBS && e.t != 0) pre = Mkt{(float)cur.S[i], HESTON ? (float)cur.v[i] : p.var_f, cur.C[i], cur.P[i], 0.0};
-        auto step = [&](int buf, int sl, int k, float2 ak) {
+        // full: every lane an env of its own (wrows == kLdsEnvs), the obs rows stored by the
+        // branch-free flush_obs_full (its rows == 64 test in flush_obs_wave held values live
+        // across a branch in every step: config 5's obs stepper spilled there)
+        auto step = [&](int buf, int sl, int k, float2 ak, auto full) {
             const int64_t koff = (int64_t)k * N;
             const float2 sc = L.sc[buf][sl][lane];
             const float vk = HESTON ? L.vv[HESTON ? buf : 0][HESTON ? sl : 0][lane] : p.var_f;
@@ -2170,7 +2188,10 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
                 float* const tile = L.stage[k & 1];
 #pragma unroll
                 for (int c = 0; c < kObs; ++c) tile[lane * kObs + c] = term ? p.rstv[4 + c] : o[c];  // SB3 autoreset obs
-                if (io.obs) flush_obs_wave(tile, io.obs + koff * kObs, base, wrows, lane);
+                if (io.obs) {
+                    if constexpr (decltype(full)::value) flush_obs_full(tile, io.obs + koff * kObs, base, lane);
+                    else flush_obs_wave(tile, io.obs + koff * kObs, base, wrows, lane);
+                }
                 pre = term ? rst : post;
                 if (term) env_reset_common(p, e);
             } else {
@@ -2184,7 +2205,10 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
                 if (so.term) env_reset_common(p, e);
             }
         };
-        run(step);
+        if (OBS && wrows == kLdsEnvs)
+            run_blk([&](int buf, int sl, int k, float2 ak, auto) { step(buf, sl, k, ak, std::true_type{}); });
+        else
+            run_blk([&](int buf, int sl, int k, float2 ak, auto) { step(buf, sl, k, ak, std::false_type{}); });
     }
     LDS_T1(OBS ? 1 : 0);
     if (!OBS && i0 < N) {
@@ -2222,16 +2246,21 @@ __device__ __forceinline__ void lds_producer(const Params& p, int k_steps, const
     const int nb = (k_steps + kLdsM - 1) / kLdsM;
     const uint32_t T = (uint32_t)p.T;
     const int64_t pi = (base + le) < N ? base + le : N - 1;
-    const int64_t gid = p.goff + pi;
     __builtin_amdgcn_s_setprio(kPrioProd);
-    const uint32_t ep0 = cur.ep[pi];
-    const uint32_t t0 = cur.t[pi];
+    // the loop carries only the chain state (Sbs, Vbs, Mbs), a0, tpb and pi: the episode
+    // counters are re-read after the loop and the Philox id is made per block, so nothing
+    // else is live across the block loop (loop-invariant values spilled around it)
+    uint64_t a0;                                     // env-step index of the launch's first step
+    uint32_t tpb;                                    // episode step before slot 0 of block bp
+    {
+        const uint32_t ep0 = cur.ep[pi], t0 = cur.t[pi];
+        const uint32_t off = t0 >= T ? T : t0;       // a0 = ep T + t (t = T: the next episode)
+        a0 = (uint64_t)ep0 * T + off;
+        tpb = off >= T ? 0u : off;
+    }
     double Sbs = cur.S[pi];                          // f64 price before slot 0 of block bp
     double Vbs = HESTON ? cur.v[pi] : 0.0;           // Heston: f64 variance before it
     double Mbs = BOOK ? cur.M[pi] : 0.0;             // book: running max of S before it
-    const uint32_t off = t0 >= T ? T : t0;           // a0 = ep T + t (t = T: the next episode)
-    const uint64_t a0 = (uint64_t)ep0 * T + off;     // env-step index of the launch's first step
-    uint32_t tpb = off >= T ? 0u : off;              // episode step before slot 0 of block bp
     const int sl0 = sub * kLdsH;
     LDS_T0();
     for (int bp = 0; bp <= nb; ++bp) {
@@ -2253,6 +2282,7 @@ __device__ __forceinline__ void lds_producer(const Params& p, int k_steps, const
                 // bits, as kLdsH interleaved chains with shared constants)
                 constexpr bool LOCK = FULL && LEAN && !HESTON;
 
+            const int64_t gid = p.goff + pi;
             const uint64_t nf = a0 + (uint64_t)(kb + sl0);
             const uint32_t tpf = (tpb + (uint32_t)sl0) % T;
             double ex[kLdsH];   // own slots' growth factors S_j / S_{j-1} (before the clamp)
@@ -2316,18 +2346,28 @@ __device__ __forceinline__ void lds_producer(const Params& p, int k_steps, const
                 // (1) Heston (market_body's full-truncation Euler, rbergomi_sim.py:454-458):
                 // Philox block n -> (z1, z2) per step; dw1 drives v, rho dw1 + sqrt(1 - rho^2)
                 // dw2 the price
+                // slot by slot (a rolled loop shifting each slot's pair in at the end, static
+                // indices only): one Philox block and Box-Muller pair live at a time
                 double w1[kLdsH], ws[kLdsH];
 #pragma unroll
+                for (int h = 0; h < kLdsH; ++h) w1[h] = ws[h] = 0.0;
+#pragma unroll 1
                 for (int h = 0; h < kLdsH; ++h) {
-                    w1[h] = 0.0;
-                    ws[h] = 0.0;
+                    double a = 0.0, b = 0.0;
                     if (FULL || sl0 + h < len) {
                         double z1, z2;
                         normals(p, gid, nf + (uint64_t)h, &z1, &z2);
                         const double dw1 = p.sqrt_dt * z1, dw2 = p.sqrt_dt * z2;
-                        w1[h] = dw1;
-                        ws[h] = p.h_rho * dw1 + p.h_sqrt1mrho2 * dw2;
+                        a = dw1;
+                        b = p.h_rho * dw1 + p.h_sqrt1mrho2 * dw2;
                     }
+#pragma unroll
+                    for (int q = 0; q + 1 < kLdsH; ++q) {
+                        w1[q] = w1[q + 1];
+                        ws[q] = ws[q + 1];
+                    }
+                    w1[kLdsH - 1] = a;
+                    ws[kLdsH - 1] = b;
                 }
                 // (2a) the variance chain of the whole block in every lane (dw1 gathered from
                 // the env's lanes): M sqrt, no exp; the lane keeps vp and sqrt(vp) of its slots
@@ -2426,41 +2466,75 @@ __device__ __forceinline__ void lds_producer(const Params& p, int k_steps, const
                 }
                 bs_call_put_n<kLdsH>(Sm, Km, p.bs, lkC, lkP);
             }
+            if constexpr (LOCK) {
 #pragma unroll
-            for (int h = 0; h < kLdsH; ++h) {
-                if (FULL || sl0 + h < len) {
-                    const bool last = tp + 1 == T;
-                    const double Sprev = (h == 0) ? Sin : Sx[h - 1];
-                    const double Sm = last ? ((tp == 0) ? p.s0 : Sprev) : Sx[h];
-                    const double Vh = HESTON ? Vx[h] : p.var;
-                    const double Vm = HESTON ? (last ? ((tp == 0) ? p.var : ((h == 0) ? Vin : Vx[h > 0 ? h - 1 : 0])) : Vh) : p.var;
-                    float C, P;
-                    if constexpr (LOCK) {
-                        C = (float)lkC[h];
-                        P = (float)lkP[h];
-                    } else {
+                for (int h = 0; h < kLdsH; ++h) {
+                    const int sl = sl0 + h;
+                    W.sc[wb][sl][le] = make_float2((float)Sx[h], (float)lkC[h]);
+                    W.pp[wb][sl][le] = (float)lkP[h];
+                }
+            } else {
+                // marks<MODE> slot by slot: a rolled loop over registers rotated by one slot per
+                // iteration (static indices only), so the Heston producers' per-slot Black-Scholes
+                // constants and ndtr tails are one slot's live set, not kLdsH interleaved ones
+                double rS[kLdsH], rV[kLdsH];
+#pragma unroll
+                for (int h = 0; h < kLdsH; ++h) {
+                    rS[h] = Sx[h];
+                    rV[h] = HESTON ? Vx[h] : p.var;
+                }
+                double Sprev = Sin, Vprev = Vin;
+#pragma unroll 1
+                for (int h = 0; h < kLdsH; ++h) {
+                    if (FULL || sl0 + h < len) {
+                        const bool last = tp + 1 == T;
+                        const double Sm = last ? ((tp == 0) ? p.s0 : Sprev) : rS[0];
+                        const double Vh = rV[0];
+                        const double Vm = HESTON ? (last ? ((tp == 0) ? p.var : Vprev) : Vh) : p.var;
+                        float C, P;
                         // the episode step of the marks: the slot's (tp + 1), or tp for the lagged ones
                         marks<MODE, !LEAN>(p, Sm, Vm, last ? tp : tp + 1u, &C, &P);
+                        const int sl = sl0 + h;
+                        W.sc[wb][sl][le] = make_float2((float)rS[0], C);
+                        W.pp[wb][sl][le] = P;
+                        if (HESTON) W.vv[HESTON ? wb : 0][HESTON ? sl : 0][le] = (float)Vh;
+                        tp = (tp + 1 == T) ? 0u : tp + 1;
                     }
-                    const int sl = sl0 + h;
-                    W.sc[wb][sl][le] = make_float2((float)Sx[h], C);
-                    W.pp[wb][sl][le] = P;
-                    if (HESTON) W.vv[HESTON ? wb : 0][HESTON ? sl : 0][le] = (float)Vh;
-                    // the book after the step into slot sl (episode step tp + 1, the new S,
-                    // not lagged): market_body's tileC
-                    if (BOOK) W.bk[wb][sl][le] = book_value<!HESTON>(p, Sx[h], Vh, (int32_t)(tp + 1), Mx[h],
-                                                                     &W.btab[0][0], &W.bopt[0]);
-                    if (kb + sl == k_steps - 1) {  // the market position after the launch
-                        const uint32_t q = off + (uint32_t)(k_steps - 1);
-                        cur.ep[pi] = ep0 + q / T;
-                        cur.t[pi] = q % T + 1u;
-                        cur.S[pi] = Sx[h];
-                        if (HESTON) cur.v[pi] = Vh;
-                        cur.C[pi] = C;
-                        cur.P[pi] = P;
-                        if (BOOK) cur.M[pi] = Mx[h];
+                    Sprev = rS[0];
+                    Vprev = rV[0];
+#pragma unroll
+                    for (int q = 0; q + 1 < kLdsH; ++q) {
+                        rS[q] = rS[q + 1];
+                        rV[q] = rV[q + 1];
                     }
-                    tp = (tp + 1 == T) ? 0u : tp + 1;
+                }
+            }
+            if constexpr (BOOK) {
+                // the book after the step into each slot (episode step tp + 1, the new S, not
+                // lagged): market_body's tileC.  One slot at a time -- a rolled loop over
+                // registers rotated by one slot per iteration (static indices only) -- so the
+                // pricer's live set is one slot's, not kLdsH interleaved ones: unrolled, the
+                // config 4 / 5 producers spilled 28 / 69 VGPRs (116 / 216 B of scratch per lane)
+                double bS[kLdsH], bV[kLdsH], bM[kLdsH];
+#pragma unroll
+                for (int h = 0; h < kLdsH; ++h) {
+                    bS[h] = Sx[h];
+                    bV[h] = HESTON ? Vx[h] : p.var;
+                    bM[h] = Mx[h];
+                }
+                uint32_t tb = tpf;
+#pragma unroll 1
+                for (int h = 0; h < kLdsH; ++h) {
+                    if (FULL || sl0 + h < len)
+                        W.bk[wb][sl0 + h][le] = book_value<!HESTON>(p, bS[0], bV[0], (int32_t)(tb + 1), bM[0],
+                                                                    &W.btab[0][0], &W.bopt[0]);
+                    tb = (tb + 1 == T) ? 0u : tb + 1;
+#pragma unroll
+                    for (int q = 0; q + 1 < kLdsH; ++q) {
+                        bS[q] = bS[q + 1];
+                        bV[q] = bV[q + 1];
+                        bM[q] = bM[q + 1];
+                    }
                 }
             }
             };
@@ -2469,6 +2543,28 @@ __device__ __forceinline__ void lds_producer(const Params& p, int k_steps, const
             tpb = (uint32_t)(((uint64_t)tpb + kLdsM) % T);
         }
         LDS_BAR();  // block bp handed to the steppers
+    }
+    // the market position after the launch: every lane ran the whole price chain (Sbs, and
+    // Heston's Vbs, the book's running max Mbs are the state after the last step); the last
+    // slot's f32 marks are read back from its LDS record (written by this wave, and no wave
+    // writes the buffers after the last barrier).  Kept out of the slot loop: a store branch
+    // there held the launch-level values (env index, episode counters) live across the pricer.
+    if (nb > 0 && sub == 0) {
+        const int sll = (k_steps - 1) - (nb - 1) * kLdsM;
+        const int wbl = (nb - 1) % LdsMarketT<MODE, BOOK, LEAN>::NB;
+        // a fresh (opaque) index: the compiler would otherwise keep the prologue's state
+        // addresses live across the block loop, in VGPR pairs, and spill them
+        int64_t j = pi;
+        asm volatile("" : "+v"(j));
+        const uint32_t ep0 = cur.ep[j], t0 = cur.t[j];   // unchanged until these stores
+        const uint32_t q = (t0 >= T ? T : t0) + (uint32_t)(k_steps - 1);
+        cur.ep[j] = ep0 + q / T;
+        cur.t[j] = q % T + 1u;
+        cur.S[j] = Sbs;
+        if (HESTON) cur.v[j] = Vbs;
+        cur.C[j] = W.sc[wbl][sll][le].y;
+        cur.P[j] = W.pp[wbl][sll][le];
+        if (BOOK) cur.M[j] = Mbs;
     }
     LDS_T1(2 + (pw < 2 ? pw : 1));
 }
