@@ -120,7 +120,7 @@ EXPORTS = [
     "he_num_episodes", "he_get_config", "he_state_size", "he_get_state", "he_set_state",
     "he_pcg64_seed_state", "he_host_episode_draws", "he_host_philox", "he_host_div_by", "he_host_div_byf", "he_time_next_step", "he_rollout_policy", "he_host_box_muller",
     "he_sync_market", "he_vecnorm_stats_len", "he_vecnorm_scratch_bytes", "he_vecnorm_init", "he_vecnorm_step",
-    "he_vecnorm_apply", "he_vecnorm_attach", "he_vecnorm_reset", "he_fixed_european_marks", "he_bs_delta_hedge", "he_count_nonfinite",
+    "he_vecnorm_apply", "he_vecnorm_attach", "he_vecnorm_attach_eval", "he_vecnorm_reset", "he_fixed_european_marks", "he_bs_delta_hedge", "he_count_nonfinite",
     "he_device_rng", "he_device_math", "he_host_math", "he_episode_summaries",
 ]
 
@@ -137,6 +137,13 @@ class HeVecnormParams(ctypes.Structure):
         ("epsilon", ctypes.c_double),
         ("reserved", ctypes.c_int32 * 4),
     ]
+
+
+class HeVecnormOut(ctypes.Structure):
+    """include/hedge_env.h he_vecnorm_out: the eval VecNormalize step's buffers."""
+    _fields_ = [(name, ctypes.c_void_p) for name in (
+        "stats", "returns", "obs_out", "reward_out", "terminal_obs_out", "ep_return", "ep_length", "ep_return_done",
+        "ep_length_done")]
 
 _lib = None
 
@@ -193,6 +200,7 @@ def load(path=LIB_PATH):
         "he_vecnorm_step": (i32, [ctypes.POINTER(HeVecnormParams), i64] + [vp] * 14 + [vp]),
         "he_vecnorm_apply": (i32, [ctypes.POINTER(HeVecnormParams), i64] + [vp] * 14 + [vp]),
         "he_vecnorm_attach": (i32, [vp, ctypes.POINTER(HeVecnormParams), vp, vp, vp]),
+        "he_vecnorm_attach_eval": (i32, [vp, ctypes.POINTER(HeVecnormParams), ctypes.POINTER(HeVecnormOut)]),
         "he_vecnorm_reset": (i32, [ctypes.POINTER(HeVecnormParams), i64] + [vp] * 5 + [vp]),
         "he_fixed_european_marks": (i32, [vp, i64, i32, ctypes.c_double, vp, vp, vp, vp]),
         "he_bs_delta_hedge": (i32, [vp, i64, i32, ctypes.c_double, ctypes.c_double, vp, vp]),

@@ -1275,6 +1275,7 @@ __device__ __forceinline__ void env_reset_common(const Params& p, Env& e) {
 struct VnHook {
     const float* tile;
     float rew;
+    bool term;
 };
 
 template <int MODE, bool INFO, bool SINGLE, bool BOOK, bool FAST, bool POL, bool GS>
@@ -1447,7 +1448,10 @@ __device__ __forceinline__ void step_body(const Params& pk, int64_t n_envs, cons
             StepOut so;
             step_env<BOOK, FAST>(p, e, pre, post, ak.x, ak.y, pv_last, so);
             pv_last = so.pv;
-            if (hook) hook->rew = (float)so.reward;
+            if (hook) {
+                hook->rew = (float)so.reward;
+                hook->term = so.term;
+            }
             if (POL) {  // the reference evaluation loops' sums, in step order
                 acc[0] = acc[0] + so.reward;
                 acc[1] = acc[1] + so.pnl;
@@ -1749,12 +1753,38 @@ __global__ __launch_bounds__(kBlock) void step1_vn_kernel(const Params* __restri
     static_assert(kEpw == 64 && kEpb == kBlock, "one env per thread");
     const int64_t r = (int64_t)blockIdx.x * kEpb + threadIdx.x;
     const double ret_prev = (vm.upd_ret && r < n) ? vm.returns[r] : 0.0;
-    double sft[vn::kD + 1];
-    vn::load_mean_shifts(vm, sft);
-    VnHook hk{nullptr, 0.0f};
+    const double col_shift = vn::load_col_shift(vm);
+    VnHook hk{nullptr, 0.0f, false};
     step_body<MODE, false, true, BOOK, FAST, false, GS>(*pc, n, tA, tB, tC, s, io, 1, slot0, blockIdx.x, &hk);
     __syncthreads();  // the workgroup's obs rows (LDS, the final ones incl. reset obs) visible to all its threads
-    vn::moments_from_rows(vm, blockIdx.x, hk.tile, hk.rew, ret_prev, sft);
+    vn::moments_from_rows(vm, blockIdx.x, hk.tile, hk.rew, ret_prev, col_shift);
+}
+
+// he_step with VecNormalize attached for evaluation (he_vecnorm_attach_eval: the statistics
+// frozen): step1_kernel, then the whole VecNormalize step over the workgroup's rows
+// (vn::apply_frozen_rows) -- no moments, so nothing crosses workgroups and no second launch.
+template <int MODE, bool BOOK, bool FAST, bool GS>
+__global__ __launch_bounds__(kBlock) void step1_vne_kernel(const Params* __restrict__ pc, int64_t n, const float4* tA,
+                                                           const float4* tB, const double* tC, State s, StepIo sio,
+                                                           int slot0, vn::ApplyArgs va) {
+    Io io;
+    io.act = sio.act;
+    io.obs = sio.obs;
+    io.rew = sio.rew;
+    io.term = sio.term;
+    io.trunc = sio.trunc;
+    io.tobs = sio.tobs;
+    io.info = he_info{};
+    io.pol_on = false;
+    io.sums = false;
+    static_assert(kEpw == 64 && kEpb == kBlock, "one env per thread");
+    const int64_t r0 = (int64_t)blockIdx.x * kEpb;
+    const vn::FrozenPre fp = vn::load_frozen(va, r0 + threadIdx.x, r0 + threadIdx.x < n);
+    VnHook hk{nullptr, 0.0f, false};
+    step_body<MODE, false, true, BOOK, FAST, false, GS>(*pc, n, tA, tB, tC, s, io, 1, slot0, blockIdx.x, &hk);
+    const int rows = (int)((n - r0) < kEpb ? n - r0 : kEpb);
+    __syncthreads();  // the workgroup's obs rows (LDS, the final ones incl. reset obs) visible to all its threads
+    vn::apply_frozen_rows(va, r0, rows, hk.tile, fp, hk.rew, hk.term, sio.tobs);
 }
 
 // The same moments after any other he_step launch (info requested, a fused market block).
@@ -3285,8 +3315,11 @@ struct he_env {
     float* rst = nullptr;     // reset market + obs (generate)
     Params* dparams = nullptr;  // device copies of tile_params(env, 0 / 1) for step1_kernel
     bool vn_on = false;          // he_vecnorm_attach: he_step also runs the VecNormalize moments
-    bool vn_fused = false;       // ... and this he_step ran them in step1_vn_kernel
+    bool vn_fused = false;       // ... and this he_step ran them in step1_vn_kernel (step1_vne_kernel)
     vn::MomentsArgs vn{};
+    bool vne_on = false;         // he_vecnorm_attach_eval: he_step also runs the eval VecNormalize step
+    vn::ApplyArgs vne{};
+    he_vecnorm_params vne_p{};
     BookOpt* dbook = nullptr;   // liability book, device copy (generate modes)
     double* dbook_tab = nullptr;  // book tau table (book_option)
     int32_t book_rows = 0;        // its rows: max expiry + 1
@@ -3590,6 +3623,14 @@ static void launch_step_gs(he_env* env, const Params& p, const Io& io, bool info
         const float4* tA = REPLAY ? p.rec : p.tileA;
         const float4* tB = REPLAY ? p.recg : p.tileB;
         StepIo sio{io.act, io.obs, io.rew, io.term, io.trunc, io.tobs};
+        if (env->vne_on && io.obs && io.rew && io.term && io.tobs) {  // + the eval VecNormalize step
+            hipEvent_t a = (hipEvent_t)env->ev_start, b = (hipEvent_t)env->ev_stop;
+            env->ev_start = env->ev_stop = nullptr;
+            hipExtLaunchKernelGGL((step1_vne_kernel<MODE, BOOK, FAST, GS>), dim3((unsigned)blocks), dim3(kBlock), 0, st,
+                                  a, b, 0, pc, p.n, tA, tB, (const double*)p.tileC, env->s, sio, slot0, env->vne);
+            env->vn_fused = true;
+            return;
+        }
         if (env->vn_on) {  // + the VecNormalize moments in the same launch
             vn::MomentsArgs vm = env->vn;
             vm.obs = io.obs;
@@ -4340,14 +4381,25 @@ he_status he_step(he_env* env, const float* actions, float* obs, float* reward, 
     }
     // he_vecnorm_attach arms THIS step only (one-shot): steps nobody armed -- the inner env
     // stepped directly, another wrapper's -- never touch a wrapper's returns or partials
-    const bool vn = env->vn_on;
-    if (vn && (!obs || !reward)) {
-        env->vn_on = false;
+    const bool vn = env->vn_on, vne = env->vne_on;
+    if ((vn || vne) && (!obs || !reward)) {
+        env->vn_on = env->vne_on = false;
         return fail(env, HE_EINVAL, "he_vecnorm_attach: he_step needs the obs and reward buffers");
+    }
+    if (vne && (!terminated || !terminal_obs)) {
+        env->vne_on = false;
+        return fail(env, HE_EINVAL, "he_vecnorm_attach_eval: he_step needs the terminated and terminal_obs buffers");
     }
     env->vn_fused = false;
     he_status s = launch_steps(env, io, want_info, 1, stream);
-    env->vn_on = false;
+    env->vn_on = env->vne_on = false;
+    if (s == HE_OK && vne && !env->vn_fused) {
+        // another step kernel ran (info requested): the eval VecNormalize step as its own launch
+        const vn::ApplyArgs& a = env->vne;
+        return he_vecnorm_apply(&env->vne_p, env->cfg.n_envs, obs, reward, terminated, terminal_obs, a.returns,
+                                const_cast<double*>(a.stats), const_cast<double*>(a.stats), a.obs_out, a.rew_out,
+                                a.tobs_out, a.ep_ret, a.ep_len, a.ep_ret_done, a.ep_len_done, stream);
+    }
     if (s != HE_OK || !vn || env->vn_fused) return s;
     // VecNormalize attached, and this step took another kernel: the moments after it
     vn::MomentsArgs vm = env->vn;
@@ -4385,6 +4437,43 @@ he_status he_vecnorm_attach(he_env* env, const he_vecnorm_params* p, double* ret
     m.part = (double*)scratch;
     env->vn = m;
     env->vn_on = m.upd_obs || m.upd_ret;
+    return HE_OK;
+}
+
+he_status he_vecnorm_attach_eval(he_env* env, const he_vecnorm_params* p, const he_vecnorm_out* out) {
+    if (!env) return HE_EINVAL;
+    if (!p) {  // disarm
+        env->vne_on = false;
+        return HE_OK;
+    }
+    if (p->obs_dim != kObs || p->training || !(p->clip_obs >= 0.0) || !(p->clip_reward >= 0.0) || !(p->epsilon >= 0.0))
+        return fail(env, HE_EINVAL, "bad he_vecnorm_params (the eval arm takes training = 0)");
+    if (!out || !out->stats || !out->returns || !out->obs_out || !out->reward_out)
+        return fail(env, HE_EINVAL, "he_vecnorm_out: stats / returns / obs_out / reward_out are NULL");
+    if ((out->ep_return != nullptr) != (out->ep_length != nullptr) ||
+        (out->ep_return && (!out->ep_return_done || !out->ep_length_done)))
+        return fail(env, HE_EINVAL, "he_vecnorm_out: the Monitor buffers come together");
+    if (kEpb != vn::kVnChunk)
+        return fail(env, HE_EINVAL, "he_vecnorm_attach_eval needs 256 envs per step workgroup");
+    vn::ApplyArgs a = {};
+    a.norm_obs = p->norm_obs != 0;
+    a.norm_reward = p->norm_reward != 0;
+    a.clip_obs = p->clip_obs;
+    a.clip_rew = p->clip_reward;
+    a.eps = p->epsilon;
+    a.stats = out->stats;
+    a.returns = out->returns;
+    a.obs_out = out->obs_out;
+    a.rew_out = out->reward_out;
+    a.tobs_out = out->terminal_obs_out;
+    a.ep_ret = out->ep_return;
+    a.ep_len = out->ep_length;
+    a.ep_ret_done = out->ep_return_done;
+    a.ep_len_done = out->ep_length_done;
+    env->vne = a;
+    env->vne_p = *p;
+    env->vne_on = true;
+    env->vn_on = false;
     return HE_OK;
 }
 

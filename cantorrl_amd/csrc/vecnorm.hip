@@ -128,28 +128,25 @@ __device__ __forceinline__ RowIn row_in(const VnArgs& a, int64_t r) {
     return in;
 }
 
+using vn::ColNorm;
+using vn::col_norm;
+using vn::norm_elem;
+
 // Launch 2: every workgroup merges all the partials itself (one block reduction in a
 // fixed order, so the same statistics everywhere; workgroup 0 stores them), then
 // normalizes its rows: obs / reward / terminal obs, returns[done] = 0, Monitor sums.
-// R > 1 (n <= kVnMaxBlocks * kVnChunk; A/B, HE_VN_APPLY_R): R * 256 rows per workgroup,
-// R per thread, so 1 / R of the workgroups each read the G partials.  Slower: rocprof
-// 7.5 (R = 1) / 10.2 (R = 2) / 15.9 us (R = 4) at 65,536 envs (r03s32) -- the merge's
-// reads are not what the launch waits on; each thread's rows are.
-#ifndef HE_VN_APPLY_R
-#define HE_VN_APPLY_R 1
-#endif
-template <int R>
+// (2 or 4 rows per thread, so fewer workgroups read the partials, measured slower: rocprof
+// 7.5 / 10.2 / 15.9 us at 65,536 envs, r03s32 -- the merge's reads are not what the launch
+// waits on; each thread's rows are.)
 __global__ void __launch_bounds__(kVnThreads) vn_apply_kernel(VnArgs a) {
+    constexpr int R = 1;
     __shared__ double sh[kVnThreads * (kPart + 1)];
     __shared__ double ssum[kPart];
-    __shared__ double snorm[kD][2];   // per obs column: mean, 1 / sqrt(var + eps)
+    __shared__ ColNorm snorm[kD];     // per obs column (col_norm)
     __shared__ double srinv;
     __shared__ float tile[kVnChunk * kD];
-    VnRows w = rows_of(a);
-    if (R > 1) {
-        w.r0 = (int64_t)blockIdx.x * (kVnChunk * R);
-        w.r1 = (w.r0 + kVnChunk * R < a.n) ? w.r0 + kVnChunk * R : a.n;
-    }
+    const VnRows w = rows_of(a);
+    const float clip = (float)a.clip_obs;
     const bool upd_ret = a.training && !a.reset;
     const int t = threadIdx.x;
     const bool resident = w.r1 - w.r0 <= kVnChunk * R;
@@ -199,18 +196,14 @@ __global__ void __launch_bounds__(kVnThreads) vn_apply_kernel(VnArgs a) {
                 }
             }
             if (c < kD) {
-                snorm[c][0] = mean;
-                snorm[c][1] = 1.0 / sqrt(var + a.eps);
+                snorm[c] = col_norm(mean, var, a.eps);
             } else {
                 srinv = 1.0 / sqrt(var + a.eps);
             }
         }
         __syncthreads();
     } else {
-        if (t < kD) {
-            snorm[t][0] = a.stats[t];
-            snorm[t][1] = 1.0 / sqrt(a.stats[kD + t] + a.eps);
-        }
+        if (t < kD) snorm[t] = col_norm(a.stats[t], a.stats[kD + t], a.eps);
         if (t == 0) srinv = 1.0 / sqrt(a.stats[2 * kD + 2] + a.eps);
         __syncthreads();
     }
@@ -227,8 +220,7 @@ __global__ void __launch_bounds__(kVnThreads) vn_apply_kernel(VnArgs a) {
 #pragma unroll
             for (int c = 0; c < kD; ++c) {
                 const float x = a.tobs[r * kD + c];
-                a.tobs_out[r * kD + c] =
-                    a.norm_obs ? (float)clipd(((double)x - snorm[c][0]) * snorm[c][1], -a.clip_obs, a.clip_obs) : x;
+                a.tobs_out[r * kD + c] = a.norm_obs ? norm_elem(x, snorm[c], clip) : x;
             }
         }
         if (dn) a.returns[r] = 0.0;   // self.returns[dones] = 0
@@ -245,16 +237,16 @@ __global__ void __launch_bounds__(kVnThreads) vn_apply_kernel(VnArgs a) {
     };
     if (resident) {
         // the obs element-wise straight from the registers the loads landed in: element
-        // k of the slice is column k % 13 (the slice starts at a row boundary)
+        // k = t + 256 q of the slice is column k % 13 (the slice starts at a row boundary),
+        // stepped by 256 % 13 = 9 per q without a division
         float* dst = a.obs_out + w.r0 * kD;
+        int c = t % kD;
 #pragma unroll
         for (int q = 0; q < R * kD; ++q) {
             const int k = t + q * kVnThreads;
-            if (k < nres) {
-                const int c = k % kD;
-                dst[k] = a.norm_obs ? (float)clipd(((double)xr[q] - snorm[c][0]) * snorm[c][1], -a.clip_obs, a.clip_obs)
-                                    : xr[q];
-            }
+            if (k < nres) dst[k] = a.norm_obs ? norm_elem(xr[q], snorm[c], clip) : xr[q];
+            c += kVnThreads % kD;
+            c = c >= kD ? c - kD : c;
         }
 #pragma unroll
         for (int j = 0; j < R; ++j)
@@ -268,10 +260,7 @@ __global__ void __launch_bounds__(kVnThreads) vn_apply_kernel(VnArgs a) {
             // the row in place in LDS, then stored back as a flat coalesced copy
             if (a.norm_obs) {
 #pragma unroll
-                for (int c = 0; c < kD; ++c) {
-                    const float x = tile[t * kD + c];
-                    tile[t * kD + c] = (float)clipd(((double)x - snorm[c][0]) * snorm[c][1], -a.clip_obs, a.clip_obs);
-                }
+                for (int c = 0; c < kD; ++c) tile[t * kD + c] = norm_elem(tile[t * kD + c], snorm[c], clip);
             }
             row_work(c0 + t, a.reset ? RowIn{} : row_in(a, c0 + t));
         }
@@ -311,13 +300,7 @@ he_status launch(VnArgs& a, void* scratch, hipStream_t s, bool moments = true) {
         hipLaunchKernelGGL(vn_moments_kernel, dim3(a.blocks), dim3(kVnThreads), 0, s, a);
         if (hipGetLastError() != hipSuccess) return HE_EHIP;
     }
-    if (HE_VN_APPLY_R > 1 && a.n <= (int64_t)kVnMaxBlocks * kVnChunk) {
-        constexpr int64_t rpb = (int64_t)kVnChunk * HE_VN_APPLY_R;
-        hipLaunchKernelGGL(vn_apply_kernel<HE_VN_APPLY_R>, dim3((unsigned)((a.n + rpb - 1) / rpb)), dim3(kVnThreads),
-                           0, s, a);
-    } else {
-        hipLaunchKernelGGL(vn_apply_kernel<1>, dim3(a.blocks), dim3(kVnThreads), 0, s, a);
-    }
+    hipLaunchKernelGGL(vn_apply_kernel, dim3(a.blocks), dim3(kVnThreads), 0, s, a);
     return hipGetLastError() == hipSuccess ? HE_OK : HE_EHIP;
 }
 

@@ -133,42 +133,167 @@ __device__ __forceinline__ void moments_body(const MomentsArgs& a, int bid) {
 
 // The same moments from rows already in LDS (step1_vn_kernel: the he_step workgroup's obs
 // staging tile, row t at tile + t * kD, after a workgroup barrier), the thread's reward
-// `rew` (its row r0 + t) and its running return before the update `ret_prev`: the same
-// operations on the same values as moments_body, with no global round trip.  Obs shift:
-// the old running mean (a.shift_mean).
-// sft: the shifts (the old running means of the obs columns and of the returns), loaded by
-// the caller before its step so they are not a round trip here.
-__device__ __forceinline__ void load_mean_shifts(const MomentsArgs& a, double* sft) {
-#pragma unroll
-    for (int c = 0; c < kD; ++c) sft[c] = a.stats[c];
-    sft[kD] = a.stats[2 * kD + 1];
+// `rew` (its row r0 + t) and its running return before the update `ret_prev`, with no global
+// round trip.  Obs shift: the old running mean (a.shift_mean).
+// col_shift: this thread's column's shift (the old running mean of obs column t % (kD + 1),
+// or of the returns), loaded by the caller before its step so it is not a round trip here.
+__device__ __forceinline__ double load_col_shift(const MomentsArgs& a) {
+    const int c = (int)(threadIdx.x % (kD + 1));
+    return a.stats[c < kD ? c : 2 * kD + 1];
 }
+// Column-major over the LDS rows: thread t < kColThreads takes column c = t % (kD + 1)
+// (13 obs columns, then the returns) and rows g, g + kColGroups, ... (g = t / (kD + 1)), summing
+// d and d^2 of its rows in f64; the kColGroups group sums of each column are then added in group
+// order by 2 (kD + 1) threads.  ~6 KB of LDS traffic per workgroup against the row-major
+// block_sum's 57 KB (every thread's 28 values written, then read back): the fused epilogue's
+// cost on the step kernel.  The summation order differs from moments_body's (row-major), so
+// the statistics agree to rounding, not bit for bit (test_fused_moments_equal_separate_launch).
+constexpr int kColGroups = kVnThreads / (kD + 1);            // 18
+constexpr int kColThreads = kColGroups * (kD + 1);           // 252
 __device__ __forceinline__ void moments_from_rows(const MomentsArgs& a, int bid, const float* tile, float rew,
-                                                  double ret_prev, const double* sft) {
+                                                  double ret_prev, double col_shift) {
+    __shared__ double rbuf[kVnThreads];
+    __shared__ double red[kColGroups][kD + 1][2];
     const int64_t r0 = (int64_t)bid * a.rows_per_block;
     const int64_t r1 = (r0 + a.rows_per_block < a.n) ? r0 + a.rows_per_block : a.n;
+    const int rows = (int)(r1 > r0 ? r1 - r0 : 0);
     const int t = threadIdx.x;
-    double v[kPart - 1];
-#pragma unroll
-    for (int c = 0; c < kPart - 1; ++c) v[c] = 0.0;
-    if (t < (int)(r1 - r0)) {
-        if (a.upd_obs) {
-#pragma unroll
-            for (int c = 0; c < kD; ++c) {
-                const double d = (double)tile[t * kD + c] - sft[c];
-                v[c] += d;
-                v[kD + 1 + c] += d * d;
+    if (a.upd_ret && t < rows) {
+        const double ret = ret_prev * a.gamma + (double)rew;   // VecNormalize._update_reward
+        a.returns[r0 + t] = ret;
+        rbuf[t] = ret;
+    }
+    __syncthreads();
+    if (t < kColThreads) {
+        const int c = t % (kD + 1), g = t / (kD + 1);
+        double s1 = 0.0, s2 = 0.0;
+        if (c < kD ? a.upd_obs : a.upd_ret) {
+            const double sh = col_shift;
+            for (int r = g; r < rows; r += kColGroups) {
+                const double x = (c < kD) ? (double)tile[r * kD + c] : rbuf[r];
+                const double d = x - sh;
+                s1 += d;
+                s2 += d * d;
             }
         }
-        if (a.upd_ret) {
-            const double ret = ret_prev * a.gamma + (double)rew;   // VecNormalize._update_reward
-            a.returns[r0 + t] = ret;
-            const double d = ret - sft[kD];
-            v[kD] += d;
-            v[2 * kD + 1] += d * d;
+        red[g][c][0] = s1;
+        red[g][c][1] = s2;
+    }
+    __syncthreads();
+    if (t < 2 * (kD + 1)) {
+        const int w = t / (kD + 1), c = t % (kD + 1);
+        double x = 0.0;
+#pragma unroll
+        for (int g = 0; g < kColGroups; ++g) x += red[g][c][w];
+        // partial layout: [count, S1[kD + 1], S2[kD + 1]] (S1[kD] / S2[kD]: the returns)
+        a.part[(1 + w * (kD + 1) + c) * kVnMaxBlocks + bid] = x;
+    }
+    if (t == 0) a.part[bid] = (double)rows;
+    double* snap = a.part + kVnMaxBlocks * kPart;
+    if (bid == 0 && t < 2 * kD + 4) snap[t] = a.stats[t];
+    if (bid == 0 && t <= kD) snap[2 * kD + 4 + t] = col_shift;   // thread t <= kD: column t
+}
+
+// ------------------------------------------------------------------ eval: the whole step fused
+// VecNormalize.step_wait with the statistics frozen (training=False, train_ppo_v2.py:450-453):
+// no moments, so nothing crosses workgroups and he_step's own launch can finish the step
+// (step1_vne_kernel, he_vecnorm_attach_eval) -- the obs rows normalized from the step's LDS
+// staging tile, the reward from the thread's register, returns[done] = 0, Monitor's sums and
+// the normalized terminal obs of done rows.  The same per-element arithmetic as vecnorm.hip's
+// apply (ColNorm, norm_elem): the same bits as he_step + he_vecnorm_apply.
+struct ColNorm {
+    double mean, s;
+};
+__device__ __forceinline__ ColNorm col_norm(double mean, double var, double eps) {
+    return ColNorm{mean, 1.0 / sqrt(var + eps)};
+}
+// VecNormalize.normalize_obs of one element: the f64 difference and product, rounded to f32
+// once and clipped in f32 (the same values as clipping in f64 first: rounding is monotonic and
+// the clip bounds are f32 values)
+__device__ __forceinline__ float norm_elem(float x, const ColNorm& n, float clip) {
+    const float r = (float)(((double)x - n.mean) * n.s);
+    return r < -clip ? -clip : (r > clip ? clip : r);   // np.clip: NaN stays NaN
+}
+__device__ __forceinline__ double clip_d(double x, double lo, double hi) { return x < lo ? lo : (x > hi ? hi : x); }
+
+struct ApplyArgs {
+    int32_t norm_obs, norm_reward;
+    double clip_obs, clip_rew, eps;
+    const double* stats;
+    double* returns;
+    float* obs_out;
+    float* rew_out;
+    float* tobs_out;
+    double* ep_ret;       // Monitor sums (NULL: none)
+    int32_t* ep_len;
+    double* ep_ret_done;
+    int32_t* ep_len_done;
+};
+// What a thread of the fused kernel loads before its step (off the epilogue's path): thread
+// t < kD the statistics of obs column t, thread kD the returns' variance; its row's Monitor sums.
+struct FrozenPre {
+    double m, v, er;
+    int32_t el;
+};
+__device__ __forceinline__ FrozenPre load_frozen(const ApplyArgs& a, int64_t r, bool live) {
+    const int t = threadIdx.x;
+    FrozenPre f{0.0, 1.0, 0.0, 0};
+    if (t < kD) {
+        f.m = a.stats[t];
+        f.v = a.stats[kD + t];
+    } else if (t == kD) {
+        f.v = a.stats[2 * kD + 2];
+    }
+    if (a.ep_ret && live) {
+        f.er = a.ep_ret[r];
+        f.el = a.ep_len[r];
+    }
+    return f;
+}
+// rows [r0, r0 + rows) of the workgroup, obs staged at tile (row t at tile + t kD, visible to
+// every thread), thread t < rows owning row r0 + t: its reward, done flag and terminal obs row.
+__device__ __forceinline__ void apply_frozen_rows(const ApplyArgs& a, int64_t r0, int rows, const float* tile,
+                                                  const FrozenPre& f, float rew, bool done, const float* tobs) {
+    __shared__ ColNorm cn[kD];
+    __shared__ double rinv;
+    const int t = threadIdx.x;
+    if (t < kD) cn[t] = col_norm(f.m, f.v, a.eps);
+    if (t == kD) rinv = 1.0 / sqrt(f.v + a.eps);
+    __syncthreads();
+    const float clip = (float)a.clip_obs;
+    // the obs as a flat coalesced copy: element k = t + 256 q is column k % 13 (rows start at a
+    // row boundary), stepped by 256 % 13 = 9 per q without a division
+    float* dst = a.obs_out + r0 * kD;
+    const int nf = rows * kD;
+    int c = t % kD;
+#pragma unroll
+    for (int q = 0; q < kD; ++q) {
+        const int k = t + q * kVnThreads;
+        if (k < nf) dst[k] = a.norm_obs ? norm_elem(tile[k], cn[c], clip) : tile[k];
+        c += kVnThreads % kD;
+        c = c >= kD ? c - kD : c;
+    }
+    if (t >= rows) return;
+    const int64_t r = r0 + t;
+    a.rew_out[r] = a.norm_reward ? (float)clip_d((double)rew * rinv, -a.clip_rew, a.clip_rew) : rew;
+    if (done && tobs && a.tobs_out) {   // rare: per-row accesses (this thread stored the row)
+#pragma unroll
+        for (int k = 0; k < kD; ++k) {
+            const float x = tobs[r * kD + k];
+            a.tobs_out[r * kD + k] = a.norm_obs ? norm_elem(x, cn[k], clip) : x;
         }
     }
-    store_partial(a, bid, v, sft, r1 > r0 ? r1 - r0 : 0);
+    if (done) a.returns[r] = 0.0;   // self.returns[dones] = 0
+    if (a.ep_ret) {                 // Monitor: sum(rewards), len(rewards)
+        const double er = f.er + (double)rew;
+        const int32_t el = f.el + 1;
+        if (done) {
+            a.ep_ret_done[r] = er;
+            a.ep_len_done[r] = el;
+        }
+        a.ep_ret[r] = done ? 0.0 : er;
+        a.ep_len[r] = done ? 0 : el;
+    }
 }
 
 }  // namespace vn

@@ -57,8 +57,9 @@ class DeviceVecNormalize:
         self._check(self.lib.he_vecnorm_init(self._p(self._stats), D, self._stream()), "he_vecnorm_init")
         # the moments half of each training step inside the env's he_step launch
         # (he_vecnorm_attach; up to 65,536 envs), then he_vecnorm_apply; else he_vecnorm_step
-        self._fusable = (getattr(venv, "_h", None) is not None and n <= 65536
-                         and os.environ.get("CANTORRL_VN_FUSED", "1") != "0")
+        on = getattr(venv, "_h", None) is not None and os.environ.get("CANTORRL_VN_FUSED", "1") != "0"
+        self._fusable = on and n <= 65536
+        self._fusable_eval = on   # the eval arm exchanges nothing between workgroups: any n
         self._actions_pending = None
         self._t_start = time.time()
 
@@ -176,7 +177,10 @@ class DeviceVecNormalize:
         except BaseException:
             if fused:  # the armed he_step did not run: nothing may keep this object's buffers
                 self.lib.he_vecnorm_attach(self.venv._h, None, None, None, None)
+                self.lib.he_vecnorm_attach_eval(self.venv._h, None, None)
             raise
+        if fused == "eval":  # he_step made the whole VecNormalize step in its own launch
+            return self._obs_out, self._rew_out, term, trunc
         fn = self.lib.he_vecnorm_apply if fused else self.lib.he_vecnorm_step
         st = fn(ctypes.byref(p), self.num_envs, self._p(obs), self._p(rew),
                                       self._p(term), self._p(self.venv._tobs), self._p(self._returns),
@@ -188,11 +192,25 @@ class DeviceVecNormalize:
         return self._obs_out, self._rew_out, term, trunc
 
     def _arm(self, p):
-        """Arm the env's next he_step (one-shot, he_vecnorm_attach) to run the moments half
-        into this object's buffers; returns whether it will.  Armed per step, so another
-        wrapper on the same env, or the inner env stepped directly, never reads or advances
-        these buffers, and the handle holds no pointer into them after the step."""
-        if not (self._fusable and p.training):
+        """Arm the env's next he_step (one-shot) to run part of this step into this object's
+        buffers: training, the moments half (he_vecnorm_attach; he_vecnorm_apply follows);
+        evaluation, the whole step (he_vecnorm_attach_eval: frozen statistics, nothing
+        crosses envs).  Returns False, True or "eval".  Armed per step, so another wrapper on
+        the same env, or the inner env stepped directly, never reads or advances these
+        buffers, and the handle holds no pointer into them after the step."""
+        if not p.training:
+            if not self._fusable_eval:
+                return False
+            o = _lib.HeVecnormOut(self._stats.data_ptr(), self._returns.data_ptr(), self._obs_out.data_ptr(),
+                                  self._rew_out.data_ptr(), self._tobs_out.data_ptr(), self._ep_ret.data_ptr(),
+                                  self._ep_len.data_ptr(), self._ep_ret_done.data_ptr(), self._ep_len_done.data_ptr())
+            st = self.lib.he_vecnorm_attach_eval(self.venv._h, ctypes.byref(p), ctypes.byref(o))
+            if st != _lib.HE_OK:
+                msg = self.lib.he_last_error(self.venv._h)
+                raise _lib.HedgeEnvError(f"he_vecnorm_attach_eval failed with status {st}: "
+                                         f"{msg.decode() if msg else ''}")
+            return "eval"
+        if not self._fusable:
             return False
         st = self.lib.he_vecnorm_attach(self.venv._h, ctypes.byref(p), self._p(self._returns),
                                         self._p(self._stats), self._p(self._scratch))

@@ -389,6 +389,27 @@ he_status he_vecnorm_apply(const he_vecnorm_params* p, int64_t n, const float* o
                            double* ep_return, int32_t* ep_length, double* ep_return_done,
                            int32_t* ep_length_done, void* stream);
 
+/* Evaluation (VecNormalize(training=False), train_ppo_v2.py:450-453): with the statistics
+ * frozen nothing of the step crosses envs, so the NEXT he_step on `env` (one-shot, consumed
+ * by that call whatever its status; p = NULL disarms) can do the whole of he_vecnorm_step's
+ * work itself -- obs_out, reward_out, terminal_obs_out of done rows, returns[done] = 0, the
+ * Monitor sums -- in its own launch: the caller then calls no he_vecnorm_* function for that
+ * step.  he_step must get the obs, reward, terminated and terminal_obs buffers; a step that
+ * takes another kernel (info requested) runs he_vecnorm_apply itself after it.  p->training
+ * must be 0; out's buffers are he_vecnorm_step's (scratch unused). */
+typedef struct he_vecnorm_out {
+    const double* stats;
+    double* returns;
+    float* obs_out;
+    float* reward_out;
+    float* terminal_obs_out;    /* may be NULL */
+    double* ep_return;          /* Monitor sums: all four NULL, or all four given */
+    int32_t* ep_length;
+    double* ep_return_done;
+    int32_t* ep_length_done;
+} he_vecnorm_out;
+he_status he_vecnorm_attach_eval(he_env* env, const he_vecnorm_params* p, const he_vecnorm_out* out);
+
 /* VecNormalize.reset: returns = 0; obs_rms.update(obs) (training && norm_obs);
  * obs_out normalized (norm_obs, else a copy). */
 he_status he_vecnorm_reset(const he_vecnorm_params* p, int64_t n, const float* obs, double* returns,

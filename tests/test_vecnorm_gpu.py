@@ -237,6 +237,40 @@ def test_fused_moments_equal_separate_launch(info, monkeypatch):
     np.testing.assert_array_equal(ta, tb)
 
 
+@pytest.mark.parametrize("info,norm_reward,n", [(False, False, 3000), (False, True, 70000), (True, False, 700)])
+def test_fused_eval_step_equals_separate_launch(info, norm_reward, n, monkeypatch):
+    """he_vecnorm_attach_eval (the whole eval VecNormalize step inside he_step's launch, or
+    he_vecnorm_apply run by he_step itself after an info step) against he_step +
+    he_vecnorm_step with the statistics frozen: obs, rewards, normalized terminal obs,
+    Monitor sums and returns bit for bit (the same per-element arithmetic), over episode
+    ends (T = 12) and a partial last workgroup (n = 700, 70000)."""
+    from cantorrl_amd.vec_env import HedgingVecEnv
+    from cantorrl_amd.vec_normalize import DeviceVecNormalize
+    outs = []
+    for fused in ("1", "0"):
+        monkeypatch.setenv("CANTORRL_VN_FUSED", fused)
+        env = HedgingVecEnv(n, mode="gbm", generate=GEN, seed=11, device=DEV, return_numpy=False,
+                            info_keys=("cash",) if info else (), **KW)
+        vn = DeviceVecNormalize(env, gamma=0.97, norm_reward=norm_reward)
+        vn.reset_tensors()
+        g = torch.Generator(device=DEV)
+        g.manual_seed(5)
+        for k in range(6):   # training steps: non-trivial statistics and returns
+            vn.step_tensors(torch.rand((n, 2), device=DEV, generator=g) * 2 - 1)
+        vn.training = False
+        got = []
+        for k in range(26):
+            o, r, t, _ = vn.step_tensors(torch.rand((n, 2), device=DEV, generator=g) * 2 - 1)
+            m = t.bool()
+            got += [o.clone(), r.clone(), t.clone(), vn.terminal_obs_tensor[m].clone(), vn._ep_ret.clone(),
+                    vn._ep_len.clone(), vn._ep_ret_done.clone(), vn._ep_len_done.clone(), vn._returns.clone()]
+        torch.cuda.synchronize()
+        outs.append(got)
+        vn.close()
+    for k, (a, b) in enumerate(zip(*outs)):
+        assert torch.equal(a, b), k
+
+
 def test_two_wrappers_on_one_env_and_inner_steps():
     """the fused moments are armed per step (he_vecnorm_attach is one-shot).
     Two DeviceVecNormalize on one env, the first dropped after the second has stepped, and

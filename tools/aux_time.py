@@ -126,7 +126,10 @@ graph_us(lambda k: vn.step_tensors(acts[k]), "he_step + VecNormalize, moments fu
 vn._fusable = False
 graph_us(lambda k: vn.step_tensors(acts[k]), "he_step + VecNormalize, separate moments launch")
 vn.training = False
-graph_us(lambda k: vn.step_tensors(acts[k]), "he_step + VecNormalize, frozen statistics (eval)")
+vn._fusable_eval = False
+graph_us(lambda k: vn.step_tensors(acts[k]), "he_step + VecNormalize, frozen statistics (eval), he_vecnorm_step launch")
+vn._fusable_eval = True
+graph_us(lambda k: vn.step_tensors(acts[k]), "he_step + VecNormalize, frozen statistics (eval), fused into he_step")
 vn.training = True
 env.close()
 
