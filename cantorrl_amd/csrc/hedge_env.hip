@@ -1779,12 +1779,14 @@ __global__ __launch_bounds__(kBlock) void step1_vne_kernel(const Params* __restr
     io.sums = false;
     static_assert(kEpw == 64 && kEpb == kBlock, "one env per thread");
     const int64_t r0 = (int64_t)blockIdx.x * kEpb;
+    __shared__ vn::FrozenNorm fz;
     const vn::FrozenPre fp = vn::load_frozen(va, r0 + threadIdx.x, r0 + threadIdx.x < n);
+    vn::prep_frozen(fz, va, fp);
     VnHook hk{nullptr, 0.0f, false};
     step_body<MODE, false, true, BOOK, FAST, false, GS>(*pc, n, tA, tB, tC, s, io, 1, slot0, blockIdx.x, &hk);
     const int rows = (int)((n - r0) < kEpb ? n - r0 : kEpb);
-    __syncthreads();  // the workgroup's obs rows (LDS, the final ones incl. reset obs) visible to all its threads
-    vn::apply_frozen_rows(va, r0, rows, hk.tile, fp, hk.rew, hk.term, sio.tobs);
+    __syncthreads();  // the workgroup's obs rows (LDS, the final ones incl. reset obs) and fz visible to all
+    vn::apply_frozen_rows(va, fz, r0, rows, hk.tile, fp, hk.rew, hk.term, sio.tobs);
 }
 
 // The same moments after any other he_step launch (info requested, a fused market block).

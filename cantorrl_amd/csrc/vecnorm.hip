@@ -128,6 +128,8 @@ __device__ __forceinline__ RowIn row_in(const VnArgs& a, int64_t r) {
     return in;
 }
 
+constexpr int kMergeLanes = 8;   // lanes per merged value (vn_apply_kernel)
+static_assert(kMergeLanes * kPart <= kVnThreads, "one merge lane group per value");
 using vn::ColNorm;
 using vn::col_norm;
 using vn::norm_elem;
@@ -140,7 +142,6 @@ using vn::norm_elem;
 // waits on; each thread's rows are.)
 __global__ void __launch_bounds__(kVnThreads) vn_apply_kernel(VnArgs a) {
     constexpr int R = 1;
-    __shared__ double sh[kVnThreads * (kPart + 1)];
     __shared__ double ssum[kPart];
     __shared__ ColNorm snorm[kD];     // per obs column (col_norm)
     __shared__ double srinv;
@@ -168,12 +169,19 @@ __global__ void __launch_bounds__(kVnThreads) vn_apply_kernel(VnArgs a) {
         if (resident && !a.reset && t + j * kVnThreads < nrows) pin[j] = row_in(a, w.r0 + t + j * kVnThreads);
     }
     if (a.upd_obs || upd_ret) {
-        const double* P = a.part + t;
-        const bool has = t < a.blocks;
-        double v[kPart];
+        // the merge, transposed: thread t < 8 kPart sums value c = t / 8 of the partials
+        // b = t % 8, t % 8 + 8, ... (in b order), then a butterfly over its 8-lane group --
+        // no block-wide LDS reduction (the row-major block_sum stored and re-read 61 KB)
+        if (t < kMergeLanes * kPart) {
+            const int c = t / kMergeLanes, j = t % kMergeLanes;
+            const double* P = a.part + (size_t)c * kVnMaxBlocks;
+            double x = 0.0;
+            for (int b = j; b < a.blocks; b += kMergeLanes) x += P[b];
 #pragma unroll
-        for (int c = 0; c < kPart; ++c) v[c] = has ? P[c * kVnMaxBlocks] : 0.0;
-        block_sum<kPart>(v, sh, ssum);   // ssum[0] = n, [1 .. kD + 1] = S1, then S2
+            for (int m = kMergeLanes / 2; m >= 1; m >>= 1) x += __shfl_xor(x, m, kMergeLanes);
+            if (j == 0) ssum[c] = x;   // ssum[0] = n, [1 .. kD + 1] = S1, then S2
+        }
+        __syncthreads();
         const int c = t;
         if (c <= kD) {
             const double* old = a.part + kVnMaxBlocks * kPart;   // launch 1's snapshot

@@ -250,16 +250,26 @@ __device__ __forceinline__ FrozenPre load_frozen(const ApplyArgs& a, int64_t r, 
     }
     return f;
 }
-// rows [r0, r0 + rows) of the workgroup, obs staged at tile (row t at tile + t kD, visible to
-// every thread), thread t < rows owning row r0 + t: its reward, done flag and terminal obs row.
-__device__ __forceinline__ void apply_frozen_rows(const ApplyArgs& a, int64_t r0, int rows, const float* tile,
-                                                  const FrozenPre& f, float rew, bool done, const float* tobs) {
-    __shared__ ColNorm cn[kD];
-    __shared__ double rinv;
+// The per-column constants in LDS, made before the step (their f64 square roots and divisions
+// overlap the step's loads; the step's own barrier publishes them).
+struct FrozenNorm {
+    ColNorm cn[kD];
+    double rinv;
+};
+__device__ __forceinline__ void prep_frozen(FrozenNorm& z, const ApplyArgs& a, const FrozenPre& f) {
     const int t = threadIdx.x;
-    if (t < kD) cn[t] = col_norm(f.m, f.v, a.eps);
-    if (t == kD) rinv = 1.0 / sqrt(f.v + a.eps);
-    __syncthreads();
+    if (t < kD) z.cn[t] = col_norm(f.m, f.v, a.eps);
+    if (t == kD) z.rinv = 1.0 / sqrt(f.v + a.eps);
+}
+// rows [r0, r0 + rows) of the workgroup, obs staged at tile (row t at tile + t kD), after a
+// workgroup barrier that follows prep_frozen; thread t < rows owns row r0 + t: its reward, done
+// flag and terminal obs row.
+__device__ __forceinline__ void apply_frozen_rows(const ApplyArgs& a, const FrozenNorm& z, int64_t r0, int rows,
+                                                  const float* tile, const FrozenPre& f, float rew, bool done,
+                                                  const float* tobs) {
+    const ColNorm* cn = z.cn;
+    const double rinv = z.rinv;
+    const int t = threadIdx.x;
     const float clip = (float)a.clip_obs;
     // the obs as a flat coalesced copy: element k = t + 256 q is column k % 13 (rows start at a
     // row boundary), stepped by 256 % 13 = 9 per q without a division

@@ -24,12 +24,25 @@ FIELDS = {".vgpr_count": "vgpr", ".agpr_count": "agpr", ".sgpr_count": "sgpr",
           ".private_segment_fixed_size": "scratch_B", ".group_segment_fixed_size": "lds_B"}
 
 
-def code_object(lib, td):
-    fb, co = os.path.join(td, "fb.bin"), os.path.join(td, "co.o")
+def code_objects(lib, td):
+    """The gfx950 code object of every translation unit: .hip_fatbin holds one offload bundle
+    per TU (hedge_env.hip, vecnorm.hip, analytics.hip), each unbundled on its own."""
+    fb = os.path.join(td, "fb.bin")
     subprocess.run(["objcopy", "-O", "binary", "--only-section=.hip_fatbin", lib, fb], check=True)
-    subprocess.run([f"{LLVM}/clang-offload-bundler", "--unbundle", "--type=o", f"--input={fb}",
-                    "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={co}"], check=True)
-    return co
+    data = open(fb, "rb").read()
+    magic = b"__CLANG_OFFLOAD_BUNDLE__"
+    starts = [m.start() for m in re.finditer(re.escape(magic), data)]
+    cos = []
+    for k, a in enumerate(starts):
+        b = starts[k + 1] if k + 1 < len(starts) else len(data)
+        part, co = os.path.join(td, "b%d.bin" % k), os.path.join(td, "co%d.o" % k)
+        with open(part, "wb") as fh:
+            fh.write(data[a:b].rstrip(b"\0") if k + 1 == len(starts) else data[a:b])
+        r = subprocess.run([f"{LLVM}/clang-offload-bundler", "--unbundle", "--type=o", f"--input={part}",
+                            "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={co}"], capture_output=True)
+        if r.returncode == 0 and os.path.getsize(co) > 0:
+            cos.append(co)
+    return cos
 
 
 def metadata(co):
@@ -99,9 +112,11 @@ def main(argv):
         else:
             lib = a
     with tempfile.TemporaryDirectory() as td:
-        co = code_object(lib, td)
-        meta = metadata(co)
-        dg = digests(co) if dig else {}
+        meta, dg = {}, {}
+        for co in code_objects(lib, td):
+            meta.update(metadata(co))
+            if dig:
+                dg.update(digests(co))
     rows = []
     for sym in sorted(meta):
         if flt and flt not in sym:
