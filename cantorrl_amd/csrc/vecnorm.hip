@@ -175,8 +175,17 @@ __global__ void __launch_bounds__(kVnThreads) vn_apply_kernel(VnArgs a) {
         if (t < kMergeLanes * kPart) {
             const int c = t / kMergeLanes, j = t % kMergeLanes;
             const double* P = a.part + (size_t)c * kVnMaxBlocks;
+            // every load issued before the first add (unrolled over the kVnMaxBlocks bound):
+            // a rolled loop waited one round trip per partial
+            double v[kVnMaxBlocks / kMergeLanes];
+#pragma unroll
+            for (int q = 0; q < kVnMaxBlocks / kMergeLanes; ++q) {
+                const int b = j + q * kMergeLanes;
+                v[q] = b < a.blocks ? P[b] : 0.0;
+            }
             double x = 0.0;
-            for (int b = j; b < a.blocks; b += kMergeLanes) x += P[b];
+#pragma unroll
+            for (int q = 0; q < kVnMaxBlocks / kMergeLanes; ++q) x += v[q];
 #pragma unroll
             for (int m = kMergeLanes / 2; m >= 1; m >>= 1) x += __shfl_xor(x, m, kMergeLanes);
             if (j == 0) ssum[c] = x;   // ssum[0] = n, [1 .. kD + 1] = S1, then S2

@@ -37,7 +37,7 @@ def code_objects(lib, td):
         b = starts[k + 1] if k + 1 < len(starts) else len(data)
         part, co = os.path.join(td, "b%d.bin" % k), os.path.join(td, "co%d.o" % k)
         with open(part, "wb") as fh:
-            fh.write(data[a:b].rstrip(b"\0") if k + 1 == len(starts) else data[a:b])
+            fh.write(data[a:b])
         r = subprocess.run([f"{LLVM}/clang-offload-bundler", "--unbundle", "--type=o", f"--input={part}",
                             "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={co}"], capture_output=True)
         if r.returncode == 0 and os.path.getsize(co) > 0:
