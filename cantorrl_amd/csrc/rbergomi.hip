@@ -209,10 +209,7 @@ __device__ __forceinline__ void normal_quad32(u32x4 c, uint32_t k0, uint32_t k1,
 // FULL: n == MO - 2 (30 steps on a 32-point grid, the reference's tenor), so the step
 // guards are compile-time; otherwise n is tested per step.
 template <int MO, int NORM, bool ATM, bool FULL>
-#ifndef RB_MC_WAVES
-#define RB_MC_WAVES 1
-#endif
-__global__ void __launch_bounds__(kMcThreads, RB_MC_WAVES) mc_kernel(McArgs a) {
+__global__ void __launch_bounds__(kMcThreads) mc_kernel(McArgs a) {
     __shared__ double s_lam[MO];
     __shared__ double s_ma[MO];
     __shared__ double s_red[kMcThreads / 64];
