@@ -319,12 +319,38 @@ __device__ __forceinline__ float4 greeks(const Params& p, float S, float v) {
     return make_float4((float)cd, (float)gam, (float)pd, 0.0f);
 }
 
+// Phi(-|d1|) for the f32 obs greeks, given ph = phi(d1) (which gamma needs anyway):
+// ph * R(|d1|), R the Mills ratio sqrt(pi/2) erfcx(a/sqrt2), evaluated as w P(w) with
+// w = 2 / (a + 2) and P a degree-10 least-squares fit over a in [0, 14] (phi underflows
+// f32 beyond).  One rcp and 11 FMAs on top of the shared exp instead of erfcf's own
+// exp and branchy rational approximations.  Error of the f32 evaluation: relative
+// < 4.8e-7 where the tail is > 0.1, < 1.3e-6 below it, absolute < 2.2e-7 -- inside the
+// obs tolerance (OBS_RTOL 1e-6, OBS_ATOL 1e-7) against the reference's f64 ndtr.
+__device__ __forceinline__ float ncdf_tail(float d1, float ph) {
+    const float a = fminf(fabsf(d1), 14.0f);
+    const float w = 2.0f * __builtin_amdgcn_rcpf(a + 2.0f);
+    float r = -2.690903097e-02f;
+    r = fmaf(r, w, 6.361111253e-02f);
+    r = fmaf(r, w, 2.313483953e-01f);
+    r = fmaf(r, w, -1.219161630e+00f);
+    r = fmaf(r, w, 2.182162046e+00f);
+    r = fmaf(r, w, -1.785471797e+00f);
+    r = fmaf(r, w, 4.304344356e-01f);
+    r = fmaf(r, w, -1.690988056e-02f);
+    r = fmaf(r, w, 3.958457112e-01f);
+    r = fmaf(r, w, 4.983069301e-01f);
+    r = fmaf(r, w, 5.000579357e-01f);
+    return ph * (r * w);
+}
+
 // Generate-mode obs greeks (market_kernel): same branches and the same f32 d1
 // numerator as greeks(), the rest in f32 instead of f64-then-cast.  N(d1) - 1 is
-// taken as -N(-d1) (no cancellation), 1/(S sigma sqrt T) through v_rcp_f32.  Within
-// 4 f32 ulp of the reference's f64 values (tests: OBS_RTOL 1e-6 on columns 7-10) at
-// about a third of the cost of the f64 chain (measured: greeks were 32% of
-// market_kernel).  Replay tables and the reset obs keep greeks() (replay_greeks).
+// taken as -N(-d1) (no cancellation, ncdf_tail sharing gamma's exp), 1/(S sigma sqrt T)
+// through v_rcp_f32.  Within OBS_RTOL 1e-6 / OBS_ATOL 1e-7 of the reference's f64
+// values (tests, columns 7-10) at well under a third of the cost of the f64 chain
+// (measured: greeks were 32% of market_kernel; ncdf_tail in place of erfcf took
+// 10-15 us off the headline launch, r04s3).  Replay tables and the reset obs keep
+// greeks() (replay_greeks).
 template <bool CONST_VAR>
 __device__ __forceinline__ float4 greeks_fast(const Params& p, float S, float v) {
     float cd, gam, pd;
@@ -361,15 +387,14 @@ __device__ __forceinline__ float4 greeks_fast(const Params& p, float S, float v)
             } else {
                 d1 = CONST_VAR ? num * p.g_inv_sst_f : num * __builtin_amdgcn_rcpf(sstf);
             }
-            // N(d1) = erfc(-x)/2 and N(d1) - 1 = -erfc(x)/2: evaluate erfc at |x| (the
-            // small tail, accurate) and take the other as 1 - tail (>= 1/2, no cancellation)
-            const float x = d1 * 0.70710678118654752f;
-            const float tail = 0.5f * erfcf(fabsf(x));
-            cd = (x >= 0.0f) ? 1.0f - tail : tail;
-            pd = (x >= 0.0f) ? -tail : tail - 1.0f;
+            // N(d1) = Phi(d1) and N(d1) - 1 = -Phi(-d1): evaluate the small tail Phi(-|d1|)
+            // (accurate) and take the other as 1 - tail (>= 1/2, no cancellation)
+            const float ph = expf(-0.5f * (d1 * d1)) * 0.398942280401432678f;
+            const float tail = ncdf_tail(d1, ph);
+            cd = (d1 >= 0.0f) ? 1.0f - tail : tail;
+            pd = (d1 >= 0.0f) ? -tail : tail - 1.0f;
             const float gd = S * sstf;
-            gam = (fabsf(gd) < 1e-9f) ? 0.0f
-                                      : (expf(-0.5f * (d1 * d1)) * 0.398942280401432678f) * __builtin_amdgcn_rcpf(gd);
+            gam = (fabsf(gd) < 1e-9f) ? 0.0f : ph * __builtin_amdgcn_rcpf(gd);
         }
     }
     return make_float4(cd, gam, pd, 0.0f);
@@ -394,12 +419,12 @@ __device__ __forceinline__ float4 greeks_lean(float S, float num_drift, float in
     const float Kc = np_maxf(K, 1e-6f);
     const float num = logf(S / Kc) + num_drift;   // f32 in the reference too
     const float d1 = num * inv_sst_f;
-    const float x = d1 * 0.70710678118654752f;
-    const float tail = 0.5f * erfcf(fabsf(x));
-    float cd = (x >= 0.0f) ? 1.0f - tail : tail;
-    float pd = (x >= 0.0f) ? -tail : tail - 1.0f;
+    const float ph = expf(-0.5f * (d1 * d1)) * 0.398942280401432678f;
+    const float tail = ncdf_tail(d1, ph);
+    float cd = (d1 >= 0.0f) ? 1.0f - tail : tail;
+    float pd = (d1 >= 0.0f) ? -tail : tail - 1.0f;
     const float gd = S * sstf;
-    float ge = (expf(-0.5f * (d1 * d1)) * 0.398942280401432678f) * __builtin_amdgcn_rcpf(gd);
+    float ge = ph * __builtin_amdgcn_rcpf(gd);
     float ct = (K == 0.0f) ? 0.5f : ((K > 0.0f) ? 0.0f : 1.0f);
     float pt = (K == 0.0f) ? -0.5f : ((K < 0.0f) ? 0.0f : -1.0f);
     HE_OPAQUE3(ge, ct, pt);
@@ -3091,6 +3116,16 @@ __global__ __launch_bounds__(256, 4) __attribute__((amdgpu_num_sgpr(kLdsNumSgpr)
     else lds_replay_loader(p, s, k_steps, lm, base, wave - 2);
 }
 
+// he_episode_summaries: the last finished episode of every env, [4][N] (the reward
+// wave's coalesced per-field stores) re-laid out as [N][4] rows -- four coalesced 4-B
+// loads and one 16-B store per env.  One launch, ~1 MB at 65,536 envs (four strided
+// hipMemcpy2DAsync calls took ~26 us on the boundary, r04s1_rccl_boundary.json).
+__global__ void summaries_kernel(const float* __restrict__ last, float4* __restrict__ out, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    out[i] = make_float4(last[i], last[n + i], last[2 * n + i], last[3 * n + i]);
+}
+
 // Test hooks (he_device_rng / he_device_math): the device build of the generate-mode
 // RNG and math, element-wise, so tests can compare device words and values bit for bit
 // with the host build, rocRAND and the oracle.
@@ -4526,12 +4561,10 @@ he_status he_episode_summaries(he_env* env, float* out, void* stream) {
     if (!env || !out) return HE_EINVAL;
     DeviceGuard dg(env->cfg.device);
     const int64_t N = env->cfg.n_envs;
-    // [4][N] -> [N][4]: a strided 2D copy on the stream (no kernel)
-    HE_HIP(env, hipMemcpy2DAsync(out, 4 * sizeof(float), env->s.last, sizeof(float), sizeof(float), (size_t)N,
-                                 hipMemcpyDeviceToDevice, (hipStream_t)stream));
-    for (int c = 1; c < 4; ++c)
-        HE_HIP(env, hipMemcpy2DAsync(out + c, 4 * sizeof(float), env->s.last + (size_t)c * N, sizeof(float),
-                                     sizeof(float), (size_t)N, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+    if ((reinterpret_cast<uintptr_t>(out) & 15u) != 0) return fail(env, HE_EINVAL, "out must be 16-byte aligned");
+    hipLaunchKernelGGL(summaries_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       env->s.last, reinterpret_cast<float4*>(out), N);
+    HE_HIP(env, hipGetLastError());
     return HE_OK;
 }
 

@@ -271,7 +271,8 @@ he_status he_rollout_policy(he_env* env, int32_t k_steps, int32_t policy, float*
  * of :481-514): out[N][4] f32 (DEVICE pointer) = {return, sum of step P&L, sum of
  * transaction costs, length} of each env's most recently finished episode (zeros before
  * the first).  Maintained by he_rollout in generate modes (the LDS path) and by
- * he_rollout_policy; the running sums restart at he_reset.  Stream-ordered. */
+ * he_rollout_policy; the running sums restart at he_reset.  Stream-ordered; out must be
+ * 16-byte aligned (one float4 row per env; HE_EINVAL otherwise). */
 he_status he_episode_summaries(he_env* env, float* out, void* stream);
 
 /* Generate modes run market_kernel for block b+1 on a library-owned side stream
