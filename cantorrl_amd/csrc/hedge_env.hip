@@ -574,8 +574,10 @@ __device__ __forceinline__ double mills(double a) {
     return a * 0.25;  // diagnostic builds only (tools/gpu): the book without its tails
 #endif
     const double d = a + kMillsC;                        // in [3.5, 41]: no special cases
+    // v_rcp_f64 is within 4.7e-8 of 1 / d on [3.5, 43], one Newton step within 2.3e-15
+    // (tools/probe/rcp_f64.hip, profiles/r04s3_rcp_f64.txt): u = A - B y then carries
+    // ~5e-15 against the fit's 1.7e-12, so the second step (exact rounding) buys nothing
     double y = __builtin_amdgcn_rcp(d);
-    y = fma(fma(-d, y, 1.0), y, y);                      // two Newton steps: 1 / d to the last bits
     y = fma(fma(-d, y, 1.0), y, y);
     const double u = fma(-kMillsB, y, kMillsA);
     double r = 2.7428474899566849e-08;
