@@ -186,8 +186,9 @@ def replay_tables(paths, cols, seed=2025):
 def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=MIN_TIMED_STEPS)
-    ap.add_argument("--warmup", type=int, default=256)
+    ap.add_argument("--steps", type=int, default=None,
+                    help=f"env: timed env-steps (default and floor {MIN_TIMED_STEPS}); rbergomi: launches (default 5)")
+    ap.add_argument("--warmup", type=int, default=None, help="env: default 256; rbergomi: default 1")
     ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS), help="BASELINE.json config")
     ap.add_argument("--envs", type=int, default=None, help="envs per GPU (default: the config's)")
     ap.add_argument("--mode", choices=["rollout", "graph", "eager"], default="rollout")
@@ -208,7 +209,11 @@ def parse(argv=None):
     ap.add_argument("--gather-rollout", action="store_true",
                     help="N > 1: also all-gather each boundary's rollout tensors (obs / reward / terminated of "
                          "the last he_rollout) in global env order (SURVEY 8(e): small N only)")
-    return ap.parse_args(argv)
+    args = ap.parse_args(argv)
+    if args.workload == "env":
+        args.steps = MIN_TIMED_STEPS if args.steps is None else args.steps
+        args.warmup = 256 if args.warmup is None else args.warmup
+    return args
 
 
 def _cpu_sample(seconds, seed=42, barrier=None, n=256, offset=0):
@@ -886,7 +891,9 @@ def rbergomi_main(args):
         if st != 0:
             raise RuntimeError(lib.rb_last_error().decode())
 
-    K, W = max(1, args.steps), max(0, args.warmup)
+    # one launch prices 1M options (~1 s in f64): a handful of launches, not the env's 25,600
+    K = max(1, 5 if args.steps is None else args.steps)
+    W = max(0, 1 if args.warmup is None else args.warmup)
     for _ in range(W):
         launch()
     torch.cuda.synchronize()

@@ -207,30 +207,9 @@ HE_HD double u01(uint32_t hi, uint32_t lo) {
 //    is a fixed-point number), so sin/cos of (pi/2) r are two short even/odd
 //    polynomials in r (Taylor to r^17 / r^16, truncation < 1e-19) and q picks the
 //    quadrant -- no Cody-Waite reduction.
-HE_HD void box_muller(double u1, double u2, double* z1, double* z2) {
-    // log(u1)
-    int e;
-    double m = frexp(u1, &e);           // u1 = m 2^e, m in [1/2, 1)
-    if (m < 0.70710678118654752) {      // -> [sqrt2/2, sqrt2)
-        m = m + m;
-        e -= 1;
-    }
-    const double s = (m - 1.0) / (m + 1.0);
-    const double s2 = s * s;
-    double p = 1.0 / 19.0;
-    p = fma_k(p, s2, 1.0 / 17.0);
-    p = fma_k(p, s2, 1.0 / 15.0);
-    p = fma_k(p, s2, 1.0 / 13.0);
-    p = fma_k(p, s2, 1.0 / 11.0);
-    p = fma_k(p, s2, 1.0 / 9.0);
-    p = fma_k(p, s2, 1.0 / 7.0);
-    p = fma_k(p, s2, 1.0 / 5.0);
-    p = fma_k(p, s2, 1.0 / 3.0);
-    const double lm = (2.0 * s) + (2.0 * s) * (s2 * p);   // 2 atanh(s)
-    const double ed = (double)e;
-    const double lg = fma(ed, 6.93147180369123816490e-01, fma(ed, 1.90821492927058770002e-10, lm));
-    const double rad = sqrt(-2.0 * lg);
-    // sin / cos of 2 pi u2
+// sin / cos of 2 pi u for u in [0, 1) of the u01 form (box_muller's): 2 pi u = (pi/2)(q + r),
+// q = rint(4 u), r = 4 u - q in [-1/2, 1/2] exactly, two short polynomials in r, q the quadrant
+HE_HD void sincos_2pi_u(double u2, double* sin_out, double* cos_out) {
     const double x = 4.0 * u2;
     const double q = rint(x);
     const double r = x - q;
@@ -259,8 +238,35 @@ HE_HD void box_muller(double u1, double u2, double* z1, double* z2) {
     const int qi = (int)q & 3;
     const bool swp = (qi & 1) != 0;
     const double s_ = swp ? cs : sn, c_ = swp ? sn : cs;
-    const double sinv = (qi & 2) ? -s_ : s_;
-    const double cosv = ((qi + 1) & 2) ? -c_ : c_;
+    *sin_out = (qi & 2) ? -s_ : s_;
+    *cos_out = ((qi + 1) & 2) ? -c_ : c_;
+}
+
+HE_HD void box_muller(double u1, double u2, double* z1, double* z2) {
+    // log(u1)
+    int e;
+    double m = frexp(u1, &e);           // u1 = m 2^e, m in [1/2, 1)
+    if (m < 0.70710678118654752) {      // -> [sqrt2/2, sqrt2)
+        m = m + m;
+        e -= 1;
+    }
+    const double s = (m - 1.0) / (m + 1.0);
+    const double s2 = s * s;
+    double p = 1.0 / 19.0;
+    p = fma_k(p, s2, 1.0 / 17.0);
+    p = fma_k(p, s2, 1.0 / 15.0);
+    p = fma_k(p, s2, 1.0 / 13.0);
+    p = fma_k(p, s2, 1.0 / 11.0);
+    p = fma_k(p, s2, 1.0 / 9.0);
+    p = fma_k(p, s2, 1.0 / 7.0);
+    p = fma_k(p, s2, 1.0 / 5.0);
+    p = fma_k(p, s2, 1.0 / 3.0);
+    const double lm = (2.0 * s) + (2.0 * s) * (s2 * p);   // 2 atanh(s)
+    const double ed = (double)e;
+    const double lg = fma(ed, 6.93147180369123816490e-01, fma(ed, 1.90821492927058770002e-10, lm));
+    const double rad = sqrt(-2.0 * lg);
+    double sinv, cosv;
+    sincos_2pi_u(u2, &sinv, &cosv);
     *z1 = rad * cosv;
     *z2 = rad * sinv;
 }

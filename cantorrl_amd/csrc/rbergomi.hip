@@ -71,6 +71,51 @@ HE_HD void normal_pair(u32x4 c, uint32_t k0, uint32_t k1, double* a, double* b) 
     box_muller(u01(x.x, x.y), u01(x.z, x.w), a, b);
 }
 
+// The MC pricer's f64 normals (mc_kernel NORM 0, its hot loop: 31 Box-Muller pairs per MC
+// path).  The env's box_muller (he_math.h) is pinned bit for bit to the oracle; these are
+// only held to their distribution (test_pricer_philox_black_scholes_limit), so the two
+// multi-instruction IEEE sequences go: s = (m - 1) / (m + 1) as (m - 1) times v_rcp_f64 with
+// one Newton step (within 2.3e-15, profiles/r04s3_rcp_f64.txt), and sqrt(-2 log u) as
+// x rsq(x) with one Newton-Raphson correction (the argument is in [1.1e-15, 75]: no scaling
+// or special cases).  The series and the sin / cos polynomials are box_muller's.
+__device__ __forceinline__ void mc_box_muller(double u1, double u2, double* z1, double* z2) {
+    int e;
+    double m = frexp(u1, &e);
+    const bool lo = m < 0.70710678118654752;
+    m = lo ? m + m : m;
+    e = lo ? e - 1 : e;
+    const double den = m + 1.0;
+    double y = __builtin_amdgcn_rcp(den);
+    y = fma(fma(-den, y, 1.0), y, y);
+    const double s = (m - 1.0) * y;
+    const double s2 = s * s;
+    double p = 1.0 / 19.0;
+    p = fma(p, s2, 1.0 / 17.0);
+    p = fma(p, s2, 1.0 / 15.0);
+    p = fma(p, s2, 1.0 / 13.0);
+    p = fma(p, s2, 1.0 / 11.0);
+    p = fma(p, s2, 1.0 / 9.0);
+    p = fma(p, s2, 1.0 / 7.0);
+    p = fma(p, s2, 1.0 / 5.0);
+    p = fma(p, s2, 1.0 / 3.0);
+    const double lm = (2.0 * s) + (2.0 * s) * (s2 * p);   // 2 atanh(s)
+    const double ed = (double)e;
+    const double lg = fma(ed, 6.93147180369123816490e-01, fma(ed, 1.90821492927058770002e-10, lm));
+    const double x = -2.0 * lg;
+    const double r0 = __builtin_amdgcn_rsq(x);
+    const double g0 = x * r0, h0 = 0.5 * r0;
+    const double rr0 = fma(-g0, h0, 0.5);
+    const double rad = fma(g0, rr0, g0);
+    double sn, cs;
+    he::sincos_2pi_u(u2, &sn, &cs);
+    *z1 = rad * cs;
+    *z2 = rad * sn;
+}
+__device__ __forceinline__ void normal_pair_mc(u32x4 c, uint32_t k0, uint32_t k1, double* a, double* b) {
+    const u32x4 x = philox4x32_10(c, k0, k1);
+    mc_box_muller(u01(x.x, x.y), u01(x.z, x.w), a, b);
+}
+
 // np.clip(x, lo, hi) (NaN passes through)
 HE_HD double np_clip(double x, double lo, double hi) { return x < lo ? lo : (x > hi ? hi : x); }
 
@@ -285,7 +330,7 @@ __global__ void __launch_bounds__(kMcThreads) mc_kernel(McArgs a) {
 #pragma unroll
             for (int b = 0; b < MO / 2; ++b) {
                 __builtin_amdgcn_sched_barrier(0);
-                normal_pair(rb_ctr((uint32_t)(m * MO + b), kDomMc, sub, gid), a.k0, a.k1, &w1[2 * b], &w1[2 * b + 1]);
+                normal_pair_mc(rb_ctr((uint32_t)(m * MO + b), kDomMc, sub, gid), a.k0, a.k1, &w1[2 * b], &w1[2 * b + 1]);
             }
         } else {
 #pragma unroll
@@ -322,7 +367,7 @@ __global__ void __launch_bounds__(kMcThreads) mc_kernel(McArgs a) {
                             w2 = wp[2 * j + 1];
                         } else if (NORM == 0) {
                             if ((j & 1) == 0)
-                                normal_pair(rb_ctr((uint32_t)(m * MO + MO / 2 + j / 2), kDomMc, sub, gid), a.k0,
+                                normal_pair_mc(rb_ctr((uint32_t)(m * MO + MO / 2 + j / 2), kDomMc, sub, gid), a.k0,
                                             a.k1, &w2q[0], &w2q[1]);
                             w2 = w2q[j & 1];
                         } else {

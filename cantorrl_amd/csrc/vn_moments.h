@@ -202,17 +202,23 @@ __device__ __forceinline__ void moments_from_rows(const MomentsArgs& a, int bid,
 // the normalized terminal obs of done rows.  The same per-element arithmetic as vecnorm.hip's
 // apply (ColNorm, norm_elem): the same bits as he_step + he_vecnorm_apply.
 struct ColNorm {
-    double mean, s;
+    float mh, mls, sh, sl;   // mean = mh + ml, s = 1 / sqrt(var + eps) = sh + sl, mls = RN(ml s)
 };
 __device__ __forceinline__ ColNorm col_norm(double mean, double var, double eps) {
-    return ColNorm{mean, 1.0 / sqrt(var + eps)};
+    const double s = 1.0 / sqrt(var + eps);
+    const float mh = (float)mean, sh = (float)s;
+    return ColNorm{mh, (float)((mean - (double)mh) * s), sh, (float)(s - (double)sh)};
 }
-// VecNormalize.normalize_obs of one element: the f64 difference and product, rounded to f32
-// once and clipped in f32 (the same values as clipping in f64 first: rounding is monotonic and
-// the clip bounds are f32 values)
+// VecNormalize.normalize_obs of one element in f32 from the merged f64 statistics, converted
+// once per column (col_norm): y = (x - mh) (sh + sl) - ml s.  x - mh is exact within a factor
+// 2 of the mean (Sterbenz), else one rounding; the two FMAs round once more (the sl and ml s
+// terms are corrections far below y's last bit).  About 1 f32 ulp of y against the f64
+// (x - mean) / sqrt(var + eps) -- the tests allow 2e-6 absolute at |y| <= clip = 10, ~2 ulp.
+// np.clip in f32 (NaN stays NaN).
 __device__ __forceinline__ float norm_elem(float x, const ColNorm& n, float clip) {
-    const float r = (float)(((double)x - n.mean) * n.s);
-    return r < -clip ? -clip : (r > clip ? clip : r);   // np.clip: NaN stays NaN
+    const float d = x - n.mh;
+    const float r = fmaf(d, n.sh, fmaf(d, n.sl, -n.mls));
+    return r < -clip ? -clip : (r > clip ? clip : r);
 }
 __device__ __forceinline__ double clip_d(double x, double lo, double hi) { return x < lo ? lo : (x > hi ? hi : x); }
 

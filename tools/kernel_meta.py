@@ -6,7 +6,8 @@ gfx950 library:
 
 Per kernel: VGPRs, AGPRs, SGPRs, VGPR / SGPR spill counts, scratch per lane
 (`.private_segment_fixed_size`), LDS (`.group_segment_fixed_size`), and with --digest a
-hash of the kernel's instructions with addresses and branch offsets stripped, so two
+hash of the kernel's instructions with addresses, branch offsets and PC-relative global
+offsets stripped, so two
 builds of the same source can be compared kernel by kernel (a refactor that must leave
 the default kernels' code unchanged).  The data come from `llvm-readelf --notes` of the
 code object unbundled from `.hip_fatbin` (AMDGPU metadata, msgpack rendered as YAML)."""
@@ -76,11 +77,12 @@ def digests(co):
     dis = subprocess.run([f"{LLVM}/llvm-objdump", "-d", "--no-show-raw-insn", co], check=True,
                          capture_output=True, text=True).stdout.split("\n")
     res, name, h, n = {}, None, None, 0
+    recent = []   # the last two opcodes: PC-relative offsets follow s_getpc_b64
     for l in dis:
         if l.endswith(">:"):
             if name:
                 res[name] = (h.hexdigest()[:16], n)
-            name, h, n = l.split("<")[1].rstrip(">:"), hashlib.sha256(), 0
+            name, h, n, recent = l.split("<")[1].rstrip(">:"), hashlib.sha256(), 0, []
             continue
         if name is None:
             continue
@@ -90,6 +92,9 @@ def digests(co):
         ops = re.sub(r"<[^>]*>", "", m.group(2))
         if m.group(1).startswith("s_cbranch") or m.group(1) == "s_branch":
             ops = ""
+        if m.group(1) in ("s_add_u32", "s_addc_u32") and "s_getpc_b64" in recent:
+            ops = re.sub(r"0x[0-9a-f]+", "REL", ops)   # a global's offset: moves with the layout
+        recent = (recent + [m.group(1)])[-2:]
         h.update((m.group(1) + " " + ops + "\n").encode())
         n += 1
     if name:
