@@ -1,9 +1,12 @@
 #!/bin/bash
 # Round measurements.  Phase "tests": the whole -m gpu suite + smoke().  Phase "bench":
 # the headline bench line (PMC traffic + CPU baseline + step API), the same command under
-# rocprofv3 --kernel-trace --stats (and config 6's), configs 3-6, and the 2-rank rehearsal of the --gpus N
-# launcher (gloo collectives, both ranks on this box's one GPU).
-#   gpurun --timeout 1200 -- bash tools/gpu/round.sh <tag> tests|bench
+# rocprofv3 --kernel-trace --stats (and config 6's), configs 3-6 (config 3 with its Gym-API
+# step line), and the 2-rank rehearsal of the --gpus N launcher (gloo collectives, both ranks
+# on this box's one GPU).  Phase "extra": VecNormalize / analytics device times
+# (tools/aux_time.py) and their rocprof summary, the rBergomi bench line under rocprof and
+# its VALU pass.
+#   gpurun --timeout 1200 -- bash tools/gpu/round.sh <tag> tests|bench|extra
 set -o pipefail
 TAG=${1:-round}; PHASE=${2:-bench}
 R=$GRAFT_REPO_ROOT; cd $R; O=$R/gpurun_out/$TAG; mkdir -p $O; export TMPDIR=/tmp
@@ -15,6 +18,26 @@ if [ "$PHASE" = tests ]; then
   echo "[$(date +%T)] smoke"
   timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
   tail -3 $O/smoke.log
+  exit 0
+fi
+if [ "$PHASE" = extra ]; then
+  echo "[$(date +%T)] aux_time"
+  timeout -k 10 300 python -u tools/aux_time.py > $O/aux_time.log 2>&1 || { tail -20 $O/aux_time.log; exit 1; }
+  grep -v amdgpu.ids $O/aux_time.log
+  echo "[$(date +%T)] aux_time under rocprofv3 --kernel-trace --stats"
+  cd /tmp
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_aux -o aux -- python3 $R/tools/aux_time.py > $O/aux_prof.log 2>&1 || { tail -20 $O/aux_prof.log; exit 1; }
+  cd $R
+  python3 tools/kstats.py $O/prof_aux | head -12
+  echo "[$(date +%T)] rbergomi bench under rocprofv3 --kernel-trace --stats"
+  cd /tmp
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/rbprof -o run -- python3 $R/bench.py --workload rbergomi --steps 3 --warmup 1 > $O/rb_rocprof.log 2>&1 || { tail -20 $O/rb_rocprof.log; exit 1; }
+  cd $R
+  grep "^{" $O/rb_rocprof.log > $O/rb_bench.jsonl
+  python3 tools/kstats.py $O/rbprof | head -6
+  echo "[$(date +%T)] rbergomi VALU pass"
+  bash tools/gpu/rb_pmc.sh $TAG/rbpmc || exit 1
+  echo "[$(date +%T)] done"
   exit 0
 fi
 echo "[$(date +%T)] bench (default: PMC + CPU baseline + step API)"
@@ -35,7 +58,8 @@ for c in 3 4 5 6; do
   echo "[$(date +%T)] bench config $c"
   # configs 4, 5 (book / Heston: producer-bound) and 6 (replay) with the PMC passes: traffic + VALU issue
   pmc=--no-pmc; [ $c != 3 ] && pmc=""
-  timeout -k 10 400 python -u bench.py --config $c $pmc --no-cpu-baseline --no-step-api > $O/b_cfg$c.log 2>&1 || { tail -20 $O/b_cfg$c.log; exit 1; }
+  sapi=--no-step-api; [ $c = 3 ] && sapi=""   # config 3: the Gym-API he_step line at 1M envs
+  timeout -k 10 400 python -u bench.py --config $c $pmc $sapi --no-cpu-baseline > $O/b_cfg$c.log 2>&1 || { tail -20 $O/b_cfg$c.log; exit 1; }
   grep "^{" $O/b_cfg$c.log >> $O/bench_cfg345.jsonl
 done
 echo "[$(date +%T)] --gpus 2 rehearsal (gloo, one GPU)"
