@@ -116,7 +116,7 @@ class HeInfo(ctypes.Structure):
 
 EXPORTS = [
     "he_config_init", "he_create", "he_destroy", "he_last_error", "he_version", "he_load_paths",
-    "he_seed", "he_reset", "he_step", "he_rollout", "he_num_envs", "he_episode_length",
+    "he_seed", "he_reset", "he_reset_episodes", "he_step", "he_rollout", "he_num_envs", "he_episode_length",
     "he_num_episodes", "he_get_config", "he_state_size", "he_get_state", "he_set_state",
     "he_pcg64_seed_state", "he_host_episode_draws", "he_host_philox", "he_host_div_by", "he_host_div_byf", "he_time_next_step", "he_rollout_policy", "he_host_box_muller",
     "he_sync_market", "he_vecnorm_stats_len", "he_vecnorm_scratch_bytes", "he_vecnorm_init", "he_vecnorm_step",
@@ -176,6 +176,7 @@ def load(path=LIB_PATH):
         "he_load_paths": (i32, [vp, vp, vp, vp, vp, i64, i64]),
         "he_seed": (i32, [vp, vp, vp, i64]),
         "he_reset": (i32, [vp, vp, i64, vp, ctypes.POINTER(HeInfo), vp]),
+        "he_reset_episodes": (i32, [vp, vp, vp, i64, vp, ctypes.POINTER(HeInfo), vp]),
         "he_step": (i32, [vp, vp, vp, vp, vp, vp, vp, ctypes.POINTER(HeInfo), vp]),
         "he_rollout": (i32, [vp, i32, vp, vp, vp, vp, vp]),
         "he_rollout_policy": (i32, [vp, i32, i32, vp, vp, vp, vp, vp, i64, vp, vp]),

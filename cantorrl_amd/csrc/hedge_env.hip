@@ -1240,6 +1240,13 @@ __device__ __forceinline__ void flush_obs_wave(const float* wtile, float* out, i
     asm volatile("" ::: "memory");
 }
 
+// The episode's S0 of row e.path (hedging_env_v2.py:156-157: < 1e-6 -> 1.0).
+__device__ __forceinline__ void replay_start(const Params& p, Env& e) {
+    float S0 = p.rec[(int64_t)e.path * (p.T + 1)].x;
+    e.s0_small = S0 < 1e-6f;
+    e.s0 = e.s0_small ? 1.0f : S0;
+}
+
 // replay reset (hedging_env_v2.py:145-173): draw the episode row from the env's
 // PCG64 stream, exactly gymnasium's np_random.integers(num_episodes).
 __device__ __forceinline__ void replay_reset(const Params& p, const State& s, int64_t i, Env& e) {
@@ -1256,9 +1263,7 @@ __device__ __forceinline__ void replay_reset(const Params& p, const State& s, in
     s.pcg[N + i] = g.sl;
     s.pcgb[i] = g.has32;
     s.pcgb[N + i] = g.buf32;
-    float S0 = p.rec[(int64_t)e.path * (p.T + 1)].x;
-    e.s0_small = S0 < 1e-6f;
-    e.s0 = e.s0_small ? 1.0f : S0;
+    replay_start(p, e);
 }
 
 __device__ __forceinline__ void env_reset_common(const Params& p, Env& e) {
@@ -3203,10 +3208,12 @@ static BSConst default_bs() {
 }
 
 // Explicit reset of envs `ids` (NULL: all).  Generate: the market position of a
-// reset env moves to the start of its next episode.
+// reset env moves to the start of its next episode.  Replay: the episode row is the env's
+// PCG64 draw, or eps[j] when given (he_reset_episodes: host-drawn indices, the env's own
+// stream not advanced).
 template <int MODE>
 __global__ __launch_bounds__(kBlock) void reset_kernel(Params p, State s, Market cur, const int64_t* ids,
-                                                       int64_t count, float* obs, he_info inf) {
+                                                       int64_t count, float* obs, he_info inf, const int64_t* eps) {
     const int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (j >= count) return;
     const int64_t i = ids ? ids[j] : j;
@@ -3216,7 +3223,12 @@ __global__ __launch_bounds__(kBlock) void reset_kernel(Params p, State s, Market
     float o[kObs];
     Mkt m;
     if (MODE == HE_MODE_REPLAY) {
-        replay_reset(p, s, i, e);
+        if (eps) {
+            e.path = (int32_t)eps[j];   // validated on the host: 0 <= eps[j] < n_paths
+            replay_start(p, e);
+        } else {
+            replay_reset(p, s, i, e);
+        }
         int64_t r = (int64_t)e.path * (p.T + 1);
         m = as_mkt(p.rec[r]);
         make_obs(p, e, m, p.recg[r], m.S, m.v, o);
@@ -3361,6 +3373,7 @@ struct he_env {
     he_vecnorm_params vne_p{};
     BookOpt* dbook = nullptr;   // liability book, device copy (generate modes)
     double* dbook_tab = nullptr;  // book tau table (book_option)
+    int64_t* d_eps = nullptr;     // he_reset_episodes: the host-drawn episode rows, staged
     int32_t book_rows = 0;        // its rows: max expiry + 1
     unsigned long long* scratch_count = nullptr;  // he_rollout_policy without records
     double book_rst = 0.0;      // book value of the reset market (host copy)
@@ -3641,10 +3654,10 @@ static he_status materialize_market(he_env* env, hipStream_t st) {
 
 template <int MODE>
 static void launch_reset(he_env* env, const int64_t* ids, int64_t count, float* obs, const he_info& inf,
-                         hipStream_t st) {
+                         hipStream_t st, const int64_t* eps = nullptr) {
     int64_t blocks = (count + kBlock - 1) / kBlock;
     hipLaunchKernelGGL(reset_kernel<MODE>, dim3((unsigned)blocks), dim3(kBlock), 0, st, env->p, env->s,
-                       env->cur, ids, count, obs, inf);
+                       env->cur, ids, count, obs, inf, eps);
 }
 
 template <int MODE, bool BOOK, bool FAST, bool GS>
@@ -4157,6 +4170,7 @@ he_status he_destroy(he_env* env) {
         if (env->dparams) (void)hipFree(env->dparams);
         if (env->dbook) (void)hipFree(env->dbook);
         if (env->dbook_tab) (void)hipFree(env->dbook_tab);
+        if (env->d_eps) (void)hipFree(env->d_eps);
         if (env->scratch_count) (void)hipFree(env->scratch_count);
         if (env->xs) {
             (void)hipStreamSynchronize(env->xs);
@@ -4395,6 +4409,35 @@ he_status he_reset(he_env* env, const int64_t* env_ids, int64_t count, float* ob
         if (c.mode == HE_MODE_GBM) launch_reset<HE_MODE_GBM>(env, env_ids, count, obs_out, inf, st);
         else launch_reset<HE_MODE_HESTON>(env, env_ids, count, obs_out, inf, st);
     }
+    HE_HIP(env, hipGetLastError());
+    env->ready = true;
+    return HE_OK;
+}
+
+he_status he_reset_episodes(he_env* env, const int64_t* env_ids, const int64_t* episode_idx, int64_t count,
+                            float* obs_out, const he_info* info, void* stream) {
+    if (!env) return HE_EINVAL;
+    const he_config& c = env->cfg;
+    if (c.mode != HE_MODE_REPLAY) return fail(env, HE_EINVAL, "he_reset_episodes: replay mode only");
+    if (!env->rec) return fail(env, HE_ESTATE, "no paths loaded (he_load_paths)");
+    if (!episode_idx) return fail(env, HE_EINVAL, "episode_idx is NULL");
+    if (count < 0 || count > c.n_envs) return fail(env, HE_EINVAL, "count %lld not in [0, n_envs]", (long long)count);
+    if (!env->ready && count != c.n_envs) return fail(env, HE_ESTATE, "the first reset must reset every env");
+    for (int64_t j = 0; j < count; ++j)
+        if (episode_idx[j] < 0 || episode_idx[j] >= env->p.n_paths)
+            return fail(env, HE_EINVAL, "episode_idx[%lld] = %lld not in [0, %lld)", (long long)j,
+                        (long long)episode_idx[j], (long long)env->p.n_paths);
+    if (count == 0) return HE_OK;
+    he_info inf;
+    if (info) inf = *info;
+    else memset(&inf, 0, sizeof(inf));
+    DeviceGuard dg(c.device);
+    hipStream_t st = (hipStream_t)stream;
+    if (!env->d_eps) HE_HIP(env, hipMalloc(&env->d_eps, (size_t)c.n_envs * sizeof(int64_t)));
+    // the staging buffer may still be read by the previous call's reset on this stream
+    HE_HIP(env, hipStreamSynchronize(st));
+    HE_HIP(env, hipMemcpy(env->d_eps, episode_idx, (size_t)count * sizeof(int64_t), hipMemcpyHostToDevice));
+    launch_reset<HE_MODE_REPLAY>(env, env_ids, count, obs_out, inf, st, env->d_eps);
     HE_HIP(env, hipGetLastError());
     env->ready = true;
     return HE_OK;

@@ -105,10 +105,14 @@ class HedgingEnv:
 
     # ------------------------------------------------------------------ gym API
     def reset(self, seed=None, options=None):
+        """hedging_env_v2.py:145-173.  options={"episode_idx": k} (replay mode, an extension:
+        the reference ignores options) starts episode row k instead of drawing it from
+        np_random -- he_reset_episodes; the env's own stream is not advanced."""
         v = self._venv
         if seed is not None:
             v.seed_envs([int(seed)])
-        obs = v.reset_tensors()
+        ep = (options or {}).get("episode_idx")
+        obs = v.reset_tensors() if ep is None else v.reset_tensors(episode_idx=[int(ep)])
         o = obs.cpu().numpy()[0].copy()
         h, s0 = self._pull()
         small = bool(s0 == np.float32(1.0) and self.current_stock_price < np.float32(1e-6))

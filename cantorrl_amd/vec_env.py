@@ -293,12 +293,32 @@ class HedgingVecEnv:
         n = self.num_envs
         return {k: flat[o:o + n * torch.empty((), dtype=dt).element_size()].view(dt) for k, dt, o in self._info_offs}
 
-    def reset_tensors(self, env_ids=None):
+    def reset_tensors(self, env_ids=None, episode_idx=None):
+        """Reset every env (or `env_ids`) and return the obs tensor.  episode_idx (replay mode):
+        the episode row of each reset env, drawn by the caller (he_reset_episodes) instead of
+        by the env's own PCG64 stream -- one per env in env_ids order (all envs when env_ids
+        is None)."""
         self._retire_view()
         if self._pending_seeds is not None:
             self.seed_envs(self._pending_seeds)
             self._pending_seeds = None
         info = _lib.ctypes.byref(self._info) if self._info_t else None
+        if episode_idx is not None:
+            eps = np.ascontiguousarray(np.asarray(episode_idx, dtype=np.int64).reshape(-1))
+            ids = None
+            if env_ids is not None:
+                ids = torch.as_tensor(env_ids, dtype=torch.int64, device=self.device).reshape(-1)
+                if ids.numel() != eps.size:
+                    raise ValueError(f"{eps.size} episode indices for {ids.numel()} envs")
+            elif eps.size != self.num_envs:
+                raise ValueError(f"{eps.size} episode indices for {self.num_envs} envs")
+            st = self.lib.he_reset_episodes(self._h, None if ids is None else ids.data_ptr(),
+                                            eps.ctypes.data, eps.size, self._obs.data_ptr(), info, self.stream)
+            _lib.check(self.lib, self._h, st, "he_reset_episodes")
+            if env_ids is None:
+                self._ep_ret[:] = 0.0
+                self._ep_len[:] = 0
+            return self._obs
         if env_ids is None:
             st = self.lib.he_reset(self._h, None, self.num_envs, self._obs.data_ptr(), info, self.stream)
         else:

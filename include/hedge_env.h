@@ -215,6 +215,16 @@ he_status he_seed(he_env* env, const int64_t* env_ids, const uint64_t* seeds, in
 he_status he_reset(he_env* env, const int64_t* env_ids, int64_t count, float* obs_out,
                    const he_info* info, void* stream);
 
+/* Replay mode: reset envs to given episode rows -- SURVEY 8(b)'s he_reset(episode_idx):
+ * hedging_env_v2.py:145-173 with current_episode_idx taken from the caller instead of the
+ * env's np_random.integers(num_episodes), so host-drawn PCG64 indices reproduce the
+ * reference's episode choice (the env's own PCG64 stream is not advanced).  episode_idx:
+ * HOST int64[count], each in [0, n_paths) (HE_EINVAL otherwise, checked before anything
+ * runs); env_ids: DEVICE int64 list as he_reset (NULL = envs 0..count-1).  Synchronises
+ * `stream` before staging the indices (a reset-path call, not a step-path one). */
+he_status he_reset_episodes(he_env* env, const int64_t* env_ids, const int64_t* episode_idx, int64_t count,
+                            float* obs_out, const he_info* info, void* stream);
+
 /* One step of every env.  actions [N][2] f32 in, obs [N][13] f32 out (the reset
  * obs for envs that terminated when autoreset=1), reward [N] f32 (f64 reward cast
  * as SB3 stores it), terminated/truncated [N] u8.  terminal_obs [N][13] receives

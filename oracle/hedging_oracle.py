@@ -422,13 +422,20 @@ class OracleVecEnv:
             if s is not None:
                 self.rngs[i] = np.random.Generator(np.random.PCG64(np.random.SeedSequence(int(s))))
 
-    def reset(self, env_ids=None, seeds=None):
+    def reset(self, env_ids=None, seeds=None, episode_idx=None):
+        """episode_idx (replay): the rows of the reset envs (in env_ids order) given instead
+        of drawn -- hedging_env_v2.py:150 with current_episode_idx supplied (he_reset_episodes);
+        the envs' generators are not advanced."""
         ids = np.arange(self.n) if env_ids is None else np.asarray(env_ids)
         if seeds is not None:
             self.seed_envs_at(ids, seeds)
         mask = np.zeros(self.n, bool)
         mask[ids] = True
-        self._reset_mask(mask)
+        given = None
+        if episode_idx is not None:
+            given = np.full(self.n, -1, np.int64)
+            given[ids] = np.asarray(episode_idx, np.int64)
+        self._reset_mask(mask, given)
         obs = self._obs()
         self.last_obs = obs.copy()
         self.ep_sums = np.zeros((self.n, 6))
@@ -461,10 +468,13 @@ class OracleVecEnv:
             self.g_seed = int(seeds[0])
             self.g_ep[:] = -1
 
-    def _reset_mask(self, mask):
+    def _reset_mask(self, mask, given=None):
         ids = np.nonzero(mask)[0]
         if self.mode == "replay":
             for i in ids:
+                if given is not None:
+                    self.idx[i] = given[i]
+                    continue
                 if self.rngs[i] is None:
                     self.rngs[i] = np.random.Generator(np.random.PCG64(np.random.SeedSequence()))
                 self.idx[i] = self.rngs[i].integers(self.num_episodes)

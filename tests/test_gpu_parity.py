@@ -1222,3 +1222,71 @@ def test_random_replay_configs_paths_agree_and_match_oracle(seed, monkeypatch):
                     rtol=1e-6 if kw["loss_type"] == "mse" else 0.0)
         compare_obs(obs.cpu().numpy(), oo, f"obs[{s}]", gk_atol=greeks_log_allowance(orc.S, orc.v))
     venv.close()
+
+
+def test_reset_episodes_match_oracle():
+    """he_reset_episodes (SURVEY 8(b)'s he_reset(episode_idx)): envs reset to host-drawn
+    episode rows -- all envs, then a partial reset of some of them -- against the oracle given
+    the same rows (hedging_env_v2.py:150 with current_episode_idx supplied): obs, rewards,
+    done flags and current_episode_idx, over steps that cross the autoreset (whose rows come
+    from the envs' own PCG64 streams again, not advanced by the explicit resets); the edge rows
+    (S0 < 25, S0 = 0, NaN marks, v <= 0, S0 = inf) chosen explicitly; out-of-range rows and
+    non-replay handles refused."""
+    from cantorrl_amd import _lib
+    from cantorrl_amd.vec_env import HedgingVecEnv
+    n, paths, T, seed = 200, 12, 9, 5
+    S, v, C, P = _edge_tables(paths, T + 1)
+    kw = dict(slippage_bps=5.0)
+    venv = HedgingVecEnv(n, tables=(S, v, C, P), seed=seed, info_keys=("current_episode_idx",),
+                         return_numpy=False, **kw)
+    orc = OracleVecEnv(n, mode="replay", data=(S, v, C, P), **kw)
+    orc.seed_envs([seed + i for i in range(n)])
+    rows = np.arange(n, dtype=np.int64) % paths          # every edge row, many times
+    compare_obs(venv.reset_tensors(episode_idx=rows).cpu().numpy(), orc.reset(episode_idx=rows), "reset_obs")
+    g = np.random.default_rng(4)
+    for s in range(2 * T + 3):
+        if s == 4:   # a partial reset to other rows mid-episode
+            ids = np.arange(3, n, 7)
+            r2 = (ids * 5 + 1) % paths
+            venv.reset_tensors(env_ids=ids, episode_idx=r2)
+            o_part = orc.reset(env_ids=ids, episode_idx=r2)
+            compare_obs(venv._obs.cpu().numpy()[ids], o_part, "partial_reset_obs")
+        a = (g.random((n, 2), dtype=np.float32) * 2.2 - 1.1).astype(np.float32)
+        obs, rew, term, _ = venv.step_tensors(torch.from_numpy(a).cuda())
+        torch.cuda.synchronize()
+        oo, orew, oterm, _, _ = orc.step(a)
+        assert_same(term.cpu().numpy().astype(bool), oterm, f"terminated[{s}]")
+        assert_same(rew.cpu().numpy(), orew.astype(np.float32), f"reward[{s}]")
+        compare_obs(obs.cpu().numpy(), oo, f"obs[{s}]")
+        live = ~oterm   # the info is the pre-reset view; the oracle's idx is after the autoreset
+        np.testing.assert_array_equal(venv.info_tensor("current_episode_idx").cpu().numpy()[live], orc.idx[live])
+    h = venv._h
+    bad = np.array([paths], dtype=np.int64)
+    ids = torch.zeros(1, dtype=torch.int64, device="cuda")
+    st = venv.lib.he_reset_episodes(h, ids.data_ptr(), bad.ctypes.data, 1, None, None, None)
+    assert st == _lib.HE_EINVAL and b"episode_idx" in venv.lib.he_last_error(h)
+    venv.close()
+    genv = HedgingVecEnv(64, mode="gbm", generate=dict(episode_length=8), seed=1, info_keys=(), return_numpy=False)
+    with pytest.raises(Exception, match="replay mode only"):
+        genv.reset_tensors(episode_idx=np.zeros(64, np.int64))
+    genv.close()
+
+
+def test_episode_summaries_alignment_and_layout():
+    """he_episode_summaries writes one 16-B row per env from the [4][N] running record (a
+    transpose kernel): rows equal the per-field view after a rollout; an output pointer that
+    is not 16-byte aligned is refused (HE_EINVAL) instead of faulting."""
+    from cantorrl_amd import _lib
+    from cantorrl_amd.vec_env import HedgingVecEnv
+    n = 1000
+    env = HedgingVecEnv(n, mode="gbm", generate=dict(episode_length=10), seed=3, info_keys=(), return_numpy=False)
+    env.reset_tensors()
+    g = torch.Generator(device="cuda")
+    g.manual_seed(1)
+    env.rollout(torch.rand((25, n, 2), device="cuda", generator=g) * 2 - 1)
+    summ = env.episode_summaries().cpu().numpy()
+    assert (summ[:, 3] == 10).all() and np.isfinite(summ).all()
+    buf = torch.zeros(4 * n + 1, dtype=torch.float32, device="cuda")
+    st = env.lib.he_episode_summaries(env._h, buf.data_ptr() + 4, env.stream)
+    assert st == _lib.HE_EINVAL and b"aligned" in env.lib.he_last_error(env._h)
+    env.close()
