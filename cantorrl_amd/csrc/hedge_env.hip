@@ -2294,6 +2294,12 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
     }
 }
 
+// s_setprio takes an immediate: kPrioProd + 1 when `up`, kPrioProd otherwise (a wave-uniform branch)
+__device__ __forceinline__ void prod_prio_toggle(bool up) {
+    if (up) __builtin_amdgcn_s_setprio(kPrioProd + 1);
+    else __builtin_amdgcn_s_setprio(kPrioProd);
+}
+
 // Producer waves: block bp of 64 envs into LDS buffer bp & 1 while the steppers consume
 // block bp - 1.  pw = producer wave index (kLdsPEnvs envs each).  Lanes past the last
 // env mirror env N-1 like the steppers' (identical values, identical addresses).
@@ -2589,6 +2595,12 @@ __device__ __forceinline__ void lds_producer(const Params& p, int k_steps, const
                 uint32_t tb = tpf;
 #pragma unroll 1
                 for (int h = 0; h < kLdsH; ++h) {
+                    // the two producer roles share each SIMD (one wave of each, from different
+                    // workgroups): which one wins the issue ties alternates slot by slot.  At one
+                    // fixed priority the same role lost them all block long (role timing: prod0
+                    // busy 6,981 / prod1 7,808 cycles per step, config 4): same box, config 4
+                    // 7.25 -> 7.08 ms, config 5 1.71 -> 1.62 ms per launch (r04s5_ab_prod_prio.txt)
+                    prod_prio_toggle((h + pw) & 1);
                     if (FULL || sl0 + h < len)
                         W.bk[wb][sl0 + h][le] = book_value<!HESTON>(p, bS[0], bV[0], (int32_t)(tb + 1), bM[0],
                                                                     &W.btab[0][0], &W.bopt[0]);
