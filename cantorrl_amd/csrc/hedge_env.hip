@@ -682,7 +682,16 @@ __device__ __forceinline__ double book_option(const Params& p, const BookOpt& o,
             const double y1 = lhs * isst + ls;
             const double ert = e[3];                             // e^{r tau}
             const double sh = exp_book_g(-lhs);                  // S / H
-            const double hs = exp_book_g(lhs);                   // H / S
+            // H / S as 1 / (S / H): v_rcp_f64 and two Newton steps (1 ulp) instead of a second
+            // exp_book; past |lhs| = 700 (S at 0 or inf) the library exp, as exp_book_g
+            double hs;
+            if (fabs(lhs) < 700.0) {
+                double y = __builtin_amdgcn_rcp(sh);
+                y = fma(fma(-sh, y, 1.0), y, y);
+                hs = fma(fma(-sh, y, 1.0), y, y);
+            } else {
+                hs = exp(lhs);
+            }
             const double p2l = exp_book_g((2.0 * b.lam) * lhs);  // (H/S)^(2 lam)
             const double p2l2 = p2l * (sh * sh);                 // (H/S)^(2 lam - 2)
             // the three tail pairs one after another (scheduling fences): interleaved, their
@@ -740,9 +749,15 @@ __device__ __forceinline__ double book_value(const Params& p, double S, double v
         b.lam = p.bk_lam;
     } else {
         b.sig = sqrt(var < 0.0 ? 0.0 : var);
-        b.isig = 1.0 / b.sig;
+        // 1 / sigma by v_rcp_f64 and two Newton steps, lam = r / sigma^2 + 1/2 from it: no IEEE
+        // division per slot (config 5 1.62 -> 1.58 ms with hs below, r04s7_ab_book_rcp.txt).  At
+        // sigma = 0 both are NaN instead of inf: only the intrinsic-value branch is live there.
+        double y = __builtin_amdgcn_rcp(b.sig);
+        y = fma(fma(-b.sig, y, 1.0), y, y);
+        y = fma(fma(-b.sig, y, 1.0), y, y);
+        b.isig = y;
         b.s2 = b.sig * b.sig;
-        b.lam = (p.r_d + 0.5 * b.s2) / b.s2;
+        b.lam = fma(p.r_d, y * y, 0.5);
     }
     double B = 0.0;
 #if HE_BOOK_DIAG == 2
