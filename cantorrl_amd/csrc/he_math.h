@@ -42,6 +42,46 @@ HE_HD double fma_kb(double a, double k, double c) {
 #endif
 }
 
+// log(x) for the liability book's log S (hedge_env.hip book_value; its bar is 1e-5 on P&L, not
+// bits): box_muller's reduction and atanh series (x = m 2^e, m in [sqrt2/2, sqrt2), s = (m - 1) /
+// (m + 1), series to s^19) with s by v_rcp_f64 and two Newton steps instead of an IEEE division;
+// within 2 ulp of the library log on positive finite x.  0, inf and NaN take the library's
+// values by selects (the reduction runs on 1.0 there), so the caller stays branch-free.
+HE_HD double log_book(double x) {
+    const bool ok = x > 0.0 && x < __builtin_inf();   // frexp takes the denormals too
+    const double xs = ok ? x : 1.0;
+    int e;
+    double m = frexp(xs, &e);
+    const bool lo = m < 0.70710678118654752;
+    m = lo ? m + m : m;
+    e = lo ? e - 1 : e;
+    const double den = m + 1.0;
+#if defined(__HIP_DEVICE_COMPILE__)
+    double y = __builtin_amdgcn_rcp(den);
+#else
+    double y = 1.0 / den;
+#endif
+    y = fma(fma(-den, y, 1.0), y, y);
+    y = fma(fma(-den, y, 1.0), y, y);
+    const double s = (m - 1.0) * y;
+    const double s2 = s * s;
+    double p = 1.0 / 19.0;
+    p = fma_k(p, s2, 1.0 / 17.0);
+    p = fma_k(p, s2, 1.0 / 15.0);
+    p = fma_k(p, s2, 1.0 / 13.0);
+    p = fma_k(p, s2, 1.0 / 11.0);
+    p = fma_k(p, s2, 1.0 / 9.0);
+    p = fma_k(p, s2, 1.0 / 7.0);
+    p = fma_k(p, s2, 1.0 / 5.0);
+    p = fma_k(p, s2, 1.0 / 3.0);
+    const double lm = (2.0 * s) + (2.0 * s) * (s2 * p);
+    const double ed = (double)e;
+    const double r = fma(ed, 6.93147180369123816490e-01, fma(ed, 1.90821492927058770002e-10, lm));
+    // log of 0 / inf / NaN or negatives: -inf / inf / NaN
+    const double sp = (x == 0.0) ? -__builtin_inf() : (x > 0.0 ? __builtin_inf() : __builtin_nan(""));
+    return ok ? r : sp;
+}
+
 // exp(x), f64, for the price advance exp((r - v/2) dt + sqrt(v) dW) (rbergomi_sim.py:459-463):
 // x = k ln2 + r with k = rint(x / ln2), r by a two-constant Cody-Waite step (k ln2_hi exact
 // for |k| < 2^21), e^r = (1 + r) + r^2 q(r) with q the Taylor series of (e^r - 1 - r) / r^2
