@@ -569,17 +569,8 @@ struct BookEnv {
 constexpr double kMillsA = 1.2590673575129534, kMillsB = 11.295336787564768, kMillsC = 5.0;
 constexpr double kMillsMax = 37.4;                       // phi(37.4) ~ 1e-304: the tail is 0 past it
 constexpr double kInvSqrt2Pi = 0.39894228040143267794;
-__device__ __forceinline__ double mills(double a) {
-#if HE_BOOK_DIAG == 1
-    return a * 0.25;  // diagnostic builds only (tools/gpu): the book without its tails
-#endif
-    const double d = a + kMillsC;                        // in [3.5, 41]: no special cases
-    // v_rcp_f64 is within 4.7e-8 of 1 / d on [3.5, 43], one Newton step within 2.3e-15
-    // (tools/probe/rcp_f64.hip, profiles/r04s3_rcp_f64.txt): u = A - B y then carries
-    // ~5e-15 against the fit's 1.7e-12, so the second step (exact rounding) buys nothing
-    double y = __builtin_amdgcn_rcp(d);
-    y = fma(fma(-d, y, 1.0), y, y);
-    const double u = fma(-kMillsB, y, kMillsA);
+// the degree-16 polynomial of mills() in u
+__device__ __forceinline__ double mills_u(double u) {
     double r = 2.7428474899566849e-08;
     r = fma_k(r, u, 1.1082671662043668e-08);
     r = fma_k(r, u, -3.9869407228616424e-07);
@@ -598,6 +589,40 @@ __device__ __forceinline__ double mills(double a) {
     r = fma_k(r, u, -0.38520383404522951);
     r = fma_k(r, u, 0.23820001819943162);
     return r;
+}
+__device__ __forceinline__ double mills(double a) {
+#if HE_BOOK_DIAG == 1
+    return a * 0.25;  // diagnostic builds only (tools/gpu): the book without its tails
+#endif
+    const double d = a + kMillsC;                        // in [3.5, 41]: no special cases
+    // v_rcp_f64 is within 4.7e-8 of 1 / d on [3.5, 43], one Newton step within 2.3e-15
+    // (tools/probe/rcp_f64.hip, profiles/r04s3_rcp_f64.txt): u = A - B y then carries
+    // ~5e-15 against the fit's 1.7e-12, so the second step (exact rounding) buys nothing
+    double y = __builtin_amdgcn_rcp(d);
+    y = fma(fma(-d, y, 1.0), y, y);
+    return mills_u(fma(-kMillsB, y, kMillsA));
+}
+// mills() of an option's two tails with one reciprocal: 1 / (d1 d2) by v_rcp_f64 and one Newton
+// step, then 1 / d1 = d2 / (d1 d2) and 1 / d2 = d1 / (d1 d2) (within 3e-15; the f64 reciprocal
+// is a quarter-rate transcendental, two per option before): config 4 6.86 -> 6.82 ms, config 5
+// 1.532 -> 1.524 ms, 3 of 3 same-box pairs (r04s9_ab_mills2.txt)
+// SEQ: the two polynomials one after the other (the barrier formula's tail pairs: interleaved,
+// they spilled the Heston producers' registers)
+template <bool SEQ = false>
+__device__ __forceinline__ void mills2(double a1, double a2, double* r1, double* r2) {
+#if HE_BOOK_DIAG == 1
+    *r1 = mills(a1);
+    *r2 = mills(a2);
+#else
+    const double d1 = a1 + kMillsC, d2 = a2 + kMillsC;
+    const double P = d1 * d2;
+    double Y = __builtin_amdgcn_rcp(P);
+    Y = fma(fma(-P, Y, 1.0), Y, Y);
+    const double u2 = fma(-kMillsB, d1 * Y, kMillsA);
+    *r1 = mills_u(fma(-kMillsB, d2 * Y, kMillsA));
+    if (SEQ) __builtin_amdgcn_sched_barrier(0);
+    *r2 = mills_u(u2);
+#endif
 }
 
 // |d| clamped to the range of the fit, and its phi
@@ -661,7 +686,9 @@ __device__ __forceinline__ double book_option(const Params& p, const BookOpt& o,
     const double SoKd = S * (o.invK * e[3]);            // S / (K e^{-r tau}) = phi(d2) / phi(d1)
     const double a1 = tail_arg(d1), a2 = tail_arg(d2);
     const double ph1 = phi_of(a1);
-    const double q1 = ph1 * mills(a1), q2 = (ph1 * SoKd) * mills(a2);
+    double m1_, m2_;
+    mills2(a1, a2, &m1_, &m2_);
+    const double q1 = ph1 * m1_, q2 = (ph1 * SoKd) * m2_;
     double n1, m1, n2, m2;
     ncdf_from_tail(d1, q1, &n1, &m1);
     ncdf_from_tail(d2, q2, &n2, &m2);
@@ -702,7 +729,9 @@ __device__ __forceinline__ double book_option(const Params& p, const BookOpt& o,
             {
                 const double ax = tail_arg(x1), ax_ = tail_arg(x1 - sst);
                 const double px = phi_of(ax);
-                const double qx = px * mills(ax), qx_ = (px * (sh * ert)) * mills(ax_);
+                double r_, r__;
+                mills2<true>(ax, ax_, &r_, &r__);
+                const double qx = px * r_, qx_ = (px * (sh * ert)) * r__;
                 ncdf_from_tail(x1, qx, &nx, &mx);
                 ncdf_from_tail(x1 - sst, qx_, &nx_, &mx_);
             }
@@ -711,7 +740,9 @@ __device__ __forceinline__ double book_option(const Params& p, const BookOpt& o,
             {
                 const double ay = tail_arg(y), ay_ = tail_arg(y - sst);
                 const double py = phi_of(ay);
-                const double qy = py * mills(ay), qy_ = (py * ((hs * hs) * (S * o.invK) * ert)) * mills(ay_);
+                double r_, r__;
+                mills2<true>(ay, ay_, &r_, &r__);
+                const double qy = py * r_, qy_ = (py * ((hs * hs) * (S * o.invK) * ert)) * r__;
                 ncdf_from_tail(y, qy, &ny, &my);
                 ncdf_from_tail(y - sst, qy_, &ny_, &my_);
             }
@@ -719,7 +750,9 @@ __device__ __forceinline__ double book_option(const Params& p, const BookOpt& o,
             {
                 const double ay1 = tail_arg(y1), ay1_ = tail_arg(y1 - sst);
                 const double py1 = phi_of(ay1);
-                const double qy1 = py1 * mills(ay1), qy1_ = (py1 * (hs * ert)) * mills(ay1_);
+                double r_, r__;
+                mills2<true>(ay1, ay1_, &r_, &r__);
+                const double qy1 = py1 * r_, qy1_ = (py1 * (hs * ert)) * r__;
                 ncdf_from_tail(y1, qy1, &ny1, &my1);
                 ncdf_from_tail(y1 - sst, qy1_, &ny1_, &my1_);
             }
