@@ -555,13 +555,14 @@ struct BookEnv {
 };
 
 // The normal tail Q(a) = Phi(-a), a >= 0, as phi(a) R(a) with the Mills ratio
-// R(a) = sqrt(pi/2) erfcx(a / sqrt 2) a degree-16 polynomial in u = A - B / (a + c), c = 5:
+// R(a) = sqrt(pi/2) erfcx(a / sqrt 2) a degree-14 polynomial in u = A - B / (a + c), c = 5:
 // the Chebyshev fit on a in [0, 38.6] (Q underflows past it) re-expanded in powers of u
-// (coefficients below 0.39 in magnitude, so Horner loses nothing), 1.7e-12 relative on Q
+// (coefficients below 0.39 in magnitude, so Horner loses nothing), 5.2e-11 relative on Q
 // against scipy.special.ndtr (tools/mills_fit.py).  The producers of the book kernels are
-// bound by VALU issue, so the degree is what costs: degree 16 against the former 20 at
-// c = 3.5 (2.6e-13): config 4 8.77 -> 8.34 ms, config 5 2.04 -> 2.00 ms
-// per launch (r03s37), the book's P&L still far inside north_star's 1e-5.  Branch-free -- every lane of a wave
+// bound by VALU issue, so the degree is what costs: degree 16 (1.7e-12) against the former 20
+// at c = 3.5 (2.6e-13) took config 4 8.77 -> 8.34 ms (r03s37); degree 14 against 16 config 4
+// 6.85 -> 6.65 ms, config 5 1.53 -> 1.51 ms (r04t2_ab_mills_deg14.txt, book / full-size /
+// randomised parity green), the book's P&L still far inside north_star's 1e-5.  Branch-free -- every lane of a wave
 // runs the same instructions whatever its d -- and phi is the caller's: d1 and d2 of a
 // Black-Scholes price share one exp (S phi(d1) = K e^{-r tau} phi(d2)).  Replaces two
 // library erfc per pair, each with its own exp and range branches (the book is an
@@ -569,25 +570,23 @@ struct BookEnv {
 constexpr double kMillsA = 1.2590673575129534, kMillsB = 11.295336787564768, kMillsC = 5.0;
 constexpr double kMillsMax = 37.4;                       // phi(37.4) ~ 1e-304: the tail is 0 past it
 constexpr double kInvSqrt2Pi = 0.39894228040143267794;
-// the degree-16 polynomial of mills() in u
+// the degree-14 polynomial of mills() in u
 __device__ __forceinline__ double mills_u(double u) {
-    double r = 2.7428474899566849e-08;
-    r = fma_k(r, u, 1.1082671662043668e-08);
-    r = fma_k(r, u, -3.9869407228616424e-07);
-    r = fma_k(r, u, 5.0477032271454544e-08);
-    r = fma_k(r, u, 4.3841769522583659e-06);
-    r = fma_k(r, u, -5.963304400844242e-06);
-    r = fma_k(r, u, -4.1102680772883148e-05);
-    r = fma_k(r, u, 0.00016913403122505337);
-    r = fma_k(r, u, 4.3092976295952224e-05);
-    r = fma_k(r, u, -0.0026775922346088865);
-    r = fma_k(r, u, 0.013231527706031554);
-    r = fma_k(r, u, -0.041271314376590838);
-    r = fma_k(r, u, 0.097294627097245595);
-    r = fma_k(r, u, -0.18472286873481761);
-    r = fma_k(r, u, 0.29086958400118978);
-    r = fma_k(r, u, -0.38520383404522951);
-    r = fma_k(r, u, 0.23820001819943162);
+    double r = -2.8897932893921865e-07;
+    r = fma_k(r, u, 9.2037477055214229e-08);
+    r = fma_k(r, u, 4.205888988230914e-06);
+    r = fma_k(r, u, -6.0256457018679174e-06);
+    r = fma_k(r, u, -4.0951820297551139e-05);
+    r = fma_k(r, u, 0.00016918165349102241);
+    r = fma_k(r, u, 4.302225968256142e-05);
+    r = fma_k(r, u, -0.0026776117165782177);
+    r = fma_k(r, u, 0.013231545706850733);
+    r = fma_k(r, u, -0.041271310285367596);
+    r = fma_k(r, u, 0.097294624847109032);
+    r = fma_k(r, u, -0.18472286911363267);
+    r = fma_k(r, u, 0.29086958410834113);
+    r = fma_k(r, u, -0.38520383403508307);
+    r = fma_k(r, u, 0.2382000181985946);
     return r;
 }
 __device__ __forceinline__ double mills(double a) {
@@ -597,7 +596,7 @@ __device__ __forceinline__ double mills(double a) {
     const double d = a + kMillsC;                        // in [3.5, 41]: no special cases
     // v_rcp_f64 is within 4.7e-8 of 1 / d on [3.5, 43], one Newton step within 2.3e-15
     // (tools/probe/rcp_f64.hip, profiles/r04s3_rcp_f64.txt): u = A - B y then carries
-    // ~5e-15 against the fit's 1.7e-12, so the second step (exact rounding) buys nothing
+    // ~5e-15 against the fit's 5e-11, so the second step (exact rounding) buys nothing
     double y = __builtin_amdgcn_rcp(d);
     y = fma(fma(-d, y, 1.0), y, y);
     return mills_u(fma(-kMillsB, y, kMillsA));

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """The Mills-ratio polynomial of hedge_env.hip `mills()`: R(a) = Phi(-a) / phi(a) =
-sqrt(pi/2) erfcx(a / sqrt 2) on a in [0, 38.6] as a degree-16 polynomial in
+sqrt(pi/2) erfcx(a / sqrt 2) on a in [0, 38.6] as a degree-14 polynomial in
 u = A - B / (a + c), c = 5 (a Chebyshev least-squares fit at 4000 Chebyshev nodes in
 u, re-expanded in powers of u).  Prints A, B, the coefficients (highest degree first,
 for Horner) and the relative error of phi(a) R(a) against scipy.special.ndtr(-a),
@@ -14,7 +14,7 @@ def R(x):
     return np.sqrt(np.pi / 2) * erfcx(x / np.sqrt(2))
 
 
-def main(XM=38.6, c=5.0, deg=16):   # HE_MILLS_DEG16=0 builds: c=3.5, deg=20
+def main(XM=38.6, c=5.0, deg=14):   # round 3: deg=16 (1.7e-12); before it c=3.5, deg=20
     tm = (XM - c) / (XM + c)
     k = 2 / (tm + 1)
     n = 4000
