@@ -630,25 +630,25 @@ __device__ __forceinline__ double tail_arg(double d) {
     return a < kMillsMax ? a : kMillsMax;                // NaN -> kMillsMax (the price is NaN anyway)
 }
 // exp(x) for the book's phi, x = -a^2 / 2 in [-700, 0] (a <= kMillsMax): exp_k's Cody-Waite
-// reduction, then e^r as its degree-11 Taylor polynomial (truncation < 7e-15 relative on
-// |r| <= ln2 / 2; the book's bar is 1e-5 on P&L) without the Fast2Sum or the range branch:
-// 16 VALU instructions instead of exp_k's 26.
+// reduction, then e^r as a degree-9 near-minimax polynomial on |r| <= ln2 / 2 (1.7e-14
+// relative, a Lawson-weighted Chebyshev fit; the book's bar is 1e-5 on P&L) without the
+// Fast2Sum or the range branch.  Round 4 against the degree-11 Taylor form (7e-15): config 4
+// 6.65 -> 6.60 ms, config 5 1.503 -> 1.497 ms, 3 of 3 pairs (r04t3_ab_exp_minimax.txt; an A/B
+// of the same change on an earlier tree was mixed, r04s3_ab_exp_book_minimax.txt).
 __device__ __forceinline__ double exp_book(double x) {
     const double k = rint(x * 1.4426950408889634074);
     const double rh = fma_kb(-k, 6.93147180369123816490e-01, x);
     const double r = fma_kb(-k, 1.90821492927058770002e-10, rh);
-    double q = 1.0 / 39916800.0;                  // 1/11!
-    q = fma_k(q, r, 1.0 / 3628800.0);
-    q = fma_k(q, r, 1.0 / 362880.0);
-    q = fma_k(q, r, 1.0 / 40320.0);
-    q = fma_k(q, r, 1.0 / 5040.0);
-    q = fma_k(q, r, 1.0 / 720.0);
-    q = fma_k(q, r, 1.0 / 120.0);
-    q = fma_k(q, r, 1.0 / 24.0);
-    q = fma_k(q, r, 1.0 / 6.0);
-    q = fma_k(q, r, 0.5);
-    q = fma_k(q, r, 1.0);
-    q = fma_k(q, r, 1.0);
+    double q = 2.7474189376171111e-06;
+    q = fma_k(q, r, 2.4883220877841942e-05);
+    q = fma_k(q, r, 0.00019841609921119712);
+    q = fma_k(q, r, 0.0013888804743864306);
+    q = fma_k(q, r, 0.0083333330025783942);
+    q = fma_k(q, r, 0.041666667017783966);
+    q = fma_k(q, r, 0.16666666667764135);
+    q = fma_k(q, r, 0.49999999999494837);
+    q = fma_k(q, r, 0.99999999999990008);
+    q = fma_k(q, r, 1.0000000000000104);
     return ldexp(q, (int)k);
 }
 // exp_book with exp_k's range guard, for the barrier formula's (H/S) powers (any sign,
