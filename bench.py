@@ -196,6 +196,7 @@ def parse(argv=None):
                     help="steps per he_rollout call (default: 256, the n_steps rollout-buffer boundary of "
                          "train_ppo_v2.py:48, on the LDS path; 64 on the tile path)")
     ap.add_argument("--no-step-api", action="store_true", help="skip the secondary graph-mode he_step run")
+    ap.add_argument("--no-sb3-api", action="store_true", help="skip the host-API (SB3 VecEnv / single env) timing")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=6.0, help="seconds per CPU-baseline leg (4 legs)")
     ap.add_argument("--seed", type=int, default=42)
@@ -320,22 +321,89 @@ REFERENCE_CPU = dict(
                      "8 fork processes x 32 envs = 31,904 env-steps/s (SURVEY.md section 6, BASELINE.md:18-20)")
 
 
-def make_env(args, dev, rank=0, prefetch="auto"):
+def make_env(args, dev, rank=0, prefetch="auto", offset=None):
+    """The config's env handle of args.envs envs at global env ids offset .. (default rank's)."""
     from cantorrl_amd.vec_env import HedgingVecEnv
     cfg = CONFIGS[args.config]
+    off = rank * args.envs if offset is None else offset
     if cfg["mode"] == "replay":
         # env i of rank r draws its episodes from PCG64(SeedSequence(seed + r * envs + i)),
         # the reference's per-env reset(seed) streams (hedging_env_v2.py:146-150)
         env = HedgingVecEnv(args.envs, tables=replay_tables(**cfg["table"]), seed=args.seed,
-                            global_env_offset=rank * args.envs, device=dev, return_numpy=False, info_keys=(),
+                            global_env_offset=off, device=dev, return_numpy=False, info_keys=(),
                             **cfg["kw"])
         env.reset_tensors()
         return env
     env = HedgingVecEnv(args.envs, mode=cfg["mode"], generate=cfg["gen"], seed=args.seed,
-                        global_env_offset=rank * args.envs, device=dev, return_numpy=False, info_keys=(),
+                        global_env_offset=off, device=dev, return_numpy=False, info_keys=(),
                         market_prefetch=prefetch, **cfg["kw"])
     env.reset_tensors()
     return env
+
+
+def bench_actions(n, rank, dev):
+    """The pre-generated U(-1, 1) actions [256, n, 2] of rank `rank` (seed 1234 + rank)."""
+    g = torch.Generator(device=dev)
+    g.manual_seed(1234 + rank)
+    return torch.rand((256, n, 2), device=dev, generator=g) * 2 - 1
+
+
+# ---------------------------------------------------------------------- shard check
+# After the timed region each rank re-runs SHARD_CHECK_ENVS envs of its NEIGHBOUR's shard
+# (the last ones of rank (r + 1) % world) in a handle of their own, with the neighbour's
+# actions and the same launches, and compares the bits of their episode summaries with the
+# rows the all-gather delivered: the shards are a partition of one global env set whatever
+# the GPU count (Philox keyed by the global env id, SURVEY 8(e)), and the gather puts them
+# in global env order.  At one rank it checks the handle's own last envs.
+SHARD_CHECK_ENVS = 64
+
+
+def shard_check_slice(rank, world, n, m=SHARD_CHECK_ENVS):
+    """(neighbour rank, its first checked env, count): the last min(m, n) envs of (r + 1) % world."""
+    m = min(m, n)
+    return (rank + 1) % world, n - m, m
+
+
+def shard_check_verdict(dist, got, gathered, nb, j0, n, device="cpu"):
+    """Bits of `got` [m, 4] against rows nb * n + j0 .. of `gathered` [world * n, 4]; every rank's
+    result combined (MIN over ranks) -> the line's `shard_check`."""
+    m = int(got.shape[0])
+    ref = gathered[nb * n + j0: nb * n + j0 + m]
+    a = got.detach().cpu().contiguous().view(torch.int32)
+    b = ref.detach().cpu().contiguous().view(torch.int32)
+    same = a.shape == b.shape and bool(torch.equal(a, b))
+    bad_rows = 0 if same else int((a != b).any(dim=1).sum()) if a.shape == b.shape else m
+    ok = torch.tensor([1 if same else 0], dtype=torch.int64, device=device)
+    bad = torch.tensor([bad_rows], dtype=torch.int64, device=device)
+    if dist is not None:
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        dist.all_reduce(bad, op=dist.ReduceOp.SUM)
+    world = dist.get_world_size() if dist is not None else 1
+    all_ok = bool(int(ok.item()))
+    finished = int((ref[:, 3] > 0).sum().item()) if m else 0
+    return dict(result="bit-identical" if all_ok else "MISMATCH", envs_per_rank=m, ranks=world,
+                mismatched_rows=int(bad.item()), finished_episodes_in_checked_rows=finished,
+                what="each rank re-ran the last %d envs of rank (r + 1) %% world in a %d-env handle at their global "
+                     "env ids (the neighbour's actions, the same launches) and compared the bits of their "
+                     "he_episode_summaries with the all-gathered rows" % (m, m))
+
+
+def shard_check_run(args, dev, stream, runs, nb, j0, m):
+    """The checked envs' episode summaries [m, 4]: a handle of m envs at global ids nb * n + j0 ..,
+    driven by the same sequence of Runner.run() calls `runs` with rank nb's actions."""
+    import copy
+    a2 = copy.copy(args)
+    a2.envs = m
+    acts = bench_actions(args.envs, nb, dev)[:, j0:j0 + m].contiguous()
+    env = make_env(a2, dev, offset=nb * args.envs + j0)
+    r = Runner(a2, env, "rollout", acts, stream)
+    with torch.cuda.stream(stream):
+        for k in runs:
+            r.run(k)
+        out = env.episode_summaries()
+    torch.cuda.synchronize()
+    env.close()
+    return out
 
 
 class Runner:
@@ -360,6 +428,7 @@ class Runner:
             self.rt = torch.empty((RK, n), dtype=torch.uint8, device=dev)
         self.graphs = []
         self.replays = 0
+        self.runs = []
         if mode == "graph":
             with torch.cuda.stream(stream):
                 # one eager block first, so each captured graph is the steady state
@@ -396,6 +465,7 @@ class Runner:
 
     def run(self, steps):
         """Enqueue `steps` env-steps (a multiple of the chunk) on self.stream."""
+        self.runs.append(steps)   # the call sequence, replayed by the shard check
         done = 0
         cs = self.stream.cuda_stream
         while done < steps:
@@ -504,10 +574,11 @@ def probe(args):
 STEP_KERNELS = r"step1?_kernel|step_market_kernel|lds_rollout_kernel|lds_replay_kernel"
 
 
-def pmc_pass(args, counters, kernels=STEP_KERNELS):
+def pmc_pass(args, counters, kernels=STEP_KERNELS, probe_argv=None):
     """One rocprofv3 --pmc pass of `bench.py --probe` (a child process: this one has not
     touched the GPU) -> {kernel short name: {counter: mean per dispatch}} for the
-    kernels matching `kernels` (the first dispatches of each skipped: warm-up)."""
+    kernels matching `kernels` (the first dispatches of each skipped: warm-up).
+    `probe_argv`: the probe's own arguments (default: the env workload of `args`)."""
     import csv
     import glob
     import re
@@ -516,10 +587,12 @@ def pmc_pass(args, counters, kernels=STEP_KERNELS):
     import tempfile
     if shutil.which("rocprofv3") is None:
         return None, "rocprofv3 not found"
+    if probe_argv is None:
+        probe_argv = ["--envs", str(args.envs), "--config", str(args.config), "--mode", args.mode,
+                      "--rollout-k", str(args.rollout_k)]
     with tempfile.TemporaryDirectory(dir="/tmp") as td:
         cmd = ["rocprofv3", "--pmc", *counters, "--output-format", "csv", "-d", td, "-o", "pmc", "--",
-               sys.executable, os.path.abspath(__file__), "--probe", "--envs", str(args.envs),
-               "--config", str(args.config), "--mode", args.mode, "--rollout-k", str(args.rollout_k)]
+               sys.executable, os.path.abspath(__file__), "--probe", *probe_argv]
         try:
             subprocess.run(cmd, check=True, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
                            timeout=240, cwd="/tmp", env=dict(os.environ, TMPDIR="/tmp"))
@@ -568,6 +641,12 @@ def pmc_valu(args):
     res, err = pmc_pass(args, VALU_COUNTERS, STEP_KERNELS + "|market_kernel")
     if res is None:
         return None, err
+    return valu_summary(res), None
+
+
+def valu_summary(res):
+    """{kernel: {counter: mean per dispatch}} of a VALU_COUNTERS pass -> per kernel the issue
+    rate, its bound for the kernel's f64 share and the f64 FLOP per dispatch."""
     out = {}
     for k, d in res.items():
         if "SQ_INSTS_VALU" not in d or not d.get("GRBM_GUI_ACTIVE"):
@@ -583,7 +662,7 @@ def pmc_valu(args):
                       f64_flop=64.0 * (2.0 * d.get("SQ_INSTS_VALU_FMA_F64", 0.0) + d.get("SQ_INSTS_VALU_ADD_F64", 0.0)
                                        + d.get("SQ_INSTS_VALU_MUL_F64", 0.0)),
                       cycles_profiled=cycles)
-    return out, None
+    return out
 
 
 class HipEvents:
@@ -759,6 +838,30 @@ def roofline(mode, n, kern_ms, rk, book=False, market="gbm", lds=False):
                 kernel_gbs=round(own / (kern_ms * 1e-3) / 1e9, 1))
 
 
+def step_api_line(n, steps, wall, rf, pmc, layout):
+    """The Gym-API (graph-mode he_step) sub-line.  Two fractions of 8 TB/s, both from the same
+    kernel time: `frac` on the bytes step1_kernel itself must move (STEP_BYTES_PER_ENV[layout]:
+    122 B per env when it evaluates the obs greeks, 134 B when it reads them from the market
+    tile) and `frac_survey_8d` on SURVEY 8(d)'s 186 B per env-step (66 of step I/O + the 120-B
+    state model, larger than this kernel's 16-B state) -- only the first is the kernel's own
+    roofline.  `traffic` is the kernel's PMC HBM bytes per launch (2 FETCH_SIZE + WRITE_SIZE)."""
+    kb = rf["kernel_bytes_per_launch"]
+    kgbs = kb / (rf["kernel_us"] * 1e-6) / 1e9
+    out = dict(mode="graph (he_step, one launch per step)", value=round(n * steps / wall, 1),
+               ms_per_step=round(wall * 1e3 / steps, 6), kernel=rf["kernel"], kernel_us=rf["kernel_us"],
+               kernel_bytes_per_launch=int(kb), kernel_bytes_per_env=int(kb // n), kernel_bytes_layout=layout,
+               achieved_gbs=round(kgbs, 1), frac=round(kgbs / HBM_PEAK_GBS, 4),
+               bytes_per_launch=rf["bytes_per_launch"], achieved_gbs_survey_8d=rf["achieved"],
+               frac_survey_8d=rf["frac"], traffic=None)
+    if pmc[0] is not None:
+        out["traffic"] = int(pmc[0])
+        out["traffic_over_kernel_bytes"] = round(pmc[0] / kb, 4)
+        out["traffic_counters_kb"] = {k: round(v, 1) for k, v in pmc[1].items()}
+    else:
+        out["traffic_note"] = pmc[1]
+    return out
+
+
 def config_bound(cfg):
     """The resource that bounds a configuration's dominant kernel, fixed per config (not by
     whether the counters ran): with a liability book or Heston the producers' f64 market work
@@ -804,6 +907,110 @@ def finish_roofline(roof, cfg, valu, pmc, kern_ms):
                              (valu[1] if valu[1] else "absent"))
     return dict(bound="valu", unit="VALU wave-instructions per SIMD-cycle", traffic=roof.pop("traffic", None),
                 hbm=hbm, **head, **{k: x for k, x in roof.items() if k != "bound"})
+
+
+# ---------------------------------------------------------------------- the host (SB3 / gym) API
+# The reference's own single env stepped in a serial loop, measured in the build container
+# (SURVEY.md section 6 / BASELINE.md:18-20: 4,782 env-steps/s over 256 envs on one core,
+# ~209 us per HedgingEnv.step) -- what `baselines.py:45-51` and `delta_and_nothing.py:69-88`
+# drive today.
+REFERENCE_SINGLE_ENV_STEPS_S = 4782.0
+SB3_API_ENVS = (2, 256, 65536)   # N_ENVS = 2 (train_ppo_v2.py:45), BASELINE config 1, the headline
+
+
+def _host_loop_timing(fn, steps, warm):
+    for _ in range(warm):
+        fn()
+    ts = np.empty(steps)
+    t0 = time.perf_counter()
+    for i in range(steps):
+        a = time.perf_counter()
+        fn()
+        ts[i] = time.perf_counter() - a
+    wall = time.perf_counter() - t0
+    return wall, ts
+
+
+def sb3_api(dev, classes=None, envs=SB3_API_ENVS, steps=504):
+    """Wall time of the host paths the unchanged agents call:
+
+    * `HedgingVecEnv.step_async` + `step_wait` with NumPy actions and NumPy results -- SB3's
+      collect_rollouts (train_ppo_v2.py:127-141,204,230) -- at N = 2, 256 and 65,536, over
+      `steps` steps (two whole episodes, so the episode-end work is averaged in), Monitor on;
+      the same behind `DeviceVecNormalize` (train_ppo_v2.py:204) at N = 2 and 65,536;
+    * the single `HedgingEnv.step` in a baselines.py:45-51-shaped loop (reset, policy, step,
+      info.get(...) sums) over two episodes of policy_delta_every_step.
+
+    `classes` = (HedgingVecEnv, HedgingEnv, DeviceVecNormalize, MONITOR_KEYWORDS) of the package
+    to time (tools/sb3_time.py passes an older tree's for an A/B); default this tree's."""
+    if classes is None:
+        from cantorrl_amd.vec_env import HedgingVecEnv, MONITOR_KEYWORDS
+        from cantorrl_amd.env import HedgingEnv
+        from cantorrl_amd.vec_normalize import DeviceVecNormalize
+        classes = (HedgingVecEnv, HedgingEnv, DeviceVecNormalize, MONITOR_KEYWORDS)
+    VecEnv, Env, VecNorm, MON = classes
+    out = dict(what="wall time per call of the host APIs the reference's agents drive (NumPy in, NumPy out): "
+                    "step_async + step_wait per vector step, HedgingEnv.step per single-env step",
+               vec_env={}, vecnorm={})
+    rng = np.random.default_rng(7)
+    for n in envs:
+        acts = rng.uniform(-1, 1, size=(4, n, 2)).astype(np.float32)
+        for wrap in (False, True):
+            if wrap and n not in (envs[0], envs[-1]):
+                continue
+            env = VecEnv(n, mode="gbm", generate=GEN, seed=11, device=dev, monitor_keywords=MON, **TRAIN_KW)
+            e = VecNorm(env, gamma=0.99) if wrap else env
+            e.reset()
+            k = [0]
+
+            def one():
+                e.step_async(acts[k[0] & 3])
+                k[0] += 1
+                return e.step_wait()
+
+            wall, ts = _host_loop_timing(one, steps, 16)
+            e.close()
+            (out["vecnorm"] if wrap else out["vec_env"])[str(n)] = dict(
+                us_per_step=round(wall / steps * 1e6, 2), us_median=round(float(np.median(ts)) * 1e6, 2),
+                us_p99=round(float(np.percentile(ts, 99)) * 1e6, 2), env_steps_per_s=round(n * steps / wall, 1),
+                steps=steps)
+    env = Env(mode="gbm", generate=GEN, **TRAIN_KW)
+    pnl = [0.0]
+
+    def policy_delta_every_step(obs):
+        # baselines.py:77-103: trade the option whose delta is usable towards zero book delta
+        # (the caller's own per-step Python, the same work on either side of the swap)
+        cd, pd = obs[7], obs[9]
+        m = env.option_contract_multiplier
+        tot = env.shares_held_fixed + (obs[3] * env.max_contracts_held * cd + obs[4] * env.max_contracts_held * pd) * m
+        tc = tp = 0.0
+        if abs(cd * m) > 1e-1:
+            tc = -tot / (cd * m)
+        elif abs(pd * m) > 1e-1:
+            tp = -tot / (pd * m)
+        lim = env.max_trade_per_step
+        return np.array([np.clip(tc, -lim, lim), np.clip(tp, -lim, lim)], dtype=env.action_space.dtype)
+
+    n_ep, t_steps = 2, 0
+    t0 = time.perf_counter()
+    for ep in range(n_ep + 1):
+        if ep == 1:   # the first episode warms up
+            t0, t_steps = time.perf_counter(), 0
+        obs, _ = env.reset()
+        term = trunc = False
+        while not (term or trunc):
+            obs, r, term, trunc, info = env.step(policy_delta_every_step(obs))
+            pnl[0] += info.get("raw_pnl_deviation_abs", 0.0) + info.get("transaction_costs_total", 0.0)
+            t_steps += 1
+    wall = time.perf_counter() - t0
+    env.close()
+    out["single_env"] = dict(loop="baselines.py:32-56 evaluate_baseline_policy shape: reset, policy_delta_every_step, "
+                                  "step, info.get sums", episodes=n_ep, steps=t_steps,
+                             us_per_step=round(wall / t_steps * 1e6, 2), steps_per_s=round(t_steps / wall, 1),
+                             reference_cpu_steps_per_s=REFERENCE_SINGLE_ENV_STEPS_S,
+                             reference_note="the reference's hedging_env_v2.HedgingEnv.step on one core of the build "
+                                            "container (SURVEY.md section 6), not timed on the GPU box")
+    return out
 
 
 # ---------------------------------------------------------------------- rbergomi workload
@@ -854,6 +1061,33 @@ def rb_cpu_baseline(seconds, base):
                 single_core_sample=f"{n1} options in {el1:.1f} s, 1 thread")
 
 
+def rb_roofline(valu, traffic, kern_ms, n_opt):
+    """mc_kernel's roofline: VALU issue.  `achieved` = VALU wave-instructions per SIMD-cycle
+    (SQ_INSTS_VALU over GRBM_GUI_ACTIVE / 8 cycles x 1,024 SIMDs), `peak` = the issue bound of
+    the kernel's own f64 / other mix (a wave64 instruction every 2 cycles per SIMD, f64 every 4),
+    plus its f64 FLOP rate against the 78.6 TF vector peak; `traffic` = HBM bytes per launch
+    from the PMC pass (about 7 f64 per option -- the path's parameters, S and v in, the mark
+    out: negligible against the 5,000 x 30 Euler steps behind each mark)."""
+    v, note = valu
+    out = dict(bound="valu", unit="VALU wave-instructions per SIMD-cycle", achieved=None, peak=None, frac=None,
+               traffic=None, kernel="mc_kernel (rb_price_atm_marks)", kernel_us=round(kern_ms * 1e3, 1),
+               algorithmic_bytes_per_launch=int(n_opt * 7 * 8))
+    if v is not None:
+        out.update(achieved=v["issue_per_simd_cycle"], peak=v["issue_bound_per_simd_cycle"], frac=v["valu_issue_frac"],
+                   f64_share=v["f64_share"], valu_insts=v["valu_insts"])
+        tf = v["f64_flop"] / (kern_ms * 1e-3) / 1e12
+        out.update(f64_tflops=round(tf, 3), f64_frac_of_vector_peak=round(tf / FP64_VECTOR_PEAK_TFLOPS, 4),
+                   peak_f64_tflops=FP64_VECTOR_PEAK_TFLOPS)
+    else:
+        out["valu_note"] = note
+    if traffic[0] is not None:
+        out["traffic"] = int(traffic[0])
+        out["traffic_counters_kb"] = {k: round(x, 1) for k, x in traffic[1].items()}
+    else:
+        out["traffic_note"] = traffic[1]
+    return out
+
+
 def rbergomi_main(args):
     """One step = one rb_price_atm_marks launch: rolling-ATM call and put marks for
     every (path, day) of args.rb_paths paths x 252 days, 5000 MC paths x 30 Euler
@@ -865,7 +1099,22 @@ def rbergomi_main(args):
     hist = np.load(os.path.join(REPO, "tests", "golden", "rb_estimate.npz"))["hist__prices"]
     base = rb.estimate_base_params(hist)
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    valu, traffic = (None, "skipped"), (None, "skipped")
+    if world == 1 and not args.probe and not args.no_pmc:
+        # counters of mc_kernel in rocprofv3 children (before this process touches the GPU)
+        pa = ["--workload", "rbergomi", "--rb-paths", str(args.rb_paths), "--rb-normals", args.rb_normals]
+        res, err = pmc_pass(args, VALU_COUNTERS, "mc_kernel", probe_argv=pa)
+        valu = (valu_summary(res).get("mc_kernel"), None) if res else (None, err)
+        tr = {}
+        for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+            res, err = pmc_pass(args, [ctr], "mc_kernel", probe_argv=pa)
+            if res is None:
+                traffic = (None, err)
+                break
+            tr[ctr] = res["mc_kernel"][ctr]
+        else:
+            traffic = ((2.0 * tr["FETCH_SIZE"] + tr["WRITE_SIZE"]) * 1024.0, tr)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.probe:
         cpu = rb_cpu_baseline(args.cpu_seconds, base)
     dist = None
     if world > 1:
@@ -891,6 +1140,11 @@ def rbergomi_main(args):
         if st != 0:
             raise RuntimeError(lib.rb_last_error().decode())
 
+    if args.probe:   # the PMC passes' program: two launches
+        for _ in range(2):
+            launch()
+        torch.cuda.synchronize()
+        return
     # one launch prices 1M options (~1 s in f64): a handful of launches, not the env's 25,600
     K = max(1, 5 if args.steps is None else args.steps)
     W = max(0, 1 if args.warmup is None else args.warmup)
@@ -944,6 +1198,7 @@ def rbergomi_main(args):
                        "bound": "valu (f64 FMA / exp, Philox): no HBM traffic to speak of "
                                 "(5 f64 in, 1 f64 out per option)"},
             "full_dataset_s": round(100000 * RB_DAYS * 2 / (n_opt * world * K / wall), 2),
+            "roofline": rb_roofline(valu, traffic, kern_ms, n_opt),
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
@@ -1034,6 +1289,7 @@ def main(argv=None):
     local = int(os.environ.get("LOCAL_RANK", "0"))
     pmc = (None, "skipped")
     valu = (None, "skipped")
+    step_pmc = (None, "skipped")
     cpu = None
     has_book = bool(CONFIGS[args.config]["gen"].get("book"))
     parent = parent_results()
@@ -1047,6 +1303,12 @@ def main(argv=None):
             # the instruction-issue side: the LDS kernel makes the market on chip, so every
             # configuration is partly VALU-bound (with a book or Heston, mostly)
             valu = pmc_valu(args)
+            if args.mode != "graph" and not args.no_step_api:
+                # the step_api line's kernel (he_step -> step1_kernel): its own HBM traffic
+                import copy
+                ga = copy.copy(args)
+                ga.mode = "graph"
+                step_pmc = pmc_traffic(ga)
         if not args.no_cpu_baseline:
             cpu = cpu_baseline(args.cpu_seconds)   # before the GPU is touched (forks workers)
     dist, backend = None, None
@@ -1058,9 +1320,7 @@ def main(argv=None):
     cfg = CONFIGS[args.config]
     n = args.envs
 
-    g = torch.Generator(device=dev)
-    g.manual_seed(1234 + rank)
-    acts = torch.rand((256, n, 2), device=dev, generator=g) * 2 - 1
+    acts = bench_actions(n, rank, dev)
     stream = torch.cuda.Stream(device=dev)
     gathered = (torch.empty((world * n, 4), dtype=torch.float32, device=dev if backend == "nccl" else "cpu")
                 if world > 1 else None)
@@ -1071,6 +1331,21 @@ def main(argv=None):
     K = -(-max(args.steps, MIN_TIMED_STEPS) // runner.chunk) * runner.chunk
     W = -(-args.warmup // runner.chunk) * runner.chunk
     wall, dev_ms = timed(runner, K, W, dist)
+    shard = None
+    if args.mode == "rollout":
+        # every env's summaries after the last launch, gathered in global env order (outside
+        # the timed region), then each rank's re-run of its neighbour's last envs
+        with torch.cuda.stream(stream):
+            final = env.episode_summaries()
+            if dist is not None:
+                allg = torch.empty((world * n, 4), dtype=torch.float32, device=gathered.device)
+                gather_summaries(dist, final, allg)
+            else:
+                allg = final
+        torch.cuda.synchronize()
+        nb, j0, m = shard_check_slice(rank, world, n)
+        got = shard_check_run(args, dev, stream, runner.runs, nb, j0, m)
+        shard = shard_check_verdict(dist, got, allg, nb, j0, n, device="cpu" if backend == "gloo" else dev)
     payload = None
     if dist is not None:
         payload = dict(what="he_episode_summaries: per-env {return, sum P&L, sum cost, length} f32 [envs, 4], "
@@ -1147,9 +1422,11 @@ def main(argv=None):
         kg = kernel_time_ms(hev, rg, 256)
         env_g.close()
         rf = roofline("graph", n, kg, 1, has_book, tile_layout(cfg["mode"], n))
-        step_api = dict(mode="graph (he_step, one launch per step)", value=round(n * Kg / wall_g, 1),
-                        ms_per_step=round(wall_g * 1e3 / Kg, 6), kernel=rf["kernel"], kernel_us=rf["kernel_us"],
-                        achieved_gbs=rf["achieved"], frac=rf["frac"], bytes_per_launch=rf["bytes_per_launch"])
+        step_api = step_api_line(n, Kg, wall_g, rf, step_pmc, tile_layout(cfg["mode"], n))
+
+    sb3 = None
+    if world == 1 and args.config == 2 and not args.no_sb3_api:
+        sb3 = sb3_api(dev)
 
     if rank == 0:
         line = {
@@ -1179,6 +1456,8 @@ def main(argv=None):
             "device_ms_per_step": round(dev_ms / K, 6),
             "roofline": roof,
             "step_api": step_api,
+            "sb3_api": sb3,
+            "shard_check": shard,
             "cpu_baseline": cpu,
         }
         if payload is not None:

@@ -159,9 +159,11 @@ struct Params {
     float4* tileB;          // [M+1][N] {call_delta, gamma, put_delta, lag}; GBM: 12-B {greeks} if tile_greeks
     float rstv[4 + kObs];   // reset market + obs (generate): {S0, v0, C0, P0, obs0[13]}, by value
     // replay
-    const float4* rec;      // [n_paths][T+1] {S, v, C, P}; C/P at T hold row T-1
-    const float4* recg;     // [n_paths][T+1] {call_delta, gamma, put_delta, lag return}
+    const float4* rec;      // [n_paths][rstride] {S, v, C, P}, row t at rrow(p, path, t); C/P at T hold row T-1
+    const float4* recg;     // [n_paths][rstride] {call_delta, gamma, put_delta, lag return}, same layout
     int64_t n_paths;
+    int64_t rstride;        // rows per path in rec / recg: T + 1 + kRowOff rounded up to whole 128-B lines
+    int32_t roff;           // row 0's slot in the path's stride (kRowOff)
     // liability book (generate modes)
     int32_t book_n;
     const BookOpt* book;    // device copy [book_n], read through the scalar cache
@@ -174,6 +176,17 @@ struct Params {
     uint64_t* tim;          // [5][8192][2]
 #endif
 };
+
+// Replay table layout.  Row t of a path sits at slot kRowOff + t of a stride of whole 128-B
+// lines (8 rows of 16 B), so rows 1..8, 9..16, ... -- the spans the LDS loaders read per
+// 8-step block from an episode start, and their 4-row halves -- begin on a line whenever the
+// block grid meets the episode at a multiple of 4 steps: always for T = 0 or 4 mod 8, e.g.
+// the reference's T = 252, so no span straddles an extra line (1.15x traffic).
+constexpr int32_t kRowOff = 7;
+__host__ __device__ __forceinline__ int64_t replay_stride(int64_t T) { return ((T + 1 + kRowOff + 7) / 8) * 8; }
+__device__ __forceinline__ int64_t rrow(const Params& p, int64_t path, int64_t t) {
+    return path * p.rstride + p.roff + t;
+}
 
 struct State {
     uint32_t* t;
@@ -1066,10 +1079,15 @@ __global__ void init_reset_kernel(Params p, float* rst) {
 __global__ __launch_bounds__(kBlock) void table_greeks_kernel(Params p, float4* recg, int64_t count) {
     int64_t k = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (k >= count) return;
+    // k runs over the padded table: slots outside rows 0 .. T of a path are padding (zeros)
+    const int64_t t = k % p.rstride - p.roff;
+    if (t < 0 || t > (int64_t)p.T) {
+        recg[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+        return;
+    }
     float4 r = p.rec[k];
     float4 g = p.record_metrics ? replay_greeks(p, r.x, r.y) : make_float4(0.f, 0.f, 0.f, 0.f);
     // row t >= 1 is stepped into from row t-1 of the same path; row 0 is only a reset obs
-    const int64_t t = k % (int64_t)(p.T + 1);
     g.w = (t == 0) ? 0.0f : lag_return(r.x, p.rec[k - 1].x);
     recg[k] = g;
 }
@@ -1279,17 +1297,24 @@ __device__ __forceinline__ void flush_obs_wave(const float* wtile, float* out, i
         d4[lane + 128] = s4[lane + 128];
         if (lane < 16) d4[lane + 192] = s4[lane + 192];
     } else if (rows > 0) {
+        // a partial wave (the last rows of N): at most 4 float4 per lane and a 1-3 float
+        // remainder, as predicated stores -- no loop carrying addresses (a loop here cost the
+        // replay obs stepper its VGPR spills)
         const int nf = rows * kObs;
         const int nv = nf >> 2;
-        for (int k = lane; k < nv; k += 64) d4[k] = s4[k];
-        for (int k = (nv << 2) + lane; k < nf; k += 64) dst[k] = wtile[k];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int k = lane + 64 * q;
+            if (k < nv) d4[k] = s4[k];
+        }
+        if (lane < nf - (nv << 2)) dst[(nv << 2) + lane] = wtile[(nv << 2) + lane];
     }
     asm volatile("" ::: "memory");
 }
 
 // The episode's S0 of row e.path (hedging_env_v2.py:156-157: < 1e-6 -> 1.0).
 __device__ __forceinline__ void replay_start(const Params& p, Env& e) {
-    float S0 = p.rec[(int64_t)e.path * (p.T + 1)].x;
+    float S0 = p.rec[rrow(p, e.path, 0)].x;
     e.s0_small = S0 < 1e-6f;
     e.s0 = e.s0_small ? 1.0f : S0;
 }
@@ -1425,7 +1450,7 @@ __device__ __forceinline__ void step_body(const Params& pk, int64_t n_envs, cons
             const float s0 = s_s0[i];
             const uint32_t tt = t0 > (uint32_t)T ? (uint32_t)T : t0;
             const uint32_t tn = t0 + 1 > (uint32_t)T ? (uint32_t)T : t0 + 1;
-            const int64_t r0 = (int64_t)path * (T + 1);
+            const int64_t r0 = rrow(p, path, 0);
             pre = as_mkt(ld4(mA, r0 + tt));
             postA = ld4(mA, r0 + tn);
             postB = ld4(mB, r0 + tn);
@@ -1471,7 +1496,7 @@ __device__ __forceinline__ void step_body(const Params& pk, int64_t n_envs, cons
         float4 gpre;
         if (REPLAY) {
             const uint32_t tt = e.t > (uint32_t)p.T ? (uint32_t)p.T : e.t;
-            gpre = tB[(int64_t)e.path * (p.T + 1) + tt];
+            gpre = tB[rrow(p, e.path, tt)];
         } else {
             if (e.t == 0) gpre = make_float4(p.rstv[4 + 7], 0.0f, p.rstv[4 + 9], 0.0f);
             else gpre = tg ? ldB((int64_t)slot0 * N + i) : gbm_greeks(pre.S);
@@ -1600,7 +1625,7 @@ __device__ __forceinline__ void step_body(const Params& pk, int64_t n_envs, cons
                 env_reset_common(p, e);
                 if (REPLAY) {
                     replay_reset(p, s, i, e);
-                    int64_t r = (int64_t)e.path * (p.T + 1);
+                    int64_t r = rrow(p, e.path, 0);
                     pre = as_mkt(tA[r]);
                     float o[kObs];
                     make_obs(p, e, pre, tB[r], pre.S, pre.v, o);
@@ -1690,7 +1715,7 @@ __device__ __forceinline__ void step_body(const Params& pk, int64_t n_envs, cons
         auto row_of = [&](int gap) {   // the post-step row of the step `gap` ahead of the current one
             const uint32_t tb = (live ? e.t : 0u) + (uint32_t)gap;
             const uint32_t tn = tb < (uint32_t)T ? tb + 1u : (uint32_t)T;
-            return (live ? (int64_t)e.path : 0) * (T + 1) + tn;
+            return rrow(p, live ? (int64_t)e.path : 0, tn);
         };
         auto load = [&](int d, int kk, int gap) {
             kk = kk < k_steps ? kk : k_steps - 1;
@@ -1718,7 +1743,7 @@ __device__ __forceinline__ void step_body(const Params& pk, int64_t n_envs, cons
 #pragma unroll
                         for (int m = 1; m <= D; ++m) {
                             const int sl = (d + m) % D;
-                            const int64_t r = (int64_t)e.path * (T + 1) + m;
+                            const int64_t r = rrow(p, e.path, m);
                             rA[sl] = ld4(mA, r);
                             rB[sl] = ld4(mB, r);
                         }
@@ -1734,7 +1759,7 @@ __device__ __forceinline__ void step_body(const Params& pk, int64_t n_envs, cons
             step_part(k, post, postB, a);
             if (REPLAY && live && k + 1 < k_steps) {
                 const uint32_t tn = e.t + 1 > (uint32_t)p.T ? (uint32_t)p.T : e.t + 1;
-                const int64_t r = (int64_t)e.path * (p.T + 1) + tn;
+                const int64_t r = rrow(p, e.path, tn);
                 if (!POL) a = act[(int64_t)(k + 1) * N + i];
                 postA = tA[r];
                 postB = tB[r];
@@ -2730,7 +2755,11 @@ __device__ __forceinline__ int lds_role(int wave) {
         const uint32_t m = (1u << sh_place[0]) | (1u << sh_place[1]) | (1u << sh_place[2]) | (1u << sh_place[3]);
         int role = wave;
 #if HE_LDS_BALANCE
+#ifdef HE_LDS_ROLE_XOR
+        if (m == 15u) role = (int)((simd ^ sh_place[4]) & 3u);
+#else
         if (m == 15u) role = (int)((simd + sh_place[4]) & 3u);
+#endif
 #endif
 #ifdef HE_LDS_HWID
         if ((threadIdx.x & 63) == 0 && blockIdx.x < 16384) {
@@ -2812,7 +2841,7 @@ __device__ __forceinline__ void lds_replay_loader(const Params& p, State s, int 
     const int64_t i0 = base + lane;
     const int64_t i = i0 < N ? i0 : N - 1;   // lanes past N mirror env N-1
     const uint32_t T = (uint32_t)p.T;
-    const int64_t W = (int64_t)T + 1;        // a path's row stride
+    const int64_t W = p.rstride;             // a path's row stride (128-B lines, row 1 line-aligned)
     const GLOBAL v4f* rec = (const GLOBAL v4f*)p.rec;
     const GLOBAL v4f* recg = (const GLOBAL v4f*)p.recg;
     const int sl0 = part * H;
@@ -2841,7 +2870,7 @@ __device__ __forceinline__ void lds_replay_loader(const Params& p, State s, int 
         rsl = te < (uint32_t)len ? (int)te : kLdsM;
         int32_t np = path;
         if (rsl < kLdsM) np = (int32_t)pcg64_integers(g, (uint64_t)p.n_paths);  // replay_reset's draw
-        const int64_t ro = (int64_t)path * W + (int64_t)t + 1, rn = (int64_t)np * W;
+        const int64_t ro = (int64_t)path * W + p.roff + (int64_t)t + 1, rn = (int64_t)np * W + p.roff;
 #pragma unroll
         for (int h = 0; h < H; ++h) {
             // slots up to the end read the old path's rows t + 1 + sl (row T holds the lagged
@@ -2907,6 +2936,15 @@ __device__ __forceinline__ void lds_replay_loader(const Params& p, State s, int 
     }
 }
 
+// The lane index within the wave, made where it is used: volatile, so the compiler can neither
+// hoist it nor merge it with threadIdx.x -- a value kept live across the block loop costs a
+// VGPR the replay steppers do not have (128 at 4 waves per SIMD).
+__device__ __forceinline__ uint32_t fresh_lane() {
+    uint32_t ln;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
+    return ln;
+}
+
 // OBS = false: the reward wave (owns the env state); OBS = true: the obs wave.  FAST: the
 // configuration of fast_replay_config (v2, loss != mse, shares_to_hedge != 0, record_metrics,
 // max_contracts_held > 0) with its uniform branches compiled out.
@@ -2942,7 +2980,7 @@ __device__ __forceinline__ void lds_replay_stepper(const Params& p, State s, con
     replay_episode_consts<FAST>(p, e);
     // the row the env stands at (step_body's replay prologue)
     const uint32_t tt = e.t > (uint32_t)T ? (uint32_t)T : e.t;
-    Mkt pre = as_mkt(ld4((const GLOBAL v4f*)p.rec, (int64_t)s.path[i] * (T + 1) + tt));
+    Mkt pre = as_mkt(ld4((const GLOBAL v4f*)p.rec, rrow(p, s.path[i], tt)));
     pre.B = 0.0;
     double pv_last = 0.0;
     double sm0 = 0.0, sm1 = 0.0, sm2 = 0.0;
@@ -3143,9 +3181,13 @@ __device__ __forceinline__ void lds_replay_stepper(const Params& p, State s, con
         }
         if (tail) {
             const int buf = nfull & 1;
+            // the env index made afresh (mbcnt lane): i itself is then dead across the block
+            // loop above, which kept it in scratch for these loads (the kernel's VGPR spill)
+            const int64_t ia = base + (int64_t)fresh_lane();
+            const int64_t it = ia < N ? ia : N - 1;
             for (int sl = 0; sl < tail; ++sl) {
                 const int k = nfull * kLdsM + sl;
-                step(buf, sl, k, ld2(gact, (int64_t)k * N + i), std::false_type{});
+                step(buf, sl, k, ld2(gact, (int64_t)k * N + it), std::false_type{});
             }
             LDS_BAR();
         }
@@ -3154,7 +3196,9 @@ __device__ __forceinline__ void lds_replay_stepper(const Params& p, State s, con
     else run(std::false_type{});
     LDS_T1(OBS ? 1 : 0);
     if (!OBS && i0 < N) {
-        int64_t j = i;
+        // the env index made afresh (the lane from mbcnt, not threadIdx): kept live across the
+        // block loop for these stores, the prologue's i was this kernel's one VGPR spill
+        int64_t j = base + (int64_t)fresh_lane();
         asm volatile("" : "+v"(j));
         s.t[j] = e.t;
         s.pos[j] = pack_pos(e.call, e.put);
@@ -3288,7 +3332,7 @@ __global__ __launch_bounds__(kBlock) void reset_kernel(Params p, State s, Market
         } else {
             replay_reset(p, s, i, e);
         }
-        int64_t r = (int64_t)e.path * (p.T + 1);
+        int64_t r = rrow(p, e.path, 0);
         m = as_mkt(p.rec[r]);
         make_obs(p, e, m, p.recg[r], m.S, m.v, o);
         s.path[i] = e.path;
@@ -3433,6 +3477,8 @@ struct he_env {
     BookOpt* dbook = nullptr;   // liability book, device copy (generate modes)
     double* dbook_tab = nullptr;  // book tau table (book_option)
     int64_t* d_eps = nullptr;     // he_reset_episodes: the host-drawn episode rows, staged
+    int64_t* h_eps = nullptr;     // ... through this pinned host buffer (an async DMA)
+    hipEvent_t ev_eps = nullptr;  // recorded after the reset that read d_eps / h_eps: guards their reuse
     int32_t book_rows = 0;        // its rows: max expiry + 1
     unsigned long long* scratch_count = nullptr;  // he_rollout_policy without records
     double book_rst = 0.0;      // book value of the reset market (host copy)
@@ -3591,6 +3637,8 @@ static void fill_params(he_env* env) {
     p.tim = g_tim;
 #endif
     p.n_paths = env->n_paths;
+    p.rstride = replay_stride(env->cfg.episode_length);
+    p.roff = kRowOff;
 }
 
 template <int MODE>
@@ -4229,7 +4277,10 @@ he_status he_destroy(he_env* env) {
         if (env->dparams) (void)hipFree(env->dparams);
         if (env->dbook) (void)hipFree(env->dbook);
         if (env->dbook_tab) (void)hipFree(env->dbook_tab);
+        if (env->ev_eps) (void)hipEventSynchronize(env->ev_eps);
         if (env->d_eps) (void)hipFree(env->d_eps);
+        if (env->h_eps) (void)hipHostFree(env->h_eps);
+        if (env->ev_eps) (void)hipEventDestroy(env->ev_eps);
         if (env->scratch_count) (void)hipFree(env->scratch_count);
         if (env->xs) {
             (void)hipStreamSynchronize(env->xs);
@@ -4251,11 +4302,12 @@ he_status he_load_paths(he_env* env, const float* S, const float* v, const float
     if (n_cols - 1 > (1 << 30)) return fail(env, HE_ESHAPE, "episode too long");
     DeviceGuard dg(env->cfg.device);
     const int64_t T = n_cols - 1;
+    const int64_t W = replay_stride(T);   // padded row stride (see kRowOff); padding slots are zeros
     std::vector<float4> rec;
     try {
-        rec.resize((size_t)(n_paths * n_cols));
+        rec.assign((size_t)(n_paths * W), make_float4(0.f, 0.f, 0.f, 0.f));
     } catch (...) {
-        return fail(env, HE_ENOMEM, "host allocation of %lld records failed", (long long)(n_paths * n_cols));
+        return fail(env, HE_ENOMEM, "host allocation of %lld records failed", (long long)(n_paths * W));
     }
     for (int64_t q = 0; q < n_paths; ++q) {
         for (int64_t t = 0; t <= T; ++t) {
@@ -4265,7 +4317,7 @@ he_status he_load_paths(he_env* env, const float* S, const float* v, const float
             r.y = v[q * n_cols + t];
             r.z = C[q * T + tc];
             r.w = P[q * T + tc];
-            rec[(size_t)(q * n_cols + t)] = r;
+            rec[(size_t)(q * W + kRowOff + t)] = r;
         }
     }
     const size_t bytes = rec.size() * sizeof(float4);
@@ -4492,12 +4544,20 @@ he_status he_reset_episodes(he_env* env, const int64_t* env_ids, const int64_t* 
     else memset(&inf, 0, sizeof(inf));
     DeviceGuard dg(c.device);
     hipStream_t st = (hipStream_t)stream;
-    if (!env->d_eps) HE_HIP(env, hipMalloc(&env->d_eps, (size_t)c.n_envs * sizeof(int64_t)));
-    // the staging buffer may still be read by the previous call's reset on this stream
-    HE_HIP(env, hipStreamSynchronize(st));
-    HE_HIP(env, hipMemcpy(env->d_eps, episode_idx, (size_t)count * sizeof(int64_t), hipMemcpyHostToDevice));
+    if (!env->d_eps) {
+        HE_HIP(env, hipMalloc(&env->d_eps, (size_t)c.n_envs * sizeof(int64_t)));
+        HE_HIP(env, hipHostMalloc((void**)&env->h_eps, (size_t)c.n_envs * sizeof(int64_t), hipHostMallocDefault));
+        HE_HIP(env, hipEventCreateWithFlags(&env->ev_eps, hipEventDisableTiming));
+    } else {
+        // the previous call's copy and reset (on any stream) may still read the staging
+        // buffers: wait for that reset alone, not for the caller's whole stream
+        HE_HIP(env, hipEventSynchronize(env->ev_eps));
+    }
+    memcpy(env->h_eps, episode_idx, (size_t)count * sizeof(int64_t));
+    HE_HIP(env, hipMemcpyAsync(env->d_eps, env->h_eps, (size_t)count * sizeof(int64_t), hipMemcpyHostToDevice, st));
     launch_reset<HE_MODE_REPLAY>(env, env_ids, count, obs_out, inf, st, env->d_eps);
     HE_HIP(env, hipGetLastError());
+    HE_HIP(env, hipEventRecord(env->ev_eps, st));
     env->ready = true;
     return HE_OK;
 }
@@ -4535,11 +4595,15 @@ he_status he_step(he_env* env, const float* actions, float* obs, float* reward, 
     he_status s = launch_steps(env, io, want_info, 1, stream);
     env->vn_on = env->vne_on = false;
     if (s == HE_OK && vne && !env->vn_fused) {
-        // another step kernel ran (info requested): the eval VecNormalize step as its own launch
+        // another step kernel ran (info requested): the eval VecNormalize step as its own
+        // launch.  he_vecnorm_step with training = 0 launches the apply kernel alone, which reads
+        // only the frozen statistics (never the scratch partials), for any n.
         const vn::ApplyArgs& a = env->vne;
-        return he_vecnorm_apply(&env->vne_p, env->cfg.n_envs, obs, reward, terminated, terminal_obs, a.returns,
-                                const_cast<double*>(a.stats), const_cast<double*>(a.stats), a.obs_out, a.rew_out,
-                                a.tobs_out, a.ep_ret, a.ep_len, a.ep_ret_done, a.ep_len_done, stream);
+        he_status sv = he_vecnorm_step(&env->vne_p, env->cfg.n_envs, obs, reward, terminated, terminal_obs,
+                                       a.returns, const_cast<double*>(a.stats), const_cast<double*>(a.stats),
+                                       a.obs_out, a.rew_out, a.tobs_out, a.ep_ret, a.ep_len, a.ep_ret_done,
+                                       a.ep_len_done, stream);
+        return sv == HE_OK ? sv : fail(env, sv, "he_step: the eval VecNormalize launch failed (status %d)", (int)sv);
     }
     if (s != HE_OK || !vn || env->vn_fused) return s;
     // VecNormalize attached, and this step took another kernel: the moments after it

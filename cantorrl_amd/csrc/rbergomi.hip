@@ -76,8 +76,10 @@ HE_HD void normal_pair(u32x4 c, uint32_t k0, uint32_t k1, double* a, double* b) 
 // only held to their distribution (test_pricer_philox_black_scholes_limit), so the two
 // multi-instruction IEEE sequences go: s = (m - 1) / (m + 1) as (m - 1) times v_rcp_f64 with
 // one Newton step (within 2.3e-15, profiles/r04s3_rcp_f64.txt), and sqrt(-2 log u) as
-// x rsq(x) with one Newton-Raphson correction (the argument is in [1.1e-15, 75]: no scaling
-// or special cases).  The series and the sin / cos polynomials are box_muller's.
+// x rsq(x) with one Newton-Raphson correction (u01 lies in [2^-53, 1 - 2^-53], so the argument
+// -2 log u lies in [2^-52 = 2.2e-16, 73.5]: normal f64 numbers whose rsq is finite, no scaling
+// or special cases; test_mc_box_muller_extreme_uniforms).  The series and the sin / cos
+// polynomials are box_muller's.
 __device__ __forceinline__ void mc_box_muller(double u1, double u2, double* z1, double* z2) {
     int e;
     double m = frexp(u1, &e);
@@ -644,6 +646,16 @@ double estimate_rho(const std::vector<double>& r) {   // :155-171
 }  // namespace
 
 // ================================================================== C ABI
+// Test hook: mc_box_muller on caller-given uniforms (rb_device_mc_box_muller).
+__global__ void mc_box_muller_kernel(const double* u1, const double* u2, int64_t n, double* z1, double* z2) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    double a, b;
+    mc_box_muller(u1[i], u2[i], &a, &b);
+    z1[i] = a;
+    z2[i] = b;
+}
+
 extern "C" {
 
 const char* rb_version(void) { return "librbergomi 0.1 (gfx950)"; }
@@ -814,6 +826,16 @@ int32_t rb_host_normals(uint64_t seed, int32_t domain, uint32_t sub, uint64_t gi
         if (i + 1 < n) out[i + 1] = z[1];
     }
     return RB_OK;
+}
+
+int32_t rb_device_mc_box_muller(const double* u1, const double* u2, int64_t n, double* z1, double* z2, void* stream) {
+    if (n < 0 || (n > 0 && (!u1 || !u2 || !z1 || !z2))) return fail(RB_EINVAL, "bad arguments");
+    if (n == 0) return RB_OK;
+    const int64_t blocks = (n + 255) / 256;
+    if (blocks > 65535) return fail(RB_EINVAL, "n too large for the test hook");
+    hipLaunchKernelGGL(mc_box_muller_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, u1, u2, n,
+                       z1, z2);
+    return hipGetLastError() == hipSuccess ? RB_OK : fail(RB_EHIP, "mc_box_muller_kernel launch failed");
 }
 
 }  // extern "C"

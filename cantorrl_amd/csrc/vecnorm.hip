@@ -419,7 +419,8 @@ he_status he_vecnorm_apply(const he_vecnorm_params* p, int64_t n, const float* o
                            void* scratch, float* obs_out, float* reward_out, float* terminal_obs_out,
                            double* ep_return, int32_t* ep_length, double* ep_return_done, int32_t* ep_length_done,
                            void* stream) {
-    if (n > (int64_t)kVnMaxBlocks * kVnThreads) return HE_EINVAL;   // the fused partials cover <= 65,536 rows
+    // training merges the fused partials, which cover <= 65,536 rows; frozen statistics read none
+    if (p && p->training && n > (int64_t)kVnMaxBlocks * kVnThreads) return HE_EINVAL;
     return vecnorm_step(p, n, obs, reward, done, terminal_obs, returns, stats, scratch, obs_out, reward_out,
                         terminal_obs_out, ep_return, ep_length, ep_return_done, ep_length_done, stream, false);
 }

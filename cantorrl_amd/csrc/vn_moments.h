@@ -207,6 +207,11 @@ struct ColNorm {
 __device__ __forceinline__ ColNorm col_norm(double mean, double var, double eps) {
     const double s = 1.0 / sqrt(var + eps);
     const float mh = (float)mean, sh = (float)s;
+    // s past FLT_MAX (var + eps = 0, e.g. epsilon = 0 on a constant column): the split terms
+    // would be inf - inf and 0 * inf = NaN for every element; with them 0 an element is
+    // (x - mh) * inf = +-inf -> +-clip, as the f64 (x - mean) / sqrt(var + eps) clips (0 / 0
+    // stays NaN, as in SB3)
+    if (!(sh <= 3.402823466e38f)) return ColNorm{mh, 0.0f, sh, 0.0f};
     return ColNorm{mh, (float)((mean - (double)mh) * s), sh, (float)(s - (double)sh)};
 }
 // VecNormalize.normalize_obs of one element in f32 from the merged f64 statistics, converted

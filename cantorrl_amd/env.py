@@ -86,12 +86,33 @@ class HedgingEnv:
         self.initial_S0_for_episode = 1.0
         self._needs_reset = True
         self._terminated = False
-        self._act = torch.zeros((1, 2), dtype=torch.float32, device=v.device)
+        # host side of one step: the action goes in through a pinned 8-B staging buffer and
+        # the env's whole io buffer (obs, reward, flags, every info field: ~7 KB) comes back
+        # as ONE copy into a pinned mirror, read through a structured dtype -- one DMA each
+        # way and one event wait per step (a step used to wait on 29 separate copies)
+        self._act_h = torch.zeros((1, 2), dtype=torch.float32, pin_memory=True)
+        self._act_np = self._act_h.numpy()
+        self._io_h = torch.zeros(v._io.numel(), dtype=torch.uint8, pin_memory=True)
+        fields = {"names": ["obs", "reward", "terminated"], "formats": [("<f4", (13,)), "<f4", "u1"],
+                  "offsets": [0, 52, 56]}
+        for k, dt, o in v._info_offs:
+            fields["names"].append(k)
+            fields["formats"].append(np.dtype(dict(_lib.INFO_FIELDS)[k]))
+            fields["offsets"].append(v._io_info0 + o)
+        fields["itemsize"] = v._io.numel()
+        self._rec = self._io_h.numpy().view(np.dtype(fields))   # shape (1,): a view, refreshed by each copy
+        self._ev = torch.cuda.Event()
 
     # ------------------------------------------------------------------ helpers
-    def _pull(self):
+    def _fetch(self):
+        """One copy of the io buffer into the pinned mirror, one wait -> the record."""
         v = self._venv
-        h = {k: t.cpu().numpy()[0] for k, t in v._info_t.items()}
+        self._io_h.copy_(v._io, non_blocking=True)
+        self._ev.record(torch.cuda.current_stream(v.device))
+        self._ev.synchronize()
+        return self._rec[0]
+
+    def _pull(self, h):
         self.current_stock_price = np.float32(h["current_stock_price"])
         self.current_volatility = np.float32(h["current_volatility"])
         self.current_call_price = np.float32(h["current_call_price"])
@@ -100,8 +121,7 @@ class HedgingEnv:
         self.call_contracts_held = np.int64(h["call_contracts"])
         self.put_contracts_held = np.int64(h["put_contracts"])
         self.cash_balance = np.float64(h["cash"])
-        s0 = np.float32(h["initial_S0_for_episode"])
-        return h, s0
+        return np.float32(h["initial_S0_for_episode"])
 
     # ------------------------------------------------------------------ gym API
     def reset(self, seed=None, options=None):
@@ -112,9 +132,13 @@ class HedgingEnv:
         if seed is not None:
             v.seed_envs([int(seed)])
         ep = (options or {}).get("episode_idx")
-        obs = v.reset_tensors() if ep is None else v.reset_tensors(episode_idx=[int(ep)])
-        o = obs.cpu().numpy()[0].copy()
-        h, s0 = self._pull()
+        if ep is None:
+            v.reset_tensors()
+        else:
+            v.reset_tensors(episode_idx=[int(ep)])
+        h = self._fetch()
+        o = h["obs"].copy()
+        s0 = self._pull(h)
         small = bool(s0 == np.float32(1.0) and self.current_stock_price < np.float32(1e-6))
         self.initial_S0_for_episode = 1.0 if small else s0
         self.current_episode_idx = int(h["current_episode_idx"])
@@ -134,12 +158,15 @@ class HedgingEnv:
             raise IndexError(f"index {self.episode_length + 1} is out of bounds for axis 0 with size "
                              f"{self.episode_length + 1}")
         a = np.asarray(action, dtype=np.float32).reshape(2)
-        self._act.copy_(torch.from_numpy(a).reshape(1, 2))
+        v = self._venv
+        self._act_np[0] = a
+        v._act.copy_(self._act_h, non_blocking=True)   # the last step's wait retired the staging
         prev_S, prev_v = self.current_stock_price, self.current_volatility
-        obs, rew, term, trunc = self._venv.step_tensors(self._act)
-        o = obs.cpu().numpy()[0].copy()
-        h, s0 = self._pull()
-        terminated = bool(term.cpu().numpy()[0])
+        v.step_tensors(v._act)
+        h = self._fetch()
+        o = h["obs"].copy()
+        self._pull(h)
+        terminated = bool(h["terminated"])
         self._terminated = terminated
         self.S_t_minus_1, self.v_t_minus_1 = prev_S, prev_v
         self.portfolio_value_t_minus_1 = np.float64(h["portfolio_value"])

@@ -79,7 +79,7 @@ class RbConfig(ctypes.Structure):
 
 EXPORTS = ["rb_version", "rb_last_error", "rb_config_init", "rb_estimate_base_params", "rb_estimate_parts",
            "rb_sample_params", "rb_simulate_paths", "rb_price_options", "rb_price_atm_marks", "rb_generate",
-           "rb_host_normals"]
+           "rb_host_normals", "rb_device_mc_box_muller"]
 
 _lib = None
 
@@ -111,6 +111,7 @@ def load(path=LIB_PATH):
         "rb_price_atm_marks": (i32, [cfgp, vp, vp, vp, vp, vp, vp]),
         "rb_generate": (i32, [cfgp, basep, vp, vp, vp, vp, vp, vp]),
         "rb_host_normals": (i32, [u64, i32, u32, u64, u32, i64, vp]),
+        "rb_device_mc_box_muller": (i32, [vp, vp, i64, vp, vp, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)

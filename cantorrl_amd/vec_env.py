@@ -39,6 +39,11 @@ GENERATE_DEFAULTS = dict(s0=496.48001098632812, variance=0.029028, mu=0.04, dt=1
 MONITOR_KEYWORDS = ("per_share_step_pnl", "raw_pnl_deviation_abs", "transaction_costs_total")
 
 _TORCH_DT = {"f8": torch.float64, "f4": torch.float32, "i4": torch.int32}
+_NP_DT = {torch.float64: np.float64, torch.float32: np.float32, torch.int32: np.int32}
+
+
+def _align(x, a):
+    return -(-x // a) * a
 
 
 def load_npz_tables(data_file_path):
@@ -182,30 +187,40 @@ class HedgingVecEnv:
         n = self.num_envs
         dev = self.device
         self._act = torch.zeros((n, 2), dtype=torch.float32, device=dev)
-        self._obs = torch.zeros((n, 13), dtype=torch.float32, device=dev)
-        self._rew = torch.zeros((n,), dtype=torch.float32, device=dev)
-        self._term = torch.zeros((n,), dtype=torch.uint8, device=dev)
-        self._trunc = torch.zeros((n,), dtype=torch.uint8, device=dev)
         self._tobs = torch.zeros((n, 13), dtype=torch.float32, device=dev)
         self.info_keys = tuple(info_keys or ())
         self._info_t = {}
         self._info = _lib.HeInfo()
         known = dict(_lib.INFO_FIELDS)
-        # every info field is a slice of ONE flat buffer (256-B aligned), so freezing a view
-        # (InfoView) is one device copy, not one per key
+        # ONE device buffer holds everything a host caller reads after a step:
+        #   [obs f32 N x 13 | reward f32 N | terminated u8 N | truncated u8 N | info fields]
+        # with every info field 256-B aligned.  step_wait copies the obs / reward / terminated
+        # prefix to the host as one DMA and HedgingEnv.step the whole buffer (~7 KB at N = 1);
+        # freezing an InfoView is one device copy of the info part, not one per key.
+        o_rew, o_term = 52 * n, 56 * n
+        o_trunc, end = o_term + n, o_term + 2 * n
+        self._io_step_bytes = o_trunc            # obs + reward + terminated
+        info0 = _align(end, 256)
         offs, tot = [], 0
         for k in self.info_keys:
             if k not in known:
                 raise KeyError(f"unknown info key {k!r}")
             dt = _TORCH_DT[known[k]]
             offs.append((k, dt, tot))
-            tot += -(-n * torch.empty((), dtype=dt).element_size() // 256) * 256
-        self._info_flat = torch.zeros(max(tot, 1), dtype=torch.uint8, device=dev)
+            tot += _align(n * torch.empty((), dtype=dt).element_size(), 256)
+        self._io = torch.zeros(info0 + tot, dtype=torch.uint8, device=dev)
+        self._obs = self._io[:o_rew].view(torch.float32).view(n, 13)
+        self._rew = self._io[o_rew:o_term].view(torch.float32)
+        self._term = self._io[o_term:o_trunc]
+        self._trunc = self._io[o_trunc:end]
+        self._io_info0 = info0
+        self._info_flat = self._io[info0:]
         for k, dt, o in offs:
             t = self._info_flat[o:o + n * torch.empty((), dtype=dt).element_size()].view(dt)
             self._info_t[k] = t
             setattr(self._info, k, t.data_ptr())
         self._info_offs = offs
+        self._ev = torch.cuda.Event()   # the one host wait of a host pull (_pull)
         # InfoView snapshots (see InfoView): freeze_infos=False skips them (a view read after
         # a later step then shows that step's values)
         self.freeze_infos = bool(freeze_infos)
@@ -214,14 +229,29 @@ class HedgingVecEnv:
         self._pending_seeds = None
         self._live_view = None  # weakref to the newest InfoView (see InfoView)
         self._actions_pending = None
-        self._ep_ret = np.zeros(n, np.float64)
-        self._ep_len = np.zeros(n, np.int64)
+        # Monitor (monitor_keywords): each env's running reward sum as f64 on the device
+        # (sum(float(r)) of Monitor.step, the same additions in the same order), and the
+        # episode length as (steps so far - the step the env's episode began), so a step
+        # that ends no episode costs the host nothing
+        self._ep_ret = torch.zeros(n, dtype=torch.float64, device=dev)
+        self._ep_start = np.zeros(n, np.int64)
+        self._steps = 0
         # failure detection: device count of non-finite obs / reward values since
         # construction (he_count_nonfinite after every step when check_finite)
         self.check_finite = bool(check_finite)
         self._nonfinite = torch.zeros(1, dtype=torch.int64, device=dev)
         self._t_start = time.time()
 
+        if self.return_numpy:
+            # the host path's pinned blocks (step outputs, actions, the episode-end pull), made
+            # now: a first hipHostMalloc costs milliseconds, inside a step it would be that step's
+            self._warm_pinned([self._io_step_bytes] * 3 + [8 * n] * 2 + [52 * n, self._info_flat.numel(), 8 * n])
+        if self.monitor_keywords is not None:
+            # the Monitor sums' torch kernels, loaded now (a first launch loads the code object:
+            # tens of ms, which the first episode end would otherwise pay)
+            self._ep_ret.add_(self._rew)
+            self._ep_ret.masked_fill_(self._term.bool(), 0.0)
+            self._ep_ret.zero_()
         self.action_space = Box(-1.0, 1.0, (2,), np.float32)
         self.observation_space = Box(OBS_LOW, OBS_HIGH, (13,), np.float32)
         # reference attribute names (hedging_env_v2.py:53-58) + the documented alias
@@ -243,6 +273,43 @@ class HedgingVecEnv:
 
     def _ptr(self, t):
         return t.data_ptr() if t is not None else None
+
+    def _pull(self, srcs):
+        """Device tensors -> numpy arrays in pinned host memory: one async copy each on the
+        current stream (behind the step that wrote them), then ONE event wait.  The pinned
+        blocks come from torch's caching host allocator, so each returned array owns its
+        memory (nothing is overwritten by a later step) and allocation is a cache hit."""
+        outs = []
+        for t in srcs:
+            h = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+            h.copy_(t, non_blocking=True)
+            outs.append(h)
+        self._ev.record(torch.cuda.current_stream(self.device))
+        self._ev.synchronize()
+        return [h.numpy() for h in outs]
+
+    @staticmethod
+    def _warm_pinned(sizes):
+        """Allocate pinned blocks of these byte sizes together and free them: torch's caching
+        host allocator keeps them, so later pulls of those sizes are cache hits."""
+        blocks = [torch.empty(max(int(b), 1), dtype=torch.uint8, pin_memory=True) for b in sizes]
+        del blocks
+
+    def _host_actions(self, actions):
+        """Host actions -> self._act through a pinned staging block (an async DMA; a
+        pageable source would make the copy synchronous)."""
+        a = torch.as_tensor(actions, dtype=torch.float32).reshape(self.num_envs, 2)
+        if not a.is_pinned():
+            stage = torch.empty((self.num_envs, 2), dtype=torch.float32, pin_memory=True)
+            stage.copy_(a)
+            a = stage
+        self._act.copy_(a, non_blocking=True)
+        return self._act
+
+    def _split_info(self, flat):
+        """Host bytes of the info part of the io buffer -> {key: numpy array}."""
+        n = self.num_envs
+        return {k: flat[o:o + n * np.dtype(_NP_DT[dt]).itemsize].view(_NP_DT[dt]) for k, dt, o in self._info_offs}
 
     def close(self):
         if getattr(self, "_h", None) and self._h.value:
@@ -288,10 +355,13 @@ class HedgingVecEnv:
             v._freeze()
 
     def _info_snapshot(self):
-        """One device copy of every info field (the flat buffer) -> {key: tensor view}."""
-        flat = self._info_flat.clone()
-        n = self.num_envs
-        return {k: flat[o:o + n * torch.empty((), dtype=dt).element_size()].view(dt) for k, dt, o in self._info_offs}
+        """One device copy of every info field (the info part of the io buffer)."""
+        return self._info_flat.clone()
+
+    def _monitor_reset(self):
+        self._ep_ret.zero_()
+        self._ep_start[:] = 0
+        self._steps = 0
 
     def reset_tensors(self, env_ids=None, episode_idx=None):
         """Reset every env (or `env_ids`) and return the obs tensor.  episode_idx (replay mode):
@@ -316,8 +386,7 @@ class HedgingVecEnv:
                                             eps.ctypes.data, eps.size, self._obs.data_ptr(), info, self.stream)
             _lib.check(self.lib, self._h, st, "he_reset_episodes")
             if env_ids is None:
-                self._ep_ret[:] = 0.0
-                self._ep_len[:] = 0
+                self._monitor_reset()
             return self._obs
         if env_ids is None:
             st = self.lib.he_reset(self._h, None, self.num_envs, self._obs.data_ptr(), info, self.stream)
@@ -327,13 +396,12 @@ class HedgingVecEnv:
                                    self.stream)
         _lib.check(self.lib, self._h, st, "he_reset")
         if env_ids is None:
-            self._ep_ret[:] = 0.0
-            self._ep_len[:] = 0
+            self._monitor_reset()
         return self._obs
 
     def reset(self):
         obs = self.reset_tensors()
-        return obs.cpu().numpy() if self.return_numpy else obs
+        return self._pull([obs])[0] if self.return_numpy else obs
 
     # ------------------------------------------------------------------ step
     def step_tensors(self, actions, terminal_obs=True, info=True):
@@ -342,10 +410,11 @@ class HedgingVecEnv:
         if isinstance(actions, torch.Tensor) and actions.device == self.device \
                 and actions.dtype == torch.float32 and actions.is_contiguous():
             act = actions
-        else:
-            a = torch.as_tensor(actions, dtype=torch.float32)
-            self._act.copy_(a.reshape(self.num_envs, 2), non_blocking=True)
+        elif isinstance(actions, torch.Tensor) and actions.is_cuda:
+            self._act.copy_(actions.reshape(self.num_envs, 2), non_blocking=True)
             act = self._act
+        else:
+            act = self._host_actions(actions)
         self._retire_view()
         st = self.lib.he_step(self._h, act.data_ptr(), self._obs.data_ptr(), self._rew.data_ptr(),
                               self._term.data_ptr(), self._trunc.data_ptr(),
@@ -371,18 +440,20 @@ class HedgingVecEnv:
         actions = self._actions_pending
         self._actions_pending = None
         obs, rew, term, _ = self.step_tensors(actions)
+        self._steps += 1
+        if self.monitor_keywords is not None:
+            self._ep_ret.add_(rew)
         if not self.return_numpy:
             return obs, rew, term.bool(), InfoView(self, None)
-        obs_h = obs.cpu().numpy()
-        rew_h = rew.cpu().numpy()
-        done_h = term.cpu().numpy().astype(bool)
-        self._ep_ret += rew_h.astype(np.float64)
-        self._ep_len += 1
+        # obs, reward and terminated are adjacent in the io buffer: one DMA, one wait
+        n = self.num_envs
+        h = self._pull([self._io[:self._io_step_bytes]])[0]
+        obs_h = h[:52 * n].view(np.float32).reshape(n, 13)
+        rew_h = h[52 * n:56 * n].view(np.float32)
+        done_h = h[56 * n:57 * n].view(np.bool_)   # the kernels store 0 / 1
         infos = InfoView(self, done_h)
         if done_h.any():
             infos._materialize_done(done_h)
-            self._ep_ret[done_h] = 0.0
-            self._ep_len[done_h] = 0
         return obs_h, rew_h, done_h, infos
 
     def step(self, actions):
@@ -507,8 +578,9 @@ class InfoView:
     device copy of the info fields' flat buffer (N x the keys' bytes: 1.5 MB for the three
     Monitor keys at 65,536 envs, a few us), not one per key.  freeze_infos=False (env
     constructor) drops the snapshots for callers that read infos before the next step.
-    Done rows (terminal obs, Monitor episode) are materialized by step_wait right away,
-    from the live buffers."""
+    The done rows' data (terminal obs, Monitor episode sums) is pulled by step_wait right
+    away, from the live buffers, in the same single copy as the info fields; every row's
+    dict is built on first access."""
 
     def __init__(self, venv, done):
         self._v = venv
@@ -516,6 +588,7 @@ class InfoView:
         self._cache = {}
         self._host = None
         self._snap = None
+        self._ends = None   # done rows' host data (_materialize_done)
         venv._retire_view()
         venv._live_view = weakref.ref(self)
 
@@ -523,26 +596,48 @@ class InfoView:
         if self._host is None and self._snap is None and self._v._info_t:
             self._snap = self._v._info_snapshot()
 
-    def _host_info(self):
+    def _host_info(self, pulled=None):
+        """Host copy of the view's info fields: ONE copy of the info bytes (live or frozen)."""
         if self._host is None:
-            src = self._snap if self._snap is not None else self._v._info_t
-            self._host = {k: t.cpu().numpy() for k, t in src.items()}
+            v = self._v
+            if pulled is None:
+                src = self._snap if self._snap is not None else v._info_flat
+                pulled = v._pull([src])[0]
+            self._host = v._split_info(pulled)
             self._snap = None
         return self._host
 
     def _materialize_done(self, done):
+        """Done rows (called by step_wait before any later step): this step's terminal obs,
+        info fields and, with Monitor, episode sums come to the host now -- one pull -- and
+        the rows' dicts are built when they are read (__getitem__), as every other row's."""
         v = self._v
-        tobs = v._tobs.cpu().numpy()  # called by step_wait before any later step
-        h = self._host_info()
-        for i in np.nonzero(done)[0]:
-            d = self[i]
-            d["terminal_observation"] = tobs[i].copy()
-            if v.monitor_keywords is not None:
-                ep = {"r": round(float(v._ep_ret[i]), 6), "l": int(v._ep_len[i]),
-                      "t": round(time.time() - v._t_start, 6)}
-                for k in v.monitor_keywords:
-                    ep[k] = h[k][i].item() if k in h else None
-                d["episode"] = ep
+        mon = v.monitor_keywords is not None
+        srcs = [v._tobs]
+        if self._host is None:
+            srcs.append(self._snap if self._snap is not None else v._info_flat)
+        if mon:
+            srcs.append(v._ep_ret)
+        got = v._pull(srcs)
+        self._host_info(got[1] if self._host is None else None)
+        er = el = None
+        if mon:
+            er = got[-1]
+            el = v._steps - v._ep_start   # a new array: _ep_start moves on below
+            v._ep_ret.masked_fill_(v._term.bool(), 0.0)   # the new episodes start at 0
+            v._ep_start[np.nonzero(done)[0]] = v._steps
+        self._ends = (got[0], er, el, round(time.time() - v._t_start, 6), mon)
+
+    def _episode_row(self, d, i):
+        """The done row i's SB3 / Monitor extras (terminal_observation, episode)."""
+        tobs, er, el, t, mon = self._ends
+        d["terminal_observation"] = tobs[i].copy()
+        if mon:
+            h = self._host
+            ep = {"r": round(float(er[i]), 6), "l": int(el[i]), "t": t}
+            for k in self._v.monitor_keywords:
+                ep[k] = h[k][i].item() if k in h else None
+            d["episode"] = ep
 
     def __len__(self):
         return self._v.num_envs
@@ -557,6 +652,8 @@ class InfoView:
             h = self._host_info()
             d = {k: h[k][i].item() for k in h}
             d["TimeLimit.truncated"] = False
+            if self._ends is not None and self._done[i]:
+                self._episode_row(d, i)
             self._cache[i] = d
         return self._cache[i]
 

@@ -47,8 +47,10 @@ class DeviceVecNormalize:
         self._stats = torch.empty(int(self.lib.he_vecnorm_stats_len(D)), dtype=torch.float64, device=dev)
         self._scratch = torch.zeros(int(self.lib.he_vecnorm_scratch_bytes(n, D)), dtype=torch.uint8, device=dev)
         self._returns = torch.zeros(n, dtype=torch.float64, device=dev)
-        self._obs_out = torch.empty((n, D), dtype=torch.float32, device=dev)
-        self._rew_out = torch.empty(n, dtype=torch.float32, device=dev)
+        # normalized obs | normalized reward in one buffer (one host copy per step_wait)
+        self._io_out = torch.empty(n * (D + 1) * 4, dtype=torch.uint8, device=dev)
+        self._obs_out = self._io_out[:n * D * 4].view(torch.float32).view(n, D)
+        self._rew_out = self._io_out[n * D * 4:].view(torch.float32)
         self._tobs_out = torch.empty((n, D), dtype=torch.float32, device=dev)
         self._ep_ret = torch.zeros(n, dtype=torch.float64, device=dev)
         self._ep_len = torch.zeros(n, dtype=torch.int32, device=dev)
@@ -61,6 +63,9 @@ class DeviceVecNormalize:
         self._fusable = on and n <= 65536
         self._fusable_eval = on   # the eval arm exchanges nothing between workgroups: any n
         self._actions_pending = None
+        self._args = None   # _call_args cache
+        if self.return_numpy:
+            venv._warm_pinned([self._io_out.numel()] * 3 + [n] * 3 + [52 * n, 8 * n, 4 * n, venv._info_flat.numel()])
         self._t_start = time.time()
 
     # ------------------------------------------------------------------ plumbing
@@ -167,11 +172,30 @@ class DeviceVecNormalize:
         self._ep_len.zero_()
         return self._obs_out
 
+    def _call_args(self):
+        """The ctypes arguments of a step, built once per parameter set: the params struct
+        (and its byref) and every buffer pointer -- the env's step outputs and this object's
+        buffers are fixed allocations, so the eager step marshals nothing new per call."""
+        key = (bool(self.training), bool(self.norm_obs), bool(self.norm_reward), float(self.gamma),
+               float(self.clip_obs), float(self.clip_reward), float(self.epsilon))
+        c = self._args
+        if c is None or c[0] != key:
+            p = self._params()
+            v = self.venv
+            ptrs = tuple(self._p(t) for t in (v._obs, v._rew, v._term, v._tobs, self._returns, self._stats,
+                                              self._scratch, self._obs_out, self._rew_out, self._tobs_out,
+                                              self._ep_ret, self._ep_len, self._ep_ret_done, self._ep_len_done))
+            out = _lib.HeVecnormOut(self._stats.data_ptr(), self._returns.data_ptr(), self._obs_out.data_ptr(),
+                                    self._rew_out.data_ptr(), self._tobs_out.data_ptr(), self._ep_ret.data_ptr(),
+                                    self._ep_len.data_ptr(), self._ep_ret_done.data_ptr(), self._ep_len_done.data_ptr())
+            c = self._args = (key, p, ctypes.byref(p), ptrs, ctypes.byref(out), out)
+        return c
+
     def step_tensors(self, actions):
         """(normalized obs, normalized reward, terminated, truncated) device tensors;
         the normalized terminal obs of done envs are in `terminal_obs_tensor`."""
-        p = self._params()
-        fused = self._arm(p)
+        c = self._call_args()
+        fused = self._arm(c)
         try:
             obs, rew, term, trunc = self.venv.step_tensors(actions)
         except BaseException:
@@ -182,29 +206,22 @@ class DeviceVecNormalize:
         if fused == "eval":  # he_step made the whole VecNormalize step in its own launch
             return self._obs_out, self._rew_out, term, trunc
         fn = self.lib.he_vecnorm_apply if fused else self.lib.he_vecnorm_step
-        st = fn(ctypes.byref(p), self.num_envs, self._p(obs), self._p(rew),
-                                      self._p(term), self._p(self.venv._tobs), self._p(self._returns),
-                                      self._p(self._stats), self._p(self._scratch), self._p(self._obs_out),
-                                      self._p(self._rew_out), self._p(self._tobs_out), self._p(self._ep_ret),
-                                      self._p(self._ep_len), self._p(self._ep_ret_done), self._p(self._ep_len_done),
-                                      self._stream())
+        st = fn(c[2], self.num_envs, *c[3], self._stream())
         self._check(st, "he_vecnorm_apply" if fused else "he_vecnorm_step")
         return self._obs_out, self._rew_out, term, trunc
 
-    def _arm(self, p):
+    def _arm(self, c):
         """Arm the env's next he_step (one-shot) to run part of this step into this object's
         buffers: training, the moments half (he_vecnorm_attach; he_vecnorm_apply follows);
         evaluation, the whole step (he_vecnorm_attach_eval: frozen statistics, nothing
         crosses envs).  Returns False, True or "eval".  Armed per step, so another wrapper on
         the same env, or the inner env stepped directly, never reads or advances these
         buffers, and the handle holds no pointer into them after the step."""
+        p, pref, ptrs = c[1], c[2], c[3]
         if not p.training:
             if not self._fusable_eval:
                 return False
-            o = _lib.HeVecnormOut(self._stats.data_ptr(), self._returns.data_ptr(), self._obs_out.data_ptr(),
-                                  self._rew_out.data_ptr(), self._tobs_out.data_ptr(), self._ep_ret.data_ptr(),
-                                  self._ep_len.data_ptr(), self._ep_ret_done.data_ptr(), self._ep_len_done.data_ptr())
-            st = self.lib.he_vecnorm_attach_eval(self.venv._h, ctypes.byref(p), ctypes.byref(o))
+            st = self.lib.he_vecnorm_attach_eval(self.venv._h, pref, c[4])
             if st != _lib.HE_OK:
                 msg = self.lib.he_last_error(self.venv._h)
                 raise _lib.HedgeEnvError(f"he_vecnorm_attach_eval failed with status {st}: "
@@ -212,8 +229,7 @@ class DeviceVecNormalize:
             return "eval"
         if not self._fusable:
             return False
-        st = self.lib.he_vecnorm_attach(self.venv._h, ctypes.byref(p), self._p(self._returns),
-                                        self._p(self._stats), self._p(self._scratch))
+        st = self.lib.he_vecnorm_attach(self.venv._h, pref, ptrs[4], ptrs[5], ptrs[6])
         # every build has the fused path and __init__ checked the env count, so any failure
         # here is a real argument error (non-finite gamma, a bad layout): raised, not hidden
         # behind the two-launch path
@@ -239,7 +255,7 @@ class DeviceVecNormalize:
     # ------------------------------------------------------------------ SB3 VecEnv API
     def reset(self):
         obs = self.reset_tensors()
-        return obs.cpu().numpy() if self.return_numpy else obs
+        return self.venv._pull([obs])[0] if self.return_numpy else obs
 
     def step_async(self, actions):
         self._actions_pending = actions
@@ -249,11 +265,14 @@ class DeviceVecNormalize:
         obs, rew, term, _ = self.step_tensors(actions)
         if not self.return_numpy:
             return obs, rew, term.bool(), InfoView(self.venv, None)
-        done = term.cpu().numpy().astype(bool)
+        n = self.num_envs
+        # normalized obs + reward are adjacent in _io_out: two copies (with the flags), one wait
+        h, t = self.venv._pull([self._io_out, term])
+        done = t.view(np.bool_)   # the kernels store 0 / 1
         infos = _NormInfoView(self, done)
         if done.any():
             infos._materialize_done(done)
-        return obs.cpu().numpy(), rew.cpu().numpy(), done, infos
+        return h[:52 * n].view(np.float32).reshape(n, 13), h[52 * n:].view(np.float32), done, infos
 
     def step(self, actions):
         self.step_async(actions)
@@ -300,17 +319,12 @@ class _NormInfoView(InfoView):
 
     def _materialize_done(self, done):
         # called by step_wait right after the step: this step's normalized terminal obs and
-        # Monitor sums are still in the wrapper's buffers
+        # Monitor sums are still in the wrapper's buffers -- one pull; the rows' dicts are
+        # built when read (InfoView.__getitem__ -> _episode_row)
         w, v = self._w, self._w.venv
-        tobs = w._tobs_out.cpu().numpy()
-        er = w._ep_ret_done.cpu().numpy()
-        el = w._ep_len_done.cpu().numpy()
-        h = self._host_info()
-        for i in np.nonzero(done)[0]:
-            d = self[i]
-            d["terminal_observation"] = tobs[i].copy()
-            if v.monitor_keywords is not None:
-                ep = {"r": round(float(er[i]), 6), "l": int(el[i]), "t": round(time.time() - w._t_start, 6)}
-                for k in v.monitor_keywords:
-                    ep[k] = h[k][i].item() if k in h else None
-                d["episode"] = ep
+        srcs = [w._tobs_out, w._ep_ret_done, w._ep_len_done]
+        if self._host is None:
+            srcs.append(self._snap if self._snap is not None else v._info_flat)
+        got = v._pull(srcs)   # one wait for all of them
+        self._host_info(got[3] if self._host is None else None)
+        self._ends = (got[0], got[1], got[2], round(time.time() - w._t_start, 6), v.monitor_keywords is not None)

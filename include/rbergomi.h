@@ -128,6 +128,11 @@ int32_t rb_generate(const rb_config* cfg, const rb_base_params* base, double* pa
 int32_t rb_host_normals(uint64_t seed, int32_t domain, uint32_t sub, uint64_t gid, uint32_t block0,
                         int64_t n, double* out);
 
+/* Test hook: the MC pricer's f64 Box-Muller pair (mc_kernel's normals) on n caller-given
+ * uniform pairs in (0, 1), device pointers, stream-ordered. */
+int32_t rb_device_mc_box_muller(const double* u1, const double* u2, int64_t n, double* z1, double* z2,
+                                void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -127,3 +127,51 @@ def test_two_rank_gloo_summary_gather_equals_one_process():
     assert (one[:, 3] == T).all()  # every env finished STEPS // T episodes of length T
     assert stats["envs"] == N_TOTAL and stats["envs_with_finished_episode"] == N_TOTAL
     assert stats["mean_length"] == pytest.approx(T)
+
+
+def _shard_check_worker(rank, world, port, q, corrupt):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    b = load_bench()
+    n = N_TOTAL // world
+    acts = np.random.default_rng(3).uniform(-1.05, 1.05, size=(STEPS, N_TOTAL, 2)).astype(np.float32)
+    local = torch.from_numpy(shard_summaries(n, rank * n, acts[:, rank * n:(rank + 1) * n]))
+    gathered = torch.empty((world * n, 4), dtype=torch.float32)
+    b.gather_summaries(dist, local, gathered)
+    # the neighbour's last 8 envs, re-run in a shard of their own at their global env ids
+    nb, j0, m = b.shard_check_slice(rank, world, n, 8)
+    assert (nb, j0, m) == ((rank + 1) % world, n - 8, 8)
+    lo = nb * n + j0
+    got = torch.from_numpy(shard_summaries(m, lo, acts[:, lo:lo + m]))
+    if corrupt and rank == 1:
+        got.view(torch.int32)[3, 1] ^= 1   # one bit of one env's P&L sum
+    q.put((rank, b.shard_check_verdict(dist, got, gathered, nb, j0, n)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("corrupt", [False, True])
+def test_two_rank_gloo_shard_check(corrupt):
+    """the self-verifying N-rank line.  Each rank re-runs its neighbour's
+    last envs in a shard of their own and compares the bits of their episode summaries with
+    the all-gathered rows; every rank reports the combined verdict (one flipped bit on one
+    rank -> MISMATCH everywhere, one mismatched row)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_shard_check_worker, args=(r, 2, port, q, corrupt)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in (0, 1):
+        v = res[r]
+        assert v["ranks"] == 2 and v["envs_per_rank"] == 8
+        if corrupt:
+            assert v["result"] == "MISMATCH" and v["mismatched_rows"] == 1
+        else:
+            assert v["result"] == "bit-identical" and v["mismatched_rows"] == 0
+            assert v["finished_episodes_in_checked_rows"] == 8

@@ -1,0 +1,96 @@
+"""The host (NumPy) paths the reference's agents drive, after round 5's single-copy rework:
+`HedgingVecEnv.step_wait` (SB3 collect_rollouts, train_ppo_v2.py:127-141,230) pulls obs,
+reward and done flags in ONE pinned copy, episode ends in one more, and builds the info
+dicts lazily; `HedgingEnv.step` (baselines.py:45-51) copies the env's whole io buffer once.
+These tests hold the contract those shortcuts must keep: returned arrays are never
+overwritten by later steps, an info list read late still shows its own step (terminal obs,
+Monitor episode), and the NumPy path returns exactly what the device path produced."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+DEV = "cuda:0"
+KW = dict(loss_type="abs", pnl_penalty_weight=0.001, lambda_cost=0.0001, theta_weight=0.0002, slippage_bps=1.0)
+GEN = dict(s0=496.48001098632812, variance=0.029028, mu=0.04, dt=1 / 252, episode_length=5)
+MON = ("per_share_step_pnl", "raw_pnl_deviation_abs", "transaction_costs_total")
+
+
+def _pair(n):
+    from cantorrl_amd.vec_env import HedgingVecEnv
+    a = HedgingVecEnv(n, mode="gbm", generate=GEN, seed=21, device=DEV, monitor_keywords=MON, **KW)
+    b = HedgingVecEnv(n, mode="gbm", generate=GEN, seed=21, device=DEV, return_numpy=False, info_keys=MON,
+                      **KW)
+    return a, b
+
+
+@pytest.mark.parametrize("n", [2, 300])
+def test_numpy_path_equals_device_path_and_late_infos_keep_their_step(n):
+    a, b = _pair(n)
+    oa = a.reset()
+    ob = b.reset_tensors().cpu().numpy()
+    assert np.array_equal(oa, ob)
+    rng = np.random.default_rng(1)
+    kept, rets = [], np.zeros(n)
+    for s in range(12):
+        act = rng.uniform(-1, 1, size=(n, 2)).astype(np.float32)
+        a.step_async(act)
+        obs, rew, done, infos = a.step_wait()
+        o2, r2, t2, _ = b.step_tensors(torch.from_numpy(act).to(DEV))
+        tobs_b = b._tobs.cpu().numpy().copy()
+        info_b = {k: b.info_tensor(k).cpu().numpy().copy() for k in MON}
+        assert obs.dtype == np.float32 and obs.shape == (n, 13) and done.dtype == np.bool_
+        assert np.array_equal(obs, o2.cpu().numpy()) and np.array_equal(rew, r2.cpu().numpy())
+        assert np.array_equal(done, t2.cpu().numpy().astype(bool))
+        rets += rew.astype(np.float64)
+        # keep every array and the info list unread, across the later steps
+        kept.append((obs, obs.copy(), rew, rew.copy(), done, done.copy(), infos, tobs_b, info_b, rets.copy()))
+        rets[done] = 0.0
+    for s, (obs, obs_c, rew, rew_c, done, done_c, infos, tobs_b, info_b, ret_s) in enumerate(kept):
+        assert np.array_equal(obs, obs_c) and np.array_equal(rew, rew_c) and np.array_equal(done, done_c), s
+        assert len(infos) == n
+        for i in range(n):
+            d = infos[i]
+            assert d["TimeLimit.truncated"] is False
+            for k in MON:
+                assert d[k] == info_b[k][i], (s, i, k)
+            if done[i]:
+                assert np.array_equal(d["terminal_observation"], tobs_b[i]), (s, i)
+                ep = d["episode"]
+                assert ep["l"] == 5 and ep["r"] == round(float(ret_s[i]), 6), (s, i, ep)
+                assert ep["per_share_step_pnl"] == info_b["per_share_step_pnl"][i]
+            else:
+                assert "terminal_observation" not in d and "episode" not in d
+    assert sum(int(k[4].sum()) for k in kept) == 2 * n   # steps 5 and 10 end every episode
+    a.close()
+    b.close()
+
+
+def test_single_env_step_matches_vector_env_and_holds_no_aliases():
+    """HedgingEnv.step's one copy per step returns the same obs / reward / info as the
+    vector env's device path, and its returned obs is a private array."""
+    from cantorrl_amd.env import HedgingEnv
+    from cantorrl_amd.vec_env import HedgingVecEnv
+    env = HedgingEnv(mode="gbm", generate=GEN, **KW)
+    ref = HedgingVecEnv(1, mode="gbm", generate=GEN, seed=7, device=DEV, autoreset=False, return_numpy=False,
+                        info_keys=("reward_step", "cash", "call_contracts", "portfolio_value"), **KW)
+    o, _ = env.reset(seed=7)
+    r0 = ref.reset_tensors().cpu().numpy()[0]
+    assert np.array_equal(o, r0)
+    prev = o
+    prev_c = o.copy()
+    for s in range(5):
+        act = np.array([0.4, -0.7], np.float32) * (s + 1) / 5
+        o, r, term, trunc, info = env.step(act)
+        ob, rb, tb, _ = ref.step_tensors(torch.from_numpy(act).reshape(1, 2).to(DEV))
+        assert np.array_equal(o, ob.cpu().numpy()[0])
+        assert r == ref.info_tensor("reward_step").cpu().numpy()[0]
+        assert info["cash"] == ref.info_tensor("cash").cpu().numpy()[0]
+        assert info["call_contracts"] == ref.info_tensor("call_contracts").cpu().numpy()[0]
+        assert term == bool(tb.cpu().numpy()[0]) and trunc is False
+        assert np.array_equal(prev, prev_c)   # the last step's obs was not overwritten
+        prev, prev_c = o, o.copy()
+    assert term
+    env.close()
+    ref.close()

@@ -43,7 +43,9 @@ def test_lds_kernels_spill_free():
     replay = {k: v for k, v in meta.items() if "lds_replay_kernel" in k}
     assert len(replay) == 2
     for k, v in replay.items():
-        assert v["vgpr"] <= 128 and v["scratch_B"] <= 16 and v["lds_B"] <= 40 * 1024, (k, v)
+        # the FAST instance (config 6's) spilled 2 VGPRs / 12 B until round 5
+        assert v["vgpr_spill"] == 0 and v["scratch_B"] == 0, (k, v)
+        assert v["vgpr"] <= 128 and v["lds_B"] <= 40 * 1024, (k, v)
 
 
 def test_headline_kernel_sgprs_fit():

@@ -237,7 +237,8 @@ def test_fused_moments_equal_separate_launch(info, monkeypatch):
     np.testing.assert_array_equal(ta, tb)
 
 
-@pytest.mark.parametrize("info,norm_reward,n", [(False, False, 3000), (False, True, 70000), (True, False, 700)])
+@pytest.mark.parametrize("info,norm_reward,n", [(False, False, 3000), (False, True, 70000), (True, False, 700),
+                                                (True, True, 70000)])
 def test_fused_eval_step_equals_separate_launch(info, norm_reward, n, monkeypatch):
     """he_vecnorm_attach_eval (the whole eval VecNormalize step inside he_step's launch, or
     he_vecnorm_apply run by he_step itself after an info step) against he_step +
@@ -321,3 +322,33 @@ def test_two_wrappers_on_one_env_and_inner_steps():
         env2.close()
     finally:
         del os.environ["CANTORRL_VN_FUSED"]
+
+
+@pytest.mark.parametrize("fused", ["1", "0"])
+def test_zero_epsilon_constant_column_clips(fused, monkeypatch):
+    """epsilon = 0 with a zero variance (a constant column) makes 1/sqrt(var + eps)
+    infinite.  Every element of that column is then (x - mean) / 0 = +-inf, clipped to
+    +-clip_obs as SB3's f64 expression does -- not NaN (the f32 split terms were inf - inf);
+    the other columns keep their normalization.  Eval arm fused into he_step and the separate
+    apply launch."""
+    from cantorrl_amd.vec_env import HedgingVecEnv
+    from cantorrl_amd.vec_normalize import DeviceVecNormalize, _RmsView
+    monkeypatch.setenv("CANTORRL_VN_FUSED", fused)
+    n = 300
+    env = HedgingVecEnv(n, mode="gbm", generate=GEN, seed=4, device=DEV, return_numpy=False, info_keys=(), **KW)
+    vn = DeviceVecNormalize(env, training=False, norm_reward=False, epsilon=0.0)
+    mean, var = np.zeros(13), np.ones(13)
+    mean[0], var[0] = 1000.0, 0.0      # no obs equals the mean: every element clips to -10
+    mean[5], var[5] = -1000.0, 0.0     # ... to +10
+    vn.obs_rms = _RmsView(mean, var, 10.0)
+    vn.reset_tensors()
+    for _ in range(3):
+        o, _, _, _ = vn.step_tensors(torch.zeros((n, 2), device=DEV))
+    got = o.cpu().numpy()
+    raw = env._obs.cpu().numpy()
+    assert np.isfinite(got).all()
+    assert (got[:, 0] == -10.0).all() and (got[:, 5] == 10.0).all()
+    rest = [c for c in range(13) if c not in (0, 5)]
+    exp = np.clip((raw[:, rest] - mean[rest]) / np.sqrt(var[rest]), -10, 10)
+    np.testing.assert_allclose(got[:, rest], exp, rtol=0, atol=2e-6)
+    vn.close()
