@@ -1998,12 +1998,25 @@ struct LdsGeom {
 // tile kernels (lds_rollout_eligible).  The producers' per-option table reads are then LDS
 // reads instead of L1/L2 gathers on their critical chain.
 constexpr int kLdsBookRows = 256;
+#ifndef HE_LDS_OBS_LAG
+#define HE_LDS_OBS_LAG 0
+#endif
+// The lean GBM kernel (no book) with HE_LDS_OBS_LAG: the reward stepper evaluates the obs
+// greeks of block b (greeks_lean, the obs stepper's own function and operands: the same bits)
+// at the start of that block into gk, and the obs stepper steps block b one block later -- so
+// the market is triple-buffered.  The obs wave then carries only the row's cheap columns.
+template <int MODE, bool BOOK, bool LEAN>
+constexpr bool lds_lag() {
+    return LEAN && !BOOK && MODE == HE_MODE_GBM && HE_LDS_OBS_LAG;
+}
 template <int MODE, bool BOOK, bool LEAN = false>
 struct LdsMarketT {
-    static constexpr int NB = 2;                                       // market buffers
+    static constexpr bool LAG = lds_lag<MODE, BOOK, LEAN>();
+    static constexpr int NB = LAG ? 3 : 2;                             // market buffers
     float2 sc[NB][kLdsM][kLdsEnvs];
     float pp[NB][kLdsM][kLdsEnvs];
     float stage[2][kLdsEnvs * kObs];                                   // obs row staging, by step parity
+    float gk[LAG ? 2 : 1][3][LAG ? kLdsM : 1][kLdsEnvs];               // LAG: {call_delta, gamma, put_delta} by block parity
     double bk[BOOK ? 2 : 1][BOOK ? kLdsM : 1][kLdsEnvs];                // book value of every slot
     float vv[MODE == HE_MODE_HESTON ? 2 : 1][MODE == HE_MODE_HESTON ? kLdsM : 1][kLdsEnvs];  // Heston: f32 v_t
     double btab[BOOK ? kLdsBookRows : 1][4];  // the book's tau table (p.book_tab), copied at launch start
@@ -2151,7 +2164,13 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
 
     // ---- the block loop over a step function step(buf, sl, k, action, in_full_block)
     constexpr int NB = LdsMarketT<MODE, BOOK, LEAN>::NB;
-    auto run_blk = [&](auto&& step) {
+    // blk(buf, b, len): once per block after its barrier (a block-wide prologue).  LAG: the obs
+    // stepper runs one block behind the reward stepper (an extra barrier first) and the reward
+    // stepper's blk makes the block's obs greeks for it (an extra barrier last), so every wave
+    // makes nb + 2 barriers (the producers one more at their end too).
+    constexpr bool LAG = LdsMarketT<MODE, BOOK, LEAN>::LAG;
+    auto run_blk2 = [&](auto&& blk, auto&& step) {
+        if (LAG && OBS) LDS_BAR();  // one block behind
         LDS_BAR();  // block 0 produced
         for (int b = 0; b < nfull; ++b) {
 #if defined(HE_LDS_DIAG) && HE_LDS_DIAG == 2
@@ -2159,6 +2178,7 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
             continue;
 #endif
             const int buf = b % NB;
+            blk(buf, b, kLdsM);
 #pragma unroll
             for (int sl = 0; sl < kLdsM; ++sl) {
                 const int k = b * kLdsM + sl;
@@ -2167,11 +2187,12 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
                 ra[sl % D] = ld2(gact, (int64_t)(kn < k_steps ? kn : k_steps - 1) * N + i);
                 step(buf, sl, k, ak, std::true_type{});
             }
-            LDS_BAR();  // buffer b & 1 handed back, block b + 1 produced
+            LDS_BAR();  // buffer b % NB handed back, block b + 1 produced
         }
         if (tail) {
 #if !(defined(HE_LDS_DIAG) && HE_LDS_DIAG == 2)
             const int buf = nfull % NB;
+            blk(buf, nfull, tail);
             for (int sl = 0; sl < tail; ++sl) {
                 const int k = nfull * kLdsM + sl;
                 step(buf, sl, k, ld2(gact, (int64_t)k * N + i), std::false_type{});
@@ -2179,7 +2200,9 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
 #endif
             LDS_BAR();
         }
+        if (LAG && !OBS) LDS_BAR();  // the obs stepper's last block
     };
+    auto run_blk = [&](auto&& step) { run_blk2([](int, int, int) {}, step); };
 
     if constexpr (LEAN) {
         // the FAST configuration's constants (fast_config): v2, loss != mse, generate mode
@@ -2199,10 +2222,16 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
             auto obs_step = [&](int buf, int sl, int k, float2 ak, auto full) {
                 const float2 r0 = L.sc[buf][sl][lane];
                 const float rP = L.pp[buf][sl][lane];
-                // the obs greeks: greeks_fast of the market price, as market_kernel makes them
-                // (the reward stepper making them one block ahead, or a block's 8 evaluated in
-                // lockstep up front, measured +-0: r03s12, r03s24)
-                const float4 g = greeks_lean(r0.x, gnd, gis, gsf);
+                // the obs greeks: greeks_fast of the market price, as market_kernel makes them;
+                // LAG: the reward stepper's, made one block ago (a block's 8 evaluated in
+                // lockstep up front here measured +-0: r03s24)
+                float4 g;
+                if constexpr (LAG) {
+                    const int gb = (k / kLdsM) & 1;
+                    g = make_float4(L.gk[gb][0][sl][lane], L.gk[gb][1][sl][lane], L.gk[gb][2][sl][lane], 0.0f);
+                } else {
+                    g = greeks_lean(r0.x, gnd, gis, gsf);
+                }
                 // (i)-(ii) of step_env: the integer trade logic (:181-200)
                 const int32_t nc = e.call + trade_round(ak.x * mt_f, mt);
                 const int32_t nq = e.put + trade_round(ak.y * mt_f, mt);
@@ -2252,7 +2281,31 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
             // reset market's book)
             double pv0 = (double)((shares_f * rst.S + 0.0f) + p.init_cash_f);
             if (BOOK) pv0 = pv0 + rst.B;
-            run_blk([&](int buf, int sl, int k, float2 ak, auto) {
+            // LAG: the obs greeks of each block (greeks_lean of the slot's price: the obs
+            // stepper's bits), for the obs stepper, which steps the block one block later
+            const float gnd = p.g_num_drift, gis = p.g_inv_sst_f, gsf = p.g_sst_f;
+            auto rew_blk = [&](int buf, int b, int len) {
+                if constexpr (LAG) {
+                    const int gb = b & 1;
+                    if (len == kLdsM) {
+#pragma unroll
+                        for (int sl = 0; sl < kLdsM; ++sl) {
+                            const float4 g = greeks_lean(L.sc[buf][sl][lane].x, gnd, gis, gsf);
+                            L.gk[gb][0][sl][lane] = g.x;
+                            L.gk[gb][1][sl][lane] = g.y;
+                            L.gk[gb][2][sl][lane] = g.z;
+                        }
+                    } else {
+                        for (int sl = 0; sl < len; ++sl) {
+                            const float4 g = greeks_lean(L.sc[buf][sl][lane].x, gnd, gis, gsf);
+                            L.gk[gb][0][sl][lane] = g.x;
+                            L.gk[gb][1][sl][lane] = g.y;
+                            L.gk[gb][2][sl][lane] = g.z;
+                        }
+                    }
+                }
+            };
+            run_blk2(rew_blk, [&](int buf, int sl, int k, float2 ak, auto) {
                 const int64_t koff = (int64_t)k * N;
                 const float2 sc = L.sc[buf][sl][lane];
                 const float pP = L.pp[buf][sl][lane];
@@ -2692,6 +2745,7 @@ __device__ __forceinline__ void lds_producer(const Params& p, int k_steps, const
         }
         LDS_BAR();  // block bp handed to the steppers
     }
+    if (LdsMarketT<MODE, BOOK, LEAN>::LAG) LDS_BAR();  // the lagged obs stepper's last block
     // the market position after the launch: every lane ran the whole price chain (Sbs, and
     // Heston's Vbs, the book's running max Mbs are the state after the last step); the last
     // slot's f32 marks are read back from its LDS record (written by this wave, and no wave

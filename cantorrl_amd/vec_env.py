@@ -40,6 +40,10 @@ MONITOR_KEYWORDS = ("per_share_step_pnl", "raw_pnl_deviation_abs", "transaction_
 
 _TORCH_DT = {"f8": torch.float64, "f4": torch.float32, "i4": torch.int32}
 _NP_DT = {torch.float64: np.float64, torch.float32: np.float32, torch.int32: np.int32}
+# the current stream's raw handle (torch's own accessor; current_stream().cuda_stream builds a
+# Stream object per call, a few us of every eager step)
+_raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None) or \
+    (lambda idx: torch.cuda.current_stream(idx).cuda_stream)
 
 
 def _align(x, a):
@@ -108,6 +112,7 @@ class HedgingVecEnv:
             raise _lib.HedgeEnvError("no HIP device visible: libhedgeenv needs an MI355X")
         dev_index = self.device.index if self.device.index is not None else torch.cuda.current_device()
         self.device = torch.device("cuda", dev_index)
+        self._dev_index = dev_index
 
         cfg = _lib.HeConfig()
         _lib.check(self.lib, None, self.lib.he_config_init(cfg, self.variant), "he_config_init")
@@ -221,6 +226,8 @@ class HedgingVecEnv:
             setattr(self._info, k, t.data_ptr())
         self._info_offs = offs
         self._ev = torch.cuda.Event()   # the one host wait of a host pull (_pull)
+        self._step_args = (self._obs.data_ptr(), self._rew.data_ptr(), self._term.data_ptr(), self._trunc.data_ptr(),
+                           self._tobs.data_ptr(), _lib.ctypes.byref(self._info) if self._info_t else None)
         # InfoView snapshots (see InfoView): freeze_infos=False skips them (a view read after
         # a later step then shows that step's values)
         self.freeze_infos = bool(freeze_infos)
@@ -269,7 +276,8 @@ class HedgingVecEnv:
     # ------------------------------------------------------------------ plumbing
     @property
     def stream(self):
-        return torch.cuda.current_stream(self.device).cuda_stream
+        """The caller's current stream on the env device (raw handle)."""
+        return _raw_stream(self._dev_index)
 
     def _ptr(self, t):
         return t.data_ptr() if t is not None else None
@@ -416,11 +424,10 @@ class HedgingVecEnv:
         else:
             act = self._host_actions(actions)
         self._retire_view()
-        st = self.lib.he_step(self._h, act.data_ptr(), self._obs.data_ptr(), self._rew.data_ptr(),
-                              self._term.data_ptr(), self._trunc.data_ptr(),
-                              self._tobs.data_ptr() if terminal_obs else None,
-                              _lib.ctypes.byref(self._info) if (info and self._info_t) else None,
-                              self.stream)
+        # the output pointers are fixed allocations: marshalled once (_step_args)
+        o, r, t, tr, tob, inf = self._step_args
+        st = self.lib.he_step(self._h, act.data_ptr(), o, r, t, tr, tob if terminal_obs else None,
+                              inf if info else None, _raw_stream(self._dev_index))
         _lib.check(self.lib, self._h, st, "he_step")
         if self.check_finite:
             for t in (self._obs, self._rew):

@@ -21,7 +21,10 @@ import numpy as np
 import torch
 
 from . import _lib
-from .vec_env import InfoView
+from .vec_env import InfoView, _raw_stream
+
+# the attributes _params() reads: assigning one drops the cached step arguments
+_PARAM_ATTRS = frozenset(("training", "norm_obs", "norm_reward", "gamma", "clip_obs", "clip_reward", "epsilon"))
 
 
 class _RmsView:
@@ -74,7 +77,7 @@ class DeviceVecNormalize:
         return ctypes.c_void_p(t.data_ptr()) if t is not None else None
 
     def _stream(self):
-        return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+        return _raw_stream(self.venv._dev_index)
 
     def _check(self, st, what):
         if st != _lib.HE_OK:
@@ -172,14 +175,20 @@ class DeviceVecNormalize:
         self._ep_len.zero_()
         return self._obs_out
 
+    def __setattr__(self, name, value):
+        object.__setattr__(self, name, value)
+        if name in _PARAM_ATTRS:   # SB3 flips `training` / `norm_reward` on the object itself
+            object.__setattr__(self, "_args", None)
+
     def _call_args(self):
-        """The ctypes arguments of a step, built once per parameter set: the params struct
-        (and its byref) and every buffer pointer -- the env's step outputs and this object's
-        buffers are fixed allocations, so the eager step marshals nothing new per call."""
-        key = (bool(self.training), bool(self.norm_obs), bool(self.norm_reward), float(self.gamma),
-               float(self.clip_obs), float(self.clip_reward), float(self.epsilon))
+        """The ctypes arguments of a step, built once per parameter set (rebuilt after any of
+        _PARAM_ATTRS is assigned): the params struct (and its byref) and every buffer pointer --
+        the env's step outputs and this object's buffers are fixed allocations, so the eager
+        step marshals nothing new per call."""
         c = self._args
-        if c is None or c[0] != key:
+        if c is None:
+            key = (bool(self.training), bool(self.norm_obs), bool(self.norm_reward), float(self.gamma),
+                   float(self.clip_obs), float(self.clip_reward), float(self.epsilon))
             p = self._params()
             v = self.venv
             ptrs = tuple(self._p(t) for t in (v._obs, v._rew, v._term, v._tobs, self._returns, self._stats,

@@ -64,30 +64,35 @@ e1.record()
 torch.cuda.synchronize()
 print(f"he_vecnorm_apply n={n} (statistics update + normalize; moments fused into he_step): "
       f"{e0.elapsed_time(e1) * 1e3 / R:.2f} us/step", flush=True)
-# env step + vecnorm, one launch each
-e0.record()
-for k in range(64):
-    vn.step_tensors(acts[k])
-e1.record()
-torch.cuda.synchronize()
-print(f"env he_step + vecnorm, eager, moments fused into he_step: {e0.elapsed_time(e1) * 1e3 / 64:.2f} us/step",
-      flush=True)
+# env step + vecnorm, eager (one Python call per step, as SB3 drives it): device time per step
+# between two events, and the host's wall time per call over 256 calls (an eager loop is
+# host-issue-bound when the latter is the larger)
+
+
+def eager_us(step, label, steps=256):
+    for k in range(8):
+        step(k)
+    torch.cuda.synchronize()
+    e0.record()
+    t0 = time.perf_counter()
+    for k in range(steps):
+        step(k % 64)
+    wall = (time.perf_counter() - t0) * 1e6 / steps
+    e1.record()
+    torch.cuda.synchronize()
+    dev_us = e0.elapsed_time(e1) * 1e3 / steps
+    print(f"eager, {label}: {dev_us:.2f} us/step device (events), {wall:.2f} us/step host wall per call", flush=True)
+    return dev_us, wall
+
+
+eager_us(lambda k: vn.step_tensors(acts[k]), "env he_step + vecnorm, moments fused into he_step")
 vn._fusable = False  # detach: he_step, then he_vecnorm_step (moments + apply)
-vn.step_tensors(acts[0])
-torch.cuda.synchronize()
-e0.record()
-for k in range(64):
-    vn.step_tensors(acts[k])
-e1.record()
-torch.cuda.synchronize()
-print(f"env he_step + vecnorm, eager, separate moments launch: {e0.elapsed_time(e1) * 1e3 / 64:.2f} us/step",
-      flush=True)
-e0.record()
-for k in range(64):
-    env.step_tensors(acts[k])
-e1.record()
-torch.cuda.synchronize()
-print(f"env he_step alone, eager: {e0.elapsed_time(e1) * 1e3 / 64:.2f} us/step", flush=True)
+eager_us(lambda k: vn.step_tensors(acts[k]), "env he_step + vecnorm, separate moments launch")
+vn._fusable = True
+vn.training = False
+eager_us(lambda k: vn.step_tensors(acts[k]), "env he_step + vecnorm eval (fused into he_step)")
+vn.training = True
+eager_us(lambda k: env.step_tensors(acts[k]), "env he_step alone")
 
 
 def graph_us(step, label, reps=20):
