@@ -2032,7 +2032,7 @@ static_assert(kLdsM > 8 || sizeof(LdsMarketT<HE_MODE_HESTON, true>) <= 40 * 1024
 // Diagnostic builds only: per wave role (0 reward, 1 obs, 2-3 producers) and workgroup,
 // {cycles from start to end, cycles spent in barriers (s_memtime), 100 MHz ticks from
 // start to end (s_memrealtime)}, read by he_debug_lds_timing.
-__device__ uint64_t g_lds_tim[4][4096][3];
+__device__ uint64_t g_lds_tim[4][4096][5];   // + the role's start and end on the 100 MHz clock
 #define LDS_T0() uint64_t tim_t0 = __builtin_amdgcn_s_memtime(), tim_bar = 0, tim_r0 = __builtin_amdgcn_s_memrealtime()
 #define LDS_BAR()                                                  \
     do {                                                           \
@@ -2045,7 +2045,10 @@ __device__ uint64_t g_lds_tim[4][4096][3];
         if ((threadIdx.x & 63) == 0 && blockIdx.x < 4096) {                              \
             g_lds_tim[role][blockIdx.x][0] = __builtin_amdgcn_s_memtime() - tim_t0;      \
             g_lds_tim[role][blockIdx.x][1] = tim_bar;                                    \
-            g_lds_tim[role][blockIdx.x][2] = __builtin_amdgcn_s_memrealtime() - tim_r0;  \
+            const uint64_t r1_ = __builtin_amdgcn_s_memrealtime();                       \
+            g_lds_tim[role][blockIdx.x][2] = r1_ - tim_r0;                               \
+            g_lds_tim[role][blockIdx.x][3] = tim_r0;                                     \
+            g_lds_tim[role][blockIdx.x][4] = r1_;                                        \
         }                                                                                \
     } while (0)
 #else
