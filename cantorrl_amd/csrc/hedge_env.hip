@@ -1956,7 +1956,26 @@ __global__ __launch_bounds__(kBlock, kFusedWaves) void step_market_kernel(const 
 // 313, 2 314 / 302, 3 305 / 296); with a book or Heston (producer-bound) at 0 (3: config 4
 // +4 %, config 5 +3 %).  The obs wave is the GBM workgroup's critical chain: it wins issue
 // over the producers.
-constexpr int kPrioRew = 3, kPrioRewBook = 0, kPrioReplayRew = 0, kPrioObs = 2, kPrioProd = 1;
+constexpr int kPrioRewBook = 0, kPrioReplayRew = 0, kPrioObs = 2, kPrioProd = 1;
+// GBM without a book (configs 2, 3): the four roles of a SIMD at four distinct priorities, the two
+// producer roles one apart.  At equal priority the SIMD's issue arbitration falls back to age, and
+// on 3 of a CU's 4 SIMDs the producer of the older workgroup won every tie: the CU's oldest
+// workgroup finished ~10 % before the median and the youngest ~7 % after it, and a launch lasts as
+// long as its slowest workgroup (tools/lds_timing.py, r05s6).  With no ties every workgroup wins one
+// producer contest and loses one: the workgroups end within 17 us of each other instead of 53, and
+// the launch takes 295.5 against 300.0 us (3 same-box pairs, r05s8_ab_prio_split.txt).
+#ifndef HE_GP_REW
+#define HE_GP_REW 3
+#endif
+#ifndef HE_GP_OBS
+#define HE_GP_OBS 2
+#endif
+#ifndef HE_GP_P0
+#define HE_GP_P0 1
+#endif
+#ifndef HE_GP_P1
+#define HE_GP_P1 0
+#endif
 // Producer lanes per env: 2 producer waves (4 waves per workgroup, 4 workgroups per CU at 128
 // VGPRs); with a book or Heston same-box A/B against 4 (r02 g2): config 4 1.11e10 -> 1.21e10,
 // config 5 1.19e10 -> 1.25e10 env-steps/s
@@ -2102,8 +2121,18 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
     const GLOBAL v2f* gact = (const GLOBAL v2f*)io.act;
     GLOBAL float* const grew = (GLOBAL float*)io.rew;
     GLOBAL uint8_t* const gterm = (GLOBAL uint8_t*)io.term;
-    if (OBS) __builtin_amdgcn_s_setprio(kPrioObs);
-    else __builtin_amdgcn_s_setprio((BOOK || HESTON) ? kPrioRewBook : kPrioRew);
+    if (!BOOK && !HESTON) {
+        if (OBS) __builtin_amdgcn_s_setprio(HE_GP_OBS);
+        else __builtin_amdgcn_s_setprio(HE_GP_REW);
+    } else {
+#ifdef HE_LDS_BOOK_SPLIT
+        // A/B (book / Heston): obs 3 > producer 0 2 > producer 1 1 > reward 0, no two waves of a SIMD tied
+        if (OBS) __builtin_amdgcn_s_setprio(kPrioObs + 1);
+#else
+        if (OBS) __builtin_amdgcn_s_setprio(kPrioObs);
+#endif
+        else __builtin_amdgcn_s_setprio(kPrioRewBook);
+    }
     LDS_T0();
     Env e{};
     Mkt pre = rst;
@@ -2444,7 +2473,12 @@ __device__ __forceinline__ void lds_producer(const Params& p, int k_steps, const
     const int nb = (k_steps + kLdsM - 1) / kLdsM;
     const uint32_t T = (uint32_t)p.T;
     const int64_t pi = (base + le) < N ? base + le : N - 1;
-    __builtin_amdgcn_s_setprio(kPrioProd);
+    if (!BOOK && !HESTON) {   // the producer roles one priority apart (HE_GP_REW's note)
+        if (pw == 0) __builtin_amdgcn_s_setprio(HE_GP_P0);
+        else __builtin_amdgcn_s_setprio(HE_GP_P1);
+    } else {
+        __builtin_amdgcn_s_setprio(kPrioProd);
+    }
     // the loop carries only the chain state (Sbs, Vbs, Mbs), a0, tpb and pi: the episode
     // counters are re-read after the loop and the Philox id is made per block, so nothing
     // else is live across the block loop (loop-invariant values spilled around it)
@@ -2728,7 +2762,11 @@ __device__ __forceinline__ void lds_producer(const Params& p, int k_steps, const
                     // fixed priority the same role lost them all block long (role timing: prod0
                     // busy 6,981 / prod1 7,808 cycles per step, config 4): same box, config 4
                     // 7.25 -> 7.08 ms, config 5 1.71 -> 1.62 ms per launch (r04s5_ab_prod_prio.txt)
+#ifdef HE_LDS_BOOK_SPLIT
+                    prod_prio_toggle(pw == 0);
+#else
                     prod_prio_toggle((h + pw) & 1);
+#endif
                     if (FULL || sl0 + h < len)
                         W.bk[wb][sl0 + h][le] = book_value<!HESTON>(p, bS[0], bV[0], (int32_t)(tb + 1), bM[0],
                                                                     &W.btab[0][0], &W.bopt[0]);
@@ -2902,7 +2940,13 @@ __device__ __forceinline__ void lds_replay_loader(const Params& p, State s, int 
     const GLOBAL v4f* rec = (const GLOBAL v4f*)p.rec;
     const GLOBAL v4f* recg = (const GLOBAL v4f*)p.recg;
     const int sl0 = part * H;
+#ifdef HE_LDS_REPLAY_SPLIT
+    // A/B: every role of a SIMD at its own priority (obs 3 > loader 0 2 > loader 1 1 > reward 0)
+    if (part == 0) __builtin_amdgcn_s_setprio(kPrioProd + 1);
+    else __builtin_amdgcn_s_setprio(kPrioProd);
+#else
     __builtin_amdgcn_s_setprio(kPrioProd);
+#endif
     LDS_T0();
     int32_t path = s.path[i];
     uint32_t t = s.t[i];                     // episode step before the next slot (< T: autoreset)
@@ -3021,7 +3065,12 @@ __device__ __forceinline__ void lds_replay_stepper(const Params& p, State s, con
     const GLOBAL v2f* gact = (const GLOBAL v2f*)io.act;
     GLOBAL float* const grew = (GLOBAL float*)io.rew;
     GLOBAL uint8_t* const gterm = (GLOBAL uint8_t*)io.term;
+#ifdef HE_LDS_REPLAY_SPLIT
+    if (OBS) __builtin_amdgcn_s_setprio(kPrioObs + 1);
+    else __builtin_amdgcn_s_setprio(kPrioReplayRew);
+#else
     __builtin_amdgcn_s_setprio(OBS ? kPrioObs : kPrioReplayRew);
+#endif
     LDS_T0();
     Env e{};
     e.t = s.t[i];
