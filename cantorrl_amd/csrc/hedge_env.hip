@@ -2925,31 +2925,37 @@ struct LdsReplay {
 };
 static_assert(kLdsM > 8 || sizeof(LdsReplay) <= 40 * 1024 - 64, "4 workgroups per CU");
 
-// Loader wave `part` (0, 1) stages slots [part * H, part * H + H) of every block, H = M / 2; both
-// walk the whole block's positions and PCG64 draws (the same values), part 0 also the
-// new-episode records and the state write-back.
+// Loader wave `part` (0, 1) stages the 32 envs [32 part, 32 part + 32) of the workgroup, two
+// lanes per env: lane l holds env 32 part + (l & 31) and its slots [4 h, 4 h + 4) of every block,
+// h = l >> 5.  Both lanes of an env walk its positions and PCG64 draws (the same values), the h = 0
+// lane also loads the new-episode records and writes the state back.
+//
+// An env's 8 rows of a block are 128 B of the table, one whole line when the block starts on a
+// line (rows t + 1 .. t + 8 with t = 0 mod 8).  With T = 4 mod 8 (the reference's 253-column
+// tables) half the episodes run at t = 4 mod 8: every block's rows are the last 64 B of one line
+// and the first 64 B of the next, whose other half is the next block's first 4 rows; read again a
+// block later that line is fetched from memory a second time (config 6: reads 1.33x their bytes,
+// r05tc1).  In that phase the h = 1 lane loads the whole second line -- its own 4 rows and the
+// next block's first 4 -- and hands the latter to its h = 0 partner (lane - 32) for the next block.
 __device__ __forceinline__ void lds_replay_loader(const Params& p, State s, int k_steps, LdsReplay& L,
                                                   int64_t base, int part) {
     constexpr int H = kLdsM / 2;
+    static_assert(kLdsM == 8, "two lanes per env, 4 slots each: one 128-B line of rows per block");
     const int lane = threadIdx.x & 63;
+    const int hh = lane >> 5;                 // the env's half of the block's slots
+    const int le = part * 32 + (lane & 31);   // local env
     const int64_t N = p.n;
-    const int64_t i0 = base + lane;
-    const int64_t i = i0 < N ? i0 : N - 1;   // lanes past N mirror env N-1
+    const int64_t i0 = base + le;
+    const int64_t i = i0 < N ? i0 : N - 1;    // lanes past N mirror env N-1
     const uint32_t T = (uint32_t)p.T;
-    const int64_t W = p.rstride;             // a path's row stride (128-B lines, row 1 line-aligned)
+    const int64_t W = p.rstride;              // a path's row stride (128-B lines, row 1 line-aligned)
     const GLOBAL v4f* rec = (const GLOBAL v4f*)p.rec;
     const GLOBAL v4f* recg = (const GLOBAL v4f*)p.recg;
-    const int sl0 = part * H;
-#ifdef HE_LDS_REPLAY_SPLIT
-    // A/B: every role of a SIMD at its own priority (obs 3 > loader 0 2 > loader 1 1 > reward 0)
-    if (part == 0) __builtin_amdgcn_s_setprio(kPrioProd + 1);
-    else __builtin_amdgcn_s_setprio(kPrioProd);
-#else
+    const int sl0 = hh * H;
     __builtin_amdgcn_s_setprio(kPrioProd);
-#endif
     LDS_T0();
     int32_t path = s.path[i];
-    uint32_t t = s.t[i];                     // episode step before the next slot (< T: autoreset)
+    uint32_t t = s.t[i];                      // episode step before the next slot (< T: autoreset)
     Pcg64 g;
     g.sh = s.pcg[i];
     g.sl = s.pcg[N + i];
@@ -2960,34 +2966,58 @@ __device__ __forceinline__ void lds_replay_loader(const Params& p, State s, int 
     float s0enc = s.s0[i];
     const int nb = (k_steps + kLdsM - 1) / kLdsM;
     float4 A[H], B[H];
+    float4 Y[H];            // h = 1 lanes: the second line's last 64 B, the next block's rows 0 .. 3
+    bool hand = false;      // the issued block handed Y on (both lanes of the env agree)
     float4 R0 = make_float4(0.f, 0.f, 0.f, 0.f), G0 = R0;  // the new episode's row 0 (lanes ending in the block)
     int rsl = kLdsM;  // slot of the episode end in the issued block (kLdsM: none)
     // the loads of block bp from the position (path, t) before it; the position advanced past it
     auto issue = [&](int bp) {
         const int kb = bp * kLdsM;
         const int len = (k_steps - kb) < kLdsM ? (k_steps - kb) : kLdsM;
+        // the previous block's hand-over: its Y, landed by now, to the h = 0 partner
+        const bool take = hand;
+        if (__ballot(take) != 0ull) {
+#pragma unroll
+            for (int h = 0; h < H; ++h) {
+                Y[h].x = __shfl(Y[h].x, lane | 32);
+                Y[h].y = __shfl(Y[h].y, lane | 32);
+                Y[h].z = __shfl(Y[h].z, lane | 32);
+                Y[h].w = __shfl(Y[h].w, lane | 32);
+            }
+        }
         // the step from t = T - 1 ends the episode (hedging_env_v2.py:217-219): slot T - 1 - t
         const uint32_t te = T - 1u - t;
         rsl = te < (uint32_t)len ? (int)te : kLdsM;
         int32_t np = path;
         if (rsl < kLdsM) np = (int32_t)pcg64_integers(g, (uint64_t)p.n_paths);  // replay_reset's draw
         const int64_t ro = (int64_t)path * W + p.roff + (int64_t)t + 1, rn = (int64_t)np * W + p.roff;
+        // hand Y on from this block: no episode end in it, rows t + 1 .. t + 8 straddling two lines
+        // by 64 B each, and the next block's slots 0 .. 3 still on this path (t + 8 <= T - 4)
+        hand = rsl == kLdsM && (ro & 7) == 4 && t + 12u <= T;
+        if (hh == 0 && take) {
 #pragma unroll
-        for (int h = 0; h < H; ++h) {
-            // slots up to the end read the old path's rows t + 1 + sl (row T holds the lagged
-            // marks), the slots after it the new path's rows 1, 2, ...
-            const int sl = sl0 + h;
-            const int64_t r = (sl <= rsl) ? ro + sl : rn + (sl - rsl);
+            for (int h = 0; h < H; ++h) A[h] = Y[h];
+        } else {
+#pragma unroll
+            for (int h = 0; h < H; ++h) {
+                // slots up to the end read the old path's rows t + 1 + sl (row T holds the lagged
+                // marks), the slots after it the new path's rows 1, 2, ...
+                const int sl = sl0 + h;
+                const int64_t r = (sl <= rsl) ? ro + sl : rn + (sl - rsl);
 #if defined(HE_REPLAY_DIAG) && HE_REPLAY_DIAG == 1
-            A[h] = make_float4(100.0f + (float)sl, 0.04f, 3.0f, 2.5f);  // diagnostic build: no table reads
-            B[h] = make_float4(0.5f, 0.01f, -0.5f, 0.0f);
+                A[h] = make_float4(100.0f + (float)sl, 0.04f, 3.0f, 2.5f);  // diagnostic build: no table reads
 #else
-            A[h] = ld4(rec, r);
+                A[h] = ld4(rec, r);
 #endif
+            }
         }
-        if (part == 0 && rsl < kLdsM) {  // lanes whose episode ends in the block (exec-masked:
-            R0 = ld4(rec, rn);           // the others fetch nothing -- loaded for every env, these
-            G0 = ld4(recg, rn);          // two 16-B records cost 2 lines per env and block)
+        if (hh == 1 && hand) {
+#pragma unroll
+            for (int h = 0; h < H; ++h) Y[h] = ld4(rec, ro + kLdsM + h);
+        }
+        if (hh == 0 && rsl < kLdsM) {   // lanes whose episode ends in the block (exec-masked:
+            R0 = ld4(rec, rn);          // the others fetch nothing -- loaded for every env, these
+            G0 = ld4(recg, rn);         // two 16-B records cost 2 lines per env and block)
         }
         if (rsl < kLdsM) {
             path = np;
@@ -3009,15 +3039,17 @@ __device__ __forceinline__ void lds_replay_loader(const Params& p, State s, int 
 #if !(defined(HE_REPLAY_DIAG) && HE_REPLAY_DIAG == 1)
                     // table_greeks_kernel's record, here from the row itself
                     B[h] = p.record_metrics ? replay_greeks(p, A[h].x, A[h].y) : make_float4(0.f, 0.f, 0.f, 0.f);
+#else
+                    B[h] = make_float4(0.5f, 0.01f, -0.5f, 0.0f);
 #endif
-                    L.mk[wb][sl][lane] = A[h];
-                    L.gd[wb][sl][lane] = make_float2(B[h].x, B[h].z);
-                    L.gg[wb][sl][lane] = B[h].y;
+                    L.mk[wb][sl][le] = A[h];
+                    L.gd[wb][sl][le] = make_float2(B[h].x, B[h].z);
+                    L.gg[wb][sl][le] = B[h].y;
                 }
             }
-            if (part == 0) {
-                L.rk[wb][lane] = R0;
-                L.rg[wb][lane] = G0;
+            if (hh == 0) {
+                L.rk[wb][le] = R0;
+                L.rg[wb][le] = G0;
                 if (rsl < kLdsM) s0enc = (R0.x < 1e-6f) ? -1.0f : R0.x;  // replay_reset's S0 (-1: python 1.0)
             }
             if (bp + 1 < nb) issue(bp + 1);  // in flight while the steppers run block bp
@@ -3025,7 +3057,7 @@ __device__ __forceinline__ void lds_replay_loader(const Params& p, State s, int 
         LDS_BAR();  // block bp handed to the steppers
     }
     LDS_T1(2 + part);
-    if (part == 0 && i0 < N) {
+    if (hh == 0 && i0 < N) {
         int64_t j = i;
         asm volatile("" : "+v"(j));
         s.path[j] = path;
@@ -3065,12 +3097,7 @@ __device__ __forceinline__ void lds_replay_stepper(const Params& p, State s, con
     const GLOBAL v2f* gact = (const GLOBAL v2f*)io.act;
     GLOBAL float* const grew = (GLOBAL float*)io.rew;
     GLOBAL uint8_t* const gterm = (GLOBAL uint8_t*)io.term;
-#ifdef HE_LDS_REPLAY_SPLIT
-    if (OBS) __builtin_amdgcn_s_setprio(kPrioObs + 1);
-    else __builtin_amdgcn_s_setprio(kPrioReplayRew);
-#else
     __builtin_amdgcn_s_setprio(OBS ? kPrioObs : kPrioReplayRew);
-#endif
     LDS_T0();
     Env e{};
     e.t = s.t[i];

@@ -1,8 +1,8 @@
 """Code-object regression guard (CPU, no GPU needed): the built gfx950 library's kernel
 metadata (tools/kernel_meta.py: llvm-readelf of the unbundled code object).  The LDS
 rollout kernels hold no VGPR spills and no scratch at 4 waves per SIMD (VERDICT r3 item 2:
-the book / Heston producers had spilled 28 / 69 VGPRs); lds_replay_kernel<true> keeps its
-two launch-level spills (12 B of scratch outside the block loop, tools/spill_map.py)."""
+the book / Heston producers had spilled 28 / 69 VGPRs); since round 5 lds_replay_kernel<true> is
+spill-free too."""
 import importlib.util
 import os
 import shutil
