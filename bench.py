@@ -613,19 +613,34 @@ def pmc_pass(args, counters, kernels=STEP_KERNELS, probe_argv=None):
             for k, d in rows.items()}, None
 
 
-def pmc_traffic(args):
-    """HBM bytes per step-kernel launch from rocprofv3 PMC counters, one counter per
-    pass (MI355X_MICROARCH.md "HBM": FETCH_SIZE reads 1/2 of a wide coalesced read on
-    gfx950, so bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024).  Runs BEFORE this process
-    touches the GPU; the profiled program is a child (`rocprofv3 ... -- python3`)."""
+READ_REQ_COUNTERS = ["TCC_EA0_RDREQ_sum", "TCC_EA0_RDREQ_32B_sum", "TCC_EA0_RDREQ_64B_sum", "TCC_EA0_RDREQ_128B_sum"]
+
+
+def traffic_bytes(c):
+    """HBM bytes from one kernel's counters {name: per-dispatch value}: the L2's memory-side read
+    requests by size (gfx950's TCC_EA0_RDREQ_{32B,64B,128B}; any request in none of the three
+    counted at 64 B) + WRITE_SIZE (KiB).  Calibrated on known byte counts (tools/traffic_calib.py,
+    profiles/r05s10_traffic_calib.log): a 1 GiB read as a coalesced stream, as 64-B half lines
+    from two waves and as a 128-B line per lane each gives 1,073.8 MB = its bytes, where
+    FETCH_SIZE gives half (MI355X_MICROARCH.md "HBM": rocprofv3's gfx950 FETCH_SIZE takes
+    TCC_BUBBLE for the 128-B requests)."""
+    r32, r64, r128 = (c["TCC_EA0_RDREQ_%s_sum" % w] for w in ("32B", "64B", "128B"))
+    other = max(c["TCC_EA0_RDREQ_sum"] - r32 - r64 - r128, 0.0)
+    return 32.0 * r32 + 64.0 * (r64 + other) + 128.0 * r128 + 1024.0 * c["WRITE_SIZE"]
+
+
+def pmc_traffic(args, kernels=STEP_KERNELS, probe_argv=None):
+    """HBM bytes per step-kernel launch from rocprofv3 PMC counters (traffic_bytes): the sized
+    read requests in one pass, WRITE_SIZE in another.  Runs BEFORE this process touches the
+    GPU; the profiled program is a child (`rocprofv3 ... -- python3`)."""
     vals = {}
-    for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
-        res, err = pmc_pass(args, [ctr])
+    for ctrs in (READ_REQ_COUNTERS, ["WRITE_SIZE"]):
+        res, err = pmc_pass(args, ctrs, kernels, probe_argv)
         if res is None:
             return None, err
-        vals[ctr] = sum(d[ctr] for d in res.values() if ctr in d)
-    traffic = (2.0 * vals["FETCH_SIZE"] + vals["WRITE_SIZE"]) * 1024.0
-    return traffic, vals
+        for ctr in ctrs:
+            vals[ctr] = sum(d[ctr] for d in res.values() if ctr in d)
+    return traffic_bytes(vals), vals
 
 
 VALU_COUNTERS = ["SQ_INSTS_VALU", "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64",
@@ -844,7 +859,7 @@ def step_api_line(n, steps, wall, rf, pmc, layout):
     122 B per env when it evaluates the obs greeks, 134 B when it reads them from the market
     tile) and `frac_survey_8d` on SURVEY 8(d)'s 186 B per env-step (66 of step I/O + the 120-B
     state model, larger than this kernel's 16-B state) -- only the first is the kernel's own
-    roofline.  `traffic` is the kernel's PMC HBM bytes per launch (2 FETCH_SIZE + WRITE_SIZE)."""
+    roofline.  `traffic` is the kernel's PMC HBM bytes per launch (traffic_bytes)."""
     kb = rf["kernel_bytes_per_launch"]
     kgbs = kb / (rf["kernel_us"] * 1e-6) / 1e9
     out = dict(mode="graph (he_step, one launch per step)", value=round(n * steps / wall, 1),
@@ -856,7 +871,7 @@ def step_api_line(n, steps, wall, rf, pmc, layout):
     if pmc[0] is not None:
         out["traffic"] = int(pmc[0])
         out["traffic_over_kernel_bytes"] = round(pmc[0] / kb, 4)
-        out["traffic_counters_kb"] = {k: round(v, 1) for k, v in pmc[1].items()}
+        out["traffic_counters"] = {k: round(v, 1) for k, v in pmc[1].items()}
     else:
         out["traffic_note"] = pmc[1]
     return out
@@ -890,7 +905,7 @@ def finish_roofline(roof, cfg, valu, pmc, kern_ms):
     if pmc[0] is not None:
         roof["traffic"] = int(pmc[0])
         roof["traffic_over_bytes"] = round(pmc[0] / roof["bytes_per_launch"], 4)
-        roof["traffic_counters_kb"] = {k: round(v, 1) for k, v in pmc[1].items()}
+        roof["traffic_counters"] = {k: round(v, 1) for k, v in pmc[1].items()}
     else:
         roof["traffic_note"] = pmc[1]
     if config_bound(cfg) != "valu":
@@ -1082,7 +1097,7 @@ def rb_roofline(valu, traffic, kern_ms, n_opt):
         out["valu_note"] = note
     if traffic[0] is not None:
         out["traffic"] = int(traffic[0])
-        out["traffic_counters_kb"] = {k: round(x, 1) for k, x in traffic[1].items()}
+        out["traffic_counters"] = {k: round(x, 1) for k, x in traffic[1].items()}
     else:
         out["traffic_note"] = traffic[1]
     return out
@@ -1105,15 +1120,7 @@ def rbergomi_main(args):
         pa = ["--workload", "rbergomi", "--rb-paths", str(args.rb_paths), "--rb-normals", args.rb_normals]
         res, err = pmc_pass(args, VALU_COUNTERS, "mc_kernel", probe_argv=pa)
         valu = (valu_summary(res).get("mc_kernel"), None) if res else (None, err)
-        tr = {}
-        for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
-            res, err = pmc_pass(args, [ctr], "mc_kernel", probe_argv=pa)
-            if res is None:
-                traffic = (None, err)
-                break
-            tr[ctr] = res["mc_kernel"][ctr]
-        else:
-            traffic = ((2.0 * tr["FETCH_SIZE"] + tr["WRITE_SIZE"]) * 1024.0, tr)
+        traffic = pmc_traffic(args, "mc_kernel", pa)
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.probe:
         cpu = rb_cpu_baseline(args.cpu_seconds, base)
     dist = None

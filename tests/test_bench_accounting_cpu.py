@@ -179,3 +179,15 @@ def test_rbergomi_roofline_from_the_valu_pass(bench):
     assert r["traffic"] == 3000000
     r0 = bench.rb_roofline((None, "rocprofv3 not found"), (None, "rocprofv3 not found"), 1000.0, 10)
     assert r0["frac"] is None and r0["valu_note"] == "rocprofv3 not found" and r0["traffic"] is None
+
+
+def test_traffic_bytes_from_sized_read_requests(bench):
+    """bench.traffic_bytes: reads by request size (32 / 64 / 128 B; unsized remainder at 64 B) +
+    WRITE_SIZE KiB -- the calibrated reading (profiles/r05s10_traffic_calib.log: a 1 GiB read is
+    8,388,608 requests of 128 B)."""
+    c = dict(TCC_EA0_RDREQ_sum=8388608.0, TCC_EA0_RDREQ_32B_sum=0.0, TCC_EA0_RDREQ_64B_sum=0.0,
+             TCC_EA0_RDREQ_128B_sum=8388608.0, WRITE_SIZE=0.0)
+    assert bench.traffic_bytes(c) == 2.0 ** 30
+    c = dict(TCC_EA0_RDREQ_sum=10.0, TCC_EA0_RDREQ_32B_sum=1.0, TCC_EA0_RDREQ_64B_sum=2.0,
+             TCC_EA0_RDREQ_128B_sum=3.0, WRITE_SIZE=2.0)
+    assert bench.traffic_bytes(c) == 32 + 64 * (2 + 4) + 128 * 3 + 2048
