@@ -682,11 +682,31 @@ __device__ __forceinline__ void ncdf_from_tail(double d, double q, double* pos, 
     *neg = p ? q : 1.0 - q;
 }
 
+// The value of a book option past its expiry (or at zero volatility): the intrinsic value, and a
+// knocked-out up-and-out call 0 -- book_option's expressions for a lane that is not live.
+__device__ __forceinline__ double book_option_intrinsic(const BookOpt& o, double S, double runmax) {
+    double v;
+    if (o.type == HE_BOOK_PUT) {
+        const double ip = o.K - S;
+        v = (ip < 0.0) ? 0.0 : ip;
+    } else {
+        const double ic = S - o.K;
+        v = (ic < 0.0) ? 0.0 : ic;
+        if (o.type == HE_BOOK_UO_CALL) v = (runmax >= o.H) ? 0.0 : v;
+    }
+    return (v < 0.0) ? 0.0 : v;
+}
+
 // One book option (branch-free in the lane-varying quantities: remaining steps, running max).
 __device__ __forceinline__ double book_option(const Params& p, const BookOpt& o, const BookEnv& b, int32_t m,
                                               double runmax, const double* tab) {
     const double K = o.K, S = b.S, r = p.r_d;
     const bool live = m > 0 && b.sig > 0.0;             // tau = m dt > 0 (else intrinsic)
+    // no lane of the wave before the option's expiry: its value is the intrinsic one on every lane,
+    // so the pricer is skipped (the same bits).  Episodes of a fixed length keep a wave's envs in
+    // step, so an option of the book past its expiry is past it on the whole wave (config 4's
+    // expiries 63 / 126 / 189 / 252: 3 of 8 options expired at an average step).
+    if (__ballot(live) == 0ull) return book_option_intrinsic(o, S, runmax);
     const int32_t mc = live ? m : 1;                    // a valid table row either way
     const double tau = (double)mc * p.dt;
     const double* e = tab + 4 * mc;
