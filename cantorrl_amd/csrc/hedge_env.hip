@@ -1984,18 +1984,9 @@ constexpr int kPrioRewBook = 0, kPrioReplayRew = 0, kPrioObs = 2, kPrioProd = 1;
 // long as its slowest workgroup (tools/lds_timing.py, r05s6).  With no ties every workgroup wins one
 // producer contest and loses one: the workgroups end within 17 us of each other instead of 53, and
 // the launch takes 295.5 against 300.0 us (3 same-box pairs, r05s8_ab_prio_split.txt).
-#ifndef HE_GP_REW
-#define HE_GP_REW 3
-#endif
-#ifndef HE_GP_OBS
-#define HE_GP_OBS 2
-#endif
-#ifndef HE_GP_P0
-#define HE_GP_P0 1
-#endif
-#ifndef HE_GP_P1
-#define HE_GP_P1 0
-#endif
+// (priority orders rew/obs/p0/p1 3/1/2/0, 2/3/1/0, 3/0/2/1, 1/2/3/0 measured +2.4 %, +0.4 %, +9 %,
+// -0.2 %: r05s9_ab_prio_perm.txt)
+constexpr int kPrioGbmRew = 3, kPrioGbmObs = 2, kPrioGbmProd0 = 1, kPrioGbmProd1 = 0;
 // Producer lanes per env: 2 producer waves (4 waves per workgroup, 4 workgroups per CU at 128
 // VGPRs); with a book or Heston same-box A/B against 4 (r02 g2): config 4 1.11e10 -> 1.21e10,
 // config 5 1.19e10 -> 1.25e10 env-steps/s
@@ -2037,25 +2028,12 @@ struct LdsGeom {
 // tile kernels (lds_rollout_eligible).  The producers' per-option table reads are then LDS
 // reads instead of L1/L2 gathers on their critical chain.
 constexpr int kLdsBookRows = 256;
-#ifndef HE_LDS_OBS_LAG
-#define HE_LDS_OBS_LAG 0
-#endif
-// The lean GBM kernel (no book) with HE_LDS_OBS_LAG: the reward stepper evaluates the obs
-// greeks of block b (greeks_lean, the obs stepper's own function and operands: the same bits)
-// at the start of that block into gk, and the obs stepper steps block b one block later -- so
-// the market is triple-buffered.  The obs wave then carries only the row's cheap columns.
-template <int MODE, bool BOOK, bool LEAN>
-constexpr bool lds_lag() {
-    return LEAN && !BOOK && MODE == HE_MODE_GBM && HE_LDS_OBS_LAG;
-}
 template <int MODE, bool BOOK, bool LEAN = false>
 struct LdsMarketT {
-    static constexpr bool LAG = lds_lag<MODE, BOOK, LEAN>();
-    static constexpr int NB = LAG ? 3 : 2;                             // market buffers
+    static constexpr int NB = 2;                                       // market buffers
     float2 sc[NB][kLdsM][kLdsEnvs];
     float pp[NB][kLdsM][kLdsEnvs];
     float stage[2][kLdsEnvs * kObs];                                   // obs row staging, by step parity
-    float gk[LAG ? 2 : 1][3][LAG ? kLdsM : 1][kLdsEnvs];               // LAG: {call_delta, gamma, put_delta} by block parity
     double bk[BOOK ? 2 : 1][BOOK ? kLdsM : 1][kLdsEnvs];                // book value of every slot
     float vv[MODE == HE_MODE_HESTON ? 2 : 1][MODE == HE_MODE_HESTON ? kLdsM : 1][kLdsEnvs];  // Heston: f32 v_t
     double btab[BOOK ? kLdsBookRows : 1][4];  // the book's tau table (p.book_tab), copied at launch start
@@ -2142,15 +2120,10 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
     GLOBAL float* const grew = (GLOBAL float*)io.rew;
     GLOBAL uint8_t* const gterm = (GLOBAL uint8_t*)io.term;
     if (!BOOK && !HESTON) {
-        if (OBS) __builtin_amdgcn_s_setprio(HE_GP_OBS);
-        else __builtin_amdgcn_s_setprio(HE_GP_REW);
+        if (OBS) __builtin_amdgcn_s_setprio(kPrioGbmObs);
+        else __builtin_amdgcn_s_setprio(kPrioGbmRew);
     } else {
-#ifdef HE_LDS_BOOK_SPLIT
-        // A/B (book / Heston): obs 3 > producer 0 2 > producer 1 1 > reward 0, no two waves of a SIMD tied
-        if (OBS) __builtin_amdgcn_s_setprio(kPrioObs + 1);
-#else
         if (OBS) __builtin_amdgcn_s_setprio(kPrioObs);
-#endif
         else __builtin_amdgcn_s_setprio(kPrioRewBook);
     }
     LDS_T0();
@@ -2216,13 +2189,7 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
 
     // ---- the block loop over a step function step(buf, sl, k, action, in_full_block)
     constexpr int NB = LdsMarketT<MODE, BOOK, LEAN>::NB;
-    // blk(buf, b, len): once per block after its barrier (a block-wide prologue).  LAG: the obs
-    // stepper runs one block behind the reward stepper (an extra barrier first) and the reward
-    // stepper's blk makes the block's obs greeks for it (an extra barrier last), so every wave
-    // makes nb + 2 barriers (the producers one more at their end too).
-    constexpr bool LAG = LdsMarketT<MODE, BOOK, LEAN>::LAG;
-    auto run_blk2 = [&](auto&& blk, auto&& step) {
-        if (LAG && OBS) LDS_BAR();  // one block behind
+    auto run_blk = [&](auto&& step) {
         LDS_BAR();  // block 0 produced
         for (int b = 0; b < nfull; ++b) {
 #if defined(HE_LDS_DIAG) && HE_LDS_DIAG == 2
@@ -2230,7 +2197,6 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
             continue;
 #endif
             const int buf = b % NB;
-            blk(buf, b, kLdsM);
 #pragma unroll
             for (int sl = 0; sl < kLdsM; ++sl) {
                 const int k = b * kLdsM + sl;
@@ -2244,7 +2210,6 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
         if (tail) {
 #if !(defined(HE_LDS_DIAG) && HE_LDS_DIAG == 2)
             const int buf = nfull % NB;
-            blk(buf, nfull, tail);
             for (int sl = 0; sl < tail; ++sl) {
                 const int k = nfull * kLdsM + sl;
                 step(buf, sl, k, ld2(gact, (int64_t)k * N + i), std::false_type{});
@@ -2252,9 +2217,7 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
 #endif
             LDS_BAR();
         }
-        if (LAG && !OBS) LDS_BAR();  // the obs stepper's last block
     };
-    auto run_blk = [&](auto&& step) { run_blk2([](int, int, int) {}, step); };
 
     if constexpr (LEAN) {
         // the FAST configuration's constants (fast_config): v2, loss != mse, generate mode
@@ -2274,16 +2237,9 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
             auto obs_step = [&](int buf, int sl, int k, float2 ak, auto full) {
                 const float2 r0 = L.sc[buf][sl][lane];
                 const float rP = L.pp[buf][sl][lane];
-                // the obs greeks: greeks_fast of the market price, as market_kernel makes them;
-                // LAG: the reward stepper's, made one block ago (a block's 8 evaluated in
-                // lockstep up front here measured +-0: r03s24)
-                float4 g;
-                if constexpr (LAG) {
-                    const int gb = (k / kLdsM) & 1;
-                    g = make_float4(L.gk[gb][0][sl][lane], L.gk[gb][1][sl][lane], L.gk[gb][2][sl][lane], 0.0f);
-                } else {
-                    g = greeks_lean(r0.x, gnd, gis, gsf);
-                }
+                // the obs greeks: greeks_fast of the market price, as market_kernel makes them
+                // (a block's 8 evaluated in lockstep up front measured +-0: r03s24)
+                const float4 g = greeks_lean(r0.x, gnd, gis, gsf);
                 // (i)-(ii) of step_env: the integer trade logic (:181-200)
                 const int32_t nc = e.call + trade_round(ak.x * mt_f, mt);
                 const int32_t nq = e.put + trade_round(ak.y * mt_f, mt);
@@ -2333,31 +2289,7 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
             // reset market's book)
             double pv0 = (double)((shares_f * rst.S + 0.0f) + p.init_cash_f);
             if (BOOK) pv0 = pv0 + rst.B;
-            // LAG: the obs greeks of each block (greeks_lean of the slot's price: the obs
-            // stepper's bits), for the obs stepper, which steps the block one block later
-            const float gnd = p.g_num_drift, gis = p.g_inv_sst_f, gsf = p.g_sst_f;
-            auto rew_blk = [&](int buf, int b, int len) {
-                if constexpr (LAG) {
-                    const int gb = b & 1;
-                    if (len == kLdsM) {
-#pragma unroll
-                        for (int sl = 0; sl < kLdsM; ++sl) {
-                            const float4 g = greeks_lean(L.sc[buf][sl][lane].x, gnd, gis, gsf);
-                            L.gk[gb][0][sl][lane] = g.x;
-                            L.gk[gb][1][sl][lane] = g.y;
-                            L.gk[gb][2][sl][lane] = g.z;
-                        }
-                    } else {
-                        for (int sl = 0; sl < len; ++sl) {
-                            const float4 g = greeks_lean(L.sc[buf][sl][lane].x, gnd, gis, gsf);
-                            L.gk[gb][0][sl][lane] = g.x;
-                            L.gk[gb][1][sl][lane] = g.y;
-                            L.gk[gb][2][sl][lane] = g.z;
-                        }
-                    }
-                }
-            };
-            run_blk2(rew_blk, [&](int buf, int sl, int k, float2 ak, auto) {
+            run_blk([&](int buf, int sl, int k, float2 ak, auto) {
                 const int64_t koff = (int64_t)k * N;
                 const float2 sc = L.sc[buf][sl][lane];
                 const float pP = L.pp[buf][sl][lane];
@@ -2493,9 +2425,9 @@ __device__ __forceinline__ void lds_producer(const Params& p, int k_steps, const
     const int nb = (k_steps + kLdsM - 1) / kLdsM;
     const uint32_t T = (uint32_t)p.T;
     const int64_t pi = (base + le) < N ? base + le : N - 1;
-    if (!BOOK && !HESTON) {   // the producer roles one priority apart (HE_GP_REW's note)
-        if (pw == 0) __builtin_amdgcn_s_setprio(HE_GP_P0);
-        else __builtin_amdgcn_s_setprio(HE_GP_P1);
+    if (!BOOK && !HESTON) {   // the producer roles one priority apart (kPrioGbmRew's note)
+        if (pw == 0) __builtin_amdgcn_s_setprio(kPrioGbmProd0);
+        else __builtin_amdgcn_s_setprio(kPrioGbmProd1);
     } else {
         __builtin_amdgcn_s_setprio(kPrioProd);
     }
@@ -2782,11 +2714,7 @@ __device__ __forceinline__ void lds_producer(const Params& p, int k_steps, const
                     // fixed priority the same role lost them all block long (role timing: prod0
                     // busy 6,981 / prod1 7,808 cycles per step, config 4): same box, config 4
                     // 7.25 -> 7.08 ms, config 5 1.71 -> 1.62 ms per launch (r04s5_ab_prod_prio.txt)
-#ifdef HE_LDS_BOOK_SPLIT
-                    prod_prio_toggle(pw == 0);
-#else
                     prod_prio_toggle((h + pw) & 1);
-#endif
                     if (FULL || sl0 + h < len)
                         W.bk[wb][sl0 + h][le] = book_value<!HESTON>(p, bS[0], bV[0], (int32_t)(tb + 1), bM[0],
                                                                     &W.btab[0][0], &W.bopt[0]);
@@ -2806,7 +2734,6 @@ __device__ __forceinline__ void lds_producer(const Params& p, int k_steps, const
         }
         LDS_BAR();  // block bp handed to the steppers
     }
-    if (LdsMarketT<MODE, BOOK, LEAN>::LAG) LDS_BAR();  // the lagged obs stepper's last block
     // the market position after the launch: every lane ran the whole price chain (Sbs, and
     // Heston's Vbs, the book's running max Mbs are the state after the last step); the last
     // slot's f32 marks are read back from its LDS record (written by this wave, and no wave
@@ -2870,11 +2797,7 @@ __device__ __forceinline__ int lds_role(int wave) {
         const uint32_t m = (1u << sh_place[0]) | (1u << sh_place[1]) | (1u << sh_place[2]) | (1u << sh_place[3]);
         int role = wave;
 #if HE_LDS_BALANCE
-#ifdef HE_LDS_ROLE_XOR
-        if (m == 15u) role = (int)((simd ^ sh_place[4]) & 3u);
-#else
         if (m == 15u) role = (int)((simd + sh_place[4]) & 3u);
-#endif
 #endif
 #ifdef HE_LDS_HWID
         if ((threadIdx.x & 63) == 0 && blockIdx.x < 16384) {
