@@ -349,18 +349,21 @@ def bench_actions(n, rank, dev):
 
 
 # ---------------------------------------------------------------------- shard check
-# After the timed region each rank re-runs SHARD_CHECK_ENVS envs of its NEIGHBOUR's shard
-# (the last ones of rank (r + 1) % world) in a handle of their own, with the neighbour's
-# actions and the same launches, and compares the bits of their episode summaries with the
-# rows the all-gather delivered: the shards are a partition of one global env set whatever
-# the GPU count (Philox keyed by the global env id), and the gather puts them
-# in global env order.  At one rank it checks the handle's own last envs.
-SHARD_CHECK_ENVS = 64
+# After the timed region each rank re-runs its NEIGHBOUR's shard (rank (r + 1) % world) in a
+# handle of its own of the same size, with the neighbour's actions and the same launches, and
+# compares the bits of its episode summaries with the rows the all-gather delivered: the shards
+# are a partition of one global env set whatever the GPU count (Philox keyed by the global env
+# id), and the gather puts them in global env order.  At one rank it checks the
+# handle's own envs.  The whole shard, not a slice: the check's launches then have the timed
+# launches' grid, so a rocprofv3 --stats summary of the run averages one launch shape (a 64-env
+# slice ran 1-workgroup launches of the same kernel that pulled the average down).
+SHARD_CHECK_ENVS = None   # None: the whole shard
 
 
 def shard_check_slice(rank, world, n, m=SHARD_CHECK_ENVS):
-    """(neighbour rank, its first checked env, count): the last min(m, n) envs of (r + 1) % world."""
-    m = min(m, n)
+    """(neighbour rank, its first checked env, count): the last min(m, n) envs of (r + 1) % world
+    (m None: all n)."""
+    m = n if m is None else min(m, n)
     return (rank + 1) % world, n - m, m
 
 
