@@ -185,6 +185,16 @@ HE_HD float div_f32_by(float a, double b, double y64) {
     return (a == 0.0f || !(fabsf(a) <= 3.4028234663852886e38f)) ? (float)q : res;
 }
 
+// f32 a / b for an f32 b with y = RN32(1/b), when a and a / b are normal f32 numbers (the lean
+// GBM obs prices over the constant max(S0, 25): S >= 1e-8, C, P >= 0): Markstein's step in f32,
+// RN32(a/b) by the theorem (y within half an ulp of 1/b, a*y within one ulp of a/b) -- the value
+// div_f32_by makes through f64.  Zero / inf / NaN dividends take a*y, as there.
+HE_HD float div_f32_byf(float a, float b, float y) {
+    const float q = a * y;
+    const float res = fmaf(fmaf(-q, b, a), y, q);
+    return (a == 0.0f || !(fabsf(a) <= 3.4028234663852886e38f)) ? q : res;
+}
+
 // np.rint(f32).astype(int64) then np.clip(., -mt, mt)  (hedging_env_v2.py:184-188).
 // x86 cvttss2si maps NaN and |x| >= 2^63 to INT64_MIN, which the clip sends to -mt.
 // Branch-free (selects only): the step kernels keep whole steps in one basic block.

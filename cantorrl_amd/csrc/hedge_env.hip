@@ -1971,6 +1971,7 @@ __global__ __launch_bounds__(kBlock, kFusedWaves) void step_market_kernel(const 
 #ifndef HE_LDS_BALANCE
 #define HE_LDS_BALANCE 1
 #endif
+
 // Wave priorities (s_setprio).  The reward stepper above the obs stepper, GBM without a book
 // (same-box A/B r03s9, config 2, two runs each: priority 0 312 / 300 us per launch, 1 319 /
 // 313, 2 314 / 302, 3 305 / 296); with a book or Heston (producer-bound) at 0 (3: config 4
@@ -2224,7 +2225,7 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
         const float mt_f = p.mt_f, maxh_f = p.maxh_f, inv_maxh_f = p.inv_maxh_f;
         const int32_t mt = p.mt, maxh = p.maxh, T = p.T;
         if (OBS) {
-            const double s0s_d = p.s0s_d, inv_s0s_d = p.inv_s0s_d;
+            const float s0s_f = p.s0s_f, inv_s0s_f = p.inv_s0s_f;
             const float T_f = p.T_f, inv_T_f = p.inv_T_f, var_f = p.var_f;
             // the per-step constants held in VGPRs (opaque: the scalar reloads they would
             // otherwise be rematerialized as share lgkmcnt with the LDS traffic)
@@ -2250,9 +2251,12 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
                 // make_obs<true> (hedging_env_v2.py:109-143) on the post-step state, or the
                 // reset obs on a terminal step (SB3 autoreset)
                 float o[kObs];
-                o[0] = div_f32_by(r0.x, s0s_d, inv_s0s_d);
-                o[1] = div_f32_by(r0.y, s0s_d, inv_s0s_d);
-                o[2] = div_f32_by(rP, s0s_d, inv_s0s_d);
+                // the three price columns over max(S0, 25) by f32 Markstein steps (div_f32_byf: the
+                // lean GBM prices are normal f32 numbers) instead of through f64: 292.6 -> 287.8 us
+                // per launch, 3 same-box pairs (r05s13_ab_obs_f32.txt)
+                o[0] = div_f32_byf(r0.x, s0s_f, inv_s0s_f);
+                o[1] = div_f32_byf(r0.y, s0s_f, inv_s0s_f);
+                o[2] = div_f32_byf(rP, s0s_f, inv_s0s_f);
                 o[3] = div_int_byf((float)cc, maxh_f, inv_maxh_f);
                 o[4] = div_int_byf((float)qq, maxh_f, inv_maxh_f);
                 o[5] = var_f;
@@ -2266,8 +2270,17 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
                 // staged in LDS (two tiles, alternating by step: the next step's row writes
                 // do not wait behind this step's read-back) and stored as whole 16-B lines
                 float* const tile = L.stage[k & 1];
+                // the reset row over it only on a step that ends an episode (a wave-uniform branch:
+                // fixed-length episodes end together) instead of 13 selects every step (with the f32
+                // quotients 287.8 -> 286.5 us, r05s13_ab_obs_f32.txt)
 #pragma unroll
-                for (int c = 0; c < kObs; ++c) tile[lane * kObs + c] = term ? ro[c] : o[c];
+                for (int c = 0; c < kObs; ++c) tile[lane * kObs + c] = o[c];
+                if (__ballot(term) != 0ull) {
+                    if (term) {
+#pragma unroll
+                        for (int c = 0; c < kObs; ++c) tile[lane * kObs + c] = ro[c];
+                    }
+                }
                 float* out = io.obs + (int64_t)k * N * kObs;
                 if constexpr (decltype(full)::value) flush_obs_full(tile, out, base, lane);
                 else flush_obs_wave(tile, out, base, wrows, lane);
