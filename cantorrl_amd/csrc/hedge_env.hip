@@ -251,6 +251,7 @@ struct Env {
     bool s0_small;
     // replay LDS steppers (EP): the episode's quotient constants (replay_episode_consts)
     double s0s_d, inv_s0s_d;  // max(S0, 25) of the obs prices (inf as DBL_MAX) and RN(1/.)
+    float s0s_f, inv_s0s_f;   // the same in f32, RN32(1/.): the FAST replay obs (lds_replay_stepper)
     double den;               // the reward denominator
 };
 
@@ -274,6 +275,8 @@ __device__ __forceinline__ void replay_episode_consts(const Params& p, Env& e) {
     const double fd = (double)f;
     e.s0s_d = (fd == __builtin_inf()) ? 1.7976931348623157e308 : fd;
     e.inv_s0s_d = 1.0 / fd;
+    e.s0s_f = f;
+    e.inv_s0s_f = 1.0f / f;
     e.den = replay_den<FAST>(p, e.s0, e.s0_small);
 }
 
@@ -3132,6 +3135,8 @@ __device__ __forceinline__ void lds_replay_stepper(const Params& p, State s, con
             e.s0_small = term ? n.s0_small : e.s0_small;
             e.s0s_d = term ? n.s0s_d : e.s0s_d;
             e.inv_s0s_d = term ? n.inv_s0s_d : e.inv_s0s_d;
+            e.s0s_f = term ? n.s0s_f : e.s0s_f;
+            e.inv_s0s_f = term ? n.inv_s0s_f : e.inv_s0s_f;
             pre.S = term ? m0.S : pre.S;
             pre.v = term ? m0.v : pre.v;
         }
@@ -3152,9 +3157,12 @@ __device__ __forceinline__ void lds_replay_stepper(const Params& p, State s, con
             const bool term = (int32_t)e.t >= T;
             float o[kObs];
             if (FAST) {  // make_obs<true, true> on the pinned constants (hedging_env_v2.py:109-143)
-                o[0] = div_f32_by(post.S, e.s0s_d, e.inv_s0s_d);
-                o[1] = div_f32_by(post.C, e.s0s_d, e.inv_s0s_d);
-                o[2] = div_f32_by(post.P, e.s0s_d, e.inv_s0s_d);
+                // f32 Markstein steps (div_f32_byf): the FAST kernel runs only on an ordinary table
+                // (he_env::table_ordinary: max(S0, 25) <= 2^24 and every price 0, NaN, inf or of
+                // magnitude >= 2^-100, so no quotient or residual leaves the normal range)
+                o[0] = div_f32_byf(post.S, e.s0s_f, e.inv_s0s_f);
+                o[1] = div_f32_byf(post.C, e.s0s_f, e.inv_s0s_f);
+                o[2] = div_f32_byf(post.P, e.s0s_f, e.inv_s0s_f);
                 o[3] = div_int_byf((float)e.call, c_maxh_f, c_inv_maxh_f);
                 o[4] = div_int_byf((float)e.put, c_maxh_f, c_inv_maxh_f);
                 o[5] = post.v;
@@ -3572,6 +3580,9 @@ struct he_env {
     unsigned long long* scratch_count = nullptr;  // he_rollout_policy without records
     double book_rst = 0.0;      // book value of the reset market (host copy)
     int64_t n_paths = 0;
+    // every price of the loaded table 0, NaN, inf or of magnitude >= 2^-100, every S0 <= 2^24
+    // (he_load_paths): the FAST replay kernel's f32 obs quotients apply (fast_replay_config)
+    bool table_ordinary = false;
     int32_t block_pos = 0;    // generate: next slot to consume; M = tile exhausted/invalid
     int32_t cur_buf = 0;      // tile buffer of the block being consumed
     int32_t next_state = 0;   // next block: 0 none, 1 generating on `xs` (ev_next), 2 ready
@@ -4070,7 +4081,7 @@ static bool lds_replay_eligible(const he_env* env, const Io& io) {
 static bool fast_replay_config(const he_env* env) {
     const he_config& c = env->cfg;
     return c.mode == HE_MODE_REPLAY && c.variant == 2 && c.loss_type != HE_LOSS_MSE && c.shares_to_hedge != 0 &&
-           c.record_metrics && c.max_contracts_held_per_type > 0 && env->p.T > 0;
+           c.record_metrics && c.max_contracts_held_per_type > 0 && env->p.T > 0 && env->table_ordinary;
 }
 
 static he_status launch_lds_replay(he_env* env, const Io& io, int k_total, hipStream_t st) {
@@ -4398,6 +4409,10 @@ he_status he_load_paths(he_env* env, const float* S, const float* v, const float
     } catch (...) {
         return fail(env, HE_ENOMEM, "host allocation of %lld records failed", (long long)(n_paths * W));
     }
+    // an ordinary table (he_env::table_ordinary): prices 0, NaN, inf or >= 2^-100 in magnitude,
+    // S0 (row 0; < 1e-6 is replaced by 1) <= 2^24
+    auto ordinary = [](float a) { return !(fabsf(a) < 7.8886090522101181e-31f) || a == 0.0f; };
+    bool ord = true;
     for (int64_t q = 0; q < n_paths; ++q) {
         for (int64_t t = 0; t <= T; ++t) {
             int64_t tc = t < T ? t : T - 1;  // terminal step keeps the last marks (:229-231)
@@ -4407,7 +4422,9 @@ he_status he_load_paths(he_env* env, const float* S, const float* v, const float
             r.z = C[q * T + tc];
             r.w = P[q * T + tc];
             rec[(size_t)(q * W + kRowOff + t)] = r;
+            ord = ord && ordinary(r.x) && ordinary(r.z) && ordinary(r.w);
         }
+        ord = ord && (S[q * n_cols] < 1e-6f || S[q * n_cols] <= 16777216.0f);
     }
     const size_t bytes = rec.size() * sizeof(float4);
     float4* d = nullptr;
@@ -4430,6 +4447,7 @@ he_status he_load_paths(he_env* env, const float* S, const float* v, const float
     env->rec = d;
     env->recg = dg2;
     env->n_paths = n_paths;
+    env->table_ordinary = ord;
     env->cfg.episode_length = (int32_t)T;
     env->ready = false;
     he_status st = upload_tables(env);
