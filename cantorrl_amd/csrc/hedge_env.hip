@@ -2032,9 +2032,16 @@ struct LdsGeom {
 // tile kernels (lds_rollout_eligible).  The producers' per-option table reads are then LDS
 // reads instead of L1/L2 gathers on their critical chain.
 constexpr int kLdsBookRows = 256;
+// The lean reward stepper's time-penalty terms theta (T - t) / 252 by episode step t, made once
+// per launch (thp in LdsMarketT; without a book: headline 287.5 -> 283.7 us, 3 of 3 same-box
+// pairs; with one config 4 lost 0.5 %, r05s17_ab_thp_table.txt): episodes of fewer than
+// lds_thp_rows steps take the lean kernel without a book (lds_lean_config)
+constexpr int lds_thp_rows() { return 512; }
 template <int MODE, bool BOOK, bool LEAN = false>
 struct LdsMarketT {
     static constexpr int NB = 2;                                       // market buffers
+    static constexpr bool THP = LEAN && !BOOK;
+    double thp[THP ? lds_thp_rows() : 1];
     float2 sc[NB][kLdsM][kLdsEnvs];
     float pp[NB][kLdsM][kLdsEnvs];
     float stage[2][kLdsEnvs * kObs];                                   // obs row staging, by step parity
@@ -2305,6 +2312,13 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
             // reset market's book)
             double pv0 = (double)((shares_f * rst.S + 0.0f) + p.init_cash_f);
             if (BOOK) pv0 = pv0 + rst.B;
+            // without a book: the time penalty by episode step, theta * (T - t1) / 252 (:257-259),
+            // into this wave's table (T < lds_thp_rows: lds_lean_config) -- an LDS read per step
+            // instead of an int conversion, an f64 quotient and a multiply; this wave's only
+            if constexpr (LdsMarketT<MODE, BOOK, LEAN>::THP) {
+                for (int t = lane; t <= T; t += 64)
+                    L.thp[t] = theta * div_int_by((double)(T - t), 252.0, inv_252);
+            }
             run_blk([&](int buf, int sl, int k, float2 ak, auto) {
                 const int64_t koff = (int64_t)k * N;
                 const float2 sc = L.sc[buf][sl][lane];
@@ -2335,7 +2349,9 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
                 const double term_v = div_by_nb(fabs(ps), den, inv_den);
                 const double rpc = (-w) * term_v;
                 const double tcp = lam * tc;
-                const double thp = theta * div_int_by((double)(T - (int32_t)t1), 252.0, inv_252);
+                const double thp = LdsMarketT<MODE, BOOK, LEAN>::THP
+                                       ? L.thp[LdsMarketT<MODE, BOOK, LEAN>::THP ? t1 : 0]
+                                       : theta * div_int_by((double)(T - (int32_t)t1), 252.0, inv_252);
                 const double reward = (rpc - tcp) - thp;
                 grew[koff + i] = (float)reward;
                 gterm[koff + i] = term ? 1 : 0;
@@ -4023,7 +4039,7 @@ static bool lds_lean_config(const he_env* env, const Io& io) {
     const bool normal_greeks = !p.tenor_small && p.g_sigma > 1e-6f && p.g_sst >= 1e-9;  // greeks_lean
     // the lean kernels' producers make rolling-ATM marks only (marks<MODE, false>)
     return fast_config(env) && io.obs && io.rew && io.term && s0 >= 1e-30 && s0 <= 1e30 && ic <= 1e30 &&
-           normal_greeks && c.mark == HE_MARK_ROLLING_ATM;
+           normal_greeks && c.mark == HE_MARK_ROLLING_ATM && (c.book_size > 0 || p.T < lds_thp_rows());
 }
 
 // he_rollout through lds_rollout_kernel: GBM or Heston, with or without a book (HE_LDS_ROLLOUT=0
