@@ -2118,7 +2118,6 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
                                             LdsMarketT<MODE, BOOK, LEAN>& L, int64_t base) {
     constexpr int D = kLdsPrefetch;
     constexpr bool HESTON = MODE == HE_MODE_HESTON;
-    static_assert(!(LEAN && HESTON), "the lean steppers take the constant GBM variance");
     const int lane = threadIdx.x & 63;
     const int64_t N = p.n;
     const int nfull = k_steps / kLdsM;          // full blocks
@@ -2245,12 +2244,21 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
             for (int c = 0; c < kObs; ++c) ro[c] = p.rstv[4 + c];
             float preS = pre.S;
             if (e.t != 0) preS = (float)cur.S[i];
+            // Heston: the slot's f32 variance v_t (obs column 5, the greeks' sigma) and the previous
+            // step's (column 12's change)
+            float preV = rst.v;
+            if (HESTON && e.t != 0) preV = (float)cur.v[i];
+            const double s0s_d = p.s0s_d, inv_s0s_d = p.inv_s0s_d;
             auto obs_step = [&](int buf, int sl, int k, float2 ak, auto full) {
                 const float2 r0 = L.sc[buf][sl][lane];
                 const float rP = L.pp[buf][sl][lane];
+                const float vk = HESTON ? L.vv[HESTON ? buf : 0][HESTON ? sl : 0][lane] : var_f;
                 // the obs greeks: greeks_fast of the market price, as market_kernel makes them
-                // (a block's 8 evaluated in lockstep up front measured +-0: r03s24)
-                const float4 g = greeks_lean(r0.x, gnd, gis, gsf);
+                // (a block's 8 evaluated in lockstep up front measured +-0: r03s24); Heston: at the
+                // slot's variance, the generic steppers' greeks_fast<false>
+                float4 g;
+                if constexpr (HESTON) g = greeks_fast<false>(p, r0.x, vk);
+                else g = greeks_lean(r0.x, gnd, gis, gsf);
                 // (i)-(ii) of step_env: the integer trade logic (:181-200)
                 const int32_t nc = e.call + trade_round(ak.x * mt_f, mt);
                 const int32_t nq = e.put + trade_round(ak.y * mt_f, mt);
@@ -2264,19 +2272,27 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
                 // the three price columns over max(S0, 25) by f32 Markstein steps (div_f32_byf: the
                 // lean GBM prices are normal f32 numbers) instead of through f64: 292.6 -> 287.8 us
                 // per launch, 3 same-box pairs (r05s13_ab_obs_f32.txt)
-                o[0] = div_f32_byf(r0.x, s0s_f, inv_s0s_f);
-                o[1] = div_f32_byf(r0.y, s0s_f, inv_s0s_f);
-                o[2] = div_f32_byf(rP, s0s_f, inv_s0s_f);
+                if constexpr (HESTON) {
+                    // through f64 (div_f32_by): at a near-zero variance the Heston marks can be
+                    // tiny, where the f32 step's residual leaves the normal range
+                    o[0] = div_f32_by(r0.x, s0s_d, inv_s0s_d);
+                    o[1] = div_f32_by(r0.y, s0s_d, inv_s0s_d);
+                    o[2] = div_f32_by(rP, s0s_d, inv_s0s_d);
+                } else {
+                    o[0] = div_f32_byf(r0.x, s0s_f, inv_s0s_f);
+                    o[1] = div_f32_byf(r0.y, s0s_f, inv_s0s_f);
+                    o[2] = div_f32_byf(rP, s0s_f, inv_s0s_f);
+                }
                 o[3] = div_int_byf((float)cc, maxh_f, inv_maxh_f);
                 o[4] = div_int_byf((float)qq, maxh_f, inv_maxh_f);
-                o[5] = var_f;
+                o[5] = vk;
                 o[6] = div_int_byf((float)(T - (int32_t)t1), T_f, inv_T_f);
                 o[7] = g.x;
                 o[8] = g.y;
                 o[9] = g.z;
                 o[10] = g.y;
                 o[11] = lag_return(r0.x, preS);
-                o[12] = (preS == 0.0f) ? 0.0f : np_clipf(var_f - var_f, -1.0f, 1.0f);
+                o[12] = (preS == 0.0f) ? 0.0f : np_clipf(vk - (HESTON ? preV : var_f), -1.0f, 1.0f);
                 // staged in LDS (two tiles, alternating by step: the next step's row writes
                 // do not wait behind this step's read-back) and stored as whole 16-B lines
                 float* const tile = L.stage[k & 1];
@@ -2298,6 +2314,7 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
                 e.call = term ? 0 : cc;
                 e.put = term ? 0 : qq;
                 preS = term ? rst.S : r0.x;
+                if (HESTON) preV = term ? rst.v : vk;
             };
             if (wrows == kLdsEnvs)
                 run_blk([&](int buf, int sl, int k, float2 ak, auto) { obs_step(buf, sl, k, ak, std::true_type{}); });
@@ -4036,7 +4053,8 @@ static bool lds_lean_config(const he_env* env, const Io& io) {
     const he_config& c = env->cfg;
     const double s0 = c.s0, ic = fabs(c.initial_cash);
     const Params& p = env->p;
-    const bool normal_greeks = !p.tenor_small && p.g_sigma > 1e-6f && p.g_sst >= 1e-9;  // greeks_lean
+    // greeks_lean's constants (GBM); the Heston lean obs takes greeks_fast<false> at the slot's v
+    const bool normal_greeks = c.mode == HE_MODE_HESTON || (!p.tenor_small && p.g_sigma > 1e-6f && p.g_sst >= 1e-9);
     // the lean kernels' producers make rolling-ATM marks only (marks<MODE, false>)
     return fast_config(env) && io.obs && io.rew && io.term && s0 >= 1e-30 && s0 <= 1e30 && ic <= 1e30 &&
            normal_greeks && c.mark == HE_MARK_ROLLING_ATM && (c.book_size > 0 || p.T < lds_thp_rows());
@@ -4060,8 +4078,11 @@ static he_status launch_lds_rollout(he_env* env, const Io& io, int k_total, hipS
     const bool book = env->cfg.book_size > 0, lean = lds_lean_config(env, io);
     void (*kern)(const Params*, State, Io, int, Market);
     int threads;
-    if (env->cfg.mode == HE_MODE_HESTON) {  // generic steppers (the lean ones take a constant variance)
-        kern = book ? lds_rollout_kernel<HE_MODE_HESTON, true, false> : lds_rollout_kernel<HE_MODE_HESTON, false, false>;
+    if (env->cfg.mode == HE_MODE_HESTON) {
+        if (lean)
+            kern = book ? lds_rollout_kernel<HE_MODE_HESTON, true, true> : lds_rollout_kernel<HE_MODE_HESTON, false, true>;
+        else
+            kern = book ? lds_rollout_kernel<HE_MODE_HESTON, true, false> : lds_rollout_kernel<HE_MODE_HESTON, false, false>;
         threads = book ? LdsGeom<HE_MODE_HESTON, true>::threads : LdsGeom<HE_MODE_HESTON, false>::threads;
     } else if (book) {
         kern = lean ? lds_rollout_kernel<HE_MODE_GBM, true, true> : lds_rollout_kernel<HE_MODE_GBM, true, false>;

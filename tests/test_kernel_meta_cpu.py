@@ -35,7 +35,7 @@ def _meta():
 def test_lds_kernels_spill_free():
     meta = _meta()
     rollout = {k: v for k, v in meta.items() if "lds_rollout_kernel" in k}
-    assert len(rollout) == 6, sorted(rollout)   # GBM / Heston x book x lean instances
+    assert len(rollout) == 8, sorted(rollout)   # GBM / Heston x book x lean instances
     for k, v in rollout.items():
         assert v["vgpr_spill"] == 0 and v["scratch_B"] == 0, (k, v)
         assert v["vgpr"] <= 128, (k, v)         # 4 waves per SIMD
