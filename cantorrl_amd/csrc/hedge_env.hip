@@ -1975,6 +1975,7 @@ __global__ __launch_bounds__(kBlock, kFusedWaves) void step_market_kernel(const 
 #define HE_LDS_BALANCE 1
 #endif
 
+
 // Wave priorities (s_setprio).  The reward stepper above the obs stepper, GBM without a book
 // (same-box A/B r03s9, config 2, two runs each: priority 0 312 / 300 us per launch, 1 319 /
 // 313, 2 314 / 302, 3 305 / 296); with a book or Heston (producer-bound) at 0 (3: config 4
@@ -2759,11 +2760,16 @@ __device__ __forceinline__ void lds_producer(const Params& p, int k_steps, const
 #pragma unroll 1
                 for (int h = 0; h < kLdsH; ++h) {
                     // the two producer roles share each SIMD (one wave of each, from different
-                    // workgroups): which one wins the issue ties alternates slot by slot.  At one
+                    // workgroups): which one wins the issue ties changes slot by slot.  At one
                     // fixed priority the same role lost them all block long (role timing: prod0
                     // busy 6,981 / prod1 7,808 cycles per step, config 4): same box, config 4
-                    // 7.25 -> 7.08 ms, config 5 1.71 -> 1.62 ms per launch (r04s5_ab_prod_prio.txt)
-                    prod_prio_toggle((h + pw) & 1);
+                    // 7.25 -> 7.08 ms, config 5 1.71 -> 1.62 ms per launch (r04s5_ab_prod_prio.txt).
+                    // Alternating 2:2 still left the second role the busier (config 4 5,533 / 6,144,
+                    // config 5 4,955 / 6,244 cycles per step).  GBM: it is up on 3 slots of 4 --
+                    // 5,696 / 5,828 and 5.71 -> 5.63 ms.  Heston keeps 2:2: 3:1 gave 5,137 / 6,072
+                    // and +0.2 %, 4:0 6,498 / 4,451 and +0.6 % (r05s20_ab_prod_toggle.txt)
+                    if (HESTON) prod_prio_toggle((h + pw) & 1);
+                    else prod_prio_toggle(pw == 1 ? (h != 3) : (h == 3));
                     if (FULL || sl0 + h < len)
                         W.bk[wb][sl0 + h][le] = book_value<!HESTON>(p, bS[0], bV[0], (int32_t)(tb + 1), bM[0],
                                                                     &W.btab[0][0], &W.bopt[0]);
