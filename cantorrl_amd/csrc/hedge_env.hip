@@ -2337,10 +2337,17 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
                 for (int t = lane; t <= T; t += 64)
                     L.thp[t] = theta * div_int_by((double)(T - t), 252.0, inv_252);
             }
+            // the marks times 100 in f64, carried from step to step: (n C) 100 = n (C 100) exactly
+            // (|n| < 2^16 contracts -- int16 positions, max_contracts_held <= 32767 -- times a 24-bit C
+            // times 100 is at most 47 bits), so the slippage and option-value terms below are the
+            // reference's products bit for bit with two conversions and two multiplies fewer a step
+            double preC100 = (double)pre.C * 100.0, preP100 = (double)pre.P * 100.0;
+            const double rstC100 = (double)rst.C * 100.0, rstP100 = (double)rst.P * 100.0;
             run_blk([&](int buf, int sl, int k, float2 ak, auto) {
                 const int64_t koff = (int64_t)k * N;
                 const float2 sc = L.sc[buf][sl][lane];
                 const float pP = L.pp[buf][sl][lane];
+                const double C100 = (double)sc.y * 100.0, P100 = (double)pP * 100.0;
                 const double pv_prev = (e.t == 0) ? pv0 : pv_last;
                 // (i)-(ii) trades (:181-200)
                 const int32_t nc = e.call + trade_round(ak.x * mt_f, mt);
@@ -2351,14 +2358,14 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
                 // (iii) commission + slippage on the pre-step marks (:203-213)
                 const int32_t adc = dc < 0 ? -dc : dc, adp = dp < 0 ? -dp : dp;
                 const double commission = (double)(adc + adp) * tcpc;
-                const double slc = (((double)adc * (double)pre.C) * 100.0) * slip_frac;
-                const double slp = (((double)adp * (double)pre.P) * 100.0) * slip_frac;
+                const double slc = ((double)adc * preC100) * slip_frac;   // (((adc C) 100) slip: :205-209)
+                const double slp = ((double)adp * preP100) * slip_frac;
                 const double tc = commission + (slc + slp);
                 const double cash = e.cash - tc;
                 // (iv)-(vi) advance, mark-to-market (:216-238)
                 const uint32_t t1 = e.t + 1;
                 const bool term = (int32_t)t1 >= T;
-                const double optv = ((double)cc * (double)sc.y) * 100.0 + ((double)qq * (double)pP) * 100.0;
+                const double optv = (double)cc * C100 + (double)qq * P100;   // (cc C) 100 + (qq P) 100
                 double pv = ((double)(shares_f * sc.x) + optv) + cash;
                 if (BOOK) pv = pv + L.bk[buf][sl][lane];  // liability book (extension): after cash
                 const double pnl = pv - pv_prev;
@@ -2380,7 +2387,8 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
                 e.call = term ? 0 : cc;
                 e.put = term ? 0 : qq;
                 e.cash = term ? init_cash : cash;
-                pre = Mkt{term ? rst.S : sc.x, rst.v, term ? rst.C : sc.y, term ? rst.P : pP, 0.0};
+                preC100 = term ? rstC100 : C100;
+                preP100 = term ? rstP100 : P100;
             });
         }
     } else {
