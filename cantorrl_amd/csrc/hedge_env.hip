@@ -430,10 +430,26 @@ __device__ __forceinline__ float4 replay_greeks(const Params& p, float S, float 
 // The select operands are made opaque (asm): left alone, the backend turns the nested
 // constant selects and the gamma quotient into exec-mask branches -- five per step in the
 // obs stepper's block, which split the unrolled steps into separate basic blocks.
+// a / b, f32, as the correctly rounded division's lowering computes it (v_rcp_f32, a Newton step,
+// the quotient and two residual corrections) without its v_div_scale / v_div_fixup: those change
+// nothing when a, b and a / b are normal and far from the exponent range's ends, as in the lean
+// obs stepper's two quotients -- S / max(rint S, 1e-6) (within a factor 2 of 1 for S >= 0.5,
+// below 5e5 under it) and (S - Sp) / Sp (0 or >= 2^-23 in magnitude) with S, Sp >= 1e-8.
+// An inf or NaN S still gives the IEEE quotient's inf / NaN.  The lean LDS steppers against the
+// tile kernels' IEEE divisions: bit for bit (test_lds_rollout_equals_tile_rollout and the suite);
+// headline 280.8 -> 277.0 us per launch, 3 of 3 same-box pairs (r05s22_ab_div_core.txt).
+__device__ __forceinline__ float div_f32_core(float a, float b) {
+    float r = __builtin_amdgcn_rcpf(b);
+    r = fmaf(fmaf(-b, r, 1.0f), r, r);
+    float q = a * r;
+    q = fmaf(fmaf(-b, q, a), r, q);
+    return fmaf(fmaf(-b, q, a), r, q);
+}
+
 __device__ __forceinline__ float4 greeks_lean(float S, float num_drift, float inv_sst_f, float sstf) {
     const float K = rintf(S);
     const float Kc = np_maxf(K, 1e-6f);
-    const float num = logf(S / Kc) + num_drift;   // f32 in the reference too
+    const float num = logf(div_f32_core(S, Kc)) + num_drift;   // f32 in the reference too
     const float d1 = num * inv_sst_f;
     const float ph = expf(-0.5f * (d1 * d1)) * 0.398942280401432678f;
     const float tail = ncdf_tail(d1, ph);
@@ -458,6 +474,13 @@ __device__ __forceinline__ float4 greeks_lean(float S, float num_drift, float in
 // slots, replay table load) and travels in the .w lane of the greeks record.
 __device__ __forceinline__ float lag_return(float S, float Sp) {
     float q = (S - Sp) / Sp;  // for every lane (opaque): a select, not a branch around the division
+    HE_OPAQUE1(q);
+    return (Sp == 0.0f) ? 0.0f : np_clipf(q, -1.0f, 1.0f);
+}
+
+// lag_return for the lean obs stepper (S, Sp >= 1e-8): the quotient by div_f32_core
+__device__ __forceinline__ float lag_return_lean(float S, float Sp) {
+    float q = div_f32_core(S - Sp, Sp);
     HE_OPAQUE1(q);
     return (Sp == 0.0f) ? 0.0f : np_clipf(q, -1.0f, 1.0f);
 }
@@ -2292,7 +2315,7 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
                 o[8] = g.y;
                 o[9] = g.z;
                 o[10] = g.y;
-                o[11] = lag_return(r0.x, preS);
+                o[11] = lag_return_lean(r0.x, preS);
                 o[12] = (preS == 0.0f) ? 0.0f : np_clipf(vk - (HESTON ? preV : var_f), -1.0f, 1.0f);
                 // staged in LDS (two tiles, alternating by step: the next step's row writes
                 // do not wait behind this step's read-back) and stored as whole 16-B lines
