@@ -292,6 +292,27 @@ HE_HD void sincos_2pi_u(double u2, double* sin_out, double* cos_out) {
     *cos_out = ((qi + 1) & 2) ? -c_ : c_;
 }
 
+// sqrt of the Box-Muller radius x = -2 log u, in [2.2e-16, 73.5] for the u01 draws: ocml's
+// correctly rounded f64 sqrt (v_rsq_f64, then Goldschmidt and two residual corrections) without
+// its range scaling and special-value selects, which never apply there -- the same operations,
+// so the same bits (the host build's sqrt: test_device_philox_words_equal_rocrand); config 2
+// -0.3 %, config 5 -0.4 %, 3 of 3 same-box pairs each (r05s24_ab_sqrt_bm.txt)
+HE_HD double sqrt_bm(double x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const double y = __builtin_amdgcn_rsq(x);
+    double g = x * y, h = y * 0.5;
+    const double r = fma(-h, g, 0.5);
+    g = fma(g, r, g);
+    double d = fma(-g, g, x);
+    h = fma(h, r, h);
+    g = fma(d, h, g);
+    d = fma(-g, g, x);
+    return fma(d, h, g);
+#else
+    return sqrt(x);
+#endif
+}
+
 HE_HD void box_muller(double u1, double u2, double* z1, double* z2) {
     // log(u1)
     int e;
@@ -314,7 +335,7 @@ HE_HD void box_muller(double u1, double u2, double* z1, double* z2) {
     const double lm = (2.0 * s) + (2.0 * s) * (s2 * p);   // 2 atanh(s)
     const double ed = (double)e;
     const double lg = fma(ed, 6.93147180369123816490e-01, fma(ed, 1.90821492927058770002e-10, lm));
-    const double rad = sqrt(-2.0 * lg);
+    const double rad = sqrt_bm(-2.0 * lg);
     double sinv, cosv;
     sincos_2pi_u(u2, &sinv, &cosv);
     *z1 = rad * cosv;
@@ -598,7 +619,7 @@ HE_HD void box_muller_n(const double* u1, const double* u2, double* z1, double* 
     for (int h = 0; h < NN; ++h) {
         const double lm = (2.0 * s[h]) + (2.0 * s[h]) * (s2[h] * p[h]);
         const double lg = fma(ed[h], 6.93147180369123816490e-01, fma(ed[h], 1.90821492927058770002e-10, lm));
-        rad[h] = sqrt(-2.0 * lg);
+        rad[h] = sqrt_bm(-2.0 * lg);
         const double x = 4.0 * u2[h];
         const double q = rint(x);
         r[h] = x - q;
