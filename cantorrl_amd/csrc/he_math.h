@@ -292,6 +292,24 @@ HE_HD void sincos_2pi_u(double u2, double* sin_out, double* cos_out) {
     *cos_out = ((qi + 1) & 2) ? -c_ : c_;
 }
 
+// (m - 1) / (m + 1) for the Box-Muller log's mantissa m in [sqrt2/2, sqrt2): the correctly rounded
+// f64 division's lowering (v_rcp_f64, two Newton steps, the quotient and one residual correction)
+// without its v_div_scale / v_div_fixup, which never act on these operands (m - 1 is 0 or at least
+// 2^-53, m + 1 within [1.7, 2.5]) -- the same operations, so the same bits (config 2 -0.4 %,
+// r05s25_ab_bm_quot.txt)
+HE_HD double bm_quot(double m) {
+    const double a = m - 1.0, b = m + 1.0;
+#if defined(__HIP_DEVICE_COMPILE__)
+    double r = __builtin_amdgcn_rcp(b);
+    r = fma(r, fma(-b, r, 1.0), r);
+    r = fma(r, fma(-b, r, 1.0), r);
+    const double q = a * r;
+    return fma(fma(-b, q, a), r, q);
+#else
+    return a / b;
+#endif
+}
+
 // sqrt of the Box-Muller radius x = -2 log u, in [2.2e-16, 73.5] for the u01 draws: ocml's
 // correctly rounded f64 sqrt (v_rsq_f64, then Goldschmidt and two residual corrections) without
 // its range scaling and special-value selects, which never apply there -- the same operations,
@@ -321,7 +339,7 @@ HE_HD void box_muller(double u1, double u2, double* z1, double* z2) {
         m = m + m;
         e -= 1;
     }
-    const double s = (m - 1.0) / (m + 1.0);
+    const double s = bm_quot(m);
     const double s2 = s * s;
     double p = 1.0 / 19.0;
     p = fma_k(p, s2, 1.0 / 17.0);
@@ -604,7 +622,7 @@ HE_HD void box_muller_n(const double* u1, const double* u2, double* z1, double* 
         const bool lo = m < 0.70710678118654752;
         m = lo ? m + m : m;
         ed[h] = (double)(lo ? e - 1 : e);
-        s[h] = (m - 1.0) / (m + 1.0);
+        s[h] = bm_quot(m);
         s2[h] = s[h] * s[h];
         p[h] = 1.0 / 19.0;
     }
