@@ -292,13 +292,11 @@ HE_HD void sincos_2pi_u(double u2, double* sin_out, double* cos_out) {
     *cos_out = ((qi + 1) & 2) ? -c_ : c_;
 }
 
-// (m - 1) / (m + 1) for the Box-Muller log's mantissa m in [sqrt2/2, sqrt2): the correctly rounded
-// f64 division's lowering (v_rcp_f64, two Newton steps, the quotient and one residual correction)
-// without its v_div_scale / v_div_fixup, which never act on these operands (m - 1 is 0 or at least
-// 2^-53, m + 1 within [1.7, 2.5]) -- the same operations, so the same bits (config 2 -0.4 %,
-// r05s25_ab_bm_quot.txt)
-HE_HD double bm_quot(double m) {
-    const double a = m - 1.0, b = m + 1.0;
+// a / b by the correctly rounded f64 division's lowering without its v_div_scale / v_div_fixup:
+// the same bits wherever those change nothing -- a and b finite, b normal and well inside the
+// exponent range, a 0 or with an exponent within a few hundred of b's (bm_quot, the FAST replay
+// reward's two quotients on an ordinary table: he_env::table_ordinary)
+HE_HD double div_f64_core(double a, double b) {
 #if defined(__HIP_DEVICE_COMPILE__)
     double r = __builtin_amdgcn_rcp(b);
     r = fma(r, fma(-b, r, 1.0), r);
@@ -309,6 +307,13 @@ HE_HD double bm_quot(double m) {
     return a / b;
 #endif
 }
+
+// (m - 1) / (m + 1) for the Box-Muller log's mantissa m in [sqrt2/2, sqrt2): the correctly rounded
+// f64 division's lowering (v_rcp_f64, two Newton steps, the quotient and one residual correction)
+// without its v_div_scale / v_div_fixup, which never act on these operands (m - 1 is 0 or at least
+// 2^-53, m + 1 within [1.7, 2.5]) -- the same operations, so the same bits (config 2 -0.4 %,
+// r05s25_ab_bm_quot.txt)
+HE_HD double bm_quot(double m) { return div_f64_core(m - 1.0, m + 1.0); }
 
 // sqrt of the Box-Muller radius x = -2 log u, in [2.2e-16, 73.5] for the u01 draws: ocml's
 // correctly rounded f64 sqrt (v_rsq_f64, then Goldschmidt and two residual corrections) without

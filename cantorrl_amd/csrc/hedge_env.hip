@@ -3228,7 +3228,7 @@ __device__ __forceinline__ void lds_replay_stepper(const Params& p, State s, con
             float o[kObs];
             if (FAST) {  // make_obs<true, true> on the pinned constants (hedging_env_v2.py:109-143)
                 // f32 Markstein steps (div_f32_byf): the FAST kernel runs only on an ordinary table
-                // (he_env::table_ordinary: max(S0, 25) <= 2^24 and every price 0, NaN, inf or of
+                // (he_env::table_ordinary: max(S0, 25) <= 2^24 and every price 0 or finite and of
                 // magnitude >= 2^-100, so no quotient or residual leaves the normal range)
                 o[0] = div_f32_byf(post.S, e.s0s_f, e.inv_s0s_f);
                 o[1] = div_f32_byf(post.C, e.s0s_f, e.inv_s0s_f);
@@ -3281,8 +3281,10 @@ __device__ __forceinline__ void lds_replay_stepper(const Params& p, State s, con
                 const double ps = so.pnl * c_inv_252;
                 const double rpc = (-c_w) * (fabs(ps) * c_inv_252);
 #else
-                const double ps = so.pnl / c_shares_d;
-                const double rpc = (-c_w) * (fabs(ps) / e.den);
+                // the division core (div_f64_core): finite P&L on an ordinary table, shares_to_hedge
+                // and the denominator normal (fast_replay_config); -0.2 %, r05s26_ab_replay_div_core.txt
+                const double ps = div_f64_core(so.pnl, c_shares_d);
+                const double rpc = (-c_w) * div_f64_core(fabs(ps), e.den);
 #endif
                 const double tcp = c_lam * so.tc;
                 const double thp = c_theta * div_int_by((double)(T - (int32_t)e.t), 252.0, c_inv_252);
@@ -3650,7 +3652,7 @@ struct he_env {
     unsigned long long* scratch_count = nullptr;  // he_rollout_policy without records
     double book_rst = 0.0;      // book value of the reset market (host copy)
     int64_t n_paths = 0;
-    // every price of the loaded table 0, NaN, inf or of magnitude >= 2^-100, every S0 <= 2^24
+    // every price of the loaded table 0 or finite and of magnitude >= 2^-100, every S0 <= 2^24
     // (he_load_paths): the FAST replay kernel's f32 obs quotients apply (fast_replay_config)
     bool table_ordinary = false;
     int32_t block_pos = 0;    // generate: next slot to consume; M = tile exhausted/invalid
@@ -4155,7 +4157,8 @@ static bool lds_replay_eligible(const he_env* env, const Io& io) {
 static bool fast_replay_config(const he_env* env) {
     const he_config& c = env->cfg;
     return c.mode == HE_MODE_REPLAY && c.variant == 2 && c.loss_type != HE_LOSS_MSE && c.shares_to_hedge != 0 &&
-           c.record_metrics && c.max_contracts_held_per_type > 0 && env->p.T > 0 && env->table_ordinary;
+           c.record_metrics && c.max_contracts_held_per_type > 0 && env->p.T > 0 && env->table_ordinary &&
+           fabs(env->p.shares_d) >= 0x1p-100 && fabs(env->p.shares_d) <= 0x1p100;
 }
 
 static he_status launch_lds_replay(he_env* env, const Io& io, int k_total, hipStream_t st) {
@@ -4483,9 +4486,11 @@ he_status he_load_paths(he_env* env, const float* S, const float* v, const float
     } catch (...) {
         return fail(env, HE_ENOMEM, "host allocation of %lld records failed", (long long)(n_paths * W));
     }
-    // an ordinary table (he_env::table_ordinary): prices 0, NaN, inf or >= 2^-100 in magnitude,
+    // an ordinary table (he_env::table_ordinary): prices 0 or finite and >= 2^-100 in magnitude,
     // S0 (row 0; < 1e-6 is replaced by 1) <= 2^24
-    auto ordinary = [](float a) { return !(fabsf(a) < 7.8886090522101181e-31f) || a == 0.0f; };
+    auto ordinary = [](float a) {   // 0, or finite and >= 2^-100 in magnitude
+        return a == 0.0f || (fabsf(a) >= 7.8886090522101181e-31f && fabsf(a) <= 3.4028234663852886e38f);
+    };
     bool ord = true;
     for (int64_t q = 0; q < n_paths; ++q) {
         for (int64_t t = 0; t <= T; ++t) {
