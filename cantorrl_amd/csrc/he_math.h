@@ -202,9 +202,15 @@ HE_HD int32_t trade_round(float f, int32_t mt) {
     const float r = rintf(f);
     const bool ok = fabsf(r) < 9.2233720368547758e18f;  // false for NaN and |x| >= 2^63
     const float lo = -(float)mt, hi = (float)mt;
+#if defined(__HIP_DEVICE_COMPILE__)
+    // the clamp as one v_med3_f32 (lo <= hi; a NaN r is replaced by -mt either way): headline
+    // 277.6 -> 274.1 us per launch, 3 of 3 same-box pairs (r05s27_ab_trade_med3.txt)
+    return ok ? (int32_t)__builtin_amdgcn_fmed3f(r, lo, hi) : -mt;
+#else
     const float c = r < lo ? lo : (r > hi ? hi : r);
     const int32_t v = ok ? (int32_t)c : 0;
     return ok ? v : -mt;
+#endif
 }
 
 // ---------------------------------------------------------------- Philox4x32-10
