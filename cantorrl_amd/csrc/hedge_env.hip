@@ -489,7 +489,7 @@ __device__ __forceinline__ float4 greeks_lean(float S, float num_drift, float in
     return make_float4(cd, gam, pd, 0.0f);
 }
 
-// np.clip(n, -maxh, maxh) of the lean steppers' positions (maxh >= 0): one v_med3_i32 (the
+// np.clip(n, -maxh, maxh) of the steppers' positions (maxh >= 0, he_create): one v_med3_i32 (the
 // compiler made v_min_i32 + a compare + a select of it; headline 271.4 -> 268.7 us, 3 of 3
 // same-box pairs, r05s30_ab_pos_med3.txt)
 __device__ __forceinline__ int32_t clamp_pos(int32_t n, int32_t maxh) {
@@ -1254,8 +1254,8 @@ __device__ __forceinline__ void step_env(const Params& p, Env& e, const Mkt& pre
     int32_t rqc = trade_round(fc, p.mt);
     int32_t rqp = trade_round(fp, p.mt);
     int32_t nc = e.call + rqc, nq = e.put + rqp;
-    nc = nc < -p.maxh ? -p.maxh : (nc > p.maxh ? p.maxh : nc);
-    nq = nq < -p.maxh ? -p.maxh : (nq > p.maxh ? p.maxh : nq);
+    nc = clamp_pos(nc, p.maxh);
+    nq = clamp_pos(nq, p.maxh);
     int32_t dc = nc - e.call, dp = nq - e.put;
     e.call = nc;
     e.put = nq;
@@ -2463,8 +2463,8 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
                 // (i)-(ii) of step_env: the integer trade logic (:181-200)
                 const int32_t nc = e.call + trade_round(ak.x * p.mt_f, p.mt);
                 const int32_t nq = e.put + trade_round(ak.y * p.mt_f, p.mt);
-                e.call = nc < -p.maxh ? -p.maxh : (nc > p.maxh ? p.maxh : nc);
-                e.put = nq < -p.maxh ? -p.maxh : (nq > p.maxh ? p.maxh : nq);
+                e.call = clamp_pos(nc, p.maxh);
+                e.put = clamp_pos(nq, p.maxh);
                 e.t = e.t + 1;
                 const bool term = (int32_t)e.t >= p.T;
                 float o[kObs];
@@ -3251,8 +3251,8 @@ __device__ __forceinline__ void lds_replay_stepper(const Params& p, State s, con
             // (i)-(ii) of step_env: the integer trade logic (:181-200)
             const int32_t nc = e.call + trade_round(ak.x * c_mt_f, c_mt);
             const int32_t nq = e.put + trade_round(ak.y * c_mt_f, c_mt);
-            e.call = nc < -c_maxh ? -c_maxh : (nc > c_maxh ? c_maxh : nc);
-            e.put = nq < -c_maxh ? -c_maxh : (nq > c_maxh ? c_maxh : nq);
+            e.call = clamp_pos(nc, c_maxh);
+            e.put = clamp_pos(nq, c_maxh);
             e.t = e.t + 1;
             const bool term = (int32_t)e.t >= T;
             float o[kObs];
@@ -3291,8 +3291,8 @@ __device__ __forceinline__ void lds_replay_stepper(const Params& p, State s, con
                 const double pv_prev = (e.t == 0) ? (double)pv0 : pv_last;
                 const int32_t nc = e.call + trade_round(ak.x * c_mt_f, c_mt);
                 const int32_t nq = e.put + trade_round(ak.y * c_mt_f, c_mt);
-                const int32_t cc = nc < -c_maxh ? -c_maxh : (nc > c_maxh ? c_maxh : nc);
-                const int32_t qq = nq < -c_maxh ? -c_maxh : (nq > c_maxh ? c_maxh : nq);
+                const int32_t cc = clamp_pos(nc, c_maxh);
+                const int32_t qq = clamp_pos(nq, c_maxh);
                 const int32_t dc = cc - e.call, dp = qq - e.put;
                 const int32_t adc = dc < 0 ? -dc : dc, adp = dp < 0 ? -dp : dp;
                 const double commission = (double)(adc + adp) * c_tcpc;
