@@ -2395,13 +2395,16 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
             // times 100 is at most 47 bits), so the slippage and option-value terms below are the
             // reference's products bit for bit with two conversions and two multiplies fewer a step
             double preC100 = (double)pre.C * 100.0, preP100 = (double)pre.P * 100.0;
+            // the previous value an episode's first step differences against is PV0 (:167-168):
+            // set where the episode starts (here, and by the autoreset below), not tested per step
+            if (e.t == 0) pv_last = pv0;
             const double rstC100 = (double)rst.C * 100.0, rstP100 = (double)rst.P * 100.0;
             run_blk([&](int buf, int sl, int k, float2 ak, auto) {
                 const int64_t koff = (int64_t)k * N;
                 const float2 sc = L.sc[buf][sl][lane];
                 const float pP = L.pp[buf][sl][lane];
                 const double C100 = (double)sc.y * 100.0, P100 = (double)pP * 100.0;
-                const double pv_prev = (e.t == 0) ? pv0 : pv_last;
+                const double pv_prev = pv_last;
                 // (i)-(ii) trades (:181-200)
                 const int32_t nc = e.call + trade_round(ak.x * mt_f, mt);
                 const int32_t nq = e.put + trade_round(ak.y * mt_f, mt);
@@ -2434,7 +2437,7 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
                 grew[koff + i] = (float)reward;
                 gterm[koff + i] = term ? 1 : 0;
                 account(reward, pnl, tc, term);
-                pv_last = pv;
+                pv_last = term ? pv0 : pv;
                 // SB3 autoreset (selects)
                 e.t = term ? 0u : t1;
                 e.call = term ? 0 : cc;
