@@ -934,6 +934,94 @@ def finish_roofline(roof, cfg, valu, pmc, kern_ms):
 # drive today.
 REFERENCE_SINGLE_ENV_STEPS_S = 4782.0
 SB3_API_ENVS = (2, 256, 65536)   # N_ENVS = 2 (train_ppo_v2.py:45), BASELINE config 1, the headline
+# the 9 info keys of the reference's evaluation loop (train_ppo_v2.py:482-499)
+EVAL_INFO_KEYS = ("per_share_step_pnl", "transaction_costs_total", "scaled_float_call", "scaled_float_put",
+                  "requested_calls_rounded_clipped", "requested_puts_rounded_clipped", "actual_calls_traded",
+                  "actual_puts_traded", "raw_pnl_deviation_abs")
+
+
+def sb3_collect_pass(infos, dones, ep_info_buffer):
+    """What SB3 2.6.0's collect_rollouts does with a step's infos on the host (restated: SB3 is not
+    installed): _update_info_buffer -- info.get("episode") / info.get("is_success") of EVERY row --
+    and the truncation-bootstrap loop over the done rows (on_policy_algorithm.py)."""
+    for idx, info in enumerate(infos):
+        maybe_ep_info = info.get("episode")
+        maybe_is_success = info.get("is_success")
+        if maybe_ep_info is not None:
+            ep_info_buffer.extend([maybe_ep_info])
+        if maybe_is_success is not None and dones[idx]:
+            pass
+    for idx, done in enumerate(dones):
+        if done and infos[idx].get("terminal_observation") is not None and infos[idx].get("TimeLimit.truncated", False):
+            pass
+
+
+def eval_pass(infos, n, sums):
+    """The info reads of train_ppo_v2.py:481-499 per env per step (9 keys; the caller's own
+    action-log dict is the same work on either side of the swap and is left out)."""
+    for i in range(n):
+        sums[0] += infos[i].get('per_share_step_pnl', 0.0)
+        sums[1] += infos[i].get('transaction_costs_total', 0.0)
+        sums[2] += float(infos[i].get('scaled_float_call', 0.0))
+        sums[2] += float(infos[i].get('scaled_float_put', 0.0))
+        sums[3] += int(infos[i].get('requested_calls_rounded_clipped', 0))
+        sums[3] += int(infos[i].get('requested_puts_rounded_clipped', 0))
+        sums[3] += int(infos[i].get('actual_calls_traded', 0))
+        sums[3] += int(infos[i].get('actual_puts_traded', 0))
+        sums[0] += float(infos[i].get('raw_pnl_deviation_abs', 0.0))
+        sums[1] += float(infos[i].get('transaction_costs_total', 0.0))
+
+
+def sb3_loop(dev, VecEnv, MON, envs=SB3_API_ENVS):
+    """what the unchanged agents' host loop pays per step, infos included.
+    sb3_loop: step_async + step_wait, then sb3_collect_pass (every row's get("episode") /
+    get("is_success"), the done loop) -- Monitor on, the 3 Monitor keys; eval_loop: the same step
+    with the 9 evaluation keys and eval_pass.  Each over whole steps; `pass_floor_us` is the same
+    pass over plain dicts made beforehand from one step's rows (what those Python loops cost even
+    if `infos` were a free list of dicts: the part no env can remove)."""
+    out = dict(what="wall time per step of step_async + step_wait + the caller's per-step reads of infos "
+                    "(SB3 collect_rollouts / the reference eval loop); Monitor on", sb3_loop={}, eval_loop={})
+    rng = np.random.default_rng(5)
+    for leg, keys in (("sb3_loop", MON), ("eval_loop", EVAL_INFO_KEYS)):
+        for n in envs:
+            # >= one episode end in the window at every n (episodes are 252 steps) for the SB3
+            # pass; the eval pass at 65,536 reads 590k keys per step: fewer steps there
+            steps = 260 if (leg == "sb3_loop" or n < 65536) else 24
+            acts = rng.uniform(-1, 1, size=(4, n, 2)).astype(np.float32)
+            env = VecEnv(n, mode="gbm", generate=GEN, seed=11, device=dev, monitor_keywords=MON, info_keys=keys,
+                         **TRAIN_KW)
+            env.reset()
+            buf, sums = [], [0.0, 0.0, 0.0, 0]
+            t_step, t_pass = np.empty(steps), np.empty(steps)
+            for i in range(steps + 8):
+                a = time.perf_counter()
+                env.step_async(acts[i & 3])
+                obs, rew, done, infos = env.step_wait()
+                b = time.perf_counter()
+                if leg == "sb3_loop":
+                    sb3_collect_pass(infos, done, buf)
+                else:
+                    eval_pass(infos, n, sums)
+                c = time.perf_counter()
+                if i >= 8:
+                    t_step[i - 8], t_pass[i - 8] = b - a, c - b
+            plain = [dict(r) for r in infos]
+            fl = []
+            for _ in range(3):
+                a = time.perf_counter()
+                if leg == "sb3_loop":
+                    sb3_collect_pass(plain, done, [])
+                else:
+                    eval_pass(plain, n, [0.0, 0.0, 0.0, 0])
+                fl.append(time.perf_counter() - a)
+            env.close()
+            tot = t_step + t_pass
+            out[leg][str(n)] = dict(
+                us_per_step=round(float(tot.mean()) * 1e6, 2), us_median=round(float(np.median(tot)) * 1e6, 2),
+                us_step_wait=round(float(t_step.mean()) * 1e6, 2), us_info_pass=round(float(t_pass.mean()) * 1e6, 2),
+                pass_floor_us=round(float(np.median(fl)) * 1e6, 2), steps=steps,
+                episodes_seen=len(buf) if leg == "sb3_loop" else None, keys=len(keys))
+    return out
 
 
 def _host_loop_timing(fn, steps, warm):
@@ -1022,6 +1110,7 @@ def sb3_api(dev, classes=None, envs=SB3_API_ENVS, steps=504):
             t_steps += 1
     wall = time.perf_counter() - t0
     env.close()
+    out.update(sb3_loop(dev, VecEnv, MON, envs))
     out["single_env"] = dict(loop="baselines.py:32-56 evaluate_baseline_policy shape: reset, policy_delta_every_step, "
                                   "step, info.get sums", episodes=n_ep, steps=t_steps,
                              us_per_step=round(wall / t_steps * 1e6, 2), steps_per_s=round(t_steps / wall, 1),

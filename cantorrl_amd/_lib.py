@@ -13,7 +13,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 # CANTORRL_HEDGEENV_LIB: an alternative build (diagnostic / A-B builds under tools/ab/)
 LIB_PATH = os.environ.get("CANTORRL_HEDGEENV_LIB") or os.path.join(HERE, "lib", "libhedgeenv.so")
 
-HE_ABI_VERSION = 3
+HE_ABI_VERSION = 4
 HE_BOOK_MAX = 8
 HE_OBS_DIM = 13
 BOOK_TYPES = {"call": 0, "put": 1, "uo_call": 2}
@@ -198,8 +198,8 @@ def load(path=LIB_PATH):
         "he_vecnorm_stats_len": (i64, [i32]),
         "he_vecnorm_scratch_bytes": (i64, [i64, i32]),
         "he_vecnorm_init": (i32, [vp, i32, vp]),
-        "he_vecnorm_step": (i32, [ctypes.POINTER(HeVecnormParams), i64] + [vp] * 14 + [vp]),
-        "he_vecnorm_apply": (i32, [ctypes.POINTER(HeVecnormParams), i64] + [vp] * 14 + [vp]),
+        "he_vecnorm_step": (i32, [ctypes.POINTER(HeVecnormParams), i64] + [vp] * 15 + [vp]),
+        "he_vecnorm_apply": (i32, [ctypes.POINTER(HeVecnormParams), i64] + [vp] * 15 + [vp]),
         "he_vecnorm_attach": (i32, [vp, ctypes.POINTER(HeVecnormParams), vp, vp, vp]),
         "he_vecnorm_attach_eval": (i32, [vp, ctypes.POINTER(HeVecnormParams), ctypes.POINTER(HeVecnormOut)]),
         "he_vecnorm_reset": (i32, [ctypes.POINTER(HeVecnormParams), i64] + [vp] * 5 + [vp]),

@@ -1,5 +1,6 @@
 """Build the gfx950 libraries in-tree: cantorrl_amd/lib/libhedgeenv.so (the env) and
-cantorrl_amd/lib/librbergomi.so (the rough-Bergomi data generator).
+cantorrl_amd/lib/librbergomi.so (the rough-Bergomi data generator), plus the host-only
+CPython module cantorrl_amd/lib/_info_rows*.so (a step's SB3 info dicts, csrc/info_rows.c).
 
     python -m cantorrl_amd.build [--force]
 
@@ -44,6 +45,14 @@ DEPS = DEPS + [VN_SRC, AN_SRC, os.path.join(HERE, "csrc", "vn_moments.h")]
 TARGETS = [([SRC, VN_SRC, AN_SRC], DEPS, OUT, ENV_FLAGS), ([RB_SRC], RB_DEPS, RB_OUT, [])]
 
 
+# host-only: the CPython module that builds a step's SB3 info dicts (csrc/info_rows.c)
+import sysconfig  # noqa: E402
+ROWS_SRC = os.path.join(HERE, "csrc", "info_rows.c")
+ROWS_OUT = os.path.join(HERE, "lib", "_info_rows" + sysconfig.get_config_var("EXT_SUFFIX"))
+ROWS_CMD = [os.environ.get("CC", "gcc"), "-O2", "-shared", "-fPIC", "-Wall", "-Werror",
+            "-I" + sysconfig.get_paths()["include"]]
+
+
 def needs_build(out=OUT, deps=DEPS):
     if not os.path.exists(out):
         return True
@@ -63,6 +72,13 @@ def build(force=False, verbose=False):
             print(" ".join(cmd))
         subprocess.run(cmd, check=True)
         os.replace(tmp, out)
+    if force or needs_build(ROWS_OUT, [ROWS_SRC]):
+        tmp = ROWS_OUT + ".tmp"
+        cmd = [*ROWS_CMD, "-o", tmp, ROWS_SRC]
+        if verbose:
+            print(" ".join(cmd))
+        subprocess.run(cmd, check=True)
+        os.replace(tmp, ROWS_OUT)
     return OUT
 
 

@@ -435,7 +435,9 @@ __device__ __forceinline__ float4 replay_greeks(const Params& p, float S, float 
 // nothing when a, b and a / b are normal and far from the exponent range's ends, as in the lean
 // obs stepper's two quotients -- S / max(rint S, 1e-6) (within a factor 2 of 1 for S >= 0.5,
 // below 5e5 under it) and (S - Sp) / Sp (0 or >= 2^-23 in magnitude) with S, Sp >= 1e-8.
-// An inf or NaN S still gives the IEEE quotient's inf / NaN.  The lean LDS steppers against the
+// An inf dividend is NOT the IEEE quotient here (a - b q = inf - inf = NaN): callers keep the
+// dividend finite (lag_return_lean caps it, greeks_lean's S / rint(S) is NaN for an inf S in IEEE
+// too).  The lean LDS steppers against the
 // tile kernels' IEEE divisions: bit for bit (test_lds_rollout_equals_tile_rollout and the suite);
 // headline 280.8 -> 277.0 us per launch, 3 of 3 same-box pairs (r05s22_ab_div_core.txt).
 __device__ __forceinline__ float div_f32_core(float a, float b) {
@@ -508,9 +510,13 @@ __device__ __forceinline__ float lag_return(float S, float Sp) {
     return (Sp == 0.0f) ? 0.0f : np_clipf(q, -1.0f, 1.0f);
 }
 
-// lag_return for the lean obs stepper (S, Sp >= 1e-8): the quotient by div_f32_core
+// lag_return for the lean obs stepper (S, Sp >= 1e-8): the quotient by div_f32_core, its
+// dividend capped at Sp -- every (S - Sp) / Sp >= 1 clips to 1 and Sp / Sp = 1 exactly, so the
+// value is the same, and an infinite S (an f32 overflow of the f64 price) gives the reference's
+// clip(inf) = 1 instead of div_f32_core's inf - inf = NaN; a NaN stays NaN (the compare is false)
 __device__ __forceinline__ float lag_return_lean(float S, float Sp) {
-    float q = div_f32_core(S - Sp, Sp);
+    const float d = S - Sp;
+    float q = div_f32_core((d > Sp) ? Sp : d, Sp);
     HE_OPAQUE1(q);
     return (Sp == 0.0f) ? 0.0f : np_clipf(q, -1.0f, 1.0f);
 }
@@ -1455,6 +1461,7 @@ __device__ __forceinline__ void env_reset_common(const Params& p, Env& e) {
 struct VnHook {
     const float* tile;
     float rew;
+    double rew64;   // the f64 reward (Monitor's sums)
     bool term;
 };
 
@@ -1630,6 +1637,7 @@ __device__ __forceinline__ void step_body(const Params& pk, int64_t n_envs, cons
             pv_last = so.pv;
             if (hook) {
                 hook->rew = (float)so.reward;
+                hook->rew64 = so.reward;
                 hook->term = so.term;
             }
             if (POL) {  // the reference evaluation loops' sums, in step order
@@ -1934,7 +1942,7 @@ __global__ __launch_bounds__(kBlock) void step1_vn_kernel(const Params* __restri
     const int64_t r = (int64_t)blockIdx.x * kEpb + threadIdx.x;
     const double ret_prev = (vm.upd_ret && r < n) ? vm.returns[r] : 0.0;
     const double col_shift = vn::load_col_shift(vm);
-    VnHook hk{nullptr, 0.0f, false};
+    VnHook hk{nullptr, 0.0f, 0.0, false};
     step_body<MODE, false, true, BOOK, FAST, false, GS>(*pc, n, tA, tB, tC, s, io, 1, slot0, blockIdx.x, &hk);
     __syncthreads();  // the workgroup's obs rows (LDS, the final ones incl. reset obs) visible to all its threads
     vn::moments_from_rows(vm, blockIdx.x, hk.tile, hk.rew, ret_prev, col_shift);
@@ -1962,11 +1970,11 @@ __global__ __launch_bounds__(kBlock) void step1_vne_kernel(const Params* __restr
     __shared__ vn::FrozenNorm fz;
     const vn::FrozenPre fp = vn::load_frozen(va, r0 + threadIdx.x, r0 + threadIdx.x < n);
     vn::prep_frozen(fz, va, fp);
-    VnHook hk{nullptr, 0.0f, false};
+    VnHook hk{nullptr, 0.0f, 0.0, false};
     step_body<MODE, false, true, BOOK, FAST, false, GS>(*pc, n, tA, tB, tC, s, io, 1, slot0, blockIdx.x, &hk);
     const int rows = (int)((n - r0) < kEpb ? n - r0 : kEpb);
     __syncthreads();  // the workgroup's obs rows (LDS, the final ones incl. reset obs) and fz visible to all
-    vn::apply_frozen_rows(va, fz, r0, rows, hk.tile, fp, hk.rew, hk.term, sio.tobs);
+    vn::apply_frozen_rows(va, fz, r0, rows, hk.tile, fp, hk.rew, hk.rew64, hk.term, sio.tobs);
 }
 
 // The same moments after any other he_step launch (info requested, a fused market block).
@@ -2323,20 +2331,19 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
                 // make_obs<true> (hedging_env_v2.py:109-143) on the post-step state, or the
                 // reset obs on a terminal step (SB3 autoreset)
                 float o[kObs];
-                // the three price columns over max(S0, 25) by f32 Markstein steps (div_f32_byf: the
-                // lean GBM prices are normal f32 numbers) instead of through f64: 292.6 -> 287.8 us
-                // per launch, 3 same-box pairs (r05s13_ab_obs_f32.txt)
+                // the price columns over max(S0, 25).  S by an f32 Markstein step (div_f32_byf: S >=
+                // 1e-8 and max(S0, 25) <= 1e20 (lds_lean_config), so S / max(S0, 25) is a normal
+                // f32 number; 292.6 -> 287.8 us per launch for all three columns, r05s13_ab_obs_f32.txt).
+                // C and P through f64 (div_f32_by): a deep out-of-the-money mark of a rolling ATM
+                // option can be tiny -- |d| past ~13 at a small S or sigma, in GBM as in Heston --
+                // where the f32 step's residual leaves the normal range
                 if constexpr (HESTON) {
-                    // through f64 (div_f32_by): at a near-zero variance the Heston marks can be
-                    // tiny, where the f32 step's residual leaves the normal range
-                    o[0] = div_f32_by(r0.x, s0s_d, inv_s0s_d);
-                    o[1] = div_f32_by(r0.y, s0s_d, inv_s0s_d);
-                    o[2] = div_f32_by(rP, s0s_d, inv_s0s_d);
+                    o[0] = div_f32_by(r0.x, s0s_d, inv_s0s_d);   // Heston: the same, S included
                 } else {
                     o[0] = div_f32_byf(r0.x, s0s_f, inv_s0s_f);
-                    o[1] = div_f32_byf(r0.y, s0s_f, inv_s0s_f);
-                    o[2] = div_f32_byf(rP, s0s_f, inv_s0s_f);
                 }
+                o[1] = div_f32_by(r0.y, s0s_d, inv_s0s_d);
+                o[2] = div_f32_by(rP, s0s_d, inv_s0s_d);
                 o[3] = div_int_byf((float)cc, maxh_f, inv_maxh_f);
                 o[4] = div_int_byf((float)qq, maxh_f, inv_maxh_f);
                 o[5] = vk;
@@ -4128,7 +4135,8 @@ static bool lds_lean_config(const he_env* env, const Io& io) {
     // greeks_lean's constants (GBM); the Heston lean obs takes greeks_fast<false> at the slot's v
     const bool normal_greeks = c.mode == HE_MODE_HESTON || (!p.tenor_small && p.g_sigma > 1e-6f && p.g_sst >= 1e-9);
     // the lean kernels' producers make rolling-ATM marks only (marks<MODE, false>)
-    return fast_config(env) && io.obs && io.rew && io.term && s0 >= 1e-30 && s0 <= 1e30 && ic <= 1e30 &&
+    // (S0 <= 1e20: S / max(S0, 25) >= 1e-8 / 1e20 stays a normal f32 for the f32 obs quotient)
+    return fast_config(env) && io.obs && io.rew && io.term && s0 >= 1e-30 && s0 <= 1e20 && ic <= 1e30 &&
            normal_greeks && c.mark == HE_MARK_ROLLING_ATM && (c.book_size > 0 || p.T < lds_thp_rows());
 }
 
@@ -4763,10 +4771,29 @@ he_status he_reset_episodes(he_env* env, const int64_t* env_ids, const int64_t* 
     else memset(&inf, 0, sizeof(inf));
     DeviceGuard dg(c.device);
     hipStream_t st = (hipStream_t)stream;
-    if (!env->d_eps) {
-        HE_HIP(env, hipMalloc(&env->d_eps, (size_t)c.n_envs * sizeof(int64_t)));
-        HE_HIP(env, hipHostMalloc((void**)&env->h_eps, (size_t)c.n_envs * sizeof(int64_t), hipHostMallocDefault));
-        HE_HIP(env, hipEventCreateWithFlags(&env->ev_eps, hipEventDisableTiming));
+    if (!env->d_eps || !env->h_eps || !env->ev_eps) {
+        // the three staging objects are made together or not at all: a partial failure frees
+        // what was made, so a later call retries from scratch instead of using a NULL buffer
+        const size_t bytes = (size_t)c.n_envs * sizeof(int64_t);
+        int64_t* d = nullptr;
+        int64_t* h = nullptr;
+        hipEvent_t ev = nullptr;
+        hipError_t e = hipMalloc(&d, bytes);
+        if (e == hipSuccess) e = hipHostMalloc((void**)&h, bytes, hipHostMallocDefault);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+        if (e != hipSuccess) {
+            if (ev) (void)hipEventDestroy(ev);
+            if (h) (void)hipHostFree(h);
+            if (d) (void)hipFree(d);
+            (void)hipGetLastError();
+            return fail(env, HE_EHIP, "he_reset_episodes: staging buffers: %s", hipGetErrorString(e));
+        }
+        if (env->ev_eps) (void)hipEventDestroy(env->ev_eps);
+        if (env->h_eps) (void)hipHostFree(env->h_eps);
+        if (env->d_eps) (void)hipFree(env->d_eps);
+        env->d_eps = d;
+        env->h_eps = h;
+        env->ev_eps = ev;
     } else {
         // the previous call's copy and reset (on any stream) may still read the staging
         // buffers: wait for that reset alone, not for the caller's whole stream
@@ -4810,6 +4837,13 @@ he_status he_step(he_env* env, const float* actions, float* obs, float* reward, 
         env->vne_on = false;
         return fail(env, HE_EINVAL, "he_vecnorm_attach_eval: he_step needs the terminated and terminal_obs buffers");
     }
+    if (vne && want_info && env->vne.ep_ret && !io.info.reward_step) {
+        // the info kernel runs, then the eval apply as its own launch: its Monitor sums add the
+        // f64 reward, which only info->reward_step carries out of the step
+        env->vne_on = false;
+        return fail(env, HE_EINVAL, "he_vecnorm_attach_eval with Monitor sums: an he_step that requests info "
+                                    "must request info->reward_step too");
+    }
     env->vn_fused = false;
     he_status s = launch_steps(env, io, want_info, 1, stream);
     env->vn_on = env->vne_on = false;
@@ -4817,11 +4851,12 @@ he_status he_step(he_env* env, const float* actions, float* obs, float* reward, 
         // another step kernel ran (info requested): the eval VecNormalize step as its own
         // launch.  he_vecnorm_step with training = 0 launches the apply kernel alone, which reads
         // only the frozen statistics (never the scratch partials), for any n.
+        // Monitor's sums take the f64 reward, which that kernel wrote to info->reward_step
         const vn::ApplyArgs& a = env->vne;
         he_status sv = he_vecnorm_step(&env->vne_p, env->cfg.n_envs, obs, reward, terminated, terminal_obs,
                                        a.returns, const_cast<double*>(a.stats), const_cast<double*>(a.stats),
                                        a.obs_out, a.rew_out, a.tobs_out, a.ep_ret, a.ep_len, a.ep_ret_done,
-                                       a.ep_len_done, stream);
+                                       a.ep_len_done, io.info.reward_step, stream);
         return sv == HE_OK ? sv : fail(env, sv, "he_step: the eval VecNormalize launch failed (status %d)", (int)sv);
     }
     if (s != HE_OK || !vn || env->vn_fused) return s;

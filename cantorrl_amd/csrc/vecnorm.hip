@@ -58,6 +58,7 @@ struct VnArgs {
     int32_t* ep_len;
     double* ep_ret_done;
     int32_t* ep_len_done;
+    const double* ep_reward;   // the env's f64 step rewards Monitor sums (he_info::reward_step)
     int reset;   // he_vecnorm_reset: returns = 0 instead of the discounted update
 };
 
@@ -112,11 +113,14 @@ __global__ void __launch_bounds__(kVnThreads) vn_moments_kernel(VnArgs a) {
     vn::moments_body(moments_args(a), blockIdx.x);
 }
 
-// A row's inputs besides its obs: reward, done flag, Monitor running sums.
+// A row's inputs besides its obs: reward, done flag, Monitor running sums and the f64
+// reward Monitor adds (Monitor wraps each env inside the VecEnv, train_ppo_v2.py:119, so it
+// sums the env's own f64 reward, hedging_env_v2.py:262,294 -- not the f32 VecEnv buffer).
 struct RowIn {
     float rw;
     bool dn;
     double er;
+    double rw64;
     int32_t el;
 };
 __device__ __forceinline__ RowIn row_in(const VnArgs& a, int64_t r) {
@@ -124,6 +128,7 @@ __device__ __forceinline__ RowIn row_in(const VnArgs& a, int64_t r) {
     in.rw = a.reward[r];
     in.dn = a.done ? a.done[r] != 0 : false;
     in.er = a.ep_ret ? a.ep_ret[r] : 0.0;
+    in.rw64 = a.ep_ret ? a.ep_reward[r] : 0.0;
     in.el = a.ep_ret ? a.ep_len[r] : 0;
     return in;
 }
@@ -241,8 +246,8 @@ __global__ void __launch_bounds__(kVnThreads) vn_apply_kernel(VnArgs a) {
             }
         }
         if (dn) a.returns[r] = 0.0;   // self.returns[dones] = 0
-        if (a.ep_ret) {                 // Monitor: sum(rewards), len(rewards)
-            const double er = in.er + (double)rw;
+        if (a.ep_ret) {                 // Monitor: sum(rewards) of the f64 rewards, len(rewards)
+            const double er = in.er + in.rw64;
             const int32_t el = in.el + 1;
             if (dn) {
                 a.ep_ret_done[r] = er;
@@ -382,11 +387,12 @@ static he_status vecnorm_step(const he_vecnorm_params* p, int64_t n, const float
                               const uint8_t* done, const float* terminal_obs, double* returns, double* stats,
                               void* scratch, float* obs_out, float* reward_out, float* terminal_obs_out,
                               double* ep_return, int32_t* ep_length, double* ep_return_done,
-                              int32_t* ep_length_done, void* stream, bool moments) {
+                              int32_t* ep_length_done, const double* ep_reward, void* stream, bool moments) {
     if (!params_ok(p) || n < 0) return HE_EINVAL;
     if (n == 0) return HE_OK;
     if (!obs || !reward || !returns || !stats || !scratch || !obs_out || !reward_out) return HE_EINVAL;
-    if ((ep_return != nullptr) != (ep_length != nullptr) || (ep_return && (!ep_return_done || !ep_length_done || !done)))
+    if ((ep_return != nullptr) != (ep_length != nullptr) ||
+        (ep_return && (!ep_return_done || !ep_length_done || !done || !ep_reward)))
         return HE_EINVAL;
     VnArgs a = base_args(p, n);
     a.obs = obs;
@@ -402,6 +408,7 @@ static he_status vecnorm_step(const he_vecnorm_params* p, int64_t n, const float
     a.ep_len = ep_length;
     a.ep_ret_done = ep_return_done;
     a.ep_len_done = ep_length_done;
+    a.ep_reward = ep_reward;
     return launch(a, scratch, (hipStream_t)stream, moments);
 }
 
@@ -409,20 +416,20 @@ he_status he_vecnorm_step(const he_vecnorm_params* p, int64_t n, const float* ob
                           const uint8_t* done, const float* terminal_obs, double* returns, double* stats,
                           void* scratch, float* obs_out, float* reward_out, float* terminal_obs_out,
                           double* ep_return, int32_t* ep_length, double* ep_return_done, int32_t* ep_length_done,
-                          void* stream) {
+                          const double* ep_reward, void* stream) {
     return vecnorm_step(p, n, obs, reward, done, terminal_obs, returns, stats, scratch, obs_out, reward_out,
-                        terminal_obs_out, ep_return, ep_length, ep_return_done, ep_length_done, stream, true);
+                        terminal_obs_out, ep_return, ep_length, ep_return_done, ep_length_done, ep_reward, stream, true);
 }
 
 he_status he_vecnorm_apply(const he_vecnorm_params* p, int64_t n, const float* obs, const float* reward,
                            const uint8_t* done, const float* terminal_obs, double* returns, double* stats,
                            void* scratch, float* obs_out, float* reward_out, float* terminal_obs_out,
                            double* ep_return, int32_t* ep_length, double* ep_return_done, int32_t* ep_length_done,
-                           void* stream) {
+                           const double* ep_reward, void* stream) {
     // training merges the fused partials, which cover <= 65,536 rows; frozen statistics read none
     if (p && p->training && n > (int64_t)kVnMaxBlocks * kVnThreads) return HE_EINVAL;
     return vecnorm_step(p, n, obs, reward, done, terminal_obs, returns, stats, scratch, obs_out, reward_out,
-                        terminal_obs_out, ep_return, ep_length, ep_return_done, ep_length_done, stream, false);
+                        terminal_obs_out, ep_return, ep_length, ep_return_done, ep_length_done, ep_reward, stream, false);
 }
 
 he_status he_vecnorm_reset(const he_vecnorm_params* p, int64_t n, const float* obs, double* returns, double* stats,

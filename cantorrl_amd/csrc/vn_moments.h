@@ -198,7 +198,8 @@ __device__ __forceinline__ void moments_from_rows(const MomentsArgs& a, int bid,
 // VecNormalize.step_wait with the statistics frozen (training=False, train_ppo_v2.py:450-453):
 // no moments, so nothing crosses workgroups and he_step's own launch can finish the step
 // (step1_vne_kernel, he_vecnorm_attach_eval) -- the obs rows normalized from the step's LDS
-// staging tile, the reward from the thread's register, returns[done] = 0, Monitor's sums and
+// staging tile, the reward from the thread's register (f32 for VecNormalize, the f64 one for
+// Monitor, which sums the env's own rewards: train_ppo_v2.py:119), returns[done] = 0, Monitor's sums and
 // the normalized terminal obs of done rows.  The same per-element arithmetic as vecnorm.hip's
 // apply (ColNorm, norm_elem): the same bits as he_step + he_vecnorm_apply.
 struct ColNorm {
@@ -276,8 +277,8 @@ __device__ __forceinline__ void prep_frozen(FrozenNorm& z, const ApplyArgs& a, c
 // workgroup barrier that follows prep_frozen; thread t < rows owns row r0 + t: its reward, done
 // flag and terminal obs row.
 __device__ __forceinline__ void apply_frozen_rows(const ApplyArgs& a, const FrozenNorm& z, int64_t r0, int rows,
-                                                  const float* tile, const FrozenPre& f, float rew, bool done,
-                                                  const float* tobs) {
+                                                  const float* tile, const FrozenPre& f, float rew, double rew64,
+                                                  bool done, const float* tobs) {
     const ColNorm* cn = z.cn;
     const double rinv = z.rinv;
     const int t = threadIdx.x;
@@ -305,8 +306,8 @@ __device__ __forceinline__ void apply_frozen_rows(const ApplyArgs& a, const Froz
         }
     }
     if (done) a.returns[r] = 0.0;   // self.returns[dones] = 0
-    if (a.ep_ret) {                 // Monitor: sum(rewards), len(rewards)
-        const double er = f.er + (double)rew;
+    if (a.ep_ret) {                 // Monitor: sum(rewards) of the env's f64 rewards, len(rewards)
+        const double er = f.er + rew64;
         const int32_t el = f.el + 1;
         if (done) {
             a.ep_ret_done[r] = er;

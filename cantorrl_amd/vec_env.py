@@ -21,6 +21,11 @@ import torch
 from . import _lib
 from .spaces import Box
 
+try:   # the C rows of an info view (csrc/info_rows.c, built with the HIP libraries)
+    from .lib import _info_rows
+except ImportError as e:  # no fallback: a missing build is an error, not a slow path
+    raise ImportError(f"cantorrl_amd/lib/_info_rows is not built ({e}): run `python -m cantorrl_amd.build`")
+
 OBS_LOW = np.array([0.1, -1.0, -1.0, -1.0, -1.0, 0.0, 0.0, -1.0, 0.0, -1.0, 0.0, -1.0, -1.0], np.float32)
 OBS_HIGH = np.array([10.0, 1.0, 1.0, 1.0, 1.0, 1.0, 1.0, 1.0, 50.0, 1.0, 50.0, 1.0, 1.0], np.float32)
 
@@ -40,6 +45,7 @@ MONITOR_KEYWORDS = ("per_share_step_pnl", "raw_pnl_deviation_abs", "transaction_
 
 _TORCH_DT = {"f8": torch.float64, "f4": torch.float32, "i4": torch.int32}
 _NP_DT = {torch.float64: np.float64, torch.float32: np.float32, torch.int32: np.int32}
+_ROW_KIND = {np.dtype(np.float64): "d", np.dtype(np.float32): "f", np.dtype(np.int32): "i"}
 # the current stream's raw handle (torch's own accessor; current_stream().cuda_stream builds a
 # Stream object per call, a few us of every eager step)
 _raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None) or \
@@ -194,6 +200,14 @@ class HedgingVecEnv:
         self._act = torch.zeros((n, 2), dtype=torch.float32, device=dev)
         self._tobs = torch.zeros((n, 13), dtype=torch.float32, device=dev)
         self.info_keys = tuple(info_keys or ())
+        self.monitor_keywords = tuple(monitor_keywords) if monitor_keywords else None
+        # Monitor sums the env's own f64 reward (it wraps each env inside the VecEnv,
+        # train_ppo_v2.py:119; hedging_env_v2.py:262,294), so with monitor_keywords the step
+        # also writes info["reward_step"] -- a hidden column unless the caller asked for it
+        layout_keys = self.info_keys
+        if self.monitor_keywords is not None and "reward_step" not in layout_keys:
+            layout_keys = layout_keys + ("reward_step",)
+        self._row_keys = self.info_keys
         self._info_t = {}
         self._info = _lib.HeInfo()
         known = dict(_lib.INFO_FIELDS)
@@ -207,7 +221,7 @@ class HedgingVecEnv:
         self._io_step_bytes = o_trunc            # obs + reward + terminated
         info0 = _align(end, 256)
         offs, tot = [], 0
-        for k in self.info_keys:
+        for k in layout_keys:
             if k not in known:
                 raise KeyError(f"unknown info key {k!r}")
             dt = _TORCH_DT[known[k]]
@@ -232,11 +246,11 @@ class HedgingVecEnv:
         # a later step then shows that step's values)
         self.freeze_infos = bool(freeze_infos)
         self.return_numpy = bool(return_numpy)
-        self.monitor_keywords = tuple(monitor_keywords) if monitor_keywords else None
+        self._rew64 = self._info_t.get("reward_step")   # the f64 rewards (Monitor's sums)
         self._pending_seeds = None
         self._live_view = None  # weakref to the newest InfoView (see InfoView)
         self._actions_pending = None
-        # Monitor (monitor_keywords): each env's running reward sum as f64 on the device
+        # Monitor (monitor_keywords): each env's running sum of its f64 rewards on the device
         # (sum(float(r)) of Monitor.step, the same additions in the same order), and the
         # episode length as (steps so far - the step the env's episode began), so a step
         # that ends no episode costs the host nothing
@@ -256,7 +270,7 @@ class HedgingVecEnv:
         if self.monitor_keywords is not None:
             # the Monitor sums' torch kernels, loaded now (a first launch loads the code object:
             # tens of ms, which the first episode end would otherwise pay)
-            self._ep_ret.add_(self._rew)
+            self._ep_ret.add_(self._rew64)
             self._ep_ret.masked_fill_(self._term.bool(), 0.0)
             self._ep_ret.zero_()
         self.action_space = Box(-1.0, 1.0, (2,), np.float32)
@@ -448,10 +462,10 @@ class HedgingVecEnv:
         self._actions_pending = None
         obs, rew, term, _ = self.step_tensors(actions)
         self._steps += 1
-        if self.monitor_keywords is not None:
-            self._ep_ret.add_(rew)
-        if not self.return_numpy:
+        if not self.return_numpy:   # device results: Monitor's episodes are not reported
             return obs, rew, term.bool(), InfoView(self, None)
+        if self.monitor_keywords is not None:
+            self._ep_ret.add_(self._rew64)   # Monitor.step: the env's f64 reward
         # obs, reward and terminated are adjacent in the io buffer: one DMA, one wait
         n = self.num_envs
         h = self._pull([self._io[:self._io_step_bytes]])[0]
@@ -574,30 +588,38 @@ class HedgingVecEnv:
         return self._info_t[key]
 
 
-class InfoView:
-    """Lazy list[dict] of per-env infos (SB3 contract) over the device info SoA.
+class InfoView(_info_rows.Rows):
+    """The step's `infos`: SB3's list of per-env info dicts, over the device info SoA.
 
-    The view reads the env's live info buffers, copied to the host on the first access.
-    It is the env's newest view until the env's next step or reset, which first freezes
-    it when it is still alive and has not been read: a view read after later steps still
-    shows its own step.  In SB3's loop (`obs, r, d, infos = env.step(a)`) the previous
-    `infos` is still referenced while step() runs, so a step usually pays the freeze: ONE
-    device copy of the info fields' flat buffer (N x the keys' bytes: 1.5 MB for the three
-    Monitor keys at 65,536 envs, a few us), not one per key.  freeze_infos=False (env
-    constructor) drops the snapshots for callers that read infos before the next step.
-    The done rows' data (terminal obs, Monitor episode sums) is pulled by step_wait right
-    away, from the live buffers, in the same single copy as the info fields; every row's
-    dict is built on first access."""
+    Rows come from the C module csrc/info_rows.c: a row answers row[k] / row.get(k) / k in row
+    straight from the step's host columns, and becomes a plain dict only when something needs
+    the whole mapping (keys, items, iteration, copy, an assignment -- SB3's VecNormalize writing
+    a normalized terminal_observation).  SB3 reads every row every step (collect_rollouts'
+    info.get("episode") / info.get("is_success")): that costs a few ms at 65,536 envs, where a
+    dict per row costs 20+ (bench.py's sb3_loop line).  A done row's "terminal_observation"
+    and Monitor "episode" are made when they are first read.
+
+    The view reads the env's live info buffers, copied to the host on the first row access.
+    It is the env's newest view until the env's next step or reset, which first freezes it
+    when it is still alive and has not been read: a view read after later steps still shows
+    its own step.  In SB3's loop (`obs, r, d, infos = env.step(a)`) the previous `infos` is
+    still referenced while step() runs, so a step usually pays the freeze: ONE device copy
+    of the info fields' flat buffer, not one per key.  freeze_infos=False (env constructor)
+    drops the snapshots for callers that read infos before the next step.  The done rows'
+    data (terminal obs, Monitor episode sums) is pulled by step_wait right away, from the
+    live buffers, in the same single copy as the info fields."""
 
     def __init__(self, venv, done):
         self._v = venv
         self._done = done
-        self._cache = {}
         self._host = None
         self._snap = None
         self._ends = None   # done rows' host data (_materialize_done)
         venv._retire_view()
         venv._live_view = weakref.ref(self)
+
+    def __len__(self):   # no host copy for len()
+        return self._v.num_envs
 
     def _freeze(self):
         if self._host is None and self._snap is None and self._v._info_t:
@@ -614,10 +636,27 @@ class InfoView:
             self._snap = None
         return self._host
 
+    def _load(self):
+        """First row access (info_rows.c): attach the host columns to the C rows."""
+        v = self._v
+        h = self._host_info() if v._info_t else {}
+        keys = tuple(k for k in v._row_keys if k in h)
+        cols = tuple(h[k] for k in keys)
+        kinds = "".join(_ROW_KIND[c.dtype] for c in cols).encode()
+        ends = None
+        done = None
+        done_keys = ()
+        if self._ends is not None:
+            done = self._done
+            mon = self._ends[4]
+            done_keys = ("terminal_observation", "episode") if mon else ("terminal_observation",)
+            ends = _episode_ends(self._ends, h, v.monitor_keywords)
+        self._attach(keys, cols, kinds, v.num_envs, "TimeLimit.truncated", False, done, done_keys, ends)
+
     def _materialize_done(self, done):
         """Done rows (called by step_wait before any later step): this step's terminal obs,
         info fields and, with Monitor, episode sums come to the host now -- one pull -- and
-        the rows' dicts are built when they are read (__getitem__), as every other row's."""
+        the rows' extra items are made when they are read."""
         v = self._v
         mon = v.monitor_keywords is not None
         srcs = [v._tobs]
@@ -635,35 +674,24 @@ class InfoView:
             v._ep_start[np.nonzero(done)[0]] = v._steps
         self._ends = (got[0], er, el, round(time.time() - v._t_start, 6), mon)
 
-    def _episode_row(self, d, i):
-        """The done row i's SB3 / Monitor extras (terminal_observation, episode)."""
-        tobs, er, el, t, mon = self._ends
-        d["terminal_observation"] = tobs[i].copy()
+
+def _episode_ends(ends, host, monitor_keywords):
+    """ends(i) of a done row: {"terminal_observation", "episode"} (SB3 DummyVecEnv and
+    Monitor.step: r = round(sum of the episode's f64 rewards, 6), l, t, + info_keywords).
+    Holds the host arrays only (no reference back to the view)."""
+    tobs, er, el, t, mon = ends
+
+    def row_ends(i):
+        d = {"terminal_observation": tobs[i].copy()}
         if mon:
-            h = self._host
             ep = {"r": round(float(er[i]), 6), "l": int(el[i]), "t": t}
-            for k in self._v.monitor_keywords:
-                ep[k] = h[k][i].item() if k in h else None
+            for k in monitor_keywords:
+                ep[k] = host[k][i].item() if k in host else None
             d["episode"] = ep
+        return d
+    return row_ends
 
-    def __len__(self):
-        return self._v.num_envs
 
-    def __getitem__(self, i):
-        if isinstance(i, slice):
-            return [self[j] for j in range(*i.indices(len(self)))]
-        i = int(i)
-        if i < 0:
-            i += len(self)
-        if i not in self._cache:
-            h = self._host_info()
-            d = {k: h[k][i].item() for k in h}
-            d["TimeLimit.truncated"] = False
-            if self._ends is not None and self._done[i]:
-                self._episode_row(d, i)
-            self._cache[i] = d
-        return self._cache[i]
-
-    def __iter__(self):
-        for i in range(len(self)):
-            yield self[i]
+# the rows are mappings (isinstance(row, collections.abc.Mapping), dict(row), **row)
+import collections.abc  # noqa: E402
+collections.abc.MutableMapping.register(_info_rows.Row)

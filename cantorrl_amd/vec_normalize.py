@@ -59,6 +59,9 @@ class DeviceVecNormalize:
         self._ep_len = torch.zeros(n, dtype=torch.int32, device=dev)
         self._ep_ret_done = torch.zeros(n, dtype=torch.float64, device=dev)
         self._ep_len_done = torch.zeros(n, dtype=torch.int32, device=dev)
+        # Monitor episode sums kept on the device when the env has Monitor (monitor_keywords):
+        # they sum its f64 step rewards (train_ppo_v2.py:119; hedging_env_v2.py:262,294)
+        self._monitor = getattr(venv, "_rew64", None) is not None
         self._check(self.lib.he_vecnorm_init(self._p(self._stats), D, self._stream()), "he_vecnorm_init")
         # the moments half of each training step inside the env's he_step launch
         # (he_vecnorm_attach; up to 65,536 envs), then he_vecnorm_apply; else he_vecnorm_step
@@ -68,7 +71,7 @@ class DeviceVecNormalize:
         self._actions_pending = None
         self._args = None   # _call_args cache
         if self.return_numpy:
-            venv._warm_pinned([self._io_out.numel()] * 3 + [n] * 3 + [52 * n, 8 * n, 4 * n, venv._info_flat.numel()])
+            venv._warm_pinned([self._io_out.numel()] * 3 + [n] * 3 + [4 * D * n, 8 * n, 4 * n, venv._info_flat.numel()])
         self._t_start = time.time()
 
     # ------------------------------------------------------------------ plumbing
@@ -191,22 +194,29 @@ class DeviceVecNormalize:
                    float(self.clip_obs), float(self.clip_reward), float(self.epsilon))
             p = self._params()
             v = self.venv
+            # Monitor's sums (venv monitor_keywords) add the env's f64 rewards (venv._rew64, the
+            # step's info["reward_step"]); without Monitor they are not kept
+            mon = (self._ep_ret, self._ep_len, self._ep_ret_done, self._ep_len_done, v._rew64) \
+                if self._monitor else (None,) * 5
             ptrs = tuple(self._p(t) for t in (v._obs, v._rew, v._term, v._tobs, self._returns, self._stats,
-                                              self._scratch, self._obs_out, self._rew_out, self._tobs_out,
-                                              self._ep_ret, self._ep_len, self._ep_ret_done, self._ep_len_done))
-            out = _lib.HeVecnormOut(self._stats.data_ptr(), self._returns.data_ptr(), self._obs_out.data_ptr(),
-                                    self._rew_out.data_ptr(), self._tobs_out.data_ptr(), self._ep_ret.data_ptr(),
-                                    self._ep_len.data_ptr(), self._ep_ret_done.data_ptr(), self._ep_len_done.data_ptr())
+                                              self._scratch, self._obs_out, self._rew_out, self._tobs_out) + mon)
+            out = _lib.HeVecnormOut(*(None if t is None else t.data_ptr() for t in (
+                self._stats, self._returns, self._obs_out, self._rew_out, self._tobs_out) + mon[:4]))
             c = self._args = (key, p, ctypes.byref(p), ptrs, ctypes.byref(out), out)
         return c
 
-    def step_tensors(self, actions):
+    def step_tensors(self, actions, info=True):
         """(normalized obs, normalized reward, terminated, truncated) device tensors;
-        the normalized terminal obs of done envs are in `terminal_obs_tensor`."""
+        the normalized terminal obs of done envs are in `terminal_obs_tensor`.  info=False
+        skips the env's info fields, except the f64 reward Monitor's sums need when this
+        step's VecNormalize work runs outside he_step's own launch (the fused eval step adds
+        it from registers)."""
         c = self._call_args()
         fused = self._arm(c)
+        if not info and self._monitor and fused != "eval":
+            info = True
         try:
-            obs, rew, term, trunc = self.venv.step_tensors(actions)
+            obs, rew, term, trunc = self.venv.step_tensors(actions, info=info)
         except BaseException:
             if fused:  # the armed he_step did not run: nothing may keep this object's buffers
                 self.lib.he_vecnorm_attach(self.venv._h, None, None, None, None)
@@ -281,7 +291,8 @@ class DeviceVecNormalize:
         infos = _NormInfoView(self, done)
         if done.any():
             infos._materialize_done(done)
-        return h[:52 * n].view(np.float32).reshape(n, 13), h[52 * n:].view(np.float32), done, infos
+        D = _lib.HE_OBS_DIM
+        return h[:n * D * 4].view(np.float32).reshape(n, D), h[n * D * 4:].view(np.float32), done, infos
 
     def step(self, actions):
         self.step_async(actions)
@@ -328,12 +339,12 @@ class _NormInfoView(InfoView):
 
     def _materialize_done(self, done):
         # called by step_wait right after the step: this step's normalized terminal obs and
-        # Monitor sums are still in the wrapper's buffers -- one pull; the rows' dicts are
-        # built when read (InfoView.__getitem__ -> _episode_row)
+        # Monitor sums are still in the wrapper's buffers -- one pull; the rows' extra items
+        # are made when read (InfoView._load -> _episode_ends)
         w, v = self._w, self._w.venv
         srcs = [w._tobs_out, w._ep_ret_done, w._ep_len_done]
         if self._host is None:
             srcs.append(self._snap if self._snap is not None else v._info_flat)
         got = v._pull(srcs)   # one wait for all of them
         self._host_info(got[3] if self._host is None else None)
-        self._ends = (got[0], got[1], got[2], round(time.time() - w._t_start, 6), v.monitor_keywords is not None)
+        self._ends = (got[0], got[1], got[2], round(time.time() - w._t_start, 6), w._monitor)

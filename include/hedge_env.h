@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define HE_ABI_VERSION 3
+#define HE_ABI_VERSION 4   /* 4: he_vecnorm_step/apply take Monitor's f64 rewards */
 #define HE_BOOK_MAX 8
 #define HE_OBS_DIM 13
 #define HE_ACT_DIM 2
@@ -374,14 +374,17 @@ he_status he_vecnorm_init(double* stats, int32_t obs_dim, void* stream);
  * ret_rms.update(returns) (training); obs_out = clip((obs - mean) / sqrt(var + eps));
  * reward_out = clip(reward / sqrt(ret_var + eps)) (norm_reward, else a copy);
  * terminal_obs_out[i] normalized for done rows (when both pointers are given);
- * returns[done] = 0.  Monitor (ep_return / ep_length non-NULL): the raw rewards are
- * summed per env, and a done row copies its episode's sum / length to
- * ep_return_done / ep_length_done and restarts from 0. */
+ * returns[done] = 0.  Monitor (ep_return / ep_length non-NULL): ep_reward [n] f64 -- the
+ * env's own f64 step rewards (he_info::reward_step), which SB3's Monitor sums because it wraps
+ * each env inside the VecEnv (train_ppo_v2.py:119; hedging_env_v2.py:262,294), not the f32
+ * VecEnv buffer -- are summed per env in step order, and a done row copies its episode's
+ * sum / length to ep_return_done / ep_length_done and restarts from 0 (ep_reward is then
+ * required: HE_EINVAL without it). */
 he_status he_vecnorm_step(const he_vecnorm_params* p, int64_t n, const float* obs, const float* reward,
                           const uint8_t* done, const float* terminal_obs, double* returns, double* stats,
                           void* scratch, float* obs_out, float* reward_out, float* terminal_obs_out,
                           double* ep_return, int32_t* ep_length, double* ep_return_done,
-                          int32_t* ep_length_done, void* stream);
+                          int32_t* ep_length_done, const double* ep_reward, void* stream);
 
 /* The same step split in two, for n <= 65,536 (one moments partial per he_step
  * workgroup): he_vecnorm_attach(env, p, returns, stats, scratch) arms the NEXT he_step on
@@ -398,7 +401,7 @@ he_status he_vecnorm_apply(const he_vecnorm_params* p, int64_t n, const float* o
                            const uint8_t* done, const float* terminal_obs, double* returns, double* stats,
                            void* scratch, float* obs_out, float* reward_out, float* terminal_obs_out,
                            double* ep_return, int32_t* ep_length, double* ep_return_done,
-                           int32_t* ep_length_done, void* stream);
+                           int32_t* ep_length_done, const double* ep_reward, void* stream);
 
 /* Evaluation (VecNormalize(training=False), train_ppo_v2.py:450-453): with the statistics
  * frozen nothing of the step crosses envs, so the NEXT he_step on `env` (one-shot, consumed
@@ -406,8 +409,10 @@ he_status he_vecnorm_apply(const he_vecnorm_params* p, int64_t n, const float* o
  * work itself -- obs_out, reward_out, terminal_obs_out of done rows, returns[done] = 0, the
  * Monitor sums -- in its own launch: the caller then calls no he_vecnorm_* function for that
  * step.  he_step must get the obs, reward, terminated and terminal_obs buffers; a step that
- * takes another kernel (info requested) runs he_vecnorm_apply itself after it.  p->training
- * must be 0; out's buffers are he_vecnorm_step's (scratch unused). */
+ * takes another kernel (info requested) runs he_vecnorm_apply itself after it, with
+ * info->reward_step as the Monitor sums' f64 rewards (required then when the Monitor buffers
+ * are given; the fused launch adds the f64 reward from its registers).  p->training must be 0;
+ * out's buffers are he_vecnorm_step's (scratch unused). */
 typedef struct he_vecnorm_out {
     const double* stats;
     double* returns;

@@ -72,8 +72,14 @@ class VecNormalizeOracle:
             self.obs_rms.update(obs)
         return self.normalize_obs(obs)
 
-    def step(self, obs, rewards, dones, terminal_obs=None):
-        """-> (obs, rewards, terminal_obs of done rows, {i: (ep_return, ep_length)})."""
+    def step(self, obs, rewards, dones, terminal_obs=None, env_rewards=None):
+        """-> (obs, rewards, terminal_obs of done rows, {i: (ep_return, ep_length)}).
+
+        rewards: the VecEnv's reward buffer (what VecNormalize sees); env_rewards: the envs'
+        own f64 step rewards, which Monitor sums -- Monitor wraps each env inside the VecEnv
+        (train_ppo_v2.py:119; monitor.py appends float(reward) of the env's step,
+        hedging_env_v2.py:262,294).  env_rewards=None sums `rewards` (an env whose reward is
+        already that buffer's dtype)."""
         if self.training and self.norm_obs:
             self.obs_rms.update(obs)
         obs_n = self.normalize_obs(obs)
@@ -85,8 +91,8 @@ class VecNormalizeOracle:
         if terminal_obs is not None:
             tobs_n = {int(i): self.normalize_obs(terminal_obs[i]) for i in np.nonzero(dones)[0]}
         self.returns[dones] = 0
-        # Monitor: sum / count of the raw rewards per episode
-        self.ep_ret += rewards.astype(np.float64)
+        # Monitor: sum / count of the envs' own (f64) rewards per episode, in step order
+        self.ep_ret += np.asarray(rewards if env_rewards is None else env_rewards, np.float64)
         self.ep_len += 1
         eps = {int(i): (self.ep_ret[i], int(self.ep_len[i])) for i in np.nonzero(dones)[0]}
         self.ep_ret[dones] = 0.0

@@ -683,6 +683,11 @@ LDS_CASES = {
                             slippage_bps=1.0), (64, 37, 100, 9)),
     "fixed_european_long_T1": (257, dict(episode_length=255, mark="fixed_european"), {}, (300, 1, 213)),
     "fixed_european_T1": (70, dict(episode_length=1, mark="fixed_european"), {}, (7, 12)),
+    # rolling-ATM marks of a small S at a small sigma (S near 1.49 / 2.45: K = 1 / 2,
+    # |d| ~ 11-14), whose deep out-of-the-money side falls to ~1e-39 -- f32 subnormals: the lean
+    # stepper's obs price columns against the tile kernels' IEEE quotients
+    "tiny_marks": (1000, dict(episode_length=60, s0=1.49, variance=0.0081), {}, (64, 37)),
+    "tiny_marks_cross": (700, dict(episode_length=90, s0=2.45, variance=0.0025), {}, (64, 64, 3)),
     "heston_fixed_european_book": (333, dict(episode_length=29, mark="fixed_european", **HESTON_GEN,
                                              book=[dict(type="put", strike=480.0, expiry=20, quantity=-10.0)]),
                                    {}, (5, 64, 13, 71)),

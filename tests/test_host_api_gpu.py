@@ -20,8 +20,8 @@ MON = ("per_share_step_pnl", "raw_pnl_deviation_abs", "transaction_costs_total")
 def _pair(n):
     from cantorrl_amd.vec_env import HedgingVecEnv
     a = HedgingVecEnv(n, mode="gbm", generate=GEN, seed=21, device=DEV, monitor_keywords=MON, **KW)
-    b = HedgingVecEnv(n, mode="gbm", generate=GEN, seed=21, device=DEV, return_numpy=False, info_keys=MON,
-                      **KW)
+    b = HedgingVecEnv(n, mode="gbm", generate=GEN, seed=21, device=DEV, return_numpy=False,
+                      info_keys=MON + ("reward_step",), **KW)
     return a, b
 
 
@@ -40,10 +40,14 @@ def test_numpy_path_equals_device_path_and_late_infos_keep_their_step(n):
         o2, r2, t2, _ = b.step_tensors(torch.from_numpy(act).to(DEV))
         tobs_b = b._tobs.cpu().numpy().copy()
         info_b = {k: b.info_tensor(k).cpu().numpy().copy() for k in MON}
+        rew64 = b.info_tensor("reward_step").cpu().numpy().copy()
         assert obs.dtype == np.float32 and obs.shape == (n, 13) and done.dtype == np.bool_
         assert np.array_equal(obs, o2.cpu().numpy()) and np.array_equal(rew, r2.cpu().numpy())
         assert np.array_equal(done, t2.cpu().numpy().astype(bool))
-        rets += rew.astype(np.float64)
+        # Monitor sums the env's f64 reward (train_ppo_v2.py:119, hedging_env_v2.py:262,294),
+        # which the f32 VecEnv reward is the cast of
+        assert np.array_equal(rew, rew64.astype(np.float32))
+        rets += rew64
         # keep every array and the info list unread, across the later steps
         kept.append((obs, obs.copy(), rew, rew.copy(), done, done.copy(), infos, tobs_b, info_b, rets.copy()))
         rets[done] = 0.0
@@ -53,6 +57,7 @@ def test_numpy_path_equals_device_path_and_late_infos_keep_their_step(n):
         for i in range(n):
             d = infos[i]
             assert d["TimeLimit.truncated"] is False
+            assert "reward_step" not in d   # Monitor's hidden f64 column is not an info key here
             for k in MON:
                 assert d[k] == info_b[k][i], (s, i, k)
             if done[i]:

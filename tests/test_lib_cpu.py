@@ -65,7 +65,7 @@ def test_create_rejects_bad_mark_without_gpu():
                             (_lib.HE_MODE_REPLAY, _lib.HE_MARK_FIXED_EUROPEAN, b"replay mode")):
         c = _lib.HeConfig()
         lib.he_config_init(c, 2)
-        assert c.mark == _lib.HE_MARK_ROLLING_ATM and c.abi_version == _lib.HE_ABI_VERSION == 3
+        assert c.mark == _lib.HE_MARK_ROLLING_ATM and c.abi_version == _lib.HE_ABI_VERSION == 4
         c.mode, c.mark = mode, mark
         h = _lib.ctypes.c_void_p()
         assert lib.he_create(c, _lib.ctypes.byref(h)) == _lib.HE_EINVAL

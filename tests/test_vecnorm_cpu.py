@@ -45,6 +45,13 @@ def test_vecnormalize_oracle_step_semantics():
     obs_n, rew_n, tobs_n, eps = vn.step(o1, rew, done, terminal_obs=o1)
     assert set(tobs_n) == {3} and set(eps) == {3}
     assert eps[3] == (float(rew[3]), 1)
+    # Monitor sums the envs' own f64 rewards when given (train_ppo_v2.py:119: Monitor wraps
+    # each env inside the VecEnv), not the VecEnv's f32 buffer
+    vn2 = VecNormalizeOracle(n, obs_dim=3, gamma=0.9)
+    vn2.reset(o0)
+    env_rew = rew.astype(np.float64) + 1e-9   # not representable in f32
+    _, _, _, eps2 = vn2.step(o1, rew, done, terminal_obs=o1, env_rewards=env_rew)
+    assert eps2[3] == (env_rew[3], 1) and eps2[3][0] != float(rew[3])
     assert vn.returns[3] == 0.0 and vn.returns[0] == rew[0]
     # frozen statistics in eval mode
     vn.training = False
@@ -60,8 +67,12 @@ def test_vecnorm_abi_rejects_bad_arguments():
     assert lib.he_vecnorm_scratch_bytes(1 << 20, 13) > 0
     p = _lib.HeVecnormParams()
     p.obs_dim, p.gamma, p.clip_obs, p.clip_reward, p.epsilon = 13, 0.99, 10.0, 10.0, 1e-8
-    assert lib.he_vecnorm_step(ctypes.byref(p), 0, *([None] * 14), None) == _lib.HE_OK      # n = 0: no-op
-    assert lib.he_vecnorm_step(ctypes.byref(p), 4, *([None] * 14), None) == _lib.HE_EINVAL  # NULL buffers
+    assert lib.he_vecnorm_step(ctypes.byref(p), 0, *([None] * 15), None) == _lib.HE_OK      # n = 0: no-op
+    assert lib.he_vecnorm_step(ctypes.byref(p), 4, *([None] * 15), None) == _lib.HE_EINVAL  # NULL buffers
+    # Monitor buffers without the f64 rewards they sum: refused before anything is launched
+    fake = [ctypes.c_void_p(4096)] * 14
+    for fn in (lib.he_vecnorm_step, lib.he_vecnorm_apply):
+        assert fn(ctypes.byref(p), 4, *fake, None, None) == _lib.HE_EINVAL
     p.obs_dim = 7
     assert lib.he_vecnorm_reset(ctypes.byref(p), 4, *([None] * 5), None) == _lib.HE_EINVAL
     assert lib.he_vecnorm_init(None, 13, None) == _lib.HE_EINVAL

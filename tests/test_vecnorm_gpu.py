@@ -12,9 +12,14 @@ KW = dict(loss_type="abs", pnl_penalty_weight=0.001, lambda_cost=0.0001, theta_w
 GEN = dict(s0=496.48001098632812, variance=0.029028, mu=0.04, dt=1 / 252, episode_length=12)
 
 
-def _env(n):
+MON = ("per_share_step_pnl",)
+
+
+def _env(n, monitor=True):
+    """Monitor on: the step also writes the f64 reward (info reward_step) that Monitor sums."""
     from cantorrl_amd.vec_env import HedgingVecEnv
-    return HedgingVecEnv(n, mode="gbm", generate=GEN, seed=7, device=DEV, return_numpy=False, info_keys=(), **KW)
+    return HedgingVecEnv(n, mode="gbm", generate=GEN, seed=7, device=DEV, return_numpy=False, info_keys=(),
+                         monitor_keywords=MON if monitor else None, **KW)
 
 
 def _run(n, steps, training=True, norm_reward=True, gamma=0.95):
@@ -32,9 +37,11 @@ def _run(n, steps, training=True, norm_reward=True, gamma=0.95):
         a = torch.as_tensor(rng.uniform(-1, 1, size=(n, 2)).astype(np.float32), device=DEV)
         o, r, term, _ = vn.step_tensors(a)
         raw_o, raw_r = env._obs.cpu().numpy(), env._rew.cpu().numpy()
+        raw_r64 = env._rew64.cpu().numpy()
+        assert np.array_equal(raw_r, raw_r64.astype(np.float32))
         done = term.cpu().numpy().astype(bool)
         tobs = env._tobs.cpu().numpy()
-        eo, er, et, eps = ref.step(raw_o, raw_r, done, tobs)
+        eo, er, et, eps = ref.step(raw_o, raw_r, done, tobs, env_rewards=raw_r64)
         so, sr, _, _ = sb3.step(raw_o, raw_r, done, tobs)
         np.testing.assert_allclose(o.cpu().numpy(), eo, rtol=0, atol=2e-6, err_msg=f"obs step {k}")
         np.testing.assert_allclose(r.cpu().numpy(), er.astype(np.float32), rtol=1e-6, atol=1e-7)
@@ -209,7 +216,7 @@ def test_fused_moments_equal_separate_launch(info, monkeypatch):
     for fused in ("1", "0"):
         monkeypatch.setenv("CANTORRL_VN_FUSED", fused)
         env = HedgingVecEnv(3000, mode="gbm", generate=GEN, seed=11, device=DEV, return_numpy=False,
-                            info_keys=("cash",) if info else (), **KW)
+                            info_keys=("cash",) if info else (), monitor_keywords=MON if info else None, **KW)
         vn = DeviceVecNormalize(env, gamma=0.97)
         assert vn._fusable == (fused == "1")
         vn.reset_tensors()
@@ -244,14 +251,16 @@ def test_fused_eval_step_equals_separate_launch(info, norm_reward, n, monkeypatc
     he_vecnorm_apply run by he_step itself after an info step) against he_step +
     he_vecnorm_step with the statistics frozen: obs, rewards, normalized terminal obs,
     Monitor sums and returns bit for bit (the same per-element arithmetic), over episode
-    ends (T = 12) and a partial last workgroup (n = 700, 70000)."""
+    ends (T = 12) and a partial last workgroup (n = 700, 70000).  Monitor is on: the fused
+    launch (info=False) adds the f64 reward from its registers, the separate launch reads the
+    step's info reward_step -- the same sums."""
     from cantorrl_amd.vec_env import HedgingVecEnv
     from cantorrl_amd.vec_normalize import DeviceVecNormalize
     outs = []
     for fused in ("1", "0"):
         monkeypatch.setenv("CANTORRL_VN_FUSED", fused)
         env = HedgingVecEnv(n, mode="gbm", generate=GEN, seed=11, device=DEV, return_numpy=False,
-                            info_keys=("cash",) if info else (), **KW)
+                            info_keys=("cash",) if info else (), monitor_keywords=MON, **KW)
         vn = DeviceVecNormalize(env, gamma=0.97, norm_reward=norm_reward)
         vn.reset_tensors()
         g = torch.Generator(device=DEV)
@@ -261,7 +270,7 @@ def test_fused_eval_step_equals_separate_launch(info, norm_reward, n, monkeypatc
         vn.training = False
         got = []
         for k in range(26):
-            o, r, t, _ = vn.step_tensors(torch.rand((n, 2), device=DEV, generator=g) * 2 - 1)
+            o, r, t, _ = vn.step_tensors(torch.rand((n, 2), device=DEV, generator=g) * 2 - 1, info=info)
             m = t.bool()
             got += [o.clone(), r.clone(), t.clone(), vn.terminal_obs_tensor[m].clone(), vn._ep_ret.clone(),
                     vn._ep_len.clone(), vn._ep_ret_done.clone(), vn._ep_len_done.clone(), vn._returns.clone()]
