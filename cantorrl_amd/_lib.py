@@ -121,7 +121,8 @@ EXPORTS = [
     "he_pcg64_seed_state", "he_host_episode_draws", "he_host_philox", "he_host_div_by", "he_host_div_byf", "he_time_next_step", "he_rollout_policy", "he_host_box_muller",
     "he_sync_market", "he_vecnorm_stats_len", "he_vecnorm_scratch_bytes", "he_vecnorm_init", "he_vecnorm_step",
     "he_vecnorm_apply", "he_vecnorm_attach", "he_vecnorm_attach_eval", "he_vecnorm_reset", "he_fixed_european_marks", "he_bs_delta_hedge", "he_count_nonfinite",
-    "he_device_rng", "he_device_math", "he_host_math", "he_episode_summaries",
+    "he_device_rng", "he_device_math", "he_host_math", "he_episode_summaries", "he_host_alloc", "he_host_free",
+    "he_stream_wait",
 ]
 
 
@@ -210,6 +211,9 @@ def load(path=LIB_PATH):
         "he_device_math": (i32, [i32, vp, i64, vp, vp]),
         "he_host_math": (i32, [i32, vp, i64, vp]),
         "he_episode_summaries": (i32, [vp, vp, vp]),
+        "he_host_alloc": (i32, [ctypes.c_size_t, ctypes.POINTER(vp), ctypes.POINTER(vp)]),
+        "he_host_free": (i32, [vp]),
+        "he_stream_wait": (i32, [vp]),
     }
     ab = path != os.path.join(HERE, "lib", "libhedgeenv.so")  # an A/B build of an older tree
     for name, (res, args) in sig.items():

@@ -5006,6 +5006,35 @@ he_status he_time_next_step(he_env* env, void* start_event, void* stop_event) {
     return HE_OK;
 }
 
+he_status he_host_alloc(size_t bytes, void** host_ptr, void** device_ptr) {
+    if (!host_ptr || !device_ptr || bytes == 0) return HE_EINVAL;
+    *host_ptr = *device_ptr = nullptr;
+    void* h = nullptr;
+    if (hipHostMalloc(&h, bytes, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
+        (void)hipGetLastError();
+        return HE_ENOMEM;
+    }
+    void* d = nullptr;
+    if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) {
+        (void)hipGetLastError();
+        (void)hipHostFree(h);
+        return HE_EHIP;
+    }
+    memset(h, 0, bytes);
+    *host_ptr = h;
+    *device_ptr = d;
+    return HE_OK;
+}
+
+he_status he_host_free(void* host_ptr) {
+    if (!host_ptr) return HE_OK;
+    return hipHostFree(host_ptr) == hipSuccess ? HE_OK : HE_EHIP;
+}
+
+he_status he_stream_wait(void* stream) {
+    return hipStreamSynchronize((hipStream_t)stream) == hipSuccess ? HE_OK : HE_EHIP;
+}
+
 int64_t he_num_envs(const he_env* env) { return env ? env->cfg.n_envs : -1; }
 int32_t he_episode_length(const he_env* env) { return env ? env->cfg.episode_length : -1; }
 int64_t he_num_episodes(const he_env* env) { return env ? env->n_paths : -1; }

@@ -59,7 +59,7 @@ class HedgingEnv:
         keys = [k for k, _ in _lib.INFO_FIELDS]
         self._venv = HedgingVecEnv(1, data_file_path, tables=tables, variant=self._variant, mode=mode,
                                    generate=generate, device=device, autoreset=False, return_numpy=False,
-                                   info_keys=keys, **kw)
+                                   info_keys=keys, host_io=True, **kw)
         v = self._venv
         self.pnl_penalty_weight = kw["pnl_penalty_weight"]
         self.lambda_cost = kw["lambda_cost"]
@@ -86,12 +86,11 @@ class HedgingEnv:
         self.initial_S0_for_episode = 1.0
         self._needs_reset = True
         self._terminated = False
-        # host side of one step: the action goes in through a pinned 8-B staging buffer and
-        # the env's whole io buffer (obs, reward, flags, every info field: ~7 KB) comes back
-        # as ONE copy into a pinned mirror, read through a structured dtype -- one DMA each
-        # way and one event wait per step (a step used to wait on 29 separate copies)
-        self._act_h = torch.zeros((1, 2), dtype=torch.float32, pin_memory=True)
-        self._act_np = self._act_h.numpy()
+        # host side of one step: the env's host-mapped block (HedgingVecEnv host_io,
+        # he_host_alloc) -- the kernel reads the action from it and writes the obs, reward,
+        # flags and every info field into it, read here through a structured dtype: one launch
+        # and one stream wait per step, no DMA.  A reset (rare) writes the device io buffer and
+        # comes back as one copy into a pinned mirror of the same layout.
         self._io_h = torch.zeros(v._io.numel(), dtype=torch.uint8, pin_memory=True)
         fields = {"names": ["obs", "reward", "terminated"], "formats": [("<f4", (13,)), "<f4", "u1"],
                   "offsets": [0, 52, 56]}
@@ -100,7 +99,9 @@ class HedgingEnv:
             fields["formats"].append(np.dtype(dict(_lib.INFO_FIELDS)[k]))
             fields["offsets"].append(v._io_info0 + o)
         fields["itemsize"] = v._io.numel()
-        self._rec = self._io_h.numpy().view(np.dtype(fields))   # shape (1,): a view, refreshed by each copy
+        rec_dt = np.dtype(fields)
+        self._rec = self._io_h.numpy().view(rec_dt)   # shape (1,): a view, refreshed by each copy
+        self._rec_step = v._hio.io.view(rec_dt)        # the mapped block: written by each step
         self._ev = torch.cuda.Event()
 
     # ------------------------------------------------------------------ helpers
@@ -159,11 +160,9 @@ class HedgingEnv:
                              f"{self.episode_length + 1}")
         a = np.asarray(action, dtype=np.float32).reshape(2)
         v = self._venv
-        self._act_np[0] = a
-        v._act.copy_(self._act_h, non_blocking=True)   # the last step's wait retired the staging
         prev_S, prev_v = self.current_stock_price, self.current_volatility
-        v.step_tensors(v._act)
-        h = self._fetch()
+        v.step_host(a)
+        h = self._rec_step[0]
         o = h["obs"].copy()
         self._pull(h)
         terminated = bool(h["terminated"])

@@ -42,6 +42,9 @@ GENERATE_DEFAULTS = dict(s0=496.48001098632812, variance=0.029028, mu=0.04, dt=1
                          heston_xi=0.3, heston_rho=-0.7, mark="rolling_atm")
 
 MONITOR_KEYWORDS = ("per_share_step_pnl", "raw_pnl_deviation_abs", "transaction_costs_total")
+# host_io="auto": the NumPy step path (step_wait) of up to this many envs steps through
+# host-mapped memory (he_host_alloc): no DMA, one launch and one stream wait per step
+HOST_IO_MAX_ENVS = 4096
 
 _TORCH_DT = {"f8": torch.float64, "f4": torch.float32, "i4": torch.int32}
 _NP_DT = {torch.float64: np.float64, torch.float32: np.float32, torch.int32: np.int32}
@@ -94,7 +97,7 @@ class HedgingVecEnv:
     def __init__(self, n_envs, data_file_path=None, *, tables=None, variant=2, mode=None,
                  generate=None, device=None, seed=None, global_env_offset=0, autoreset=True,
                  return_numpy=True, info_keys=MONITOR_KEYWORDS, monitor_keywords=None, freeze_infos=True,
-                 market_block=64, market_prefetch="auto", check_finite=False, **env_kwargs):
+                 market_block=64, market_prefetch="auto", check_finite=False, host_io="auto", **env_kwargs):
         self.lib = _lib.load()
         self.num_envs = int(n_envs)
         self.variant = int(variant)
@@ -262,6 +265,13 @@ class HedgingVecEnv:
         self.check_finite = bool(check_finite)
         self._nonfinite = torch.zeros(1, dtype=torch.int64, device=dev)
         self._t_start = time.time()
+        # the small-N host path (step_wait, HedgingEnv.step): actions in and every output out
+        # through one host-mapped block the step kernel reads and writes itself (_HostIo);
+        # Monitor's sums then live on the host too (the same f64 additions)
+        if host_io == "auto":
+            host_io = self.return_numpy and n <= HOST_IO_MAX_ENVS
+        self._hio = _HostIo(self) if host_io else None
+        self._ep_ret_h = np.zeros(n, np.float64)
 
         if self.return_numpy:
             # the host path's pinned blocks (step outputs, actions, the episode-end pull), made
@@ -338,6 +348,10 @@ class HedgingVecEnv:
             torch.cuda.synchronize(self.device)
             self.lib.he_destroy(self._h)
             self._h = _lib.ctypes.c_void_p()
+        hio = getattr(self, "_hio", None)
+        if hio is not None:
+            hio.free()
+            self._hio = None
 
     def __del__(self):
         try:
@@ -382,6 +396,7 @@ class HedgingVecEnv:
 
     def _monitor_reset(self):
         self._ep_ret.zero_()
+        self._ep_ret_h[:] = 0.0
         self._ep_start[:] = 0
         self._steps = 0
 
@@ -460,6 +475,8 @@ class HedgingVecEnv:
     def step_wait(self):
         actions = self._actions_pending
         self._actions_pending = None
+        if self._hio is not None and self.return_numpy:
+            return self._step_wait_host(actions)
         obs, rew, term, _ = self.step_tensors(actions)
         self._steps += 1
         if not self.return_numpy:   # device results: Monitor's episodes are not reported
@@ -480,6 +497,49 @@ class HedgingVecEnv:
     def step(self, actions):
         self.step_async(actions)
         return self.step_wait()
+
+    def step_host(self, actions):
+        """One he_step through the host-mapped block (host_io): the actions are written into
+        it, the kernel reads them and writes obs / reward / flags / terminal obs / info fields
+        back into it, and one stream wait ends the step.  Returns the block (_HostIo); its
+        arrays hold this step's outputs until the next step_host."""
+        z = self._hio
+        np.copyto(z.act, np.asarray(actions, dtype=np.float32).reshape(self.num_envs, 2))
+        self._retire_view()
+        st = self.lib.he_step(self._h, *z.step_args, _raw_stream(self._dev_index))
+        _lib.check(self.lib, self._h, st, "he_step")
+        if self.check_finite:
+            for p, c in ((z.d_obs, 13 * self.num_envs), (z.d_rew, self.num_envs)):
+                _lib.check(self.lib, self._h, self.lib.he_count_nonfinite(p, c, self._nonfinite.data_ptr(),
+                                                                          self.stream), "he_count_nonfinite")
+        _lib.check(self.lib, self._h, self.lib.he_stream_wait(_raw_stream(self._dev_index)), "he_stream_wait")
+        return z
+
+    def _step_wait_host(self, actions):
+        """step_wait of the host_io path: the step's outputs are copied out of the mapped block
+        once (private arrays: a later step never overwrites them), the info view starts with
+        its host columns, and the Monitor sums are host f64 additions of the env's rewards."""
+        z = self.step_host(actions)
+        self._steps += 1
+        n = self.num_envs
+        h = z.io.copy()
+        obs_h = h[:52 * n].view(np.float32).reshape(n, 13)
+        rew_h = h[52 * n:56 * n].view(np.float32)
+        done_h = h[56 * n:57 * n].view(np.bool_)   # the kernels store 0 / 1
+        infos = InfoView(self, done_h)
+        host = infos._host = self._split_info(h[self._io_info0:])
+        mon = self.monitor_keywords is not None
+        if mon:
+            self._ep_ret_h += host["reward_step"]   # Monitor.step: the env's f64 reward
+        if done_h.any():
+            er = el = None
+            if mon:
+                er = self._ep_ret_h.copy()
+                el = self._steps - self._ep_start
+                self._ep_ret_h[done_h] = 0.0
+                self._ep_start[done_h] = self._steps
+            infos._ends = (z.tobs.copy(), er, el, round(time.time() - self._t_start, 6), mon)
+        return obs_h, rew_h, done_h, infos
 
     def sync_market(self):
         """Join the library's market prefetch into the current stream (call before
@@ -586,6 +646,41 @@ class HedgingVecEnv:
 
     def info_tensor(self, key):
         return self._info_t[key]
+
+
+class _HostIo:
+    """The host-mapped block of the small-N host path (he_host_alloc): the env's io layout
+    [obs | reward | terminated | truncated | info fields] (as the device io buffer), then the
+    actions [N, 2] and the terminal obs [N, 13], each 256-B aligned.  The step kernel reads the
+    actions and writes everything else in place."""
+
+    def __init__(self, venv):
+        lib, n = venv.lib, venv.num_envs
+        c = _lib.ctypes
+        self.lib = lib
+        io_b = venv._io.numel()
+        a_off = _align(io_b, 256)
+        t_off = _align(a_off + 8 * n, 256)
+        total = t_off + 52 * n
+        hp, dp = c.c_void_p(), c.c_void_p()
+        _lib.check(lib, None, lib.he_host_alloc(total, c.byref(hp), c.byref(dp)), "he_host_alloc")
+        self.host = hp.value
+        base = np.frombuffer((c.c_uint8 * total).from_address(hp.value), np.uint8)
+        d = dp.value
+        self.io = base[:io_b]
+        self.act = base[a_off:a_off + 8 * n].view(np.float32).reshape(n, 2)
+        self.tobs = base[t_off:t_off + 52 * n].view(np.float32).reshape(n, 13)
+        self.d_obs, self.d_rew = d, d + 52 * n
+        self.info = _lib.HeInfo()
+        for k, dt, o in venv._info_offs:
+            setattr(self.info, k, d + venv._io_info0 + o)
+        self.step_args = (d + a_off, d, d + 52 * n, d + 56 * n, d + 57 * n, d + t_off,
+                          c.byref(self.info) if venv._info_offs else None)
+
+    def free(self):
+        if self.host:
+            self.lib.he_host_free(self.host)
+            self.host = None
 
 
 class InfoView(_info_rows.Rows):

@@ -299,6 +299,18 @@ he_status he_sync_market(he_env* env, void* stream);
  * without the launch gaps.  One-shot; NULL, NULL cancels. */
 he_status he_time_next_step(he_env* env, void* start_event, void* stop_event);
 
+/* Host-mapped I/O for small env counts (no reference equivalent: the reference's env is a
+ * host object, src/env/hedging_env_v2.py:175-294, stepped from baselines.py:45-51 and through
+ * SubprocVecEnv pipes, train_ppo_v2.py:127-141).  he_host_alloc returns `bytes` of zeroed
+ * pinned host memory (hipHostMalloc mapped + coherent) and the address a kernel uses for it:
+ * he_step's actions / obs / reward / flags / terminal_obs / info pointers may point into it, so a
+ * step is one launch and one he_stream_wait, with no DMA in either direction -- the host path of
+ * N_ENVS = 2 (train_ppo_v2.py:45) and of the single env.  Free with he_host_free after the last
+ * step that used it has completed.  he_stream_wait(stream) = hipStreamSynchronize. */
+he_status he_host_alloc(size_t bytes, void** host_ptr, void** device_ptr);
+he_status he_host_free(void* host_ptr);
+he_status he_stream_wait(void* stream);
+
 /* Introspection. */
 int64_t he_num_envs(const he_env* env);
 int32_t he_episode_length(const he_env* env);

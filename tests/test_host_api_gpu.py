@@ -17,17 +17,20 @@ GEN = dict(s0=496.48001098632812, variance=0.029028, mu=0.04, dt=1 / 252, episod
 MON = ("per_share_step_pnl", "raw_pnl_deviation_abs", "transaction_costs_total")
 
 
-def _pair(n):
+def _pair(n, host_io="auto"):
     from cantorrl_amd.vec_env import HedgingVecEnv
-    a = HedgingVecEnv(n, mode="gbm", generate=GEN, seed=21, device=DEV, monitor_keywords=MON, **KW)
+    a = HedgingVecEnv(n, mode="gbm", generate=GEN, seed=21, device=DEV, monitor_keywords=MON, host_io=host_io, **KW)
     b = HedgingVecEnv(n, mode="gbm", generate=GEN, seed=21, device=DEV, return_numpy=False,
                       info_keys=MON + ("reward_step",), **KW)
     return a, b
 
 
-@pytest.mark.parametrize("n", [2, 300])
-def test_numpy_path_equals_device_path_and_late_infos_keep_their_step(n):
-    a, b = _pair(n)
+@pytest.mark.parametrize("n,host_io", [(2, "auto"), (300, "auto"), (300, False), (5000, "auto")])
+def test_numpy_path_equals_device_path_and_late_infos_keep_their_step(n, host_io):
+    """step_wait through the host-mapped block (host_io: n <= 4096 by default) and through the
+    device io buffer + one pinned DMA (n = 5000, or host_io=False) against step_tensors."""
+    a, b = _pair(n, host_io)
+    assert (a._hio is not None) == (host_io == "auto" and n <= 4096)
     oa = a.reset()
     ob = b.reset_tensors().cpu().numpy()
     assert np.array_equal(oa, ob)
