@@ -203,6 +203,7 @@ def parse(argv=None):
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC traffic pass")
     ap.add_argument("--probe", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--launch-dry-run", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--dist-selftest", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--workload", choices=["env", "rbergomi"], default="env",
                     help="env: the hedging-env step (headline); rbergomi: the rough-Bergomi MC mark generator")
     ap.add_argument("--rb-paths", type=int, default=2048, help="rbergomi: paths per GPU (x 252 days x call/put)")
@@ -517,22 +518,70 @@ class Runner:
 
 
 GATHER_EVERY = 256  # train_ppo_v2.py:48 n_steps
+# Fail fast: a rank that never joins, or a collective that stalls, ends the
+# run after this many seconds (init_process_group's timeout) instead of the driver's wall limit
+DIST_TIMEOUT_S = float(os.environ.get("BENCH_DIST_TIMEOUT", "120"))
+# the `--gpus N` launcher's wall limit on its torch.distributed.run child
+LAUNCH_TIMEOUT_S = float(os.environ.get("BENCH_LAUNCH_TIMEOUT", "900"))
+
+
+def rank_phase(phase, rank=None, world=None):
+    """One rank's progress record: a line on stderr ("[bench rank r/w] phase (t s)") and, under
+    the `--gpus N` launcher, the rank's status file, which the launcher reads to name the ranks
+    that did not finish when the child fails or times out."""
+    rank = int(os.environ.get("RANK", "0")) if rank is None else rank
+    world = int(os.environ.get("WORLD_SIZE", "1")) if world is None else world
+    if world <= 1:
+        return
+    t = round(time.time() - _T0, 2)
+    print(f"[bench rank {rank}/{world}] {phase} ({t} s)", file=sys.stderr, flush=True)
+    d = os.environ.get("BENCH_RANK_STATUS_DIR")
+    if d and os.path.isdir(d):
+        with open(os.path.join(d, f"rank{rank}"), "a") as fh:
+            fh.write(f"{t} {phase}\n")
+
+
+_T0 = time.time()
 
 
 def init_dist(local):
     """One rank per GPU over RCCL (backend "nccl").  BENCH_DIST_BACKEND=gloo is the
     rehearsal of the N-rank path on a box with fewer GPUs than ranks (ranks share
-    device local % device_count, host-side collectives); the driver's runs use RCCL."""
+    device local % device_count, host-side collectives; on a host with no GPU, the CPU
+    test of the launcher); the driver's runs use RCCL.  The process group's timeout is
+    DIST_TIMEOUT_S: a rank that never joins fails the others' init within it."""
+    import datetime
     import torch.distributed as dist
     backend = os.environ.get("BENCH_DIST_BACKEND", "nccl")
-    ndev = torch.cuda.device_count()
-    dev_index = local if backend == "nccl" else local % max(ndev, 1)
-    torch.cuda.set_device(dev_index)
+    timeout = datetime.timedelta(seconds=DIST_TIMEOUT_S)
+    rank_phase("init_process_group(%s, timeout %g s)" % (backend, DIST_TIMEOUT_S))
     if backend == "nccl":
-        dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=timeout)
     else:
-        dist.init_process_group(backend)
+        if torch.cuda.is_available():
+            torch.cuda.set_device(local % max(torch.cuda.device_count(), 1))
+        dist.init_process_group(backend, timeout=timeout)
+    rank_phase("ready")
     return dist, backend
+
+
+def dist_selftest():
+    """`--dist-selftest` (tests/test_bench_launcher_cpu.py): the ranks' rendezvous and one
+    collective only, through the real launcher path.  BENCH_TEST_STALL_RANK=r makes rank r
+    never join (it sleeps), to show the run fails within DIST_TIMEOUT_S and names it."""
+    stall = os.environ.get("BENCH_TEST_STALL_RANK")
+    rank = int(os.environ.get("RANK", "0"))
+    rank_phase("start")
+    if stall is not None and int(stall) == rank:
+        rank_phase("stalling (BENCH_TEST_STALL_RANK)")
+        time.sleep(3600)
+    dist, _ = init_dist(int(os.environ.get("LOCAL_RANK", "0")))
+    t = torch.ones(1)
+    dist.all_reduce(t)
+    rank_phase("all_reduce %g" % float(t.item()))
+    dist.destroy_process_group()
+    rank_phase("done")
 
 
 def gather_summaries(dist, local, gathered):
@@ -1217,9 +1266,7 @@ def rbergomi_main(args):
         cpu = rb_cpu_baseline(args.cpu_seconds, base)
     dist = None
     if world > 1:
-        import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dist, _ = init_dist(local)
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
@@ -1303,6 +1350,7 @@ def rbergomi_main(args):
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+    rank_phase("done")
 
 
 def free_port():
@@ -1338,16 +1386,56 @@ def launch(args, argv):
     fd, path = tempfile.mkstemp(prefix="bench_parent_", suffix=".json", dir="/tmp")
     with os.fdopen(fd, "w") as fh:
         json.dump(parent, fh)
+    status_dir = tempfile.mkdtemp(prefix="bench_ranks_", dir="/tmp")
     cmd = launcher_cmd(argv, args.gpus, free_port())
-    env = dict(os.environ, BENCH_PARENT_RESULTS=path)
+    env = dict(os.environ, BENCH_PARENT_RESULTS=path, BENCH_RANK_STATUS_DIR=status_dir)
     try:
         if args.launch_dry_run:
             print(json.dumps(dict(cmd=cmd, parent_results=path, cuda_initialized=torch.cuda.is_initialized())),
                   flush=True)
             return 0
-        return subprocess.run(cmd, env=env).returncode
+        # the child in a session of its own, so a wall-limit kill takes its whole process group
+        # (torch.distributed.run and every rank) and nothing else
+        proc = subprocess.Popen(cmd, env=env, start_new_session=True)
+        try:
+            rc = proc.wait(timeout=LAUNCH_TIMEOUT_S)
+            why = None if rc == 0 else f"exit status {rc}"
+        except subprocess.TimeoutExpired:
+            import signal
+            for sig, grace in ((signal.SIGTERM, 15), (signal.SIGKILL, 15)):
+                try:
+                    os.killpg(proc.pid, sig)
+                except ProcessLookupError:
+                    break
+                try:
+                    proc.wait(timeout=grace)
+                    break
+                except subprocess.TimeoutExpired:
+                    continue
+            rc, why = 124, f"wall limit {LAUNCH_TIMEOUT_S:g} s (BENCH_LAUNCH_TIMEOUT)"
+        if why is not None:
+            report_ranks(status_dir, args.gpus, why)
+        return rc
     finally:
         os.unlink(path)
+        import shutil
+        shutil.rmtree(status_dir, ignore_errors=True)
+
+
+def report_ranks(status_dir, world, why):
+    """After a failed or timed-out `--gpus N` child: each rank's last recorded phase, and the
+    ranks that never reached "done" named, on stderr and as one JSON line on stdout."""
+    last = {}
+    for r in range(world):
+        f = os.path.join(status_dir, f"rank{r}")
+        lines = open(f).read().splitlines() if os.path.exists(f) else []
+        last[r] = lines[-1].split(" ", 1)[1] if lines else "no record (never started)"
+    stalled = [r for r in range(world) if last[r] != "done"]
+    for r in range(world):
+        print(f"[bench launcher] rank {r}: last phase: {last[r]}", file=sys.stderr, flush=True)
+    print(f"[bench launcher] FAILED ({why}); ranks not done: {stalled}", file=sys.stderr, flush=True)
+    print(json.dumps(dict(error="bench --gpus %d failed: %s" % (world, why), ranks_not_done=stalled,
+                          last_phase={str(r): last[r] for r in range(world)})), flush=True)
 
 
 def parent_results():
@@ -1369,6 +1457,9 @@ def main(argv=None):
             lds0 = args.mode == "rollout" and lds_rollout(CONFIGS[args.config])
             args.rollout_k = 256 if (lds0 or CONFIGS[args.config]["mode"] == "replay") else M_BLOCK
         sys.exit(launch(args, argv))
+    if args.dist_selftest:
+        dist_selftest()
+        return
     if args.workload == "rbergomi":
         rbergomi_main(args)
         return
@@ -1429,7 +1520,9 @@ def main(argv=None):
     # at least two full episodes (504 steps) in the timed window
     K = -(-max(args.steps, MIN_TIMED_STEPS) // runner.chunk) * runner.chunk
     W = -(-args.warmup // runner.chunk) * runner.chunk
+    rank_phase("env made; warmup %d + timed %d steps" % (W, K))
     wall, dev_ms = timed(runner, K, W, dist)
+    rank_phase("timed region done")
     shard = None
     if args.mode == "rollout":
         # every env's summaries after the last launch, gathered in global env order (outside
@@ -1445,6 +1538,7 @@ def main(argv=None):
         nb, j0, m = shard_check_slice(rank, world, n)
         got = shard_check_run(args, dev, stream, runner.runs, nb, j0, m)
         shard = shard_check_verdict(dist, got, allg, nb, j0, n, device="cpu" if backend == "gloo" else dev)
+        rank_phase("shard check: %s" % shard.get("result") if isinstance(shard, dict) else "shard check")
     payload = None
     if dist is not None:
         payload = dict(what="he_episode_summaries: per-env {return, sum P&L, sum cost, length} f32 [envs, 4], "
@@ -1571,6 +1665,7 @@ def main(argv=None):
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+    rank_phase("done")
 
 
 if __name__ == "__main__":

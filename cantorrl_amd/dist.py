@@ -25,20 +25,24 @@ def shard_offset(n_per_rank, rank):
     return n_per_rank * rank
 
 
-def init(backend=None, force=False):
+def init(backend=None, force=False, timeout_s=120.0):
     """Initialise the default process group for this process's device (at world size 1
-    only with force=True: a one-rank group, e.g. to exercise RCCL on a one-GPU box)."""
+    only with force=True: a one-rank group, e.g. to exercise RCCL on a one-GPU box).
+    timeout_s bounds the rendezvous and every collective: a rank that never joins fails
+    the others within it instead of hanging the job."""
+    import datetime
     import torch.distributed as dist
     rank, local, world = world_info()
     if dist.is_initialized() or (world == 1 and not force):
         return rank, local, world
     if backend is None:
         backend = "nccl" if torch.cuda.is_available() else "gloo"
+    timeout = datetime.timedelta(seconds=float(timeout_s))
     if backend == "nccl":
         torch.cuda.set_device(local)
-        dist.init_process_group(backend, device_id=torch.device("cuda", local))
+        dist.init_process_group(backend, device_id=torch.device("cuda", local), timeout=timeout)
     else:
-        dist.init_process_group(backend)
+        dist.init_process_group(backend, timeout=timeout)
     return rank, local, world
 
 

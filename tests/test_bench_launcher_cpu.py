@@ -175,3 +175,43 @@ def test_two_rank_gloo_shard_check(corrupt):
         else:
             assert v["result"] == "bit-identical" and v["mismatched_rows"] == 0
             assert v["finished_episodes_in_checked_rows"] == 8
+
+
+# ------------------------------------------------------------------ failing fast
+def _selftest(extra_env, timeout=240):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(BENCH_DIST_BACKEND="gloo", **extra_env)
+    import time
+    t0 = time.time()
+    out = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--dist-selftest", "--no-pmc", "--no-cpu-baseline"],
+                         capture_output=True, text=True, timeout=timeout, env=env, cwd=REPO)
+    return out, time.time() - t0
+
+
+def test_two_rank_launch_completes_and_records_phases():
+    out, _ = _selftest(dict(BENCH_DIST_TIMEOUT="60"))
+    assert out.returncode == 0, out.stderr[-2000:]
+    for r in (0, 1):
+        assert f"[bench rank {r}/2] ready" in out.stderr and f"[bench rank {r}/2] done" in out.stderr
+
+
+def test_rank_that_never_joins_fails_fast_and_is_named():
+    """Rank 1 never calls init_process_group: rank 0's rendezvous times out after
+    BENCH_DIST_TIMEOUT (not the driver's wall limit), the launcher exits non-zero and names
+    rank 1 as not done, with its last phase."""
+    out, took = _selftest(dict(BENCH_DIST_TIMEOUT="8", BENCH_TEST_STALL_RANK="1"))
+    assert out.returncode != 0
+    assert took < 120, took
+    assert "ranks not done: [0, 1]" in out.stderr or "ranks not done: [1]" in out.stderr, out.stderr[-3000:]
+    assert "rank 1: last phase: stalling" in out.stderr
+    rep = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][-1])
+    assert 1 in rep["ranks_not_done"] and rep["last_phase"]["1"].startswith("stalling")
+
+
+def test_launch_wall_limit_kills_the_child_group():
+    """A child that outlives BENCH_LAUNCH_TIMEOUT is killed as a process group (rc 124) and
+    the stalled rank is named."""
+    out, took = _selftest(dict(BENCH_DIST_TIMEOUT="600", BENCH_TEST_STALL_RANK="1", BENCH_LAUNCH_TIMEOUT="15"))
+    assert out.returncode == 124, (out.returncode, out.stderr[-2000:])
+    assert took < 90, took
+    assert "wall limit 15 s" in out.stderr and "rank 1: last phase: stalling" in out.stderr
