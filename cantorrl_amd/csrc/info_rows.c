@@ -48,6 +48,10 @@ typedef struct {
     int has_done;
     Py_buffer done;
     char kinds[MAX_KEYS];
+    Py_hash_t hash[MAX_KEYS];      /* the column keys' hashes: a miss costs no string compare */
+    Py_hash_t extra_hash;
+    Py_ssize_t n_done_keys;
+    Py_hash_t done_hash[MAX_KEYS];
     Py_buffer buf[MAX_KEYS];
 } Cols;
 
@@ -89,21 +93,23 @@ static inline int row_done(const Cols* c, Py_ssize_t i) {
     return c->has_done && ((const uint8_t*)c->done.buf)[i] != 0;
 }
 
-/* index of `key` among the column keys (-1 none, -2 error): identity first (the keys are
- * interned literals on both sides in practice), then equality */
-static Py_ssize_t key_index(PyObject* keys, Py_ssize_t nk, PyObject* key) {
-    for (Py_ssize_t k = 0; k < nk; ++k)
-        if (PyTuple_GET_ITEM(keys, k) == key) return k;
+/* index of `key` (hash h) among keys (-1 none, -2 error): the hash first (a str caches its
+ * own), then identity (the keys are interned literals on both sides in practice), then
+ * equality -- as a dict lookup does */
+static Py_ssize_t key_index(PyObject* keys, const Py_hash_t* hashes, Py_ssize_t nk, PyObject* key, Py_hash_t h) {
     for (Py_ssize_t k = 0; k < nk; ++k) {
-        const int eq = PyObject_RichCompareBool(PyTuple_GET_ITEM(keys, k), key, Py_EQ);
+        if (hashes[k] != h) continue;
+        PyObject* kk = PyTuple_GET_ITEM(keys, k);
+        if (kk == key) return k;
+        const int eq = PyObject_RichCompareBool(kk, key, Py_EQ);
         if (eq < 0) return -2;
         if (eq) return k;
     }
     return -1;
 }
 
-static int key_eq(PyObject* a, PyObject* key) {
-    if (a == Py_None) return 0;
+static int key_eq(PyObject* a, Py_hash_t ha, PyObject* key, Py_hash_t h) {
+    if (a == Py_None || ha != h) return 0;
     if (a == key) return 1;
     return PyObject_RichCompareBool(a, key, Py_EQ);
 }
@@ -118,33 +124,25 @@ typedef struct {
 
 static PyTypeObject RowType;
 
+/* A Row is not a GC object: 65,536 of them per step at SB3's loop would trigger the cyclic
+ * collector's generation-0 pass every 700 and, through the long-lived count, full passes over
+ * every object of the process (torch's included): 90 ms per step measured, against 25 ms.
+ * A Row refers to its Cols (no cycle: a Cols never refers to a Row) and, once materialized,
+ * to its dict; a cycle through that dict (a row stored into itself) is not collected. */
 static PyObject* row_new(Cols* c, Py_ssize_t i) {
-    Row* r = PyObject_GC_New(Row, &RowType);
+    Row* r = PyObject_New(Row, &RowType);
     if (!r) return NULL;
     Py_INCREF(c);
     r->c = c;
     r->i = i;
     r->d = NULL;
-    PyObject_GC_Track(r);
     return (PyObject*)r;
 }
 
 static void row_dealloc(Row* r) {
-    PyObject_GC_UnTrack(r);
     Py_XDECREF(r->c);
     Py_XDECREF(r->d);
-    PyObject_GC_Del(r);
-}
-
-static int row_traverse(Row* r, visitproc visit, void* arg) {
-    Py_VISIT(r->c);
-    Py_VISIT(r->d);
-    return 0;
-}
-
-static int row_clear(Row* r) {
-    Py_CLEAR(r->d);
-    return 0;
+    PyObject_Del(r);
 }
 
 /* the whole row as a dict (made once; the row then forwards to it) */
@@ -191,13 +189,15 @@ static int row_find(Row* r, PyObject* key, PyObject** out) {
         return PyErr_Occurred() ? -1 : 0;
     }
     const Cols* c = r->c;
-    const Py_ssize_t k = key_index(c->keys, c->nk, key);
+    const Py_hash_t h = PyObject_Hash(key);
+    if (h == -1) return -1;
+    const Py_ssize_t k = key_index(c->keys, c->hash, c->nk, key, h);
     if (k == -2) return -1;
     if (k >= 0) {
         *out = col_value(c, k, r->i);
         return *out ? 1 : -1;
     }
-    int eq = key_eq(c->extra_key, key);
+    int eq = key_eq(c->extra_key, c->extra_hash, key, h);
     if (eq < 0) return -1;
     if (eq) {
         Py_INCREF(c->extra_val);
@@ -205,7 +205,7 @@ static int row_find(Row* r, PyObject* key, PyObject** out) {
         return 1;
     }
     if (row_done(c, r->i)) {
-        const Py_ssize_t m = key_index(c->done_keys, PyTuple_GET_SIZE(c->done_keys), key);
+        const Py_ssize_t m = key_index(c->done_keys, c->done_hash, c->n_done_keys, key, h);
         if (m == -2) return -1;
         if (m >= 0) {
             if (!row_dict(r)) return -1;
@@ -348,10 +348,8 @@ static PyTypeObject RowType = {
     .tp_as_sequence = &row_as_sequence,
     .tp_as_mapping = &row_as_mapping,
     .tp_hash = PyObject_HashNotImplemented,
-    .tp_flags = Py_TPFLAGS_DEFAULT | Py_TPFLAGS_HAVE_GC,
+    .tp_flags = Py_TPFLAGS_DEFAULT,
     .tp_doc = "One env's info of one step (a dict once anything needs the whole mapping).",
-    .tp_traverse = (traverseproc)row_traverse,
-    .tp_clear = (inquiry)row_clear,
     .tp_richcompare = (richcmpfunc)row_richcompare,
     .tp_iter = (getiterfunc)row_iter,
     .tp_methods = row_methods,
@@ -426,7 +424,19 @@ static PyObject* rows_attach(Rows* s, PyObject* args) {
     c->done_keys = done_keys;
     Py_INCREF(ends);
     c->ends = ends;
+    c->extra_hash = 0;
+    c->n_done_keys = 0;
     PyObject_GC_Track(c);
+    if (extra_key != Py_None && (c->extra_hash = PyObject_Hash(extra_key)) == -1) goto fail;
+    if (PyTuple_GET_SIZE(done_keys) > MAX_KEYS) {
+        PyErr_SetString(PyExc_ValueError, "_attach: at most 64 done keys");
+        goto fail;
+    }
+    for (Py_ssize_t k = 0; k < PyTuple_GET_SIZE(done_keys); ++k)
+        if ((c->done_hash[k] = PyObject_Hash(PyTuple_GET_ITEM(done_keys, k))) == -1) goto fail;
+    c->n_done_keys = PyTuple_GET_SIZE(done_keys);
+    for (Py_ssize_t k = 0; k < nk; ++k)
+        if ((c->hash[k] = PyObject_Hash(PyTuple_GET_ITEM(keys, k))) == -1) goto fail;
     for (Py_ssize_t k = 0; k < nk; ++k) {
         const char t = kinds[k];
         const Py_ssize_t isz = (t == 'd') ? 8 : (t == 'f' || t == 'i') ? 4 : 0;

@@ -20,9 +20,14 @@ from . import _lib
 from .vec_env import (HedgingVecEnv, OBS_HIGH, OBS_LOW)
 from .spaces import Box
 
-_INFO_F64 = ["step_pnl_total", "per_share_step_pnl", "raw_pnl_deviation_abs", "transaction_costs_total",
-             "commission_cost", "slippage_cost", "reward_pnl_component", "transaction_cost_penalty",
-             "theta_penalty", "reward_step", "portfolio_value"]
+# the info fields HedgingEnv.step reads from the step's block, by dtype (hedging_env_v2.py:268-293)
+_STEP_F8 = ["step_pnl_total", "per_share_step_pnl", "raw_pnl_deviation_abs", "transaction_costs_total",
+            "commission_cost", "slippage_cost", "reward_pnl_component", "transaction_cost_penalty",
+            "theta_penalty", "reward_step", "portfolio_value", "cash"]
+_STEP_I4 = ["call_contracts", "put_contracts", "requested_calls_rounded_clipped", "requested_puts_rounded_clipped",
+            "actual_calls_traded", "actual_puts_traded", "current_step"]
+_STEP_F4 = ["scaled_float_call", "scaled_float_put", "current_stock_price", "current_volatility",
+            "current_call_price", "current_put_price"]
 
 
 class HedgingEnv:
@@ -101,8 +106,13 @@ class HedgingEnv:
         fields["itemsize"] = v._io.numel()
         rec_dt = np.dtype(fields)
         self._rec = self._io_h.numpy().view(rec_dt)   # shape (1,): a view, refreshed by each copy
-        self._rec_step = v._hio.io.view(rec_dt)        # the mapped block: written by each step
         self._ev = torch.cuda.Event()
+        # a step reads the mapped block by three gathers (f64, i32, f32 fields), whose numpy
+        # scalars fill the info dict: ~45 structured-field reads cost more than the step itself
+        offs = {k: v._io_info0 + o for k, dt, o in v._info_offs}
+        self._g8 = np.array([offs[k] // 8 for k in _STEP_F8], np.intp)
+        self._g4i = np.array([offs[k] // 4 for k in _STEP_I4], np.intp)
+        self._g4f = np.array([offs[k] // 4 for k in _STEP_F4], np.intp)
 
     # ------------------------------------------------------------------ helpers
     def _fetch(self):
@@ -161,37 +171,40 @@ class HedgingEnv:
         a = np.asarray(action, dtype=np.float32).reshape(2)
         v = self._venv
         prev_S, prev_v = self.current_stock_price, self.current_volatility
-        v.step_host(a)
-        h = self._rec_step[0]
-        o = h["obs"].copy()
-        self._pull(h)
-        terminated = bool(h["terminated"])
+        io = v.step_host(a).io
+        o = io[:52].view(np.float32).copy()
+        terminated = bool(io[56])
+        # numpy scalars of the reference's dtypes: f64 P&L fields, int64 positions, f32 market
+        pnl, ps, rab, tc, com, slip, rpc, tcp, thp, rew, pv, cash = io.view(np.float64)[self._g8]
+        cc, pc, rqc, rqp, dc, dp, t = io.view(np.int32)[self._g4i].astype(np.int64)
+        sfc, sfp, S, vv, C, P = io.view(np.float32)[self._g4f]
+        self.current_stock_price, self.current_volatility = S, vv
+        self.current_call_price, self.current_put_price = C, P
+        self.current_step = int(t)
+        self.call_contracts_held, self.put_contracts_held = cc, pc
+        self.cash_balance = cash
         self._terminated = terminated
         self.S_t_minus_1, self.v_t_minus_1 = prev_S, prev_v
-        self.portfolio_value_t_minus_1 = np.float64(h["portfolio_value"])
-        reward = np.float64(h["reward_step"])
-        info = {k: np.float64(h[k]) for k in _INFO_F64}
+        self.portfolio_value_t_minus_1 = pv
         if self._variant == 2:
-            info["theta_penalty"] = float(h["theta_penalty"])
+            info = {"step_pnl_total": pnl, "per_share_step_pnl": ps, "raw_pnl_deviation_abs": rab,
+                    "transaction_costs_total": tc, "commission_cost": com, "slippage_cost": slip,
+                    "reward_pnl_component": rpc, "transaction_cost_penalty": tcp, "theta_penalty": float(thp),
+                    "reward_step": rew, "portfolio_value": pv}
         else:
-            for k in ("commission_cost", "slippage_cost", "theta_penalty"):
-                info.pop(k)
+            info = {"step_pnl_total": pnl, "per_share_step_pnl": ps, "raw_pnl_deviation_abs": rab,
+                    "transaction_costs_total": tc, "reward_pnl_component": rpc, "transaction_cost_penalty": tcp,
+                    "reward_step": rew, "portfolio_value": pv}
         info.update({
-            "call_contracts": np.int64(h["call_contracts"]),
-            "put_contracts": np.int64(h["put_contracts"]),
-            "cash": np.float64(h["cash"]),
-            "raw_action_call": a[0],
-            "raw_action_put": a[1],
-            "scaled_float_call": np.float32(h["scaled_float_call"]),
-            "scaled_float_put": np.float32(h["scaled_float_put"]),
-            "requested_calls_rounded_clipped": np.int64(h["requested_calls_rounded_clipped"]),
-            "requested_puts_rounded_clipped": np.int64(h["requested_puts_rounded_clipped"]),
-            "actual_calls_traded": np.int64(h["actual_calls_traded"]),
-            "actual_puts_traded": np.int64(h["actual_puts_traded"]),
+            "call_contracts": cc, "put_contracts": pc, "cash": cash,
+            "raw_action_call": a[0], "raw_action_put": a[1],
+            "scaled_float_call": sfc, "scaled_float_put": sfp,
+            "requested_calls_rounded_clipped": rqc, "requested_puts_rounded_clipped": rqp,
+            "actual_calls_traded": dc, "actual_puts_traded": dp,
             "loss_type_used": self.loss_type,
             "initial_S0_for_episode": self.initial_S0_for_episode,
         })
-        return o, reward, terminated, False, info
+        return o, rew, terminated, False, info
 
     def render(self):
         pass
