@@ -204,6 +204,9 @@ def parse(argv=None):
     ap.add_argument("--probe", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--launch-dry-run", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--dist-selftest", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--action-sets", type=int, default=1,
+                    help="rollout mode: cycle through this many distinct pre-generated action buffers (a "
+                         "footprint past the 256 MB Infinity Cache; default 1)")
     ap.add_argument("--workload", choices=["env", "rbergomi"], default="env",
                     help="env: the hedging-env step (headline); rbergomi: the rough-Bergomi MC mark generator")
     ap.add_argument("--rb-paths", type=int, default=2048, help="rbergomi: paths per GPU (x 252 days x call/put)")
@@ -342,8 +345,12 @@ def make_env(args, dev, rank=0, prefetch="auto", offset=None):
     return env
 
 
-def bench_actions(n, rank, dev):
-    """The pre-generated U(-1, 1) actions [256, n, 2] of rank `rank` (seed 1234 + rank)."""
+def bench_actions(n, rank, dev, sets=1):
+    """The pre-generated U(-1, 1) actions [256, n, 2] of rank `rank` (seed 1234 + rank).
+    sets > 1 (--action-sets): [sets, 256, n, 2], set s from seed 1234 + rank + 7919 s, the
+    rollouts cycling through them (a footprint past the 256 MB Infinity Cache: DESIGN 9)."""
+    if sets > 1:
+        return torch.stack([bench_actions(n, rank + 7919 * s, dev) for s in range(sets)])
     g = torch.Generator(device=dev)
     g.manual_seed(1234 + rank)
     return torch.rand((256, n, 2), device=dev, generator=g) * 2 - 1
@@ -398,7 +405,7 @@ def shard_check_run(args, dev, stream, runs, nb, j0, m):
     import copy
     a2 = copy.copy(args)
     a2.envs = m
-    acts = bench_actions(args.envs, nb, dev)[:, j0:j0 + m].contiguous()
+    acts = bench_actions(args.envs, nb, dev, args.action_sets)[..., j0:j0 + m, :].contiguous()
     env = make_env(a2, dev, offset=nb * args.envs + j0)
     r = Runner(a2, env, "rollout", acts, stream)
     with torch.cuda.stream(stream):
@@ -414,6 +421,10 @@ class Runner:
     """Enqueues env-steps of one handle in one mode (rollout / graph / eager)."""
 
     def __init__(self, args, env, mode, acts, stream, dist=None, gathered=None):
+        # acts [256, n, 2], or [S, 256, n, 2] (--action-sets S): launch i reads set i % S
+        self.sets = acts if acts.dim() == 4 else acts.unsqueeze(0)
+        self.launches = 0
+        acts = self.sets[0]
         self.args, self.env, self.mode, self.acts, self.stream = args, env, mode, acts, stream
         self.dist, self.gathered = dist, gathered
         self.summaries = torch.zeros((args.envs, 4), dtype=torch.float32, device=acts.device)
@@ -461,7 +472,9 @@ class Runner:
     def rollout(self, done, s):
         RK = self.args.rollout_k
         a0 = done % self.ring
-        a = self.acts[a0:a0 + RK] if a0 + RK <= self.ring else self.acts[:RK]
+        acts = self.sets[self.launches % self.sets.shape[0]]
+        self.launches += 1
+        a = acts[a0:a0 + RK] if a0 + RK <= self.ring else acts[:RK]
         st = self.lib.he_rollout(self.h, RK, a.data_ptr(), self.ro.data_ptr(), self.rr.data_ptr(),
                                  self.rt.data_ptr(), s)
         if st:
@@ -1510,13 +1523,14 @@ def main(argv=None):
     cfg = CONFIGS[args.config]
     n = args.envs
 
-    acts = bench_actions(n, rank, dev)
+    acts = bench_actions(n, rank, dev, args.action_sets)
     stream = torch.cuda.Stream(device=dev)
     gathered = (torch.empty((world * n, 4), dtype=torch.float32, device=dev if backend == "nccl" else "cpu")
                 if world > 1 else None)
 
     env = make_env(args, dev, rank)
     runner = Runner(args, env, args.mode, acts, stream, dist, gathered)
+    acts = runner.acts   # [256, n, 2]: set 0 (the other legs below use one set)
     # at least two full episodes (504 steps) in the timed window
     K = -(-max(args.steps, MIN_TIMED_STEPS) // runner.chunk) * runner.chunk
     W = -(-args.warmup // runner.chunk) * runner.chunk
@@ -1645,6 +1659,7 @@ def main(argv=None):
                        "episode_length": (cfg["table"]["cols"] - 1) if replay else cfg["gen"]["episode_length"],
                        "mode": args.mode,
                        "rollout_k": args.rollout_k if args.mode == "rollout" else None,
+                       "action_sets": args.action_sets,
                        "parallelism": f"env-shard x{world}"},
             "device_ms_per_step": round(dev_ms / K, 6),
             "roofline": roof,

@@ -1,0 +1,36 @@
+#!/bin/bash
+# Round 6 measurements: host step timing; same-box A/B of this tree's kernels against round 5's
+# (tools/ab/r05.so) on the headline; the action footprint (config 2 with 4 action sets =
+# 537 MB, past the 256 MB Infinity Cache) against config 3.
+#   gpurun --timeout 900 -- bash tools/gpu/r06_measure.sh <tag> [host|ab|mall|all]
+set -o pipefail
+TAG=${1:-r06m}; PHASE=${2:-all}
+R=$GRAFT_REPO_ROOT; cd $R; O=$R/gpurun_out/$TAG; mkdir -p $O; export TMPDIR=/tmp
+Q="--no-pmc --no-cpu-baseline --no-step-api --no-sb3-api"
+line() { python3 -c "
+import json,sys
+d=[json.loads(l) for l in open(sys.argv[1]) if l.startswith('{')][0]; r=d['roofline']
+print(sys.argv[1].split('/')[-1], 'value %.4g'%d['value'], 'kernel_us', r.get('kernel_us'), 'frac', r.get('frac'))
+" $1; }
+if [ "$PHASE" = host ] || [ "$PHASE" = all ]; then
+  echo "[$(date +%T)] host step timing"
+  timeout -k 10 200 python -u tools/host_step_timing.py > $O/host_step.log 2>&1 || { tail -20 $O/host_step.log; exit 1; }
+  grep -v amdgpu.ids $O/host_step.log
+fi
+if [ "$PHASE" = ab ] || [ "$PHASE" = all ]; then
+  for rep in 1 2 3; do
+    for v in base r05; do
+      lib=""; [ "$v" != base ] && lib=$R/tools/ab/$v.so
+      CANTORRL_HEDGEENV_LIB=$lib timeout -k 10 300 python -u bench.py $Q > $O/ab_${v}_$rep.log 2>&1 || { tail -5 $O/ab_${v}_$rep.log; exit 1; }
+      line $O/ab_${v}_$rep.log
+    done
+  done
+fi
+if [ "$PHASE" = mall ] || [ "$PHASE" = all ]; then
+  for a in "--config 2" "--config 2 --action-sets 4" "--config 3" "--config 2" "--config 2 --action-sets 4" "--config 3"; do
+    f=$O/mall_$(echo $a | tr -d ' -').log
+    timeout -k 10 300 python -u bench.py $Q $a > $f 2>&1 || { tail -5 $f; exit 1; }
+    line $f
+  done
+fi
+echo "[$(date +%T)] done"
