@@ -24,6 +24,7 @@
 
 #include <math.h>
 #include <stdarg.h>
+#include <stdlib.h>
 #include <stdio.h>
 #include <string.h>
 
@@ -406,6 +407,206 @@ __global__ void __launch_bounds__(kMcThreads) mc_kernel(McArgs a) {
     }
 }
 
+// ------------------------------------------------------------------ MC pricer, matrix cores
+// mc_kernel's work for the reference tenor (30 Euler steps on the 32-point grid, MO = 32, FULL)
+// with the fractional convolution on the f64 matrix pipe: for 16 MC paths at
+// a time, X = T W with T[j][i] = lam_{(j - i) mod 32} the circulant of lam (a 32 x 32 constant of
+// the option) and W = Re W of the 16 paths (32 x 16), as 2 row tiles x 8 k-steps of
+// v_mfma_f64_16x16x4_f64 -- 960 f64 FMAs per MC path off the VALU, which keeps Philox, Box-Muller
+// and the Euler steps.
+//
+// Layouts (v_mfma_f64_16x16x4_f64: lane l holds A[row l & 15][k l >> 4], B[k l >> 4][col l & 15],
+// D[row (l >> 4) + 4 r][col l & 15], r = 0..3).  With g = l >> 4 and c = l & 15, lane l works on
+// MC path base + c, and the rows and k of T are permuted so that every lane's operands and results
+// are ITS OWN path's: k-step s, k = g <-> i = 8 g + s, and D row g + 4 r of row tile t <-> j =
+// 8 g + 4 t + r.  So lane (g, c) draws Re W[8g .. 8g + 7] and Im W[8g .. 8g + 7] of path base + c
+// (the same Philox blocks as mc_kernel: the same normals), feeds them as B, and receives X[8g ..
+// 8g + 7]: the A fragment of (t, s) is lam[(8 (c & 3) + 4 t + (c >> 2) - 8 g - s) & 31], held in
+// registers for the whole option.  No LDS, no transposes.
+//
+// The Euler chain L_{j+1} = max(L_j + a_j, Lf) of mc_kernel is then split over the 4 lanes of a
+// path: each lane computes a_j of its 8 steps (their exp, drift, diffusion) and composes its 8
+// steps into one map L -> max(L + s, b) (s = sum a, b = max(b + a, Lf), exact in real
+// arithmetic: max distributes over +); the 4 maps, fetched by __shfl, are applied in order.  The
+// sums' order is not mc_kernel's, so a mark moves by ~1e-16 relative: the reference-draw parity
+// (tests/test_rbergomi_gpu.py, 1e-10) runs through this kernel.
+typedef double v4d __attribute__((ext_vector_type(4)));
+
+template <int NORM, bool ATM>
+__global__ void __launch_bounds__(kMcThreads) mc_mfma_kernel(McArgs a) {
+    constexpr int MO = 32;
+    __shared__ double s_lam[MO];
+    __shared__ double s_ma[MO];
+    __shared__ double s_red[kMcThreads / 64];
+    const int tid = threadIdx.x;
+    const int64_t o = (ATM ? a.o_base : 0) + (int64_t)blockIdx.x;
+    const int type = ATM ? (int)blockIdx.y : a.type;
+    double S0, K, xi, H, eta, rho;
+    uint64_t gid;
+    uint32_t sub;
+    if (ATM) {
+        const int64_t p = o / a.T;
+        const int d = (int)(o - p * a.T);
+        S0 = a.paths[p * (a.T + 1) + d];
+        xi = a.vol[p * (a.T + 1) + d];
+        K = rint(S0);                       // cp.round (:409)
+        H = a.params[2 * a.n_opt + p];
+        eta = a.params[3 * a.n_opt + p];
+        rho = a.params[4 * a.n_opt + p];
+        gid = a.off + (uint64_t)p;
+        sub = (uint32_t)(d * 2 + type);
+    } else {
+        S0 = a.S0[o];
+        K = a.K[o];
+        xi = a.xi[o];
+        H = a.H[o];
+        eta = a.eta[o];
+        rho = a.rho[o];
+        gid = a.off + (uint64_t)o;
+        sub = (uint32_t)type;
+    }
+    double* out = ATM ? ((type == RB_CALL) ? a.call : a.put) : a.price;
+    if (tid < MO) {   // lam_k and ma_k on the option grid (:274-278, :254), as mc_kernel
+        const int k = tid;
+        const double t = (k == a.n) ? a.tstop : (double)k * a.tstep;
+        const double pw = (k <= a.n) ? pow(t, 2.0 * H) : 0.0;
+        s_lam[k] = (k <= a.n) ? 0.5 * pw : 0.0;
+        s_ma[k] = -0.5 * eta * eta * pw;
+    }
+    __syncthreads();
+    const int lane = tid & 63, wave = tid >> 6;
+    const int g = lane >> 4, c = lane & 15;
+    double A[2][8];   // the permuted circulant's fragments (see above)
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int q = 0; q < 8; ++q) A[t][q] = s_lam[(8 * (c & 3) + 4 * t + (c >> 2) - 8 * g - q) & 31];
+    double ma[8];     // ma_j of this lane's steps j = 8 g + q
+#pragma unroll
+    for (int q = 0; q < 8; ++q) ma[q] = s_ma[8 * g + q];
+    const double cx = sqrt(2.0 * H) * eta;
+    const double rq = sqrt(np_max(0.0, 1.0 - rho * rho));
+    const double sxi = sqrt(np_max(0.0, xi));
+    const bool s0_pos = !(S0 <= 0.0);
+    const double Sb = s0_pos ? S0 : 1e-8;
+    const double Lf = s0_pos ? log(1e-8) - log(S0) : 0.0;
+    const double ninf = -__builtin_inf();
+    double acc = 0.0;
+    // every wave takes 16 paths per iteration: [base, base + 16), base = 16 wave + 64 k
+    for (int base = 16 * wave; base < a.n_mc; base += 4 * 16) {
+        const int m = base + c;
+        const bool live = m < a.n_mc;
+        double w1[8], w2[8];   // Re W, Im W at i = j = 8 g + q
+        const double* wp = (NORM == 2 && live) ? a.W + ((o * a.n_mc + m) * (int64_t)MO) * 2 : nullptr;
+        if (NORM == 2) {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                w1[q] = live ? wp[2 * (8 * g + q)] : 0.0;
+                w2[q] = live ? wp[2 * (8 * g + q) + 1] : 0.0;
+            }
+        } else if (NORM == 0) {   // mc_kernel's blocks: Re pairs b = 4g .. 4g + 3, Im pairs 16 + 4g ..
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                __builtin_amdgcn_sched_barrier(0);
+                normal_pair_mc(rb_ctr((uint32_t)(m * MO + 4 * g + b), kDomMc, sub, gid), a.k0, a.k1, &w1[2 * b],
+                               &w1[2 * b + 1]);
+            }
+        } else {                  // Re quads 2g, 2g + 1; Im quads 8 + 2g, 9 + 2g
+#pragma unroll
+            for (int b = 0; b < 2; ++b) {
+                __builtin_amdgcn_sched_barrier(0);
+                normal_quad32(rb_ctr((uint32_t)(m * (MO / 2) + 2 * g + b), kDomMc, sub, gid), a.k0, a.k1, &w1[4 * b]);
+            }
+        }
+        if (NORM != 2 && !live) {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) w1[q] = 0.0;
+        }
+        // X[8g + 4t + r] of path m: 16 MFMAs
+        v4d X0 = {0.0, 0.0, 0.0, 0.0}, X1 = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            X0 = __builtin_amdgcn_mfma_f64_16x16x4f64(A[0][q], w1[q], X0, 0, 0, 0);
+            X1 = __builtin_amdgcn_mfma_f64_16x16x4f64(A[1][q], w1[q], X1, 0, 0, 0);
+        }
+        if (NORM == 0) {   // Im W while the matrix pipe works
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                __builtin_amdgcn_sched_barrier(0);
+                normal_pair_mc(rb_ctr((uint32_t)(m * MO + MO / 2 + 4 * g + b), kDomMc, sub, gid), a.k0, a.k1,
+                               &w2[2 * b], &w2[2 * b + 1]);
+            }
+        } else if (NORM == 1) {
+#pragma unroll
+            for (int b = 0; b < 2; ++b) {
+                __builtin_amdgcn_sched_barrier(0);
+                normal_quad32(rb_ctr((uint32_t)(m * (MO / 2) + MO / 4 + 2 * g + b), kDomMc, sub, gid), a.k0, a.k1,
+                              &w2[4 * b]);
+            }
+        }
+        // this lane's 8 Euler steps composed: L -> max(L + cs, cb)
+        double cs = 0.0, cb = ninf;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const int j = 8 * g + q;
+            const double Xq = (q < 4) ? X0[q] : X1[q - 4];
+            const double Xj = cx * (Xq * a.inv_sqrt_m);
+            const double e = exp(0.5 * (Xj + ma[q]));
+            const double v = xi * (e * e);
+            const double dW = rho * (a.sdt * w1[q]) + rq * (a.sdt * w2[q]);
+            const double drift = (a.r - 0.5 * v) * a.dt;
+            const double diff = (sxi * e) * dW;
+            const double st = drift + diff;
+            const bool step = j < MO - 2;           // steps 0 .. 29; rows 30, 31 unused
+            double ns = cs + st, nb = np_max(cb + st, Lf);
+            if (j == 0 && !s0_pos) {                // S0 <= 0: S_1 = 1e-8 whatever a_0 (L_1 = 0)
+                ns = ninf;
+                nb = 0.0;
+            }
+            cs = step ? ns : cs;
+            cb = step ? nb : cb;
+        }
+        // the path's 4 maps in step order
+        double L = 0.0;
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {
+            const double sh = __shfl(cs, c + 16 * h, 64), bh = __shfl(cb, c + 16 * h, 64);
+            L = np_max(L + sh, bh);
+        }
+        const double S = Sb * exp(L);
+        const double pay = (type == RB_CALL) ? np_max(S - K, 0.0) : np_max(K - S, 0.0);   // :299-303
+        acc += (g == 0 && live) ? pay : 0.0;
+    }
+#pragma unroll
+    for (int s = 32; s >= 1; s >>= 1) acc += __shfl_xor(acc, s, 64);
+    if ((tid & 63) == 0) s_red[tid >> 6] = acc;
+    __syncthreads();
+    if (tid == 0) {
+        double sum = 0.0;
+#pragma unroll
+        for (int w = 0; w < kMcThreads / 64; ++w) sum += s_red[w];
+        out[o] = (sum / (double)a.n_mc) * a.disc;   // mean(payoff) exp(-r T) (:305)
+    }
+}
+
+// RB_MC_VALU=1 (read per launch; A/B and tests): the reference tenor through mc_kernel instead
+bool mc_mfma_enabled() {
+    const char* e = getenv("RB_MC_VALU");
+    return !(e && e[0] == '1');
+}
+
+void launch_mc_mfma(const McArgs& a, int norm, bool atm, dim3 grid, hipStream_t s) {
+    if (atm) {
+        if (norm == RB_NORMALS_F32) hipLaunchKernelGGL((mc_mfma_kernel<1, true>), grid, dim3(kMcThreads), 0, s, a);
+        else hipLaunchKernelGGL((mc_mfma_kernel<0, true>), grid, dim3(kMcThreads), 0, s, a);
+    } else {
+        if (a.W) hipLaunchKernelGGL((mc_mfma_kernel<2, false>), grid, dim3(kMcThreads), 0, s, a);
+        else if (norm == RB_NORMALS_F32)
+            hipLaunchKernelGGL((mc_mfma_kernel<1, false>), grid, dim3(kMcThreads), 0, s, a);
+        else hipLaunchKernelGGL((mc_mfma_kernel<0, false>), grid, dim3(kMcThreads), 0, s, a);
+    }
+}
+
 // ------------------------------------------------------------------ host helpers
 int check_cfg(const rb_config* c) {
     if (!c) return fail(RB_EINVAL, "config is NULL");
@@ -478,8 +679,12 @@ void launch_mc_v(const McArgs& a, int norm, bool atm, dim3 grid, hipStream_t s) 
 
 template <int MO>
 int launch_mc_mo(const McArgs& a, int norm, bool atm, dim3 grid, hipStream_t s) {
-    if (MO == 32 && a.n == MO - 2) launch_mc_v<MO, true>(a, norm, atm, grid, s);
-    else launch_mc_v<MO, false>(a, norm, atm, grid, s);
+    if (MO == 32 && a.n == MO - 2) {
+        if (mc_mfma_enabled()) launch_mc_mfma(a, norm, atm, grid, s);
+        else launch_mc_v<MO, true>(a, norm, atm, grid, s);
+    } else {
+        launch_mc_v<MO, false>(a, norm, atm, grid, s);
+    }
     RB_HIP(hipGetLastError());
     return RB_OK;
 }

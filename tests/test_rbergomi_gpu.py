@@ -255,3 +255,31 @@ def test_mc_box_muller_extreme_uniforms():
     e1, e2 = r * np.cos(2 * np.pi * u2), r * np.sin(2 * np.pi * u2)
     np.testing.assert_allclose(g1, e1, rtol=0, atol=1e-13 * r.max())
     np.testing.assert_allclose(g2, e2, rtol=0, atol=1e-13 * r.max())
+
+
+@pytest.mark.parametrize("normals", ["f64", "f32"])
+def test_mfma_pricer_equals_valu_pricer(normals, monkeypatch):
+    """The reference tenor's MC pricer on the matrix cores (mc_mfma_kernel: the fractional
+    convolution as v_mfma_f64_16x16x4_f64, the Euler chain composed over 4 lanes) against
+    mc_kernel (RB_MC_VALU=1) on the same Philox normals: the same marks up to the summation
+    order (~1e-16 relative per value); n_mc = 1000 leaves a partial last tile of paths, and the
+    ATM generator (rb_price_atm_marks) is compared too."""
+    rb = _rb()
+    rng = np.random.default_rng(11)
+    n = 40
+    S0 = rng.uniform(50, 600, n)
+    S0[:3] = (0.0, -1.0, 1e-9)
+    K = np.round(S0 * rng.uniform(0.9, 1.1, n))
+    xi = rng.uniform(0.005, 0.09, n)
+    H, eta, rho = rng.uniform(0.03, 0.45, n), rng.uniform(0.5, 3.0, n), rng.uniform(-0.95, -0.05, n)
+    hist = _history()
+    out = {}
+    for valu in ("0", "1"):
+        monkeypatch.setenv("RB_MC_VALU", valu)
+        got = [rb.price_rbergomi_option(S0, K, 30 / 252, 0.04, xi, H, eta, rho, kind, 1000, 1 / 252, device=DEV,
+                                        normals=normals, seed=21).cpu().numpy() for kind in ("call", "put")]
+        res = rb.generate_paths_and_options(hist, 6, n_mc=300, device=DEV, seed=3, normals=normals)
+        out[valu] = got + [res["call_prices_atm"].cpu().numpy(), res["put_prices_atm"].cpu().numpy()]
+    for a, b in zip(out["0"], out["1"]):
+        assert np.isfinite(a).all()
+        np.testing.assert_allclose(a, b, rtol=1e-11, atol=1e-11 * 600)

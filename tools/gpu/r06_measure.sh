@@ -33,4 +33,22 @@ if [ "$PHASE" = mall ] || [ "$PHASE" = all ]; then
     line $f
   done
 fi
+if [ "$PHASE" = rb ] || [ "$PHASE" = all ]; then
+  echo "[$(date +%T)] rbergomi tests"
+  timeout -k 10 300 python -u -m pytest tests/test_rbergomi_gpu.py -x -q --timeout 120 --timeout-method thread > $O/rb_pytest.log 2>&1 || { tail -30 $O/rb_pytest.log; exit 1; }
+  tail -1 $O/rb_pytest.log
+  for rep in 1 2; do
+    for nm in f64 f32; do
+      for valu in 0 1; do
+        f=$O/rb_${nm}_valu${valu}_$rep.log
+        RB_MC_VALU=$valu timeout -k 10 300 python -u bench.py --workload rbergomi --rb-normals $nm --no-pmc --no-cpu-baseline > $f 2>&1 || { tail -5 $f; exit 1; }
+        python3 -c "
+import json,sys
+d=[json.loads(l) for l in open(sys.argv[1]) if l.startswith('{')][0]
+print(sys.argv[1].split('/')[-1], 'options/s %.4g' % d['value'], 'kernel ms', d['kernel']['ms_per_launch'])
+" $f
+      done
+    done
+  done
+fi
 echo "[$(date +%T)] done"
