@@ -2946,23 +2946,40 @@ __device__ __forceinline__ int lds_role(int wave) {
 // and at 106 the 4 x 6 waves of 4 workgroups no longer fit a CU -- at 65,536 envs the
 // launch ran in two rounds of workgroups (536 vs ~270 us).  The spills go to VGPR lanes.
 constexpr int kLdsNumSgpr = 96;
-template <int MODE, bool BOOK, bool LEAN>
+template <int MODE, bool BOOK, bool LEAN, bool PERSIST = false>
 __global__ __launch_bounds__((LdsGeom<MODE, BOOK>::threads), (LdsGeom<MODE, BOOK>::minwaves))
     __attribute__((amdgpu_num_sgpr(kLdsNumSgpr))) void lds_rollout_kernel(const Params* __restrict__ pc, State s, Io io,
                                                                  int k_steps, Market cur) {
     __shared__ __attribute__((aligned(16))) LdsMarketT<MODE, BOOK, LEAN> lm;
     const Params& p = *pc;  // read through the scalar cache (a by-value copy spills)
     const int wave = lds_role<LdsGeom<MODE, BOOK>::threads / 64>(__builtin_amdgcn_readfirstlane(threadIdx.x >> 6));
-    const int64_t base = (int64_t)blockIdx.x * kLdsEnvs;
     if constexpr (BOOK) {  // the tau table into LDS (rows <= kLdsBookRows: lds_rollout_eligible)
         const int nv = 4 * p.book_rows;
         for (int k = threadIdx.x; k < nv; k += LdsGeom<MODE, BOOK>::threads) (&lm.btab[0][0])[k] = p.book_tab[k];
         if ((int)threadIdx.x < p.book_n) lm.bopt[threadIdx.x] = p.book[threadIdx.x];
         __syncthreads();
     }
-    if (wave == 0) lds_stepper<MODE, BOOK, LEAN, false>(p, s, io, k_steps, cur, lm, base);
-    else if (wave == 1) lds_stepper<MODE, BOOK, LEAN, true>(p, s, io, k_steps, cur, lm, base);
-    else lds_producer<MODE, BOOK, LEAN>(p, k_steps, cur, lm, base, wave - 2);
+    if constexpr (!PERSIST) {   // one workgroup per 64-env tile
+        const int64_t base = (int64_t)blockIdx.x * kLdsEnvs;
+        if (wave == 0) lds_stepper<MODE, BOOK, LEAN, false>(p, s, io, k_steps, cur, lm, base);
+        else if (wave == 1) lds_stepper<MODE, BOOK, LEAN, true>(p, s, io, k_steps, cur, lm, base);
+        else lds_producer<MODE, BOOK, LEAN>(p, k_steps, cur, lm, base, wave - 2);
+        return;
+    }
+    // PERSIST (launch_lds_rollout, more tiles than the device holds workgroups at once): a
+    // workgroup runs tiles blockIdx.x, + gridDim.x, ..., the whole K-step rollout of each, so
+    // the roles placed once (lds_role's per-CU balance) hold for every tile
+    const int64_t tiles = (p.n + kLdsEnvs - 1) / kLdsEnvs;
+    for (int64_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
+        // nothing hoisted out of the tile loop: each role's values stay inside its own code
+        // (hoisted, the three roles' invariants all lived across the loop and spilled)
+        asm volatile("" ::: "memory");
+        const int64_t base = tile * kLdsEnvs;
+        if (wave == 0) lds_stepper<MODE, BOOK, LEAN, false>(p, s, io, k_steps, cur, lm, base);
+        else if (wave == 1) lds_stepper<MODE, BOOK, LEAN, true>(p, s, io, k_steps, cur, lm, base);
+        else lds_producer<MODE, BOOK, LEAN>(p, k_steps, cur, lm, base, wave - 2);
+        if (tile + gridDim.x < tiles) __syncthreads();   // every role done with lm before the next tile
+    }
 }
 
 // ------------------------------------------------------------------ replay rollouts in LDS
@@ -3700,6 +3717,12 @@ struct he_env {
     int32_t next_state = 0;   // next block: 0 none, 1 generating on `xs` (ev_next), 2 ready
     bool fuse_market = true;  // rollouts: next block's market in the step grid (HE_FUSED_MARKET=0: side stream)
     bool lds_rollout = true;  // he_rollout (GBM, no book): lds_rollout_kernel (HE_LDS_ROLLOUT=0: tile kernels)
+    // lds_rollout_kernel's grid: at most this many workgroups, each looping over 64-env tiles
+    // (0: one workgroup per tile).  The device's resident count (CUs x workgroups per CU) unless
+    // HE_LDS_PERSIST=0; HE_LDS_MAX_GRID=<n> caps it (tests: many tiles per workgroup).
+    int64_t lds_grid = -1;    // -1: not computed yet
+    int64_t lds_grid_cap = 0; // HE_LDS_MAX_GRID
+    bool lds_persist = true;
     int32_t prefetch_mode = 0; // 0 auto, 1 never, 2 always: market_kernel(b+1) on `xs` during block b
     hipStream_t xs = nullptr; // library side stream for market prefetch
     hipEvent_t ev_fork = nullptr, ev_next = nullptr;
@@ -4157,27 +4180,52 @@ static he_status launch_lds_rollout(he_env* env, const Io& io, int k_total, hipS
     const Params* pc = env->dparams;  // buffer 0's copy: the tile pointers are not used
     const bool book = env->cfg.book_size > 0, lean = lds_lean_config(env, io);
     void (*kern)(const Params*, State, Io, int, Market);
+    void (*kern_p)(const Params*, State, Io, int, Market);   // the persistent-grid instance
     int threads;
+#define HE_LDS_PICK(M, B, L)                                 \
+    do {                                                     \
+        kern = lds_rollout_kernel<M, B, L, false>;           \
+        kern_p = lds_rollout_kernel<M, B, L, true>;          \
+        threads = LdsGeom<M, B>::threads;                    \
+    } while (0)
     if (env->cfg.mode == HE_MODE_HESTON) {
-        if (lean)
-            kern = book ? lds_rollout_kernel<HE_MODE_HESTON, true, true> : lds_rollout_kernel<HE_MODE_HESTON, false, true>;
-        else
-            kern = book ? lds_rollout_kernel<HE_MODE_HESTON, true, false> : lds_rollout_kernel<HE_MODE_HESTON, false, false>;
-        threads = book ? LdsGeom<HE_MODE_HESTON, true>::threads : LdsGeom<HE_MODE_HESTON, false>::threads;
+        if (lean) {
+            if (book) HE_LDS_PICK(HE_MODE_HESTON, true, true);
+            else HE_LDS_PICK(HE_MODE_HESTON, false, true);
+        } else {
+            if (book) HE_LDS_PICK(HE_MODE_HESTON, true, false);
+            else HE_LDS_PICK(HE_MODE_HESTON, false, false);
+        }
     } else if (book) {
-        kern = lean ? lds_rollout_kernel<HE_MODE_GBM, true, true> : lds_rollout_kernel<HE_MODE_GBM, true, false>;
-        threads = LdsGeom<HE_MODE_GBM, true>::threads;
+        if (lean) HE_LDS_PICK(HE_MODE_GBM, true, true);
+        else HE_LDS_PICK(HE_MODE_GBM, true, false);
     } else {
-        kern = lean ? lds_rollout_kernel<HE_MODE_GBM, false, true> : lds_rollout_kernel<HE_MODE_GBM, false, false>;
-        threads = LdsGeom<HE_MODE_GBM, false>::threads;
+        if (lean) HE_LDS_PICK(HE_MODE_GBM, false, true);
+        else HE_LDS_PICK(HE_MODE_GBM, false, false);
     }
+#undef HE_LDS_PICK
+    // the persistent grid: as many workgroups as the device holds at once (one round), each
+    // looping over tiles -- past one round, workgroups that start as others finish take their
+    // roles from a ticket that no longer lines up with the SIMDs they land on
+    int64_t grid = blocks;
+    if (env->lds_persist) {
+        int per_cu = 0, cus = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern_p, threads, 0) == hipSuccess &&
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, env->cfg.device) == hipSuccess &&
+            per_cu > 0 && cus > 0 && grid > (int64_t)per_cu * cus)
+            grid = (int64_t)per_cu * cus;
+        (void)hipGetLastError();
+    }
+    if (env->lds_grid_cap > 0 && grid > env->lds_grid_cap) grid = env->lds_grid_cap;
+    env->lds_grid = grid;
+    if (grid < blocks) kern = kern_p;
     if (env->ev_start) {  // one-shot: bracket exactly this dispatch
         hipEvent_t a = (hipEvent_t)env->ev_start, b = (hipEvent_t)env->ev_stop;
         env->ev_start = env->ev_stop = nullptr;
-        hipExtLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(threads), 0, st, a, b, 0, pc, env->s, io, k_total,
+        hipExtLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(threads), 0, st, a, b, 0, pc, env->s, io, k_total,
                               env->cur);
     } else {
-        hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(threads), 0, st, pc, env->s, io, k_total, env->cur);
+        hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(threads), 0, st, pc, env->s, io, k_total, env->cur);
     }
     HE_HIP(env, hipGetLastError());
     env->block_pos = env->cfg.market_block;
@@ -4441,6 +4489,10 @@ he_status he_create(const he_config* cfg, he_env** out) {
             env->fuse_market = !(ev && ev[0] == '0');
             const char* el = getenv("HE_LDS_ROLLOUT");
             env->lds_rollout = !(el && el[0] == '0');
+            const char* ep = getenv("HE_LDS_PERSIST");
+            env->lds_persist = !(ep && ep[0] == '0');
+            const char* eg = getenv("HE_LDS_MAX_GRID");
+            env->lds_grid_cap = eg ? atoll(eg) : 0;
         }
         HE_HIP(env, hipStreamCreateWithFlags(&env->xs, hipStreamNonBlocking));
         HE_HIP(env, hipEventCreateWithFlags(&env->ev_fork, hipEventDisableTiming));

@@ -723,6 +723,15 @@ def test_lds_rollout_equals_tile_rollout(case, monkeypatch):
         assert torch.equal(a, b), (case, i)
 
 
+@pytest.mark.parametrize("case", ["long_K", "book8", "heston_barrier_ragged", "tiny_marks", "train"])
+def test_lds_persistent_grid_equals_tile_rollout(case, monkeypatch):
+    """The persistent grid of lds_rollout_kernel (a workgroup loops over
+    64-env tiles once there are more tiles than resident workgroups; HE_LDS_MAX_GRID=5 forces
+    many tiles per workgroup here) against the tile kernels, bit for bit."""
+    monkeypatch.setenv("HE_LDS_MAX_GRID", "5")
+    test_lds_rollout_equals_tile_rollout(case, monkeypatch)
+
+
 def _bench_module():
     import importlib.util
     spec = importlib.util.spec_from_file_location(

@@ -33,6 +33,21 @@ if [ "$PHASE" = mall ] || [ "$PHASE" = all ]; then
     line $f
   done
 fi
+if [ "$PHASE" = persist ]; then
+  echo "[$(date +%T)] parity (LDS / persistent grid / tiny marks)"
+  timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py -x -q -k "lds_rollout or lds_persistent or full_size" --timeout 120 --timeout-method thread > $O/persist_pytest.log 2>&1 || { tail -30 $O/persist_pytest.log; exit 1; }
+  tail -1 $O/persist_pytest.log
+  for rep in 1 2; do
+    for ps in 1 0; do
+      f=$O/persist${ps}_cfg3_$rep.log
+      HE_LDS_PERSIST=$ps timeout -k 10 300 python -u bench.py $Q --config 3 > $f 2>&1 || { tail -5 $f; exit 1; }
+      line $f
+    done
+    f=$O/persist1_cfg2_$rep.log
+    timeout -k 10 300 python -u bench.py $Q --config 2 > $f 2>&1 || { tail -5 $f; exit 1; }
+    line $f
+  done
+fi
 if [ "$PHASE" = rb ] || [ "$PHASE" = all ]; then
   echo "[$(date +%T)] rbergomi tests"
   timeout -k 10 300 python -u -m pytest tests/test_rbergomi_gpu.py -x -q --timeout 120 --timeout-method thread > $O/rb_pytest.log 2>&1 || { tail -30 $O/rb_pytest.log; exit 1; }
