@@ -589,10 +589,16 @@ __global__ void __launch_bounds__(kMcThreads) mc_mfma_kernel(McArgs a) {
     }
 }
 
-// RB_MC_VALU=1 (read per launch; A/B and tests): the reference tenor through mc_kernel instead
+// RB_MC_MFMA=1 (read per launch): the reference tenor through mc_mfma_kernel.  Not the default:
+// measured slower than mc_kernel on MI355X (f64 normals 9.75e5 vs 1.02e6 options/s, f32
+// 1.74e6 vs 2.02e6, profiles/r06m_rb_ab.txt) -- the f64 matrix pipe does the 960 FMAs per MC
+// path at the vector rate, and splitting each path's Euler chain over 4 lanes (the 4 maps,
+// the 8 shuffles, a final exp per lane, the NaN-safe max) costs more VALU issue than the
+// convolution it takes off (2301 VALU instructions per lane per 16-path tile against 1884 for a
+// quarter MC path of mc_kernel).  Kept as the tested alternative (test_mfma_pricer_equals_valu_pricer).
 bool mc_mfma_enabled() {
-    const char* e = getenv("RB_MC_VALU");
-    return !(e && e[0] == '1');
+    const char* e = getenv("RB_MC_MFMA");
+    return e && e[0] == '1';
 }
 
 void launch_mc_mfma(const McArgs& a, int norm, bool atm, dim3 grid, hipStream_t s) {

@@ -41,7 +41,14 @@ def _bs(S, K, T, r, sig):
     return c, c - S + K * math.exp(-r * T)
 
 
-def test_pricer_reference_draws_match_golden():
+@pytest.fixture(params=["valu", "mfma"])
+def mc_kernel_kind(request, monkeypatch):
+    """The reference-draw parity through both MC pricers of the reference tenor."""
+    monkeypatch.setenv("RB_MC_MFMA", "1" if request.param == "mfma" else "0")
+    return request.param
+
+
+def test_pricer_reference_draws_match_golden(mc_kernel_kind):
     rb = _rb()
     g = np.load(os.path.join(GOLD, "rb_price.npz"))
     S0, K, xi, H, eta, rho = (g[k] for k in ("S0", "K", "xi", "H", "eta", "rho"))
@@ -61,7 +68,7 @@ def test_pricer_reference_draws_match_golden():
                                        err_msg=f"{kind} tenor {T}")
 
 
-def test_generator_reference_draws_match_golden():
+def test_generator_reference_draws_match_golden(mc_kernel_kind):
     """Every stage fed the draws the reference consumed: params from the unit
     normals, paths from W_main, and each day's marks from that day's W (call, put)."""
     import torch
@@ -98,7 +105,7 @@ def test_generator_reference_draws_match_golden():
         np.testing.assert_allclose(got, g[key], rtol=MARK_RTOL, atol=1e-10 * g["paths"].max(), err_msg=key)
 
 
-def test_pricer_edge_inputs_follow_reference():
+def test_pricer_edge_inputs_follow_reference(mc_kernel_kind):
     """S0 <= 0, xi < 0 and NaN inputs through the oracle restatement (same draws)."""
     rb = _rb()
     rng = np.random.default_rng(4)
@@ -259,9 +266,9 @@ def test_mc_box_muller_extreme_uniforms():
 
 @pytest.mark.parametrize("normals", ["f64", "f32"])
 def test_mfma_pricer_equals_valu_pricer(normals, monkeypatch):
-    """The reference tenor's MC pricer on the matrix cores (mc_mfma_kernel: the fractional
-    convolution as v_mfma_f64_16x16x4_f64, the Euler chain composed over 4 lanes) against
-    mc_kernel (RB_MC_VALU=1) on the same Philox normals: the same marks up to the summation
+    """The reference tenor's MC pricer on the matrix cores (mc_mfma_kernel, RB_MC_MFMA=1: the
+    fractional convolution as v_mfma_f64_16x16x4_f64, the Euler chain composed over 4 lanes)
+    against mc_kernel (the default) on the same Philox normals: the same marks up to the summation
     order (~1e-16 relative per value); n_mc = 1000 leaves a partial last tile of paths, and the
     ATM generator (rb_price_atm_marks) is compared too."""
     rb = _rb()
@@ -275,7 +282,7 @@ def test_mfma_pricer_equals_valu_pricer(normals, monkeypatch):
     hist = _history()
     out = {}
     for valu in ("0", "1"):
-        monkeypatch.setenv("RB_MC_VALU", valu)
+        monkeypatch.setenv("RB_MC_MFMA", "1" if valu == "0" else "0")
         got = [rb.price_rbergomi_option(S0, K, 30 / 252, 0.04, xi, H, eta, rho, kind, 1000, 1 / 252, device=DEV,
                                         normals=normals, seed=21).cpu().numpy() for kind in ("call", "put")]
         res = rb.generate_paths_and_options(hist, 6, n_mc=300, device=DEV, seed=3, normals=normals)

@@ -56,7 +56,7 @@ if [ "$PHASE" = rb ] || [ "$PHASE" = all ]; then
     for nm in f64 f32; do
       for valu in 0 1; do
         f=$O/rb_${nm}_valu${valu}_$rep.log
-        RB_MC_VALU=$valu timeout -k 10 300 python -u bench.py --workload rbergomi --rb-normals $nm --no-pmc --no-cpu-baseline > $f 2>&1 || { tail -5 $f; exit 1; }
+        RB_MC_MFMA=$((1 - valu)) timeout -k 10 300 python -u bench.py --workload rbergomi --rb-normals $nm --no-pmc --no-cpu-baseline > $f 2>&1 || { tail -5 $f; exit 1; }
         python3 -c "
 import json,sys
 d=[json.loads(l) for l in open(sys.argv[1]) if l.startswith('{')][0]
