@@ -48,6 +48,19 @@ if [ "$PHASE" = persist ]; then
     line $f
   done
 fi
+if [ "$PHASE" = clock ]; then
+  # config 2 over a timed region as long as config 3's (1,600 launches, ~0.43 s) against the default 100
+  for rep in 1 2; do
+    for st in 25600 409600; do
+      f=$O/clock_cfg2_${st}_$rep.log
+      timeout -k 10 300 python -u bench.py $Q --config 2 --steps $st > $f 2>&1 || { tail -5 $f; exit 1; }
+      line $f
+    done
+    f=$O/clock_cfg3_$rep.log
+    timeout -k 10 300 python -u bench.py $Q --config 3 > $f 2>&1 || { tail -5 $f; exit 1; }
+    line $f
+  done
+fi
 if [ "$PHASE" = rb ] || [ "$PHASE" = all ]; then
   echo "[$(date +%T)] rbergomi tests"
   timeout -k 10 300 python -u -m pytest tests/test_rbergomi_gpu.py -x -q --timeout 120 --timeout-method thread > $O/rb_pytest.log 2>&1 || { tail -30 $O/rb_pytest.log; exit 1; }
