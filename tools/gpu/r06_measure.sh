@@ -61,6 +61,18 @@ if [ "$PHASE" = clock ]; then
     line $f
   done
 fi
+if [ "$PHASE" = scan ]; then
+  # the per-env-step kernel time against the env count (rounds of workgroups, footprint) and K
+  for a in "--envs 65536" "--envs 131072" "--envs 262144" "--envs 524288" "--envs 1048576" "--envs 1048576 --rollout-k 64" "--envs 65536 --rollout-k 64" "--envs 2097152"; do
+    f=$O/scan_$(echo $a | tr -d ' -').log
+    timeout -k 10 300 python -u bench.py $Q --config 2 $a > $f 2>&1 || { tail -5 $f; exit 1; }
+    python3 -c "
+import json,sys
+d=[json.loads(l) for l in open(sys.argv[1]) if l.startswith('{')][0]; r=d['roofline']; c=d['config']
+print(sys.argv[1].split('/')[-1], 'envs', c['envs_per_gpu'], 'K', c['rollout_k'], 'kernel_us %.1f' % r['kernel_us'], 'ns/env-step %.4f' % (r['kernel_us'] * 1e3 / (c['envs_per_gpu'] * c['rollout_k'])), 'frac', r['frac'])
+" $f
+  done
+fi
 if [ "$PHASE" = rb ] || [ "$PHASE" = all ]; then
   echo "[$(date +%T)] rbergomi tests"
   timeout -k 10 300 python -u -m pytest tests/test_rbergomi_gpu.py -x -q --timeout 120 --timeout-method thread > $O/rb_pytest.log 2>&1 || { tail -30 $O/rb_pytest.log; exit 1; }
