@@ -4,6 +4,7 @@ loop's policy alone.
 
     python tools/host_step_timing.py
 """
+import ctypes
 import os
 import sys
 import time
@@ -48,6 +49,27 @@ def main():
         lib.he_step(v._h, *z.step_args, st)
     out["he_step launch only (no wait)"] = med(launch_only, 2000, 100)
     torch.cuda.synchronize()
+    # the same step with device-resident buffers (no host-mapped reads / writes in the kernel)
+    dev_args = (v._act.data_ptr(), v._obs.data_ptr(), v._rew.data_ptr(), v._term.data_ptr(), v._trunc.data_ptr(),
+                v._tobs.data_ptr(), z.step_args[-1])
+
+    def raw_dev():
+        lib.he_step(v._h, *dev_args, st)
+        lib.he_stream_wait(st)
+    out["he_step (device buffers)+he_stream_wait"] = med(raw_dev)
+    hip = ctypes.CDLL("libamdhip64.so")
+    hip.hipStreamQuery.argtypes = [ctypes.c_void_p]
+    hip.hipStreamQuery.restype = ctypes.c_int
+
+    def raw_spin():   # completion by polling hipStreamQuery instead of a blocking synchronize
+        lib.he_step(v._h, *z.step_args, st)
+        while hip.hipStreamQuery(st) != 0:
+            pass
+    out["he_step+poll hipStreamQuery"] = med(raw_spin)
+
+    def empty_sync():
+        lib.he_stream_wait(st)
+    out["he_stream_wait on an idle stream"] = med(empty_sync)
     out["step_host"] = med(lambda: v.step_host(act))
     env.reset()
 
