@@ -12,7 +12,7 @@ import json,sys
 d=[json.loads(l) for l in open(sys.argv[1]) if l.startswith('{')][0]; r=d['roofline']
 print(sys.argv[1].split('/')[-1], 'value %.4g'%d['value'], 'kernel_us', r.get('kernel_us'), 'frac', r.get('frac'))
 " $1; }
-if [ "$PHASE" = host ] || [ "$PHASE" = all ]; then
+if [ "$PHASE" = host ] || [ "$PHASE" = all ] || [ "$PHASE" = scan ]; then
   echo "[$(date +%T)] host step timing"
   timeout -k 10 200 python -u tools/host_step_timing.py > $O/host_step.log 2>&1 || { tail -20 $O/host_step.log; exit 1; }
   grep -v amdgpu.ids $O/host_step.log
@@ -71,6 +71,17 @@ import json,sys
 d=[json.loads(l) for l in open(sys.argv[1]) if l.startswith('{')][0]; r=d['roofline']; c=d['config']
 print(sys.argv[1].split('/')[-1], 'envs', c['envs_per_gpu'], 'K', c['rollout_k'], 'kernel_us %.1f' % r['kernel_us'], 'ns/env-step %.4f' % (r['kernel_us'] * 1e3 / (c['envs_per_gpu'] * c['rollout_k'])), 'frac', r['frac'])
 " $f
+  done
+fi
+if [ "$PHASE" = persist45 ]; then
+  for rep in 1 2; do
+    for c in 4 5; do
+      for ps in 1 0; do
+        f=$O/persist${ps}_cfg${c}_$rep.log
+        HE_LDS_PERSIST=$ps timeout -k 10 300 python -u bench.py $Q --config $c > $f 2>&1 || { tail -5 $f; exit 1; }
+        line $f
+      done
+    done
   done
 fi
 if [ "$PHASE" = rb ] || [ "$PHASE" = all ]; then
