@@ -84,6 +84,21 @@ if [ "$PHASE" = persist45 ]; then
     done
   done
 fi
+if [ "$PHASE" = balance ]; then
+  echo "[$(date +%T)] parity (LDS / persistent / replay)"
+  timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py -x -q -k "lds or full_size or replay" --timeout 120 --timeout-method thread > $O/bal_pytest.log 2>&1 || { tail -30 $O/bal_pytest.log; exit 1; }
+  tail -1 $O/bal_pytest.log
+  for c in 3 4 5 2 6 3 4 5; do
+    for v in claim_nopersist claim_persist noclaim_nopersist; do
+      lib=""; ps=0
+      [ $v = claim_persist ] && ps=1
+      [ $v = noclaim_nopersist ] && lib=$R/tools/ab/noclaim.so
+      f=$O/bal_cfg${c}_$v.log; [ -e $f ] && f=$O/bal_cfg${c}_${v}_2.log
+      CANTORRL_HEDGEENV_LIB=$lib HE_LDS_PERSIST=$ps timeout -k 10 300 python -u bench.py $Q --config $c > $f 2>&1 || { tail -5 $f; exit 1; }
+      line $f
+    done
+  done
+fi
 if [ "$PHASE" = rb ] || [ "$PHASE" = all ]; then
   echo "[$(date +%T)] rbergomi tests"
   timeout -k 10 300 python -u -m pytest tests/test_rbergomi_gpu.py -x -q --timeout 120 --timeout-method thread > $O/rb_pytest.log 2>&1 || { tail -30 $O/rb_pytest.log; exit 1; }
