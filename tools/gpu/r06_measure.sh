@@ -99,6 +99,22 @@ if [ "$PHASE" = balance ]; then
     done
   done
 fi
+if [ "$PHASE" = clk ]; then
+  # the shader clock the timing build reports (s_memtime per s_memrealtime tick), config 2 and
+  # 3 back to back twice, then the plain bench lines of both
+  for rep in 1 2; do
+    for n in 65536 1048576; do
+      echo "== timing build, $n envs (rep $rep)"
+      CANTORRL_HEDGEENV_LIB=$R/tools/abt/timing.so timeout -k 10 200 python -u tools/lds_timing.py $n 256 > $O/clk_${n}_$rep.log 2>&1 || { tail -5 $O/clk_${n}_$rep.log; exit 1; }
+      grep -v amdgpu.ids $O/clk_${n}_$rep.log | head -8
+    done
+    for c in 2 3; do
+      f=$O/clk_bench_cfg${c}_$rep.log
+      timeout -k 10 300 python -u bench.py $Q --config $c > $f 2>&1 || { tail -5 $f; exit 1; }
+      line $f
+    done
+  done
+fi
 if [ "$PHASE" = rb ] || [ "$PHASE" = all ]; then
   echo "[$(date +%T)] rbergomi tests"
   timeout -k 10 300 python -u -m pytest tests/test_rbergomi_gpu.py -x -q --timeout 120 --timeout-method thread > $O/rb_pytest.log 2>&1 || { tail -30 $O/rb_pytest.log; exit 1; }
