@@ -63,7 +63,7 @@ if [ "$PHASE" = clock ]; then
 fi
 if [ "$PHASE" = scan ]; then
   # the per-env-step kernel time against the env count (rounds of workgroups, footprint) and K
-  for a in "--envs 65536" "--envs 131072" "--envs 262144" "--envs 524288" "--envs 1048576" "--envs 1048576 --rollout-k 64" "--envs 65536 --rollout-k 64" "--envs 2097152"; do
+  for a in "--envs 65536" "--envs 131072" "--envs 262144" "--envs 524288" "--envs 1048576" "--envs 1048576 --rollout-k 64" "--envs 1048576 --rollout-k 16" "--envs 65536 --rollout-k 64" "--envs 65536 --rollout-k 16" "--envs 2097152"; do
     f=$O/scan_$(echo $a | tr -d ' -').log
     timeout -k 10 300 python -u bench.py $Q --config 2 $a > $f 2>&1 || { tail -5 $f; exit 1; }
     python3 -c "
