@@ -2900,18 +2900,6 @@ __device__ __forceinline__ void lds_producer(const Params& p, int k_steps, const
 #if HE_LDS_BALANCE || defined(HE_LDS_HWID)
 __device__ uint32_t g_cu_ticket[4096];
 #endif
-// HE_LDS_CLAIM (with HE_LDS_BALANCE): the role permutation is a per-CU slot, claimed at the
-// workgroup's start and released at its end (g_cu_taken: a bit per permutation in use), so a
-// workgroup that starts on a CU when another finished there -- past the first round of a launch,
-// configs 3, 4, 5 -- takes that one's permutation, the one its waves' SIMDs are missing.  With
-// the plain ticket (ticket mod 4) it takes whatever the per-CU counter says, and a SIMD can end
-// up with two waves of one role and none of another.
-#ifndef HE_LDS_CLAIM
-#define HE_LDS_CLAIM 1
-#endif
-#if HE_LDS_BALANCE && HE_LDS_CLAIM
-__device__ uint32_t g_cu_taken[4096];
-#endif
 #ifdef HE_LDS_HWID
 // Diagnostic builds only: {HW_ID, XCC_ID, ticket, role} of every wave of the last launch
 // (he_debug_lds_hwid)
@@ -2921,42 +2909,16 @@ __device__ __forceinline__ uint32_t hw_cu_key(uint32_t hw, uint32_t xcc) {
     // XCC 4 bits | SE_ID 3 | SH_ID 1 | CU_ID 4
     return ((xcc & 15u) << 8) | (((hw >> 13) & 7u) << 5) | (((hw >> 12) & 1u) << 4) | ((hw >> 8) & 15u);
 }
-// lds_role's per-workgroup record in LDS: [0, 4) the SIMD of each wave, [4] the ticket or the
-// claimed permutation (one LDS allocation per kernel: every call returns the same address)
-__device__ __forceinline__ uint32_t* lds_place() {
-    __shared__ uint32_t sh_place[5];
-    return sh_place;
-}
 template <int NWAVES>
 __device__ __forceinline__ int lds_role(int wave) {
 #if HE_LDS_BALANCE || defined(HE_LDS_HWID)
     if constexpr (NWAVES == 4) {
-        uint32_t* sh_place = lds_place();
+        __shared__ uint32_t sh_place[5];
         const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);     // HW_REG_HW_ID, 32 bits
         const uint32_t xcc = __builtin_amdgcn_s_getreg((15 << 11) | 20);   // HW_REG_XCC_ID
         const uint32_t simd = (hw >> 4) & 3u;
         if ((threadIdx.x & 63) == 0) sh_place[wave] = simd;
-        if (threadIdx.x == 0) {
-            const uint32_t key = hw_cu_key(hw, xcc & 15u);
-            uint32_t t = atomicAdd(&g_cu_ticket[key], 1u);
-#if HE_LDS_BALANCE && HE_LDS_CLAIM
-            // claim the lowest free permutation: the one a finished workgroup released (4 tries
-            // at most; none free -- more than 4 workgroups of these kernels on the CU at once --
-            // keeps the ticket's, released as nothing at the end)
-            uint32_t taken = __hip_atomic_load(&g_cu_taken[key], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            uint32_t got = 4u;
-            for (int tries = 0; tries < 4 && got == 4u; ++tries) {
-                const uint32_t fr = ~taken & 15u;
-                if (!fr) break;
-                const uint32_t b = __builtin_ctz(fr);
-                const uint32_t old = atomicOr(&g_cu_taken[key], 1u << b);
-                if (!(old & (1u << b))) got = b;
-                else taken = old | (1u << b);
-            }
-            t = (got < 4u) ? got : (t | 0x100u);   // 0x100: no slot claimed (release nothing)
-#endif
-            sh_place[4] = t;
-        }
+        if (threadIdx.x == 0) sh_place[4] = atomicAdd(&g_cu_ticket[hw_cu_key(hw, xcc & 15u)], 1u);
         __syncthreads();
         const uint32_t m = (1u << sh_place[0]) | (1u << sh_place[1]) | (1u << sh_place[2]) | (1u << sh_place[3]);
         int role = wave;
@@ -2975,23 +2937,6 @@ __device__ __forceinline__ int lds_role(int wave) {
     }
 #endif
     return wave;
-}
-
-// The workgroup's end: its role permutation back to the CU's free slots (HE_LDS_CLAIM), after
-// every wave is done (the next workgroup on these SIMDs can only start once they all exit).
-template <int NWAVES>
-__device__ __forceinline__ void lds_release() {
-#if HE_LDS_BALANCE && HE_LDS_CLAIM
-    if constexpr (NWAVES == 4) {
-        __syncthreads();
-        const uint32_t t = lds_place()[4];
-        if (threadIdx.x == 0 && t < 4u) {
-            const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);
-            const uint32_t xcc = __builtin_amdgcn_s_getreg((15 << 11) | 20);
-            atomicAnd(&g_cu_taken[hw_cu_key(hw, xcc & 15u)], ~(1u << t));
-        }
-    }
-#endif
 }
 
 // Wave roles are uniform (readfirstlane), so each role's loop is plain scalar control
@@ -3019,7 +2964,6 @@ __global__ __launch_bounds__((LdsGeom<MODE, BOOK>::threads), (LdsGeom<MODE, BOOK
         if (wave == 0) lds_stepper<MODE, BOOK, LEAN, false>(p, s, io, k_steps, cur, lm, base);
         else if (wave == 1) lds_stepper<MODE, BOOK, LEAN, true>(p, s, io, k_steps, cur, lm, base);
         else lds_producer<MODE, BOOK, LEAN>(p, k_steps, cur, lm, base, wave - 2);
-        lds_release<LdsGeom<MODE, BOOK>::threads / 64>();
         return;
     }
     // PERSIST (launch_lds_rollout, more tiles than the device holds workgroups at once): a
@@ -3036,7 +2980,6 @@ __global__ __launch_bounds__((LdsGeom<MODE, BOOK>::threads), (LdsGeom<MODE, BOOK
         else lds_producer<MODE, BOOK, LEAN>(p, k_steps, cur, lm, base, wave - 2);
         if (tile + gridDim.x < tiles) __syncthreads();   // every role done with lm before the next tile
     }
-    lds_release<LdsGeom<MODE, BOOK>::threads / 64>();
 }
 
 // ------------------------------------------------------------------ replay rollouts in LDS
@@ -3507,7 +3450,6 @@ __global__ __launch_bounds__(256, 4) __attribute__((amdgpu_num_sgpr(kLdsNumSgpr)
     if (wave == 0) lds_replay_stepper<false, FAST>(p, s, io, k_steps, lm, base);
     else if (wave == 1) lds_replay_stepper<true, FAST>(p, s, io, k_steps, lm, base);
     else lds_replay_loader(p, s, k_steps, lm, base, wave - 2);
-    lds_release<4>();
 }
 
 // he_episode_summaries: the last finished episode of every env, [4][N] (the reward
@@ -4243,7 +4185,7 @@ static he_status launch_lds_rollout(he_env* env, const Io& io, int k_total, hipS
 #define HE_LDS_PICK(M, B, L)                                 \
     do {                                                     \
         kern = lds_rollout_kernel<M, B, L, false>;           \
-        kern_p = lds_rollout_kernel<M, B, L, true>;          \
+        kern_p = lds_rollout_kernel<M, B, L, !(B)>;          \
         threads = LdsGeom<M, B>::threads;                    \
     } while (0)
     if (env->cfg.mode == HE_MODE_HESTON) {
@@ -4276,7 +4218,10 @@ static he_status launch_lds_rollout(he_env* env, const Io& io, int k_total, hipS
     }
     if (env->lds_grid_cap > 0 && grid > env->lds_grid_cap) grid = env->lds_grid_cap;
     env->lds_grid = grid;
-    if (grid < blocks) kern = kern_p;
+    // with a book the persistent instance spills (13 VGPRs) and measured slower (config 4
+    // 5.64 vs 5.48 ms, config 5 1.49 vs 1.46 ms, profiles/r06bal_*): one workgroup per tile there
+    if (grid < blocks && !book) kern = kern_p;
+    else grid = blocks;
     if (env->ev_start) {  // one-shot: bracket exactly this dispatch
         hipEvent_t a = (hipEvent_t)env->ev_start, b = (hipEvent_t)env->ev_stop;
         env->ev_start = env->ev_stop = nullptr;
