@@ -37,6 +37,9 @@ lib.he_debug_lds_timing.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
 buf = np.zeros((4, 4096, 5), np.uint64)
 assert lib.he_debug_lds_timing(buf.ctypes.data, buf.nbytes) == 0
 wg = min((n + 63) // 64, 4096)
+# the persistent grid (more tiles than resident workgroups): only blockIdx < grid hold records
+# (each its last tile's); keep the filled rows
+wg = int(min(wg, max(1, (buf[0, :, 2] > 0).sum())))
 for role, name in enumerate(("reward", "obs", "prod0", "prod1")):
     tot = buf[role, :wg, 0].astype(np.float64)
     bar = buf[role, :wg, 1].astype(np.float64)
