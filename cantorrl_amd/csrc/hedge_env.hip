@@ -113,6 +113,7 @@ struct BookOpt {
     double K, H, q100;
     double lnK, lnH, lnH2K;   // log K, log H, 2 log H - log K (host)
     double invK;              // 1 / K (host)
+    double invH;              // 1 / H (host)
 };
 
 struct Params {
@@ -802,7 +803,10 @@ __device__ __forceinline__ double book_option(const Params& p, const BookOpt& o,
             const double y = (o.lnH2K - b.lnS) * isst + ls;      // log(H^2 / (S K)) / sst + lam sst
             const double y1 = lhs * isst + ls;
             const double ert = e[3];                             // e^{r tau}
-            const double sh = exp_book_g(-lhs);                  // S / H
+            // S / H as a product (one exp_book_g less per option and slot than exp(log S - log H):
+            // the up-and-out call is the whole book of config 5); S = 0 or inf gives 0 or inf as
+            // the exp did
+            const double sh = S * o.invH;
             // H / S as 1 / (S / H): v_rcp_f64 and two Newton steps (1 ulp) instead of a second
             // exp_book; past |lhs| = 700 (S at 0 or inf) the library exp, as exp_book_g
             double hs;
@@ -4514,6 +4518,7 @@ he_status he_create(const he_config* cfg, he_env** out) {
             hb[k].lnH = log(hb[k].H);
             hb[k].lnH2K = 2.0 * hb[k].lnH - hb[k].lnK;
             hb[k].invK = 1.0 / hb[k].K;
+            hb[k].invH = 1.0 / hb[k].H;
         }
         HE_HIP(env, hipMalloc(&env->dbook, HE_BOOK_MAX * sizeof(BookOpt)));
         HE_HIP(env, hipMemcpy(env->dbook, hb, c.book_size * sizeof(BookOpt), hipMemcpyHostToDevice));

@@ -115,6 +115,19 @@ if [ "$PHASE" = clk ]; then
     done
   done
 fi
+if [ "$PHASE" = book ]; then
+  echo "[$(date +%T)] parity (books / Heston)"
+  timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_book_cpu.py -x -q -k "book or heston or barrier or full_size" --timeout 120 --timeout-method thread > $O/book_pytest.log 2>&1 || { tail -30 $O/book_pytest.log; exit 1; }
+  tail -1 $O/book_pytest.log
+  for rep in 1 2 3; do
+    for v in base pre_sh; do
+      lib=""; [ "$v" != base ] && lib=$R/tools/ab/$v.so
+      f=$O/book_cfg5_${v}_$rep.log
+      CANTORRL_HEDGEENV_LIB=$lib timeout -k 10 300 python -u bench.py $Q --config 5 > $f 2>&1 || { tail -5 $f; exit 1; }
+      line $f
+    done
+  done
+fi
 if [ "$PHASE" = rb ] || [ "$PHASE" = all ]; then
   echo "[$(date +%T)] rbergomi tests"
   timeout -k 10 300 python -u -m pytest tests/test_rbergomi_gpu.py -x -q --timeout 120 --timeout-method thread > $O/rb_pytest.log 2>&1 || { tail -30 $O/rb_pytest.log; exit 1; }
