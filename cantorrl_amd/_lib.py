@@ -122,7 +122,7 @@ EXPORTS = [
     "he_sync_market", "he_vecnorm_stats_len", "he_vecnorm_scratch_bytes", "he_vecnorm_init", "he_vecnorm_step",
     "he_vecnorm_apply", "he_vecnorm_attach", "he_vecnorm_attach_eval", "he_vecnorm_reset", "he_fixed_european_marks", "he_bs_delta_hedge", "he_count_nonfinite",
     "he_device_rng", "he_device_math", "he_host_math", "he_episode_summaries", "he_host_alloc", "he_host_free",
-    "he_stream_wait",
+    "he_stream_wait", "he_step_signal", "he_signal_seq", "he_signal_wait",
 ]
 
 
@@ -214,6 +214,9 @@ def load(path=LIB_PATH):
         "he_host_alloc": (i32, [ctypes.c_size_t, ctypes.POINTER(vp), ctypes.POINTER(vp)]),
         "he_host_free": (i32, [vp]),
         "he_stream_wait": (i32, [vp]),
+        "he_step_signal": (i32, [vp, vp]),
+        "he_signal_seq": (ctypes.c_uint32, [vp]),
+        "he_signal_wait": (i32, [vp, vp, vp]),
     }
     ab = path != os.path.join(HERE, "lib", "libhedgeenv.so")  # an A/B build of an older tree
     for name, (res, args) in sig.items():

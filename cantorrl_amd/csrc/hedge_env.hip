@@ -30,6 +30,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <chrono>
 #include <new>
 #include <type_traits>
 
@@ -236,6 +237,11 @@ struct Io {
     PolIo pol;
     bool pol_on;
     bool sums;         // he_rollout: keep the episode summaries (State::sum / last)
+    // he_step_signal (he_step only): the step's sequence number stored into `sig` (host-mapped)
+    // after every output of the launch; `sig_cnt` counts the workgroups done (device word)
+    uint32_t* sig;
+    uint32_t* sig_cnt;
+    uint32_t sig_seq;
 };
 
 struct Mkt {
@@ -1469,6 +1475,25 @@ struct VnHook {
     bool term;
 };
 
+// he_step_signal: the end of an he_step launch, raised in host-mapped memory so the host can
+// see the step's outputs without the runtime's completion path (~8 us of a small-N step,
+// profiles/r06h_flag_probe.txt).  Every thread makes its own stores visible system-wide, the
+// workgroup meets, and one thread per workgroup counts the workgroup done; the last one to count
+// re-arms the counter for the next step and stores the sequence number with release semantics.
+__device__ __forceinline__ void raise_step_signal(const Io& io) {
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t nwg = gridDim.x;
+        const uint32_t prev =
+            nwg == 1u ? 0u : __hip_atomic_fetch_add(io.sig_cnt, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        if (prev == nwg - 1u) {
+            if (nwg > 1u) __hip_atomic_store(io.sig_cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(io.sig, io.sig_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+}
+
 template <int MODE, bool INFO, bool SINGLE, bool BOOK, bool FAST, bool POL, bool GS>
 __device__ __forceinline__ void step_body(const Params& pk, int64_t n_envs, const float4* tA, const float4* tB,
                                           const double* tC, State s, Io io, int k_steps_arg, int slot0,
@@ -1880,6 +1905,9 @@ __device__ __forceinline__ void step_body(const Params& pk, int64_t n_envs, cons
         }
         if (io.trunc) ((GLOBAL uint8_t*)io.trunc)[i] = 0;
     }
+    if constexpr (SINGLE) {
+        if (io.sig) raise_step_signal(io);
+    }
     HE_TIM(4);
 }
 
@@ -1903,6 +1931,9 @@ struct StepIo {
     uint8_t* term;
     uint8_t* trunc;
     float* tobs;
+    uint32_t* sig;      // he_step_signal (Io::sig)
+    uint32_t* sig_cnt;
+    uint32_t sig_seq;
 };
 template <int MODE, bool BOOK, bool FAST, bool GS>
 __global__ __launch_bounds__(kBlock) void step1_kernel(const Params* __restrict__ pc, int64_t n, const float4* tA,
@@ -1918,6 +1949,9 @@ __global__ __launch_bounds__(kBlock) void step1_kernel(const Params* __restrict_
     io.info = he_info{};
     io.pol_on = false;
     io.sums = false;
+    io.sig = sio.sig;
+    io.sig_cnt = sio.sig_cnt;
+    io.sig_seq = sio.sig_seq;
     step_body<MODE, false, true, BOOK, FAST, false, GS>(*pc, n, tA, tB, tC, s, io, 1, slot0, blockIdx.x);
 }
 
@@ -1940,6 +1974,7 @@ __global__ __launch_bounds__(kBlock) void step1_vn_kernel(const Params* __restri
     io.info = he_info{};
     io.pol_on = false;
     io.sums = false;
+    io.sig = nullptr;  // more work follows the step in this launch
     // this thread's env (kEpw == 64: env = workgroup base + threadIdx.x): its running return
     // is loaded before the step, so the moments need no further memory round trip
     static_assert(kEpw == 64 && kEpb == kBlock, "one env per thread");
@@ -1969,6 +2004,7 @@ __global__ __launch_bounds__(kBlock) void step1_vne_kernel(const Params* __restr
     io.info = he_info{};
     io.pol_on = false;
     io.sums = false;
+    io.sig = nullptr;
     static_assert(kEpw == 64 && kEpb == kBlock, "one env per thread");
     const int64_t r0 = (int64_t)blockIdx.x * kEpb;
     __shared__ vn::FrozenNorm fz;
@@ -3733,6 +3769,9 @@ struct he_env {
     bool ready = false;       // a reset happened since create/seed
     void* ev_start = nullptr; // he_time_next_step events (hipEvent_t)
     void* ev_stop = nullptr;
+    uint32_t* sig_flag = nullptr;  // he_step_signal: the armed flag (device address of host-mapped memory)
+    uint32_t* d_sig_cnt = nullptr; // ... its workgroup counter (device word, 0 between steps)
+    uint32_t sig_seq = 0;          // sequence number of the last armed he_step
     std::vector<std::pair<size_t, void*>> fields;  // (bytes, device ptr) for get/set_state
 };
 
@@ -4020,7 +4059,7 @@ static void launch_step_gs(he_env* env, const Params& p, const Io& io, bool info
         const Params* pc = env->dparams + (REPLAY ? 0 : env->cur_buf);
         const float4* tA = REPLAY ? p.rec : p.tileA;
         const float4* tB = REPLAY ? p.recg : p.tileB;
-        StepIo sio{io.act, io.obs, io.rew, io.term, io.trunc, io.tobs};
+        StepIo sio{io.act, io.obs, io.rew, io.term, io.trunc, io.tobs, io.sig, io.sig_cnt, io.sig_seq};
         if (env->vne_on && io.obs && io.rew && io.term && io.tobs) {  // + the eval VecNormalize step
             hipEvent_t a = (hipEvent_t)env->ev_start, b = (hipEvent_t)env->ev_stop;
             env->ev_start = env->ev_stop = nullptr;
@@ -4560,6 +4599,7 @@ he_status he_destroy(he_env* env) {
         if (env->h_eps) (void)hipHostFree(env->h_eps);
         if (env->ev_eps) (void)hipEventDestroy(env->ev_eps);
         if (env->scratch_count) (void)hipFree(env->scratch_count);
+        if (env->d_sig_cnt) (void)hipFree(env->d_sig_cnt);
         if (env->xs) {
             (void)hipStreamSynchronize(env->xs);
             (void)hipStreamDestroy(env->xs);
@@ -4904,8 +4944,20 @@ he_status he_step(he_env* env, const float* actions, float* obs, float* reward, 
         return fail(env, HE_EINVAL, "he_vecnorm_attach_eval with Monitor sums: an he_step that requests info "
                                     "must request info->reward_step too");
     }
+    uint32_t* const sig = env->sig_flag;  // he_step_signal: one-shot, this step only
+    env->sig_flag = nullptr;
+    if (sig) {
+        if (vn || vne) {
+            env->vn_on = env->vne_on = false;
+            return fail(env, HE_EINVAL, "he_step_signal: the signal covers a step with no VecNormalize attached");
+        }
+        io.sig = sig;
+        io.sig_cnt = env->d_sig_cnt;
+        io.sig_seq = env->sig_seq + 1u == 0u ? 1u : env->sig_seq + 1u;
+    }
     env->vn_fused = false;
     he_status s = launch_steps(env, io, want_info, 1, stream);
+    if (sig && s == HE_OK) env->sig_seq = io.sig_seq;
     env->vn_on = env->vne_on = false;
     if (s == HE_OK && vne && !env->vn_fused) {
         // another step kernel ran (info requested): the eval VecNormalize step as its own
@@ -5093,6 +5145,50 @@ he_status he_host_free(void* host_ptr) {
 
 he_status he_stream_wait(void* stream) {
     return hipStreamSynchronize((hipStream_t)stream) == hipSuccess ? HE_OK : HE_EHIP;
+}
+
+he_status he_step_signal(he_env* env, uint32_t* flag) {
+    if (!env) return HE_EINVAL;
+    if (flag && (reinterpret_cast<uintptr_t>(flag) & 3u) != 0) return fail(env, HE_EINVAL, "flag must be 4-byte aligned");
+    if (flag && !env->d_sig_cnt) {
+        DeviceGuard dg(env->cfg.device);
+        uint32_t* c = nullptr;
+        HE_HIP(env, hipMalloc(&c, 256));
+        if (hipMemset(c, 0, 256) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+            (void)hipGetLastError();
+            (void)hipFree(c);
+            return fail(env, HE_EHIP, "he_step_signal: counter allocation failed");
+        }
+        env->d_sig_cnt = c;
+    }
+    env->sig_flag = flag;
+    return HE_OK;
+}
+
+uint32_t he_signal_seq(const he_env* env) { return env ? env->sig_seq : 0u; }
+
+he_status he_signal_wait(he_env* env, const uint32_t* flag_host, void* stream) {
+    if (!env || !flag_host) return HE_EINVAL;
+    if (env->sig_seq == 0u) return fail(env, HE_ESTATE, "he_signal_wait: no he_step has been signalled");
+    const uint32_t want = env->sig_seq;
+    // spin on the host's view of the flag: a small-N step lands in ~5-10 us.  Past kSpin the
+    // runtime's blocking wait takes over (a step queued behind long work burns no core), and
+    // the flag must then hold the step's number: the kernel raises it before it ends.
+    constexpr double kSpinUs = 200.0;
+    if (__atomic_load_n(flag_host, __ATOMIC_ACQUIRE) == want) return HE_OK;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t it = 1;; ++it) {
+        if (__atomic_load_n(flag_host, __ATOMIC_ACQUIRE) == want) return HE_OK;
+        __builtin_ia32_pause();
+        if ((it & 255u) == 0u &&
+            std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() > kSpinUs)
+            break;
+    }
+    DeviceGuard dg(env->cfg.device);
+    HE_HIP(env, hipStreamSynchronize((hipStream_t)stream));
+    if (__atomic_load_n(flag_host, __ATOMIC_ACQUIRE) == want) return HE_OK;
+    return fail(env, HE_ESTATE, "he_signal_wait: the stream is idle and the flag holds %u, not step %u",
+                (unsigned)__atomic_load_n(flag_host, __ATOMIC_ACQUIRE), (unsigned)want);
 }
 
 int64_t he_num_envs(const he_env* env) { return env ? env->cfg.n_envs : -1; }

@@ -506,13 +506,20 @@ class HedgingVecEnv:
         z = self._hio
         np.copyto(z.act, np.asarray(actions, dtype=np.float32).reshape(self.num_envs, 2))
         self._retire_view()
-        st = self.lib.he_step(self._h, *z.step_args, _raw_stream(self._dev_index))
-        _lib.check(self.lib, self._h, st, "he_step")
-        if self.check_finite:
-            for p, c in ((z.d_obs, 13 * self.num_envs), (z.d_rew, self.num_envs)):
-                _lib.check(self.lib, self._h, self.lib.he_count_nonfinite(p, c, self._nonfinite.data_ptr(),
-                                                                          self.stream), "he_count_nonfinite")
-        _lib.check(self.lib, self._h, self.lib.he_stream_wait(_raw_stream(self._dev_index)), "he_stream_wait")
+        lib, h = self.lib, self._h
+        stream = _raw_stream(self._dev_index)
+        if not self.check_finite:
+            # the step kernel raises the block's flag word after its outputs (he_step_signal):
+            # the host reads it instead of waiting for the runtime's completion (~5 us less)
+            _lib.check(lib, h, lib.he_step_signal(h, z.d_flag), "he_step_signal")
+            _lib.check(lib, h, lib.he_step(h, *z.step_args, stream), "he_step")
+            _lib.check(lib, h, lib.he_signal_wait(h, z.h_flag, stream), "he_signal_wait")
+            return z
+        _lib.check(lib, h, lib.he_step(h, *z.step_args, stream), "he_step")
+        for p, c in ((z.d_obs, 13 * self.num_envs), (z.d_rew, self.num_envs)):
+            _lib.check(lib, h, lib.he_count_nonfinite(p, c, self._nonfinite.data_ptr(), self.stream),
+                       "he_count_nonfinite")
+        _lib.check(lib, h, lib.he_stream_wait(stream), "he_stream_wait")
         return z
 
     def _step_wait_host(self, actions):
@@ -651,8 +658,8 @@ class HedgingVecEnv:
 class _HostIo:
     """The host-mapped block of the small-N host path (he_host_alloc): the env's io layout
     [obs | reward | terminated | truncated | info fields] (as the device io buffer), then the
-    actions [N, 2] and the terminal obs [N, 13], each 256-B aligned.  The step kernel reads the
-    actions and writes everything else in place."""
+    actions [N, 2], the terminal obs [N, 13] and the step's completion flag (one u32), each 256-B
+    aligned.  The step kernel reads the actions and writes everything else in place."""
 
     def __init__(self, venv):
         lib, n = venv.lib, venv.num_envs
@@ -661,7 +668,8 @@ class _HostIo:
         io_b = venv._io.numel()
         a_off = _align(io_b, 256)
         t_off = _align(a_off + 8 * n, 256)
-        total = t_off + 52 * n
+        f_off = _align(t_off + 52 * n, 256)   # the step's completion flag (he_step_signal)
+        total = f_off + 4
         hp, dp = c.c_void_p(), c.c_void_p()
         _lib.check(lib, None, lib.he_host_alloc(total, c.byref(hp), c.byref(dp)), "he_host_alloc")
         self.host = hp.value
@@ -671,6 +679,7 @@ class _HostIo:
         self.act = base[a_off:a_off + 8 * n].view(np.float32).reshape(n, 2)
         self.tobs = base[t_off:t_off + 52 * n].view(np.float32).reshape(n, 13)
         self.d_obs, self.d_rew = d, d + 52 * n
+        self.d_flag, self.h_flag = d + f_off, hp.value + f_off
         self.info = _lib.HeInfo()
         for k, dt, o in venv._info_offs:
             setattr(self.info, k, d + venv._io_info0 + o)

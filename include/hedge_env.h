@@ -311,6 +311,21 @@ he_status he_host_alloc(size_t bytes, void** host_ptr, void** device_ptr);
 he_status he_host_free(void* host_ptr);
 he_status he_stream_wait(void* stream);
 
+/* Step completion signal for the host-mapped path (the same host loops as he_host_alloc).
+ * he_step_signal(env, flag) arms the handle's NEXT he_step (one-shot; NULL cancels): `flag` is the
+ * DEVICE address of a 4-byte word of he_host_alloc'd memory.  The armed he_step's kernel stores the
+ * step's sequence number (he_signal_seq: 1, 2, ... per handle) into the word after every output of
+ * the step, with system-scope release ordering, so once the CPU reads that number the step's
+ * host-mapped outputs are in place.  he_signal_wait(env, flag_host, stream) waits for the last
+ * signalled step by reading the word through its HOST address: a short spin, then (a step queued behind
+ * long work) hipStreamSynchronize(stream) and a final check (HE_ESTATE if the flag still differs).
+ * It replaces he_stream_wait when that step is the last work on the stream the caller waits for;
+ * he_step with VecNormalize attached refuses the signal (HE_EINVAL).  The kernel's end is still
+ * reported to the runtime as usual, so later stream-ordered work and events are unaffected. */
+he_status he_step_signal(he_env* env, uint32_t* flag);
+uint32_t he_signal_seq(const he_env* env);
+he_status he_signal_wait(he_env* env, const uint32_t* flag_host, void* stream);
+
 /* Introspection. */
 int64_t he_num_envs(const he_env* env);
 int32_t he_episode_length(const he_env* env);

@@ -102,3 +102,53 @@ def test_single_env_step_matches_vector_env_and_holds_no_aliases():
     assert term
     env.close()
     ref.close()
+
+
+@pytest.mark.parametrize("n", [2, 3000])
+def test_step_signal_raises_each_armed_step_once(n):
+    """he_step_signal / he_signal_wait (the host_io step's completion): the armed step's kernel
+    stores its sequence number after its outputs -- with 12 workgroups (n = 3000) only the last one
+    to finish, its counter re-armed for the next step; an unarmed step leaves the word alone; the
+    signal refuses a step with VecNormalize attached."""
+    import ctypes
+    from cantorrl_amd import _lib
+    a, b = _pair(n)
+    z = a._hio
+    lib, h = a.lib, a._h
+    flag = np.frombuffer((ctypes.c_uint32 * 1).from_address(z.h_flag), np.uint32)
+    st = torch.cuda.current_stream().cuda_stream
+    a.reset()
+    b.reset_tensors()
+    assert lib.he_signal_wait(h, z.h_flag, st) == _lib.HE_ESTATE   # nothing signalled yet
+    assert lib.he_step_signal(h, z.d_flag + 1) == _lib.HE_EINVAL   # misaligned
+    rng = np.random.default_rng(3)
+    for s in range(1, 41):
+        act = rng.uniform(-1, 1, size=(n, 2)).astype(np.float32)
+        obs, rew, done, _ = a.step(act)
+        o2, r2, t2, _ = b.step_tensors(torch.from_numpy(act).to(DEV))
+        assert lib.he_signal_seq(h) == s and int(flag[0]) == s
+        assert np.array_equal(obs, o2.cpu().numpy()) and np.array_equal(rew, r2.cpu().numpy())
+        assert np.array_equal(done, t2.cpu().numpy().astype(bool))
+    # one-shot: a step nobody armed does not touch the word
+    np.copyto(z.act, 0.0)
+    assert lib.he_step(h, *z.step_args, st) == _lib.HE_OK
+    torch.cuda.synchronize()
+    assert int(flag[0]) == 40 and lib.he_signal_seq(h) == 40
+    # armed again: the counter of the 12-workgroup grid was left at 0 by the last signalled step
+    assert lib.he_step_signal(h, z.d_flag) == _lib.HE_OK
+    assert lib.he_step(h, *z.step_args, st) == _lib.HE_OK
+    assert lib.he_signal_wait(h, z.h_flag, st) == _lib.HE_OK and int(flag[0]) == 41
+    # with VecNormalize armed the signal is refused (the launch would not end with the step)
+    p = _lib.HeVecnormParams(obs_dim=13, training=1, norm_obs=1, norm_reward=1, gamma=0.99,
+                             clip_obs=10.0, clip_reward=10.0, epsilon=1e-8)
+    ret = torch.zeros(n, dtype=torch.float64, device=DEV)
+    stats = torch.zeros(int(lib.he_vecnorm_stats_len(13)), dtype=torch.float64, device=DEV)
+    scr = torch.zeros(int(lib.he_vecnorm_scratch_bytes(n, 13)), dtype=torch.uint8, device=DEV)
+    assert lib.he_vecnorm_attach(h, ctypes.byref(p), ret.data_ptr(), stats.data_ptr(), scr.data_ptr()) == _lib.HE_OK
+    assert lib.he_step_signal(h, z.d_flag) == _lib.HE_OK
+    assert lib.he_step(h, *z.step_args, st) == _lib.HE_EINVAL
+    assert b"VecNormalize" in lib.he_last_error(h)
+    torch.cuda.synchronize()
+    assert int(flag[0]) == 41
+    a.close()
+    b.close()

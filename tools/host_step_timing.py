@@ -45,6 +45,12 @@ def main():
         lib.he_stream_wait(st)
     out["he_step+he_stream_wait"] = med(raw)
 
+    def raw_sig():   # the kernel raises the block's flag word (he_step_signal), the host reads it
+        lib.he_step_signal(v._h, z.d_flag)
+        lib.he_step(v._h, *z.step_args, st)
+        lib.he_signal_wait(v._h, z.h_flag, st)
+    out["he_step_signal+he_step+he_signal_wait"] = med(raw_sig)
+
     def launch_only():
         lib.he_step(v._h, *z.step_args, st)
     out["he_step launch only (no wait)"] = med(launch_only, 2000, 100)
