@@ -1,0 +1,48 @@
+"""Device time of he_rollout_policy (the baseline policies fused into the rollout, baselines.py:74-103,
+delta_and_nothing.py:122-163) at the headline's env count, against he_rollout with stored actions.
+
+    python tools/policy_time.py [n_envs] [K] [launches]
+"""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402
+from cantorrl_amd.vec_env import HedgingVecEnv  # noqa: E402
+
+
+def timed(fn, launches):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(launches):
+        fn()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / launches * 1e3
+
+
+def main():
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
+    K = int(sys.argv[2]) if len(sys.argv) > 2 else 256
+    L = int(sys.argv[3]) if len(sys.argv) > 3 else 20
+    env = HedgingVecEnv(n, mode="gbm", generate=bench.GEN, seed=42, return_numpy=False, info_keys=(), **bench.TRAIN_KW)
+    env.reset_tensors()
+    acts = torch.rand((K, n, 2), device="cuda") * 2 - 1
+    obs = torch.empty((K, n, 13), device="cuda")
+    rew = torch.empty((K, n), device="cuda")
+    term = torch.empty((K, n), dtype=torch.uint8, device="cuda")
+    us = timed(lambda: env.rollout(acts, obs, rew, term), L)
+    print(f"he_rollout (stored actions)       {us:9.1f} us per launch  {n * K / us * 1e6:.3e} env-steps/s", flush=True)
+    for pol in ("no_hedge", "delta_every_step", "delta_threshold"):
+        us = timed(lambda: env.rollout_policy(K, pol, obs=obs, reward=rew, terminated=term), L)
+        print(f"he_rollout_policy {pol:16s} {us:9.1f} us per launch  {n * K / us * 1e6:.3e} env-steps/s", flush=True)
+    env.close()
+
+
+if __name__ == "__main__":
+    main()
