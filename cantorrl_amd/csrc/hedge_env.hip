@@ -2215,9 +2215,16 @@ __device__ __forceinline__ void flush_obs_full(const float* img, float* out, int
 // different outstanding memory ops.  (A copy of a pending load's register at a merge,
 // e.g. the action ring at a loop back-edge behind a `break`, costs an s_waitcnt
 // vmcnt(0): every store of the wave drained.)  A partial last block takes a generic loop.
-template <int MODE, bool BOOK, bool LEAN, bool OBS>
+// POL (he_rollout_policy, lean configurations): the baseline policy is evaluated by BOTH steppers
+// from the obs row each has in hand -- the same function of the same operands, so the same action
+// bits -- the obs stepper from the row it just made, the reward stepper from the positions it
+// tracks and the obs greeks it re-evaluates from the slot's market; no action crosses the waves,
+// and the LDS block pipeline is the stored-action rollout's.  The reward stepper keeps the
+// evaluation loops' episode sums and records (step_body's POL), the obs stepper stores the actions.
+template <int MODE, bool BOOK, bool LEAN, bool OBS, bool POL = false>
 __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& io, int k_steps, const Market& cur,
                                             LdsMarketT<MODE, BOOK, LEAN>& L, int64_t base) {
+    static_assert(!POL || LEAN, "policy rollouts on the lean steppers only (lds_policy_eligible)");
     constexpr int D = kLdsPrefetch;
     constexpr bool HESTON = MODE == HE_MODE_HESTON;
     const int lane = threadIdx.x & 63;
@@ -2296,8 +2303,40 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
         slen = term ? 0u : n;
     };
     float2 ra[D];
+    if constexpr (!POL) {
 #pragma unroll
-    for (int d = 0; d < D; ++d) ra[d] = ld2(gact, (int64_t)(d < k_steps ? d : k_steps - 1) * N + i);
+        for (int d = 0; d < D; ++d) ra[d] = ld2(gact, (int64_t)(d < k_steps ? d : k_steps - 1) * N + i);
+    } else {
+#pragma unroll
+        for (int d = 0; d < D; ++d) ra[d] = make_float2(0.0f, 0.0f);
+    }
+    // POL: the obs columns the policies read (3, 4, 7, 9) of the env's current obs row, as
+    // step_body makes them at a launch start, and the episode sums of the evaluation loops
+    const int pol = POL ? io.pol.policy : HE_POLICY_NO_HEDGE;
+    const bool pol_greeks = POL && pol != HE_POLICY_NO_HEDGE;   // wave-uniform
+    float po3 = 0.0f, po4 = 0.0f, pcd = 0.0f, ppd = 0.0f;
+    double acc[7] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+    uint32_t acc_len = 0;
+    if constexpr (POL) {
+        po3 = div_int_byf((float)e.call, p.maxh_f, p.inv_maxh_f);   // lean: max_contracts_held > 0
+        po4 = div_int_byf((float)e.put, p.maxh_f, p.inv_maxh_f);
+        if (e.t == 0) {
+            pcd = p.rstv[4 + 7];
+            ppd = p.rstv[4 + 9];
+        } else if (pol_greeks) {
+            const float S0f = (float)cur.S[i];
+            float4 g0;
+            if constexpr (HESTON) g0 = greeks_fast<false>(p, S0f, (float)cur.v[i]);
+            else g0 = greeks_lean(S0f, p.g_num_drift, p.g_inv_sst_f, p.g_sst_f);
+            pcd = g0.x;
+            ppd = g0.z;
+        }
+        if (!OBS) {
+#pragma unroll
+            for (int c = 0; c < 7; ++c) acc[c] = s.acc[(int64_t)c * N + i];
+            acc_len = s.acc_len[i];
+        }
+    }
 
     // ---- the block loop over a step function step(buf, sl, k, action, in_full_block)
     constexpr int NB = LdsMarketT<MODE, BOOK, LEAN>::NB;
@@ -2313,8 +2352,10 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
             for (int sl = 0; sl < kLdsM; ++sl) {
                 const int k = b * kLdsM + sl;
                 const float2 ak = ra[sl % D];
-                const int kn = k + D;
-                ra[sl % D] = ld2(gact, (int64_t)(kn < k_steps ? kn : k_steps - 1) * N + i);
+                if constexpr (!POL) {
+                    const int kn = k + D;
+                    ra[sl % D] = ld2(gact, (int64_t)(kn < k_steps ? kn : k_steps - 1) * N + i);
+                }
                 step(buf, sl, k, ak, std::true_type{});
             }
             LDS_BAR();  // buffer b % NB handed back, block b + 1 produced
@@ -2324,7 +2365,7 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
             const int buf = nfull % NB;
             for (int sl = 0; sl < tail; ++sl) {
                 const int k = nfull * kLdsM + sl;
-                step(buf, sl, k, ld2(gact, (int64_t)k * N + i), std::false_type{});
+                step(buf, sl, k, POL ? make_float2(0.0f, 0.0f) : ld2(gact, (int64_t)k * N + i), std::false_type{});
             }
 #endif
             LDS_BAR();
@@ -2361,6 +2402,13 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
                 float4 g;
                 if constexpr (HESTON) g = greeks_fast<false>(p, r0.x, vk);
                 else g = greeks_lean(r0.x, gnd, gis, gsf);
+                if constexpr (POL) {   // the policy on the obs row this env stands at (step_body's POL)
+                    ak = policy_action(p, pol, e.call, e.put, po3, po4, pcd, ppd);
+                    if (io.pol.act_out) {
+                        v2f av = {ak.x, ak.y};
+                        ((GLOBAL v2f*)io.pol.act_out)[(int64_t)k * N + i] = av;
+                    }
+                }
                 // (i)-(ii) of step_env: the integer trade logic (:181-200)
                 const int32_t nc = e.call + trade_round(ak.x * mt_f, mt);
                 const int32_t nq = e.put + trade_round(ak.y * mt_f, mt);
@@ -2408,9 +2456,17 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
                         for (int c = 0; c < kObs; ++c) tile[lane * kObs + c] = ro[c];
                     }
                 }
-                float* out = io.obs + (int64_t)k * N * kObs;
-                if constexpr (decltype(full)::value) flush_obs_full(tile, out, base, lane);
-                else flush_obs_wave(tile, out, base, wrows, lane);
+                if (!POL || io.obs) {   // policy rollouts may return no obs (a kernel argument: uniform)
+                    float* out = io.obs + (int64_t)k * N * kObs;
+                    if constexpr (decltype(full)::value) flush_obs_full(tile, out, base, lane);
+                    else flush_obs_wave(tile, out, base, wrows, lane);
+                }
+                if constexpr (POL) {   // the row this step returns (the reset row on a terminal step)
+                    po3 = term ? ro[3] : o[3];
+                    po4 = term ? ro[4] : o[4];
+                    pcd = term ? ro[7] : o[7];
+                    ppd = term ? ro[9] : o[9];
+                }
                 e.t = term ? 0u : t1;
                 e.call = term ? 0 : cc;
                 e.put = term ? 0 : qq;
@@ -2446,12 +2502,16 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
             // set where the episode starts (here, and by the autoreset below), not tested per step
             if (e.t == 0) pv_last = pv0;
             const double rstC100 = (double)rst.C * 100.0, rstP100 = (double)rst.P * 100.0;
+            // POL: the reset row's policy columns, and the obs greeks' constants
+            const float rs3 = p.rstv[4 + 3], rs4 = p.rstv[4 + 4], rs7 = p.rstv[4 + 7], rs9 = p.rstv[4 + 9];
+            const float gnd = p.g_num_drift, gis = p.g_inv_sst_f, gsf = p.g_sst_f;
             run_blk([&](int buf, int sl, int k, float2 ak, auto) {
                 const int64_t koff = (int64_t)k * N;
                 const float2 sc = L.sc[buf][sl][lane];
                 const float pP = L.pp[buf][sl][lane];
                 const double C100 = (double)sc.y * 100.0, P100 = (double)pP * 100.0;
                 const double pv_prev = pv_last;
+                if constexpr (POL) ak = policy_action(p, pol, e.call, e.put, po3, po4, pcd, ppd);
                 // (i)-(ii) trades (:181-200)
                 const int32_t nc = e.call + trade_round(ak.x * mt_f, mt);
                 const int32_t nq = e.put + trade_round(ak.y * mt_f, mt);
@@ -2481,9 +2541,64 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
                                        ? L.thp[LdsMarketT<MODE, BOOK, LEAN>::THP ? t1 : 0]
                                        : theta * div_int_by((double)(T - (int32_t)t1), 252.0, inv_252);
                 const double reward = (rpc - tcp) - thp;
-                grew[koff + i] = (float)reward;
-                gterm[koff + i] = term ? 1 : 0;
-                account(reward, pnl, tc, term);
+                if (!POL || grew) grew[koff + i] = (float)reward;
+                if (!POL || gterm) gterm[koff + i] = term ? 1 : 0;
+                if constexpr (POL) {
+                    // step_body's POL sums, in step order, and the record of a finished episode
+                    acc[0] = acc[0] + reward;
+                    acc[1] = acc[1] + pnl;
+                    acc[2] = acc[2] + fabs(ps);
+                    acc[3] = acc[3] + tc;
+                    acc[4] = acc[4] + rpc;
+                    acc[5] = acc[5] + tcp;
+                    acc[6] = acc[6] + ps;
+                    acc_len += 1u;
+                    if (__ballot(term) != 0ull) {   // fixed-length episodes end together: uniform
+                        if (term) {
+                            if (i0 < N) {   // not the lanes mirroring env N - 1
+                                const unsigned long long r = atomicAdd(io.pol.count, 1ull);
+                                if ((int64_t)r < io.pol.cap) {
+                                    he_episode_record rec;
+                                    rec.env_id = p.goff + i;
+                                    rec.length = (int32_t)acc_len;
+                                    rec.reserved = 0;
+                                    rec.reward_sum = acc[0];
+                                    rec.pnl_sum = acc[1];
+                                    rec.abs_pnl_sum = acc[2];
+                                    rec.cost_sum = acc[3];
+                                    rec.pnl_penalty_sum = acc[4];
+                                    rec.cost_penalty_sum = acc[5];
+                                    rec.per_share_pnl_sum = acc[6];
+                                    rec.reserved2 = 0.0;
+                                    io.pol.rec[r] = rec;
+                                }
+                            }
+                            last0 = (float)acc[0];
+                            last1 = (float)acc[1];
+                            last2 = (float)acc[3];
+                            last3 = (float)acc_len;
+#pragma unroll
+                            for (int c = 0; c < 7; ++c) acc[c] = 0.0;
+                            acc_len = 0;
+                        }
+                    }
+                    // the obs row this step returns, as the obs stepper makes it: the positions'
+                    // columns and the greeks of the slot's market (greeks_lean / greeks_fast<false>)
+                    float gx = 0.0f, gz = 0.0f;
+                    if (pol_greeks) {
+                        float4 g;
+                        if constexpr (HESTON) g = greeks_fast<false>(p, sc.x, L.vv[HESTON ? buf : 0][HESTON ? sl : 0][lane]);
+                        else g = greeks_lean(sc.x, gnd, gis, gsf);
+                        gx = g.x;
+                        gz = g.z;
+                    }
+                    po3 = term ? rs3 : div_int_byf((float)cc, maxh_f, p.inv_maxh_f);
+                    po4 = term ? rs4 : div_int_byf((float)qq, maxh_f, p.inv_maxh_f);
+                    pcd = term ? rs7 : gx;
+                    ppd = term ? rs9 : gz;
+                } else {
+                    account(reward, pnl, tc, term);
+                }
                 pv_last = term ? pv0 : pv;
                 // SB3 autoreset (selects)
                 e.t = term ? 0u : t1;
@@ -2553,10 +2668,16 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
         s.t[j] = e.t;
         s.pos[j] = pack_pos(e.call, e.put);
         s.cash[j] = e.cash;
-        s.sum[j] = sm0;
-        s.sum[N + j] = sm1;
-        s.sum[2 * N + j] = sm2;
-        s.sum_len[j] = slen;
+        if constexpr (POL) {   // step_body's POL state: the evaluation sums (s.sum untouched)
+#pragma unroll
+            for (int c = 0; c < 7; ++c) s.acc[(int64_t)c * N + j] = acc[c];
+            s.acc_len[j] = acc_len;
+        } else {
+            s.sum[j] = sm0;
+            s.sum[N + j] = sm1;
+            s.sum[2 * N + j] = sm2;
+            s.sum_len[j] = slen;
+        }
         s.last[j] = last0;
         s.last[N + j] = last1;
         s.last[2 * N + j] = last2;
@@ -2986,7 +3107,7 @@ __device__ __forceinline__ int lds_role(int wave) {
 // and at 106 the 4 x 6 waves of 4 workgroups no longer fit a CU -- at 65,536 envs the
 // launch ran in two rounds of workgroups (536 vs ~270 us).  The spills go to VGPR lanes.
 constexpr int kLdsNumSgpr = 96;
-template <int MODE, bool BOOK, bool LEAN, bool PERSIST = false>
+template <int MODE, bool BOOK, bool LEAN, bool PERSIST = false, bool POL = false>
 __global__ __launch_bounds__((LdsGeom<MODE, BOOK>::threads), (LdsGeom<MODE, BOOK>::minwaves))
     __attribute__((amdgpu_num_sgpr(kLdsNumSgpr))) void lds_rollout_kernel(const Params* __restrict__ pc, State s, Io io,
                                                                  int k_steps, Market cur) {
@@ -3001,8 +3122,8 @@ __global__ __launch_bounds__((LdsGeom<MODE, BOOK>::threads), (LdsGeom<MODE, BOOK
     }
     if constexpr (!PERSIST) {   // one workgroup per 64-env tile
         const int64_t base = (int64_t)blockIdx.x * kLdsEnvs;
-        if (wave == 0) lds_stepper<MODE, BOOK, LEAN, false>(p, s, io, k_steps, cur, lm, base);
-        else if (wave == 1) lds_stepper<MODE, BOOK, LEAN, true>(p, s, io, k_steps, cur, lm, base);
+        if (wave == 0) lds_stepper<MODE, BOOK, LEAN, false, POL>(p, s, io, k_steps, cur, lm, base);
+        else if (wave == 1) lds_stepper<MODE, BOOK, LEAN, true, POL>(p, s, io, k_steps, cur, lm, base);
         else lds_producer<MODE, BOOK, LEAN>(p, k_steps, cur, lm, base, wave - 2);
         return;
     }
@@ -3015,8 +3136,8 @@ __global__ __launch_bounds__((LdsGeom<MODE, BOOK>::threads), (LdsGeom<MODE, BOOK
         // (hoisted, the three roles' invariants all lived across the loop and spilled)
         asm volatile("" ::: "memory");
         const int64_t base = tile * kLdsEnvs;
-        if (wave == 0) lds_stepper<MODE, BOOK, LEAN, false>(p, s, io, k_steps, cur, lm, base);
-        else if (wave == 1) lds_stepper<MODE, BOOK, LEAN, true>(p, s, io, k_steps, cur, lm, base);
+        if (wave == 0) lds_stepper<MODE, BOOK, LEAN, false, POL>(p, s, io, k_steps, cur, lm, base);
+        else if (wave == 1) lds_stepper<MODE, BOOK, LEAN, true, POL>(p, s, io, k_steps, cur, lm, base);
         else lds_producer<MODE, BOOK, LEAN>(p, k_steps, cur, lm, base, wave - 2);
         if (tile + gridDim.x < tiles) __syncthreads();   // every role done with lm before the next tile
     }
@@ -3763,6 +3884,7 @@ struct he_env {
     int64_t lds_grid = -1;    // -1: not computed yet
     int64_t lds_grid_cap = 0; // HE_LDS_MAX_GRID
     bool lds_persist = true;
+    bool lds_policy = true;   // he_rollout_policy on lds_rollout_kernel<..., POL> (HE_LDS_POLICY=0: the tile kernels)
     int32_t prefetch_mode = 0; // 0 auto, 1 never, 2 always: market_kernel(b+1) on `xs` during block b
     hipStream_t xs = nullptr; // library side stream for market prefetch
     hipEvent_t ev_fork = nullptr, ev_next = nullptr;
@@ -4216,20 +4338,35 @@ static bool lds_rollout_eligible(const he_env* env) {
            (env->cfg.book_size == 0 || env->book_rows <= kLdsBookRows);
 }
 
+// he_rollout_policy through lds_rollout_kernel<..., POL>: the lean configurations (the policy in
+// both lean steppers), autoreset; the obs / reward / terminated buffers may be absent.
+static bool lds_policy_eligible(const he_env* env, const Io& io) {
+    Io o = io;
+    o.obs = o.obs ? o.obs : reinterpret_cast<float*>(16);   // (lds_lean_config's output test only)
+    o.rew = o.rew ? o.rew : reinterpret_cast<float*>(16);
+    o.term = o.term ? o.term : reinterpret_cast<uint8_t*>(16);
+    return env->lds_policy && env->cfg.autoreset && lds_rollout_eligible(env) && lds_lean_config(env, o);
+}
+
 static he_status launch_lds_rollout(he_env* env, const Io& io, int k_total, hipStream_t st) {
     he_status s = materialize_market(env, st);
     if (s != HE_OK) return s;
     const int64_t blocks = (env->cfg.n_envs + kLdsEnvs - 1) / kLdsEnvs;
     const Params* pc = env->dparams;  // buffer 0's copy: the tile pointers are not used
-    const bool book = env->cfg.book_size > 0, lean = lds_lean_config(env, io);
+    const bool book = env->cfg.book_size > 0, pol = io.pol_on, lean = pol || lds_lean_config(env, io);
     void (*kern)(const Params*, State, Io, int, Market);
     void (*kern_p)(const Params*, State, Io, int, Market);   // the persistent-grid instance
     int threads;
-#define HE_LDS_PICK(M, B, L)                                 \
-    do {                                                     \
-        kern = lds_rollout_kernel<M, B, L, false>;           \
-        kern_p = lds_rollout_kernel<M, B, L, !(B)>;          \
-        threads = LdsGeom<M, B>::threads;                    \
+#define HE_LDS_PICK(M, B, L)                                                  \
+    do {                                                                      \
+        if (pol) {                                                            \
+            kern = lds_rollout_kernel<M, B, true, false, true>;               \
+            kern_p = lds_rollout_kernel<M, B, true, !(B), true>;              \
+        } else {                                                              \
+            kern = lds_rollout_kernel<M, B, L, false>;                        \
+            kern_p = lds_rollout_kernel<M, B, L, !(B)>;                       \
+        }                                                                     \
+        threads = LdsGeom<M, B>::threads;                                     \
     } while (0)
     if (env->cfg.mode == HE_MODE_HESTON) {
         if (lean) {
@@ -4326,6 +4463,7 @@ static he_status launch_steps(he_env* env, Io io, bool info, int k_total, void* 
         return HE_OK;
     }
     if (rollout && !info && !io.pol_on && lds_rollout_eligible(env)) return launch_lds_rollout(env, io, k_total, st);
+    if (io.pol_on && lds_policy_eligible(env, io)) return launch_lds_rollout(env, io, k_total, st);
     const int32_t M = c.market_block;
     const int64_t N = c.n_envs;
     int done = 0;
@@ -4537,6 +4675,8 @@ he_status he_create(const he_config* cfg, he_env** out) {
             env->lds_rollout = !(el && el[0] == '0');
             const char* ep = getenv("HE_LDS_PERSIST");
             env->lds_persist = !(ep && ep[0] == '0');
+            const char* eo = getenv("HE_LDS_POLICY");
+            env->lds_policy = !(eo && eo[0] == '0');
             const char* eg = getenv("HE_LDS_MAX_GRID");
             env->lds_grid_cap = eg ? atoll(eg) : 0;
         }

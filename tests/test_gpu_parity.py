@@ -1304,3 +1304,68 @@ def test_episode_summaries_alignment_and_layout():
     st = env.lib.he_episode_summaries(env._h, buf.data_ptr() + 4, env.stream)
     assert st == _lib.HE_EINVAL and b"aligned" in env.lib.he_last_error(env._h)
     env.close()
+
+
+_POL_BOOK = [dict(type="call", strike=500.0, expiry=30, quantity=-20.0),
+             dict(type="uo_call", strike=496.0, barrier=530.0, expiry=40, quantity=-50.0)]
+
+
+@pytest.mark.parametrize("mode,book", [("gbm", None), ("heston", None), ("gbm", _POL_BOOK), ("heston", _POL_BOOK)])
+@pytest.mark.parametrize("policy", ["no_hedge", "delta_every_step", "delta_threshold"])
+def test_lds_policy_rollout_equals_tile_policy_rollout(mode, book, policy, monkeypatch):
+    """he_rollout_policy on lds_rollout_kernel<..., POL> (the policy evaluated by both lean steppers)
+    against the tile kernels' step_kernel<POL> (HE_LDS_POLICY=0), bit for bit: actions, obs, rewards,
+    done flags of every launch (ragged K, episode ends inside and across launches, a partial last
+    workgroup), the episode records (per env in finishing order), the record count, the episode
+    summaries and the whole checkpointed state; one launch without obs / reward / done buffers."""
+    from cantorrl_amd import _lib
+    from cantorrl_amd.vec_env import HedgingVecEnv
+    n = 1000
+    gen = dict(s0=496.48001098632812, variance=0.029028, mu=0.04, dt=1 / 252, episode_length=40)
+    if mode == "heston":
+        gen.update(heston_kappa=2.0, heston_theta=0.029028, heston_xi=0.3, heston_rho=-0.7)
+    if book is not None:
+        gen["book"] = book
+    kw = dict(loss_type="abs", pnl_penalty_weight=0.001, lambda_cost=0.0001, theta_weight=0.0002, slippage_bps=1.0)
+    envs = []
+    for lds in (True, False):
+        if not lds:
+            monkeypatch.setenv("HE_LDS_POLICY", "0")
+        envs.append(HedgingVecEnv(n, mode=mode, generate=gen, seed=5, return_numpy=False, info_keys=(), **kw))
+        monkeypatch.delenv("HE_LDS_POLICY", raising=False)
+    cap = 8 * n   # 230 steps of 40-step episodes: 5 or 6 records per env
+    bufs = []
+    for e in envs:
+        e.reset_tensors()
+        bufs.append((torch.zeros((cap, 80), dtype=torch.uint8, device="cuda"),
+                     torch.zeros(1, dtype=torch.int64, device="cuda")))
+    for li, K in enumerate((37, 64, 5, 100, 1, 23)):
+        outs = []
+        for e, (recs, cnt) in zip(envs, bufs):
+            if li == 4:   # no per-step outputs (evaluate_policy's call), actions only
+                a = torch.empty((K, n, 2), device="cuda")
+                e.rollout_policy(K, policy, a, records=recs, record_count=cnt)
+                outs.append((a,))
+            else:
+                a = torch.empty((K, n, 2), device="cuda")
+                o = torch.empty((K, n, 13), device="cuda")
+                r = torch.empty((K, n), device="cuda")
+                t = torch.empty((K, n), dtype=torch.uint8, device="cuda")
+                e.rollout_policy(K, policy, a, o, r, t, recs, cnt)
+                outs.append((a, o, r, t))
+        torch.cuda.synchronize()
+        for x, y in zip(*outs):
+            assert torch.equal(x, y), (li, K)
+    m = [int(c.item()) for _, c in bufs]
+    assert m[0] == m[1] and m[0] > 0
+    recs = [r[:m[0]].cpu().numpy().view(_lib.EPISODE_RECORD).reshape(m[0]) for r, _ in bufs]
+    for i in range(0, n, 37):   # per env in finishing order (the atomic index grows with time)
+        a_i, b_i = recs[0][recs[0]["env_id"] == i], recs[1][recs[1]["env_id"] == i]
+        assert a_i.tobytes() == b_i.tobytes(), i
+    assert np.array_equal(np.sort(recs[0], order=["env_id", "length"]), np.sort(recs[1], order=["env_id", "length"]))
+    s = [e.episode_summaries().cpu().numpy() for e in envs]
+    assert np.array_equal(s[0], s[1])
+    st = [e.get_state() for e in envs]
+    assert np.array_equal(st[0], st[1])
+    for e in envs:
+        e.close()
