@@ -3328,7 +3328,9 @@ __device__ __forceinline__ uint32_t fresh_lane() {
 // OBS = false: the reward wave (owns the env state); OBS = true: the obs wave.  FAST: the
 // configuration of fast_replay_config (v2, loss != mse, shares_to_hedge != 0, record_metrics,
 // max_contracts_held > 0) with its uniform branches compiled out.
-template <bool OBS, bool FAST>
+// POL (he_rollout_policy in replay mode): the baseline policy evaluated by both steppers, as
+// lds_stepper's POL -- here both read the rows' obs greeks from the loaders' LDS records.
+template <bool OBS, bool FAST, bool POL = false>
 __device__ __forceinline__ void lds_replay_stepper(const Params& p, State s, const Io& io, int k_steps,
                                                    LdsReplay& L, int64_t base) {
     constexpr int D = kLdsPrefetch;  // steps of actions in flight (8: +-0, r03s18)
@@ -3380,7 +3382,27 @@ __device__ __forceinline__ void lds_replay_stepper(const Params& p, State s, con
     }
     float2 ra[D];
 #pragma unroll
-    for (int d = 0; d < D; ++d) ra[d] = ld2(gact, (int64_t)(d < k_steps ? d : k_steps - 1) * N + i);
+    for (int d = 0; d < D; ++d)
+        ra[d] = POL ? make_float2(0.0f, 0.0f) : ld2(gact, (int64_t)(d < k_steps ? d : k_steps - 1) * N + i);
+    // POL: the policy columns (3, 4, 7, 9) of the env's current obs row (step_body's replay
+    // prologue: the greeks of the row it stands at), and the evaluation loops' episode sums
+    const int pol = POL ? io.pol.policy : HE_POLICY_NO_HEDGE;
+    const bool pmh = FAST || p.maxh != 0, prm = FAST || p.record_metrics;
+    float po3 = 0.0f, po4 = 0.0f, pcd = 0.0f, ppd = 0.0f;
+    double acc[7] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+    uint32_t acc_len = 0;
+    if constexpr (POL) {
+        po3 = pmh ? div_int_byf((float)e.call, p.maxh_f, p.inv_maxh_f) : 0.0f;
+        po4 = pmh ? div_int_byf((float)e.put, p.maxh_f, p.inv_maxh_f) : 0.0f;
+        const float4 g0 = ld4((const GLOBAL v4f*)p.recg, rrow(p, s.path[i], tt));
+        pcd = prm ? g0.x : 0.0f;
+        ppd = prm ? g0.z : 0.0f;
+        if (!OBS) {
+#pragma unroll
+            for (int c = 0; c < 7; ++c) acc[c] = s.acc[(int64_t)c * N + i];
+            acc_len = s.acc_len[i];
+        }
+    }
     // FAST: the per-handle constants of the step held in VGPRs (opaque).  Left to step_env's
     // Params reads, the SGPR-capped kernel re-loads them from the scalar cache inside every
     // step, and each such load's lgkmcnt(0) wait also drains the step's LDS reads.
@@ -3433,7 +3455,12 @@ __device__ __forceinline__ void lds_replay_stepper(const Params& p, State s, con
         const int64_t koff = (int64_t)k * N;
         Mkt post = as_mkt(L.mk[buf][sl][lane]);
         post.B = 0.0;
+        if constexpr (POL) ak = policy_action(p, pol, e.call, e.put, po3, po4, pcd, ppd);
         if (OBS) {
+            if (POL && io.pol.act_out) {
+                v2f av = {ak.x, ak.y};
+                ((GLOBAL v2f*)io.pol.act_out)[koff + i] = av;
+            }
             const float2 gd = L.gd[buf][sl][lane];
             const float4 g = make_float4(gd.x, L.gg[buf][sl][lane], gd.y, lag_return(post.S, pre.S));
             // (i)-(ii) of step_env: the integer trade logic (:181-200)
@@ -3466,12 +3493,20 @@ __device__ __forceinline__ void lds_replay_stepper(const Params& p, State s, con
             }
             pre = post;
             new_episode_obs(buf, term, o);  // SB3 autoreset: the reset obs
+            if constexpr (POL) {   // the row this step returns
+                po3 = o[3];
+                po4 = o[4];
+                pcd = o[7];
+                ppd = o[9];
+            }
             float* const tile = L.stage[k & 1];
 #pragma unroll
             for (int c = 0; c < kObs; ++c) tile[lane * kObs + c] = o[c];
-            float* out = io.obs + koff * kObs;
-            if constexpr (decltype(full)::value) flush_obs_full(tile, out, base, lane);
-            else flush_obs_wave(tile, out, base, wrows, lane);
+            if (!POL || io.obs) {
+                float* out = io.obs + koff * kObs;
+                if constexpr (decltype(full)::value) flush_obs_full(tile, out, base, lane);
+                else flush_obs_wave(tile, out, base, wrows, lane);
+            }
         } else {
             StepOut so;
             if (FAST) {  // step_env<false, true, true> on the pinned constants (hedging_env_v2.py:175-262)
@@ -3507,26 +3542,80 @@ __device__ __forceinline__ void lds_replay_stepper(const Params& p, State s, con
                 const double tcp = c_lam * so.tc;
                 const double thp = c_theta * div_int_by((double)(T - (int32_t)e.t), 252.0, c_inv_252);
                 so.reward = (rpc - tcp) - thp;
+                so.ps = ps;   // (POL's sums; dead otherwise)
+                so.rpc = rpc;
+                so.tcp = tcp;
             } else {
                 step_env<false, FAST, true>(p, e, pre, post, ak.x, ak.y, pv_last, so);
             }
             pv_last = so.pv;
 #if !(defined(HE_REPLAY_DIAG) && HE_REPLAY_DIAG == 3)  // diagnostic build: no reward / done stores
-            grew[koff + i] = (float)so.reward;
-            gterm[koff + i] = so.term ? 1 : 0;
+            if (!POL || grew) grew[koff + i] = (float)so.reward;
+            if (!POL || gterm) gterm[koff + i] = so.term ? 1 : 0;
 #endif
+            if constexpr (POL) {
+                // step_body's POL sums, in step order, and the record of a finished episode
+                acc[0] = acc[0] + so.reward;
+                acc[1] = acc[1] + so.pnl;
+                acc[2] = acc[2] + fabs(so.ps);
+                acc[3] = acc[3] + so.tc;
+                acc[4] = acc[4] + so.rpc;
+                acc[5] = acc[5] + so.tcp;
+                acc[6] = acc[6] + so.ps;
+                acc_len += 1u;
+                if (__ballot(so.term) != 0ull) {
+                    if (so.term) {
+                        if (i0 < N) {   // not the lanes mirroring env N - 1
+                            const unsigned long long r = atomicAdd(io.pol.count, 1ull);
+                            if ((int64_t)r < io.pol.cap) {
+                                he_episode_record rec;
+                                rec.env_id = p.goff + i;
+                                rec.length = (int32_t)acc_len;
+                                rec.reserved = 0;
+                                rec.reward_sum = acc[0];
+                                rec.pnl_sum = acc[1];
+                                rec.abs_pnl_sum = acc[2];
+                                rec.cost_sum = acc[3];
+                                rec.pnl_penalty_sum = acc[4];
+                                rec.cost_penalty_sum = acc[5];
+                                rec.per_share_pnl_sum = acc[6];
+                                rec.reserved2 = 0.0;
+                                io.pol.rec[r] = rec;
+                            }
+                        }
+                        last0 = (float)acc[0];
+                        last1 = (float)acc[1];
+                        last2 = (float)acc[3];
+                        last3 = (float)acc_len;
+#pragma unroll
+                        for (int c = 0; c < 7; ++c) acc[c] = 0.0;
+                        acc_len = 0;
+                    }
+                }
+                // the policy columns of the row this step returns, as the obs stepper makes them:
+                // the post-trade positions and the slot's greeks, or the new episode's row 0
+                const float2 gd = L.gd[buf][sl][lane];
+                const float4 rg = L.rg[buf][lane];
+                const bool tm = so.term;
+                po3 = pmh ? div_int_byf((float)(tm ? 0 : e.call), p.maxh_f, p.inv_maxh_f) : 0.0f;
+                po4 = pmh ? div_int_byf((float)(tm ? 0 : e.put), p.maxh_f, p.inv_maxh_f) : 0.0f;
+                pcd = prm ? (tm ? rg.x : gd.x) : 0.0f;
+                ppd = prm ? (tm ? rg.z : gd.y) : 0.0f;
+            }
             const double a0 = sm0 + so.reward, a1 = sm1 + so.pnl, a2 = sm2 + so.tc;
             const uint32_t n1 = slen + 1u;
             float f0 = (float)a0, f1 = (float)a1, f2 = (float)a2, f3 = (float)n1;
             asm volatile("" : "+v"(f0), "+v"(f1), "+v"(f2), "+v"(f3));
-            last0 = so.term ? f0 : last0;
-            last1 = so.term ? f1 : last1;
-            last2 = so.term ? f2 : last2;
-            last3 = so.term ? f3 : last3;
-            sm0 = so.term ? 0.0 : a0;
-            sm1 = so.term ? 0.0 : a1;
-            sm2 = so.term ? 0.0 : a2;
-            slen = so.term ? 0u : n1;
+            if constexpr (!POL) {
+                last0 = so.term ? f0 : last0;
+                last1 = so.term ? f1 : last1;
+                last2 = so.term ? f2 : last2;
+                last3 = so.term ? f3 : last3;
+                sm0 = so.term ? 0.0 : a0;
+                sm1 = so.term ? 0.0 : a1;
+                sm2 = so.term ? 0.0 : a2;
+                slen = so.term ? 0u : n1;
+            }
             // SB3 autoreset, branch-free (the block's steps stay one basic block): the new
             // episode's row 0 is read every step, its denominator and the reset state selected
             const float4 r0 = L.rk[buf][lane];
@@ -3559,8 +3648,10 @@ __device__ __forceinline__ void lds_replay_stepper(const Params& p, State s, con
                 const float2 ak = make_float2(0.3f * (float)(sl - 4), -0.2f);
 #else
                 const float2 ak = ra[sl % D];
-                const int kn = k + D;
-                ra[sl % D] = ld2(gact, (int64_t)(kn < k_steps ? kn : k_steps - 1) * N + i);
+                if constexpr (!POL) {
+                    const int kn = k + D;
+                    ra[sl % D] = ld2(gact, (int64_t)(kn < k_steps ? kn : k_steps - 1) * N + i);
+                }
 #endif
                 step(buf, sl, k, ak, full);
             }
@@ -3574,7 +3665,7 @@ __device__ __forceinline__ void lds_replay_stepper(const Params& p, State s, con
             const int64_t it = ia < N ? ia : N - 1;
             for (int sl = 0; sl < tail; ++sl) {
                 const int k = nfull * kLdsM + sl;
-                step(buf, sl, k, ld2(gact, (int64_t)k * N + it), std::false_type{});
+                step(buf, sl, k, POL ? make_float2(0.0f, 0.0f) : ld2(gact, (int64_t)k * N + it), std::false_type{});
             }
             LDS_BAR();
         }
@@ -3590,10 +3681,16 @@ __device__ __forceinline__ void lds_replay_stepper(const Params& p, State s, con
         s.t[j] = e.t;
         s.pos[j] = pack_pos(e.call, e.put);
         s.cash[j] = e.cash;
-        s.sum[j] = sm0;
-        s.sum[N + j] = sm1;
-        s.sum[2 * N + j] = sm2;
-        s.sum_len[j] = slen;
+        if constexpr (POL) {   // step_body's POL state: the evaluation sums (s.sum untouched)
+#pragma unroll
+            for (int c = 0; c < 7; ++c) s.acc[(int64_t)c * N + j] = acc[c];
+            s.acc_len[j] = acc_len;
+        } else {
+            s.sum[j] = sm0;
+            s.sum[N + j] = sm1;
+            s.sum[2 * N + j] = sm2;
+            s.sum_len[j] = slen;
+        }
         s.last[j] = last0;
         s.last[N + j] = last1;
         s.last[2 * N + j] = last2;
@@ -3601,15 +3698,15 @@ __device__ __forceinline__ void lds_replay_stepper(const Params& p, State s, con
     }
 }
 
-template <bool FAST>
+template <bool FAST, bool POL = false>
 __global__ __launch_bounds__(256, 4) __attribute__((amdgpu_num_sgpr(kLdsNumSgpr))) void lds_replay_kernel(
     const Params* __restrict__ pc, State s, Io io, int k_steps) {
     __shared__ __attribute__((aligned(16))) LdsReplay lm;
     const Params& p = *pc;
     const int wave = lds_role<4>(__builtin_amdgcn_readfirstlane(threadIdx.x >> 6));
     const int64_t base = (int64_t)blockIdx.x * kLdsEnvs;
-    if (wave == 0) lds_replay_stepper<false, FAST>(p, s, io, k_steps, lm, base);
-    else if (wave == 1) lds_replay_stepper<true, FAST>(p, s, io, k_steps, lm, base);
+    if (wave == 0) lds_replay_stepper<false, FAST, POL>(p, s, io, k_steps, lm, base);
+    else if (wave == 1) lds_replay_stepper<true, FAST, POL>(p, s, io, k_steps, lm, base);
     else lds_replay_loader(p, s, k_steps, lm, base, wave - 2);
 }
 
@@ -4433,11 +4530,24 @@ static bool fast_replay_config(const he_env* env) {
            fabs(env->p.shares_d) >= 0x1p-100 && fabs(env->p.shares_d) <= 0x1p100;
 }
 
+// he_rollout_policy in replay mode through lds_replay_kernel<..., POL> (the obs / reward /
+// terminated buffers may be absent)
+static bool lds_replay_policy_eligible(const he_env* env, const Io& io) {
+    Io o = io;
+    o.obs = o.obs ? o.obs : reinterpret_cast<float*>(16);   // (lds_replay_eligible's output test only)
+    o.rew = o.rew ? o.rew : reinterpret_cast<float*>(16);
+    o.term = o.term ? o.term : reinterpret_cast<uint8_t*>(16);
+    return env->lds_policy && lds_replay_eligible(env, o);
+}
+
 static he_status launch_lds_replay(he_env* env, const Io& io, int k_total, hipStream_t st) {
     const int64_t blocks = (env->cfg.n_envs + kLdsEnvs - 1) / kLdsEnvs;
     const Params* pc = env->dparams;
-    void (*kern)(const Params*, State, Io, int) = fast_replay_config(env) ? lds_replay_kernel<true>
-                                                                          : lds_replay_kernel<false>;
+    // policy rollouts on the generic steppers in every configuration (the FAST instance with the
+    // policy's sums spilled 25 VGPRs)
+    const bool fast = fast_replay_config(env);
+    void (*kern)(const Params*, State, Io, int) =
+        io.pol_on ? lds_replay_kernel<false, true> : (fast ? lds_replay_kernel<true> : lds_replay_kernel<false>);
     if (env->ev_start) {  // one-shot: bracket exactly this dispatch
         hipEvent_t a = (hipEvent_t)env->ev_start, b = (hipEvent_t)env->ev_stop;
         env->ev_start = env->ev_stop = nullptr;
@@ -4458,6 +4568,7 @@ static he_status launch_steps(he_env* env, Io io, bool info, int k_total, void* 
     io.sums = rollout && !io.pol_on;
     if (c.mode == HE_MODE_REPLAY) {
         if (rollout && !info && !io.pol_on && lds_replay_eligible(env, io)) return launch_lds_replay(env, io, k_total, st);
+        if (io.pol_on && lds_replay_policy_eligible(env, io)) return launch_lds_replay(env, io, k_total, st);
         launch_step<HE_MODE_REPLAY, false, false>(env, env->p, io, info, k_total, 0, st);
         HE_HIP(env, hipGetLastError());
         return HE_OK;
@@ -4659,6 +4770,13 @@ he_status he_create(const he_config* cfg, he_env** out) {
         off += (f.bytes + 255) & ~(size_t)255;
     }
     HE_HIP(env, hipMemset(mem, 0, total));
+    {   // every mode: the LDS rollout kernels (HE_LDS_ROLLOUT=0) and policy rollouts on them
+        // (HE_LDS_POLICY=0) can be switched off for A/B and parity runs against the tile kernels
+        const char* el = getenv("HE_LDS_ROLLOUT");
+        env->lds_rollout = !(el && el[0] == '0');
+        const char* eo = getenv("HE_LDS_POLICY");
+        env->lds_policy = !(eo && eo[0] == '0');
+    }
     if (is_generate(env)) {
         // 2 buffers x ({S,v,C,P} | {greeks, lag}) float4 slots (+ 2 x f64 book slots)
         size_t tb = (size_t)4 * (size_t)(c.market_block + 1) * (size_t)N * sizeof(float4);
@@ -4671,12 +4789,8 @@ he_status he_create(const he_config* cfg, he_env** out) {
         {
             const char* ev = getenv("HE_FUSED_MARKET");
             env->fuse_market = !(ev && ev[0] == '0');
-            const char* el = getenv("HE_LDS_ROLLOUT");
-            env->lds_rollout = !(el && el[0] == '0');
             const char* ep = getenv("HE_LDS_PERSIST");
             env->lds_persist = !(ep && ep[0] == '0');
-            const char* eo = getenv("HE_LDS_POLICY");
-            env->lds_policy = !(eo && eo[0] == '0');
             const char* eg = getenv("HE_LDS_MAX_GRID");
             env->lds_grid_cap = eg ? atoll(eg) : 0;
         }

@@ -1355,7 +1355,7 @@ def test_lds_policy_rollout_equals_tile_policy_rollout(mode, book, policy, monke
                 outs.append((a, o, r, t))
         torch.cuda.synchronize()
         for x, y in zip(*outs):
-            assert torch.equal(x, y), (li, K)
+            assert torch.equal(_bits(x), _bits(y)), (li, K)
     m = [int(c.item()) for _, c in bufs]
     assert m[0] == m[1] and m[0] > 0
     recs = [r[:m[0]].cpu().numpy().view(_lib.EPISODE_RECORD).reshape(m[0]) for r, _ in bufs]
@@ -1365,6 +1365,64 @@ def test_lds_policy_rollout_equals_tile_policy_rollout(mode, book, policy, monke
     assert np.array_equal(np.sort(recs[0], order=["env_id", "length"]), np.sort(recs[1], order=["env_id", "length"]))
     s = [e.episode_summaries().cpu().numpy() for e in envs]
     assert np.array_equal(s[0], s[1])
+    st = [e.get_state() for e in envs]
+    assert np.array_equal(st[0], st[1])
+    for e in envs:
+        e.close()
+
+
+def _bits(t):
+    """Bit pattern of a float / byte tensor (NaN-aware bitwise equality)."""
+    return t.view(torch.int32) if t.dtype == torch.float32 else t
+
+
+@pytest.mark.parametrize("case", ["train", "T8_edges", "mse_nometrics_cash", "v1_edges"])
+@pytest.mark.parametrize("policy", ["no_hedge", "delta_every_step", "delta_threshold"])
+def test_lds_replay_policy_rollout_equals_tile_policy_rollout(case, policy, monkeypatch):
+    """he_rollout_policy in replay mode on lds_replay_kernel<false, POL> against the tile kernels
+    (HE_LDS_POLICY=0), bit for bit, over the edge tables (S0 < 25, S0 = 0, tiny prices, NaN marks,
+    v <= 0, S0 = inf): actions, obs, rewards, done flags of every launch (one without per-step
+    outputs), the episode records per env, the summaries and the checkpointed state."""
+    from cantorrl_amd import _lib
+    from cantorrl_amd.vec_env import HedgingVecEnv
+    n, paths, T, variant, kw, ks = REPLAY_LDS_CASES[case]
+    tables = _edge_tables(paths, T + 1)
+    envs = []
+    for lds in (True, False):
+        if not lds:
+            monkeypatch.setenv("HE_LDS_POLICY", "0")
+        envs.append(HedgingVecEnv(n, tables=tables, variant=variant, seed=77, return_numpy=False, info_keys=(), **kw))
+        monkeypatch.delenv("HE_LDS_POLICY", raising=False)
+    total = sum(ks)
+    cap = n * (total // T + 2)
+    bufs = []
+    for e in envs:
+        e.reset_tensors()
+        bufs.append((torch.zeros((cap, 80), dtype=torch.uint8, device="cuda"),
+                     torch.zeros(1, dtype=torch.int64, device="cuda")))
+    for li, K in enumerate(ks):
+        outs = []
+        for e, (recs, cnt) in zip(envs, bufs):
+            a = torch.empty((K, n, 2), device="cuda")
+            if li == 1:   # no per-step outputs (evaluate_policy's call)
+                e.rollout_policy(K, policy, a, records=recs, record_count=cnt)
+                outs.append((a,))
+            else:
+                o = torch.empty((K, n, 13), device="cuda")
+                r = torch.empty((K, n), device="cuda")
+                t = torch.empty((K, n), dtype=torch.uint8, device="cuda")
+                e.rollout_policy(K, policy, a, o, r, t, recs, cnt)
+                outs.append((a, o, r, t))
+        torch.cuda.synchronize()
+        for x, y in zip(*outs):
+            assert torch.equal(_bits(x), _bits(y)), (case, li, K)
+    m = [int(c.item()) for _, c in bufs]
+    assert m[0] == m[1] and 0 < m[0] <= cap
+    recs = [r[:m[0]].cpu().numpy().view(_lib.EPISODE_RECORD).reshape(m[0]) for r, _ in bufs]
+    for i in range(n):   # per env in finishing order
+        assert recs[0][recs[0]["env_id"] == i].tobytes() == recs[1][recs[1]["env_id"] == i].tobytes(), (case, i)
+    s = [e.episode_summaries().cpu().numpy() for e in envs]
+    assert s[0].tobytes() == s[1].tobytes()
     st = [e.get_state() for e in envs]
     assert np.array_equal(st[0], st[1])
     for e in envs:

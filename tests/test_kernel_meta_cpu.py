@@ -35,14 +35,15 @@ def _meta():
 def test_lds_kernels_spill_free():
     meta = _meta()
     rollout = {k: v for k, v in meta.items() if "lds_rollout_kernel" in k}
-    # GBM / Heston x book x lean instances, + the persistent-grid instances without a book
-    assert len(rollout) == 12, sorted(rollout)
+    # GBM / Heston x book x lean instances, + the persistent-grid instances without a book, + the
+    # policy rollouts' lean instances (POL: 4 one-workgroup-per-tile, 2 persistent)
+    assert len(rollout) == 18, sorted(rollout)
     for k, v in rollout.items():
         assert v["vgpr_spill"] == 0 and v["scratch_B"] == 0, (k, v)
         assert v["vgpr"] <= 128, (k, v)         # 4 waves per SIMD
         assert v["lds_B"] <= 40 * 1024, (k, v)  # 4 workgroups per CU
     replay = {k: v for k, v in meta.items() if "lds_replay_kernel" in k}
-    assert len(replay) == 2
+    assert len(replay) == 3   # <FAST>, <generic>, <generic, POL>
     for k, v in replay.items():
         # the FAST instance (config 6's) spilled 2 VGPRs / 12 B until round 5
         assert v["vgpr_spill"] == 0 and v["scratch_B"] == 0, (k, v)
@@ -55,7 +56,7 @@ def test_headline_kernel_sgprs_fit():
     6 at up to 112 SGPRs.  (kLdsNumSgpr's 96 dates from 6-wave workgroups, which 106 SGPRs left
     room for 3 of; round 5's kernel reports 106 and runs 4 per CU: r05s17_ab_thp_table.txt.)"""
     meta = _meta()
-    k = [k for k in meta if "lds_rollout_kernelILi1ELb0ELb1ELb0E" in k]   # one workgroup per tile
+    k = [k for k in meta if "lds_rollout_kernelILi1ELb0ELb1ELb0ELb0E" in k]   # one workgroup per tile, no policy
     assert len(k) == 1
     sg = meta[k[0]]["sgpr"]
     assert 800 // (-(-sg // 16) * 16 + 16) >= 4, meta[k[0]]

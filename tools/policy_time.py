@@ -1,7 +1,10 @@
 """Device time of he_rollout_policy (the baseline policies fused into the rollout, baselines.py:74-103,
 delta_and_nothing.py:122-163) at the headline's env count, against he_rollout with stored actions.
 
-    python tools/policy_time.py [n_envs] [K] [launches]
+    python tools/policy_time.py [n_envs] [K] [launches] [gbm|replay]
+
+replay: the baselines' own setting (baselines.py:132-138: the v1 env on an NPZ of paths), here a
+synthetic 100,000 x 253 table (bench.replay_tables).
 """
 import os
 import sys
@@ -30,7 +33,14 @@ def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
     K = int(sys.argv[2]) if len(sys.argv) > 2 else 256
     L = int(sys.argv[3]) if len(sys.argv) > 3 else 20
-    env = HedgingVecEnv(n, mode="gbm", generate=bench.GEN, seed=42, return_numpy=False, info_keys=(), **bench.TRAIN_KW)
+    mode = sys.argv[4] if len(sys.argv) > 4 else "gbm"
+    if mode == "replay":
+        env = HedgingVecEnv(n, tables=bench.replay_tables(paths=100000, cols=253), variant=1, seed=42,
+                            return_numpy=False, info_keys=())
+    else:
+        env = HedgingVecEnv(n, mode="gbm", generate=bench.GEN, seed=42, return_numpy=False, info_keys=(),
+                            **bench.TRAIN_KW)
+    print(f"mode {mode}, {n} envs, K = {K}, {L} launches", flush=True)
     env.reset_tensors()
     acts = torch.rand((K, n, 2), device="cuda") * 2 - 1
     obs = torch.empty((K, n, 13), device="cuda")
