@@ -197,6 +197,8 @@ def parse(argv=None):
                          "train_ppo_v2.py:48, on the LDS path; 64 on the tile path)")
     ap.add_argument("--no-step-api", action="store_true", help="skip the secondary graph-mode he_step run")
     ap.add_argument("--no-sb3-api", action="store_true", help="skip the host-API (SB3 VecEnv / single env) timing")
+    ap.add_argument("--no-policy-api", action="store_true",
+                    help="skip the closed-loop baseline-policy rollout (he_rollout_policy) timing")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=6.0, help="seconds per CPU-baseline leg (4 legs)")
     ap.add_argument("--seed", type=int, default=42)
@@ -1099,6 +1101,38 @@ def _host_loop_timing(fn, steps, warm):
     return wall, ts
 
 
+def policy_api(args, dev, K, stored_us, launches=100, warm_s=0.3):
+    """Closed loop: he_rollout_policy, the reference's baseline policy evaluated on the env's own obs
+    inside the rollout (baselines.py:77-103's policy_delta_every_step; on the LDS kernels with the
+    policy in both lean / replay steppers), K steps per launch with obs / reward / done out, against
+    the stored-action rollout of the same launch shape (`stored_us`)."""
+    env = make_env(args, dev)
+    n = env.num_envs
+    obs = torch.empty((K, n, 13), dtype=torch.float32, device=dev)
+    rew = torch.empty((K, n), dtype=torch.float32, device=dev)
+    term = torch.empty((K, n), dtype=torch.uint8, device=dev)
+    # warm until the clocks are back up after the env's construction (as the timed region's
+    # MIN_WARMUP_SECONDS): batches of 20 launches for warm_s seconds
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < warm_s:
+        for _ in range(20):
+            env.rollout_policy(K, "delta_every_step", None, obs, rew, term)
+        torch.cuda.synchronize(dev)
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(launches):
+        env.rollout_policy(K, "delta_every_step", None, obs, rew, term)
+    b.record()
+    torch.cuda.synchronize(dev)
+    us = a.elapsed_time(b) * 1e3 / launches
+    env.close()
+    return dict(policy="delta_every_step", launches=launches, rollout_k=K, kernel_us=round(us, 3),
+                value=round(n * K / us * 1e6, 1), unit="env-steps/s",
+                vs_stored_actions=round(stored_us / us, 4) if stored_us else None,
+                what="device time per he_rollout_policy launch (HIP events around %d launches on the env's "
+                     "stream): the actions come from the policy on each step's obs, not from memory" % launches)
+
+
 def sb3_api(dev, classes=None, envs=SB3_API_ENVS, steps=504):
     """Wall time of the host paths the unchanged agents call:
 
@@ -1634,6 +1668,9 @@ def main(argv=None):
     sb3 = None
     if world == 1 and args.config == 2 and not args.no_sb3_api:
         sb3 = sb3_api(dev)
+    pol = None
+    if world == 1 and args.mode == "rollout" and not args.no_policy_api:
+        pol = policy_api(args, dev, args.rollout_k, kern_ms * 1e3)
 
     if rank == 0:
         line = {
@@ -1665,6 +1702,7 @@ def main(argv=None):
             "roofline": roof,
             "step_api": step_api,
             "sb3_api": sb3,
+            "policy_api": pol,
             "shard_check": shard,
             "cpu_baseline": cpu,
         }
