@@ -43,8 +43,10 @@ GENERATE_DEFAULTS = dict(s0=496.48001098632812, variance=0.029028, mu=0.04, dt=1
 
 MONITOR_KEYWORDS = ("per_share_step_pnl", "raw_pnl_deviation_abs", "transaction_costs_total")
 # host_io="auto": the NumPy step path (step_wait) of up to this many envs steps through
-# host-mapped memory (he_host_alloc): no DMA, one launch and one stream wait per step
-HOST_IO_MAX_ENVS = 4096
+# host-mapped memory (he_host_alloc): no DMA, one launch, the kernel-raised completion word.
+# The crossover (MI355X, step_async + step_wait with Monitor, profiles/r06h_host_io_scan.txt):
+# 53 against 67 us at 8,192 envs, 105 against 79 us at 16,384 (the kernel's PCIe writes).
+HOST_IO_MAX_ENVS = 8192
 
 _TORCH_DT = {"f8": torch.float64, "f4": torch.float32, "i4": torch.int32}
 _NP_DT = {torch.float64: np.float64, torch.float32: np.float32, torch.int32: np.int32}

@@ -25,12 +25,13 @@ def _pair(n, host_io="auto"):
     return a, b
 
 
-@pytest.mark.parametrize("n,host_io", [(2, "auto"), (300, "auto"), (300, False), (5000, "auto")])
+@pytest.mark.parametrize("n,host_io", [(2, "auto"), (300, "auto"), (300, False), (5000, "auto"), (9000, "auto")])
 def test_numpy_path_equals_device_path_and_late_infos_keep_their_step(n, host_io):
-    """step_wait through the host-mapped block (host_io: n <= 4096 by default) and through the
-    device io buffer + one pinned DMA (n = 5000, or host_io=False) against step_tensors."""
+    """step_wait through the host-mapped block (host_io: n <= HOST_IO_MAX_ENVS by default) and through
+    the device io buffer + one pinned DMA (n = 9000, or host_io=False) against step_tensors."""
     a, b = _pair(n, host_io)
-    assert (a._hio is not None) == (host_io == "auto" and n <= 4096)
+    from cantorrl_amd.vec_env import HOST_IO_MAX_ENVS
+    assert (a._hio is not None) == (host_io == "auto" and n <= HOST_IO_MAX_ENVS)
     oa = a.reset()
     ob = b.reset_tensors().cpu().numpy()
     assert np.array_equal(oa, ob)
