@@ -153,3 +153,36 @@ def test_step_signal_raises_each_armed_step_once(n):
     assert int(flag[0]) == 41
     a.close()
     b.close()
+
+
+def test_signal_wait_behind_long_work_falls_back_to_the_stream():
+    """he_signal_wait on a step queued behind ~1 ms of other work on the same stream: the host's
+    spin (200 us) runs out, the stream synchronize takes over, and the flag then holds the step."""
+    import ctypes
+    import time
+    from cantorrl_amd import _lib
+    from cantorrl_amd.vec_env import HedgingVecEnv
+    a, b = _pair(2)
+    b.close()
+    z = a._hio
+    lib, h = a.lib, a._h
+    flag = np.frombuffer((ctypes.c_uint32 * 1).from_address(z.h_flag), np.uint32)
+    st = torch.cuda.current_stream().cuda_stream
+    a.reset()
+    big = HedgingVecEnv(65536, mode="gbm", generate=GEN, seed=3, device=DEV, return_numpy=False, info_keys=(), **KW)
+    big.reset_tensors()
+    acts = torch.rand((256, 65536, 2), device=DEV) * 2 - 1
+    torch.cuda.synchronize()
+    for _ in range(4):          # ~1 ms of rollouts ahead of the step on the same stream
+        big.rollout(acts)
+    np.copyto(z.act, 0.25)
+    seq = lib.he_signal_seq(h) + 1
+    assert lib.he_step_signal(h, z.d_flag) == _lib.HE_OK
+    assert lib.he_step(h, *z.step_args, st) == _lib.HE_OK
+    t0 = time.perf_counter()
+    assert lib.he_signal_wait(h, z.h_flag, st) == _lib.HE_OK
+    waited = time.perf_counter() - t0
+    assert int(flag[0]) == seq == lib.he_signal_seq(h)
+    assert waited > 200e-6   # the rollouts were still running when the wait began
+    big.close()
+    a.close()
