@@ -28,13 +28,13 @@ if [ "$PHASE" = extra ]; then
   cd /tmp
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_aux -o aux -- python3 $R/tools/aux_time.py > $O/aux_prof.log 2>&1 || { tail -20 $O/aux_prof.log; exit 1; }
   cd $R
-  python3 tools/kstats.py $O/prof_aux | head -12
+  python3 tools/kstats.py $O/prof_aux > $O/kstats_aux.txt; head -12 $O/kstats_aux.txt
   echo "[$(date +%T)] rbergomi bench under rocprofv3 --kernel-trace --stats"
   cd /tmp
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/rbprof -o run -- python3 $R/bench.py --workload rbergomi --steps 3 --warmup 1 > $O/rb_rocprof.log 2>&1 || { tail -20 $O/rb_rocprof.log; exit 1; }
   cd $R
   grep "^{" $O/rb_rocprof.log > $O/rb_bench.jsonl
-  python3 tools/kstats.py $O/rbprof | head -6
+  python3 tools/kstats.py $O/rbprof > $O/kstats_rb.txt; head -6 $O/kstats_rb.txt
   echo "[$(date +%T)] rbergomi VALU pass"
   bash tools/gpu/rb_pmc.sh $TAG/rbpmc || exit 1
   echo "[$(date +%T)] done"
@@ -48,12 +48,12 @@ cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 $R/bench.py --no-pmc --no-cpu-baseline --no-step-api > $O/bench_rocprof.log 2>&1 || { tail -20 $O/bench_rocprof.log; exit 1; }
 cd $R
 grep "^{" $O/bench_rocprof.log > $O/bench_under_rocprof.jsonl
-python3 tools/kstats.py $O/prof | head -4
+python3 tools/kstats.py $O/prof > $O/kstats.txt; head -4 $O/kstats.txt
 echo "[$(date +%T)] config 6 under rocprofv3 --kernel-trace --stats"
 cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof6 -o run -- python3 $R/bench.py --config 6 --no-pmc --no-cpu-baseline --no-step-api > $O/bench6_rocprof.log 2>&1 || { tail -20 $O/bench6_rocprof.log; exit 1; }
 cd $R
-python3 tools/kstats.py $O/prof6 | head -4
+python3 tools/kstats.py $O/prof6 > $O/kstats6.txt; head -4 $O/kstats6.txt
 for c in 3 4 5 6; do
   echo "[$(date +%T)] bench config $c"
   # configs 4, 5 (book / Heston: producer-bound) and 6 (replay) with the PMC passes: traffic + VALU issue
@@ -70,6 +70,6 @@ import json
 for f in ("bench.jsonl", "bench_under_rocprof.jsonl", "bench_cfg345.jsonl", "bench_gpus2_rehearsal.jsonl"):
     for l in open("$O/" + f):
         d = json.loads(l); r = d.get("roofline", {})
-        print(f, d["config"].get("config_index"), d["n_gpus"], "%.4g" % d["value"], r.get("kernel_us"), r.get("frac"), r.get("traffic_over_bytes"), (r.get("valu") or {}).get("valu_issue_frac"), d.get("gather", {}).get("envs_with_finished_episode"))
+        print(f, d["config"].get("config_index"), d["n_gpus"], "%.4g" % d["value"], r.get("kernel_us"), r.get("frac"), r.get("traffic_over_bytes"), (r.get("valu") or {}).get("valu_issue_frac"), d.get("gather", {}).get("envs_with_finished_episode"), (d.get("policy_api") or {}).get("kernel_us"))
 PY
 echo "[$(date +%T)] done"
