@@ -1310,14 +1310,17 @@ _POL_BOOK = [dict(type="call", strike=500.0, expiry=30, quantity=-20.0),
              dict(type="uo_call", strike=496.0, barrier=530.0, expiry=40, quantity=-50.0)]
 
 
-@pytest.mark.parametrize("mode,book", [("gbm", None), ("heston", None), ("gbm", _POL_BOOK), ("heston", _POL_BOOK)])
+@pytest.mark.parametrize("mode,book,grid", [("gbm", None, 0), ("heston", None, 0), ("gbm", _POL_BOOK, 0),
+                                            ("heston", _POL_BOOK, 0), ("gbm", None, 3), ("heston", None, 5)])
 @pytest.mark.parametrize("policy", ["no_hedge", "delta_every_step", "delta_threshold"])
-def test_lds_policy_rollout_equals_tile_policy_rollout(mode, book, policy, monkeypatch):
+def test_lds_policy_rollout_equals_tile_policy_rollout(mode, book, grid, policy, monkeypatch):
     """he_rollout_policy on lds_rollout_kernel<..., POL> (the policy evaluated by both lean steppers)
     against the tile kernels' step_kernel<POL> (HE_LDS_POLICY=0), bit for bit: actions, obs, rewards,
     done flags of every launch (ragged K, episode ends inside and across launches, a partial last
     workgroup), the episode records (per env in finishing order), the record count, the episode
-    summaries and the whole checkpointed state; one launch without obs / reward / done buffers."""
+    summaries and the whole checkpointed state; one launch without obs / reward / done buffers.
+    grid > 0: the persistent instance, its grid capped (HE_LDS_MAX_GRID) so each workgroup runs
+    several of the 16 tiles."""
     from cantorrl_amd import _lib
     from cantorrl_amd.vec_env import HedgingVecEnv
     n = 1000
@@ -1331,8 +1334,11 @@ def test_lds_policy_rollout_equals_tile_policy_rollout(mode, book, policy, monke
     for lds in (True, False):
         if not lds:
             monkeypatch.setenv("HE_LDS_POLICY", "0")
+        elif grid:
+            monkeypatch.setenv("HE_LDS_MAX_GRID", str(grid))
         envs.append(HedgingVecEnv(n, mode=mode, generate=gen, seed=5, return_numpy=False, info_keys=(), **kw))
         monkeypatch.delenv("HE_LDS_POLICY", raising=False)
+        monkeypatch.delenv("HE_LDS_MAX_GRID", raising=False)
     cap = 8 * n   # 230 steps of 40-step episodes: 5 or 6 records per env
     bufs = []
     for e in envs:
