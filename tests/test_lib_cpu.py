@@ -230,3 +230,13 @@ def test_lockstep_math_equals_scalar_forms():
     u = rng.random(2 * 30001)
     u[:8] = [0.125, 0.25, 0.5, 0.75, 1 - 2 ** -53, 2 ** -53, 0.70710678118654752, 0.5 + 2 ** -40]
     assert np.array_equal(run(5, u).view(np.int64), run(4, u).view(np.int64))
+
+
+def test_step_signal_entry_points_reject_null_without_gpu():
+    """he_step_signal / he_signal_seq / he_signal_wait (the host-mapped step's completion word):
+    argument errors come back as status codes, with no handle and no GPU."""
+    lib = _lib.load()
+    flag = (_lib.ctypes.c_uint32 * 1)()
+    assert lib.he_step_signal(None, _lib.ctypes.addressof(flag)) == _lib.HE_EINVAL
+    assert lib.he_signal_seq(None) == 0
+    assert lib.he_signal_wait(None, _lib.ctypes.addressof(flag), None) == _lib.HE_EINVAL
