@@ -320,7 +320,9 @@ he_status he_stream_wait(void* stream);
  * signalled step by reading the word through its HOST address: a short spin, then (a step queued behind
  * long work) hipStreamSynchronize(stream) and a final check (HE_ESTATE if the flag still differs).
  * It replaces he_stream_wait when that step is the last work on the stream the caller waits for;
- * he_step with VecNormalize attached refuses the signal (HE_EINVAL).  The kernel's end is still
+ * he_step with VecNormalize attached refuses the signal (HE_EINVAL).  A handle's first
+ * he_step_signal allocates the device word that counts the step's workgroups (a device
+ * synchronize, once); later calls only arm.  The kernel's end is still
  * reported to the runtime as usual, so later stream-ordered work and events are unaffected. */
 he_status he_step_signal(he_env* env, uint32_t* flag);
 uint32_t he_signal_seq(const he_env* env);

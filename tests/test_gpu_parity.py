@@ -1433,3 +1433,40 @@ def test_lds_replay_policy_rollout_equals_tile_policy_rollout(case, policy, monk
     assert np.array_equal(st[0], st[1])
     for e in envs:
         e.close()
+
+
+@pytest.mark.parametrize("policy", ["delta_every_step", "delta_threshold"])
+def test_policy_rollout_sharding_invariance(policy):
+    """Policy rollouts on the LDS kernels (§1d) keep env g's trajectory a function of (seed, g): a
+    2-way shard by global_env_offset equals the whole, actions, obs, rewards and done flags, and the
+    episode records carry the global env id (the multi-GPU partition)."""
+    from cantorrl_amd import _lib
+    from cantorrl_amd.vec_env import HedgingVecEnv
+    n, K = 640, 90
+    gen = dict(s0=496.48001098632812, variance=0.029028, mu=0.04, dt=1 / 252, episode_length=40)
+    kw = dict(loss_type="abs", pnl_penalty_weight=0.001, lambda_cost=0.0001, theta_weight=0.0002, slippage_bps=1.0)
+    envs = [HedgingVecEnv(m, mode="gbm", generate=gen, seed=9, global_env_offset=off, return_numpy=False,
+                          info_keys=(), **kw) for m, off in ((n, 0), (n // 2, 0), (n // 2, n // 2))]
+    outs = []
+    for e in envs:
+        e.reset_tensors()
+        m = e.num_envs
+        a = torch.empty((K, m, 2), device="cuda")
+        o = torch.empty((K, m, 13), device="cuda")
+        r = torch.empty((K, m), device="cuda")
+        t = torch.empty((K, m), dtype=torch.uint8, device="cuda")
+        recs = torch.zeros((4 * m, 80), dtype=torch.uint8, device="cuda")
+        cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+        e.rollout_policy(K, policy, a, o, r, t, recs, cnt)
+        torch.cuda.synchronize()
+        k = int(cnt.item())
+        rv = recs[:k].cpu().numpy().view(_lib.EPISODE_RECORD).reshape(k)
+        outs.append((a, o, r, t, np.sort(rv, order=["env_id", "length"])))
+    for j in range(4):
+        assert torch.equal(outs[0][j], torch.cat([outs[1][j], outs[2][j]], dim=1)), j
+    whole = outs[0][4]
+    halves = np.sort(np.concatenate([outs[1][4], outs[2][4]]), order=["env_id", "length"])
+    assert len(whole) == 2 * n and whole.tobytes() == halves.tobytes()
+    assert set(outs[2][4]["env_id"].tolist()) == set(range(n // 2, n))
+    for e in envs:
+        e.close()

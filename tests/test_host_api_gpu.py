@@ -169,12 +169,14 @@ def test_signal_wait_behind_long_work_falls_back_to_the_stream():
     flag = np.frombuffer((ctypes.c_uint32 * 1).from_address(z.h_flag), np.uint32)
     st = torch.cuda.current_stream().cuda_stream
     a.reset()
+    a.step(np.zeros((2, 2), np.float32))   # the first armed step allocates the counter (a device sync)
     big = HedgingVecEnv(65536, mode="gbm", generate=GEN, seed=3, device=DEV, return_numpy=False, info_keys=(), **KW)
     big.reset_tensors()
     acts = torch.rand((256, 65536, 2), device=DEV) * 2 - 1
+    outs = big.rollout(acts)    # the output buffers allocated (a fresh hipMalloc synchronizes)
     torch.cuda.synchronize()
     for _ in range(4):          # ~1 ms of rollouts ahead of the step on the same stream
-        big.rollout(acts)
+        big.rollout(acts, *outs)
     np.copyto(z.act, 0.25)
     seq = lib.he_signal_seq(h) + 1
     assert lib.he_step_signal(h, z.d_flag) == _lib.HE_OK
