@@ -2224,7 +2224,6 @@ __device__ __forceinline__ void flush_obs_full(const float* img, float* out, int
 template <int MODE, bool BOOK, bool LEAN, bool OBS, bool POL = false>
 __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& io, int k_steps, const Market& cur,
                                             LdsMarketT<MODE, BOOK, LEAN>& L, int64_t base) {
-    static_assert(!POL || LEAN, "policy rollouts on the lean steppers only (lds_policy_eligible)");
     constexpr int D = kLdsPrefetch;
     constexpr bool HESTON = MODE == HE_MODE_HESTON;
     const int lane = threadIdx.x & 63;
@@ -2317,16 +2316,20 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
     float po3 = 0.0f, po4 = 0.0f, pcd = 0.0f, ppd = 0.0f;
     double acc[7] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
     uint32_t acc_len = 0;
+    // (the lean configuration has max_contracts_held > 0 and record_metrics; the generic steppers
+    // test them, as make_obs does)
+    const bool pmh = LEAN || p.maxh != 0, prm = LEAN || p.record_metrics;
     if constexpr (POL) {
-        po3 = div_int_byf((float)e.call, p.maxh_f, p.inv_maxh_f);   // lean: max_contracts_held > 0
-        po4 = div_int_byf((float)e.put, p.maxh_f, p.inv_maxh_f);
+        po3 = pmh ? div_int_byf((float)e.call, p.maxh_f, p.inv_maxh_f) : 0.0f;
+        po4 = pmh ? div_int_byf((float)e.put, p.maxh_f, p.inv_maxh_f) : 0.0f;
         if (e.t == 0) {
             pcd = p.rstv[4 + 7];
             ppd = p.rstv[4 + 9];
-        } else if (pol_greeks) {
+        } else if (pol_greeks && prm) {
             const float S0f = (float)cur.S[i];
             float4 g0;
-            if constexpr (HESTON) g0 = greeks_fast<false>(p, S0f, (float)cur.v[i]);
+            if constexpr (!LEAN) g0 = greeks_fast<!HESTON>(p, S0f, HESTON ? (float)cur.v[i] : p.var_f);
+            else if constexpr (HESTON) g0 = greeks_fast<false>(p, S0f, (float)cur.v[i]);
             else g0 = greeks_lean(S0f, p.g_num_drift, p.g_inv_sst_f, p.g_sst_f);
             pcd = g0.x;
             ppd = g0.z;
@@ -2337,6 +2340,46 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
             acc_len = s.acc_len[i];
         }
     }
+    // POL, the reward wave: step_body's sums in step order and the record of a finished episode
+    auto pol_account = [&](double reward, double pnl, double ps, double tc, double rpc, double tcp, bool term) {
+        acc[0] = acc[0] + reward;
+        acc[1] = acc[1] + pnl;
+        acc[2] = acc[2] + fabs(ps);
+        acc[3] = acc[3] + tc;
+        acc[4] = acc[4] + rpc;
+        acc[5] = acc[5] + tcp;
+        acc[6] = acc[6] + ps;
+        acc_len += 1u;
+        if (__ballot(term) != 0ull) {   // fixed-length episodes end together: uniform
+            if (term) {
+                if (i0 < N) {   // not the lanes mirroring env N - 1
+                    const unsigned long long r = atomicAdd(io.pol.count, 1ull);
+                    if ((int64_t)r < io.pol.cap) {
+                        he_episode_record rec;
+                        rec.env_id = p.goff + i;
+                        rec.length = (int32_t)acc_len;
+                        rec.reserved = 0;
+                        rec.reward_sum = acc[0];
+                        rec.pnl_sum = acc[1];
+                        rec.abs_pnl_sum = acc[2];
+                        rec.cost_sum = acc[3];
+                        rec.pnl_penalty_sum = acc[4];
+                        rec.cost_penalty_sum = acc[5];
+                        rec.per_share_pnl_sum = acc[6];
+                        rec.reserved2 = 0.0;
+                        io.pol.rec[r] = rec;
+                    }
+                }
+                last0 = (float)acc[0];
+                last1 = (float)acc[1];
+                last2 = (float)acc[3];
+                last3 = (float)acc_len;
+#pragma unroll
+                for (int c = 0; c < 7; ++c) acc[c] = 0.0;
+                acc_len = 0;
+            }
+        }
+    };
 
     // ---- the block loop over a step function step(buf, sl, k, action, in_full_block)
     constexpr int NB = LdsMarketT<MODE, BOOK, LEAN>::NB;
@@ -2544,44 +2587,7 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
                 if (!POL || grew) grew[koff + i] = (float)reward;
                 if (!POL || gterm) gterm[koff + i] = term ? 1 : 0;
                 if constexpr (POL) {
-                    // step_body's POL sums, in step order, and the record of a finished episode
-                    acc[0] = acc[0] + reward;
-                    acc[1] = acc[1] + pnl;
-                    acc[2] = acc[2] + fabs(ps);
-                    acc[3] = acc[3] + tc;
-                    acc[4] = acc[4] + rpc;
-                    acc[5] = acc[5] + tcp;
-                    acc[6] = acc[6] + ps;
-                    acc_len += 1u;
-                    if (__ballot(term) != 0ull) {   // fixed-length episodes end together: uniform
-                        if (term) {
-                            if (i0 < N) {   // not the lanes mirroring env N - 1
-                                const unsigned long long r = atomicAdd(io.pol.count, 1ull);
-                                if ((int64_t)r < io.pol.cap) {
-                                    he_episode_record rec;
-                                    rec.env_id = p.goff + i;
-                                    rec.length = (int32_t)acc_len;
-                                    rec.reserved = 0;
-                                    rec.reward_sum = acc[0];
-                                    rec.pnl_sum = acc[1];
-                                    rec.abs_pnl_sum = acc[2];
-                                    rec.cost_sum = acc[3];
-                                    rec.pnl_penalty_sum = acc[4];
-                                    rec.cost_penalty_sum = acc[5];
-                                    rec.per_share_pnl_sum = acc[6];
-                                    rec.reserved2 = 0.0;
-                                    io.pol.rec[r] = rec;
-                                }
-                            }
-                            last0 = (float)acc[0];
-                            last1 = (float)acc[1];
-                            last2 = (float)acc[3];
-                            last3 = (float)acc_len;
-#pragma unroll
-                            for (int c = 0; c < 7; ++c) acc[c] = 0.0;
-                            acc_len = 0;
-                        }
-                    }
+                    pol_account(reward, pnl, ps, tc, rpc, tcp, term);
                     // the obs row this step returns, as the obs stepper makes it: the positions'
                     // columns and the greeks of the slot's market (greeks_lean / greeks_fast<false>)
                     float gx = 0.0f, gz = 0.0f;
@@ -2621,7 +2627,12 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
             const float2 sc = L.sc[buf][sl][lane];
             const float vk = HESTON ? L.vv[HESTON ? buf : 0][HESTON ? sl : 0][lane] : p.var_f;
             const Mkt post{sc.x, vk, sc.y, L.pp[buf][sl][lane], BOOK ? L.bk[buf][sl][lane] : 0.0};
+            if constexpr (POL) ak = policy_action(p, pol, e.call, e.put, po3, po4, pcd, ppd);
             if (OBS) {
+                if (POL && io.pol.act_out) {
+                    v2f av = {ak.x, ak.y};
+                    ((GLOBAL v2f*)io.pol.act_out)[koff + i] = av;
+                }
                 // the obs greeks of market_body's greeks records (Heston: of the slot's v)
                 float4 g = p.record_metrics ? greeks_fast<!HESTON>(p, post.S, post.v) : make_float4(0.f, 0.f, 0.f, 0.f);
                 g.w = lag_return(post.S, pre.S);
@@ -2637,6 +2648,12 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
                 float* const tile = L.stage[k & 1];
 #pragma unroll
                 for (int c = 0; c < kObs; ++c) tile[lane * kObs + c] = term ? p.rstv[4 + c] : o[c];  // SB3 autoreset obs
+                if constexpr (POL) {   // the row this step returns
+                    po3 = term ? p.rstv[4 + 3] : o[3];
+                    po4 = term ? p.rstv[4 + 4] : o[4];
+                    pcd = term ? p.rstv[4 + 7] : o[7];
+                    ppd = term ? p.rstv[4 + 9] : o[9];
+                }
                 if (io.obs) {
                     if constexpr (decltype(full)::value) flush_obs_full(tile, io.obs + koff * kObs, base, lane);
                     else flush_obs_wave(tile, io.obs + koff * kObs, base, wrows, lane);
@@ -2649,7 +2666,23 @@ __device__ __forceinline__ void lds_stepper(const Params& p, State s, const Io& 
                 pv_last = so.pv;
                 if (grew) grew[koff + i] = (float)so.reward;
                 if (gterm) gterm[koff + i] = so.term ? 1 : 0;
-                account(so.reward, so.pnl, so.tc, so.term);
+                if constexpr (POL) {
+                    pol_account(so.reward, so.pnl, so.ps, so.tc, so.rpc, so.tcp, so.term);
+                    // the row this step returns, as the obs stepper makes it (make_obs<false>'s columns
+                    // of the post-trade positions and the slot's greeks, or the reset row)
+                    float gx = 0.0f, gz = 0.0f;
+                    if (pol_greeks && prm) {
+                        const float4 g = greeks_fast<!HESTON>(p, post.S, post.v);
+                        gx = g.x;
+                        gz = g.z;
+                    }
+                    po3 = so.term ? p.rstv[4 + 3] : (pmh ? div_int_byf((float)e.call, p.maxh_f, p.inv_maxh_f) : 0.0f);
+                    po4 = so.term ? p.rstv[4 + 4] : (pmh ? div_int_byf((float)e.put, p.maxh_f, p.inv_maxh_f) : 0.0f);
+                    pcd = so.term ? p.rstv[4 + 7] : gx;
+                    ppd = so.term ? p.rstv[4 + 9] : gz;
+                } else {
+                    account(so.reward, so.pnl, so.tc, so.term);
+                }
                 pre = so.term ? rst : post;
                 if (so.term) env_reset_common(p, e);
             }
@@ -4435,14 +4468,11 @@ static bool lds_rollout_eligible(const he_env* env) {
            (env->cfg.book_size == 0 || env->book_rows <= kLdsBookRows);
 }
 
-// he_rollout_policy through lds_rollout_kernel<..., POL>: the lean configurations (the policy in
-// both lean steppers), autoreset; the obs / reward / terminated buffers may be absent.
-static bool lds_policy_eligible(const he_env* env, const Io& io) {
-    Io o = io;
-    o.obs = o.obs ? o.obs : reinterpret_cast<float*>(16);   // (lds_lean_config's output test only)
-    o.rew = o.rew ? o.rew : reinterpret_cast<float*>(16);
-    o.term = o.term ? o.term : reinterpret_cast<uint8_t*>(16);
-    return env->lds_policy && env->cfg.autoreset && lds_rollout_eligible(env) && lds_lean_config(env, o);
+// he_rollout_policy through lds_rollout_kernel<..., POL>: every generate configuration the LDS
+// rollout takes (the policy in both steppers, lean or generic), autoreset; the obs / reward /
+// terminated buffers may be absent.
+static bool lds_policy_eligible(const he_env* env) {
+    return env->lds_policy && env->cfg.autoreset && lds_rollout_eligible(env);
 }
 
 static he_status launch_lds_rollout(he_env* env, const Io& io, int k_total, hipStream_t st) {
@@ -4450,15 +4480,23 @@ static he_status launch_lds_rollout(he_env* env, const Io& io, int k_total, hipS
     if (s != HE_OK) return s;
     const int64_t blocks = (env->cfg.n_envs + kLdsEnvs - 1) / kLdsEnvs;
     const Params* pc = env->dparams;  // buffer 0's copy: the tile pointers are not used
-    const bool book = env->cfg.book_size > 0, pol = io.pol_on, lean = pol || lds_lean_config(env, io);
+    const bool book = env->cfg.book_size > 0, pol = io.pol_on;
+    bool lean = lds_lean_config(env, io);
+    if (pol) {   // policy rollouts may return no obs / reward / done: the lean test on the rest
+        Io o = io;
+        o.obs = o.obs ? o.obs : reinterpret_cast<float*>(16);
+        o.rew = o.rew ? o.rew : reinterpret_cast<float*>(16);
+        o.term = o.term ? o.term : reinterpret_cast<uint8_t*>(16);
+        lean = lds_lean_config(env, o);
+    }
     void (*kern)(const Params*, State, Io, int, Market);
     void (*kern_p)(const Params*, State, Io, int, Market);   // the persistent-grid instance
     int threads;
 #define HE_LDS_PICK(M, B, L)                                                  \
     do {                                                                      \
         if (pol) {                                                            \
-            kern = lds_rollout_kernel<M, B, true, false, true>;               \
-            kern_p = lds_rollout_kernel<M, B, true, !(B), true>;              \
+            kern = lds_rollout_kernel<M, B, L, false, true>;                  \
+            kern_p = lds_rollout_kernel<M, B, L, !(B), true>;                 \
         } else {                                                              \
             kern = lds_rollout_kernel<M, B, L, false>;                        \
             kern_p = lds_rollout_kernel<M, B, L, !(B)>;                       \
@@ -4574,7 +4612,7 @@ static he_status launch_steps(he_env* env, Io io, bool info, int k_total, void* 
         return HE_OK;
     }
     if (rollout && !info && !io.pol_on && lds_rollout_eligible(env)) return launch_lds_rollout(env, io, k_total, st);
-    if (io.pol_on && lds_policy_eligible(env, io)) return launch_lds_rollout(env, io, k_total, st);
+    if (io.pol_on && lds_policy_eligible(env)) return launch_lds_rollout(env, io, k_total, st);
     const int32_t M = c.market_block;
     const int64_t N = c.n_envs;
     int done = 0;

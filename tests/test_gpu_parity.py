@@ -1310,10 +1310,21 @@ _POL_BOOK = [dict(type="call", strike=500.0, expiry=30, quantity=-20.0),
              dict(type="uo_call", strike=496.0, barrier=530.0, expiry=40, quantity=-50.0)]
 
 
-@pytest.mark.parametrize("mode,book,grid", [("gbm", None, 0), ("heston", None, 0), ("gbm", _POL_BOOK, 0),
-                                            ("heston", _POL_BOOK, 0), ("gbm", None, 3), ("heston", None, 5)])
+_POL_GENERIC = {   # configurations outside the lean one: the generic LDS steppers with the policy
+    None: {},
+    "v1": dict(variant=1),
+    "mse_nometrics": dict(loss_type="mse", record_metrics=False, initial_cash=1000.0),
+    "fixed_european": dict(mark="fixed_european"),
+}
+
+
+@pytest.mark.parametrize("mode,book,grid,generic", [
+    ("gbm", None, 0, None), ("heston", None, 0, None), ("gbm", _POL_BOOK, 0, None), ("heston", _POL_BOOK, 0, None),
+    ("gbm", None, 3, None), ("heston", None, 5, None),
+    ("gbm", None, 0, "v1"), ("heston", _POL_BOOK, 0, "mse_nometrics"), ("gbm", None, 0, "fixed_european"),
+    ("heston", None, 4, "v1")])
 @pytest.mark.parametrize("policy", ["no_hedge", "delta_every_step", "delta_threshold"])
-def test_lds_policy_rollout_equals_tile_policy_rollout(mode, book, grid, policy, monkeypatch):
+def test_lds_policy_rollout_equals_tile_policy_rollout(mode, book, grid, generic, policy, monkeypatch):
     """he_rollout_policy on lds_rollout_kernel<..., POL> (the policy evaluated by both lean steppers)
     against the tile kernels' step_kernel<POL> (HE_LDS_POLICY=0), bit for bit: actions, obs, rewards,
     done flags of every launch (ragged K, episode ends inside and across launches, a partial last
@@ -1330,6 +1341,13 @@ def test_lds_policy_rollout_equals_tile_policy_rollout(mode, book, grid, policy,
     if book is not None:
         gen["book"] = book
     kw = dict(loss_type="abs", pnl_penalty_weight=0.001, lambda_cost=0.0001, theta_weight=0.0002, slippage_bps=1.0)
+    extra = dict(_POL_GENERIC[generic])
+    if "mark" in extra:
+        gen["mark"] = extra.pop("mark")
+    if extra.get("variant") == 1:
+        kw.pop("theta_weight")
+        kw.pop("slippage_bps")
+    kw.update(extra)
     envs = []
     for lds in (True, False):
         if not lds:

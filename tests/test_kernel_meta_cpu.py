@@ -35,9 +35,9 @@ def _meta():
 def test_lds_kernels_spill_free():
     meta = _meta()
     rollout = {k: v for k, v in meta.items() if "lds_rollout_kernel" in k}
-    # GBM / Heston x book x lean instances, + the persistent-grid instances without a book, + the
-    # policy rollouts' lean instances (POL: 4 one-workgroup-per-tile, 2 persistent)
-    assert len(rollout) == 18, sorted(rollout)
+    # GBM / Heston x book x lean instances, + the persistent-grid instances without a book, and the
+    # same 12 again for policy rollouts (POL)
+    assert len(rollout) == 24, sorted(rollout)
     for k, v in rollout.items():
         assert v["vgpr_spill"] == 0 and v["scratch_B"] == 0, (k, v)
         assert v["vgpr"] <= 128, (k, v)         # 4 waves per SIMD

@@ -1,7 +1,7 @@
 """Device time of he_rollout_policy (the baseline policies fused into the rollout, baselines.py:74-103,
 delta_and_nothing.py:122-163) at the headline's env count, against he_rollout with stored actions.
 
-    python tools/policy_time.py [n_envs] [K] [launches] [gbm|replay]
+    python tools/policy_time.py [n_envs] [K] [launches] [gbm|gbm_v1|replay]
 
 replay: the baselines' own setting (baselines.py:132-138: the v1 env on an NPZ of paths), here a
 synthetic 100,000 x 253 table (bench.replay_tables).
@@ -34,7 +34,10 @@ def main():
     K = int(sys.argv[2]) if len(sys.argv) > 2 else 256
     L = int(sys.argv[3]) if len(sys.argv) > 3 else 20
     mode = sys.argv[4] if len(sys.argv) > 4 else "gbm"
-    if mode == "replay":
+    if mode == "gbm_v1":   # a configuration outside the lean one: the generic LDS steppers
+        env = HedgingVecEnv(n, mode="gbm", generate=bench.GEN, variant=1, seed=42, return_numpy=False,
+                            info_keys=())
+    elif mode == "replay":
         env = HedgingVecEnv(n, tables=bench.replay_tables(paths=100000, cols=253), variant=1, seed=42,
                             return_numpy=False, info_keys=())
     else:
