@@ -1488,3 +1488,36 @@ def test_policy_rollout_sharding_invariance(policy):
     assert set(outs[2][4]["env_id"].tolist()) == set(range(n // 2, n))
     for e in envs:
         e.close()
+
+
+def test_evaluate_policy_returns_the_first_episodes_of_the_fused_rollouts():
+    """HedgingVecEnv.evaluate_policy (baselines.py:32-72's loop as fused rollouts of `chunk` steps):
+    the records it returns are the records a manual he_rollout_policy loop over a twin handle
+    collects, as multisets (the ring order across envs is the atomics'), and their statistics
+    (evaluation.baseline_statistics) agree."""
+    from cantorrl_amd import _lib
+    from cantorrl_amd.evaluation import baseline_statistics
+    from cantorrl_amd.vec_env import HedgingVecEnv
+    n, T = 512, 40
+    gen = dict(s0=496.48001098632812, variance=0.029028, mu=0.04, dt=1 / 252, episode_length=T)
+    a = HedgingVecEnv(n, mode="gbm", generate=gen, variant=1, seed=4, return_numpy=False, info_keys=(),
+                      pnl_penalty_weight=0.0, lambda_cost=0.0)
+    b = HedgingVecEnv(n, mode="gbm", generate=gen, variant=1, seed=4, return_numpy=False, info_keys=(),
+                      pnl_penalty_weight=0.0, lambda_cost=0.0)
+    a.reset_tensors()
+    b.reset_tensors()
+    got = a.evaluate_policy("delta_every_step", num_episodes=2 * n, chunk=64)
+    assert len(got) == 2 * n
+    recs = torch.zeros((4 * n, 80), dtype=torch.uint8, device="cuda")
+    cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+    while int(cnt.item()) < 2 * n:
+        b.rollout_policy(64, "delta_every_step", records=recs, record_count=cnt)
+    m = int(cnt.item())
+    exp = recs[:m].cpu().numpy().view(_lib.EPISODE_RECORD).reshape(m)
+    # every env finishes its first two episodes at the same step: exactly those 2 n records
+    gs = np.sort(got, order=["env_id", "length", "reward_sum"])
+    es = np.sort(exp[:2 * n], order=["env_id", "length", "reward_sum"])
+    assert gs.tobytes() == es.tobytes()
+    assert baseline_statistics(gs) == baseline_statistics(es)
+    a.close()
+    b.close()
