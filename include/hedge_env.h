@@ -32,7 +32,8 @@
  *                      (src/agents/baselines.py:32-103) and run_benchmark_strategy(
  *                      delta_hedging_action_selector) (src/benchmark/delta_and_nothing.py:33-163):
  *                      the policy evaluated on the device from each step's obs, fused
- *                      into the step kernel, with per-episode sums recorded on device
+ *                      into the rollout kernel (the LDS kernels' steppers, or the tile
+ *                      step kernel), with per-episode sums recorded on device
  *   he_get_state / he_set_state  <- env pickling by SubprocVecEnv / checkpoints (no
  *                      reference equivalent; state is otherwise lost across processes)
  */
@@ -286,7 +287,7 @@ he_status he_rollout_policy(he_env* env, int32_t k_steps, int32_t policy, float*
 he_status he_episode_summaries(he_env* env, float* out, void* stream);
 
 /* Generate modes run market_kernel for block b+1 on a library-owned side stream
- * while the step kernels of block b run on `stream` (he_step, policy rollouts, books;
+ * while the step kernels of block b run on `stream` (he_step, tile-path policy rollouts, books;
  * he_rollout otherwise generates it inside its own grid on `stream`, which needs no
  * join).  he_sync_market makes `stream` wait for a side-stream prefetch: call it
  * before ending a hipGraph capture that contains he_step/he_rollout calls.  No-op in
