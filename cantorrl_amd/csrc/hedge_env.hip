@@ -5203,6 +5203,8 @@ he_status he_reset_episodes(he_env* env, const int64_t* env_ids, const int64_t* 
 he_status he_step(he_env* env, const float* actions, float* obs, float* reward, uint8_t* terminated,
                   uint8_t* truncated, float* terminal_obs, const he_info* info, void* stream) {
     if (!env) return HE_EINVAL;
+    uint32_t* const sig = env->sig_flag;  // he_step_signal: one-shot, this step only (consumed on any return)
+    env->sig_flag = nullptr;
     if (!actions) return fail(env, HE_EINVAL, "actions is NULL");
     Io io;
     memset(&io, 0, sizeof(io));
@@ -5236,8 +5238,6 @@ he_status he_step(he_env* env, const float* actions, float* obs, float* reward, 
         return fail(env, HE_EINVAL, "he_vecnorm_attach_eval with Monitor sums: an he_step that requests info "
                                     "must request info->reward_step too");
     }
-    uint32_t* const sig = env->sig_flag;  // he_step_signal: one-shot, this step only
-    env->sig_flag = nullptr;
     if (sig) {
         if (vn || vne) {
             env->vn_on = env->vne_on = false;

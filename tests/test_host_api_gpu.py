@@ -135,6 +135,13 @@ def test_step_signal_raises_each_armed_step_once(n):
     assert lib.he_step(h, *z.step_args, st) == _lib.HE_OK
     torch.cuda.synchronize()
     assert int(flag[0]) == 40 and lib.he_signal_seq(h) == 40
+    # an armed step that fails its argument checks consumes the arm too
+    args = list(z.step_args)
+    assert lib.he_step_signal(h, z.d_flag) == _lib.HE_OK
+    assert lib.he_step(h, None, *args[1:], st) == _lib.HE_EINVAL
+    assert lib.he_step(h, *z.step_args, st) == _lib.HE_OK
+    torch.cuda.synchronize()
+    assert int(flag[0]) == 40 and lib.he_signal_seq(h) == 40
     # armed again: the counter of the 12-workgroup grid was left at 0 by the last signalled step
     assert lib.he_step_signal(h, z.d_flag) == _lib.HE_OK
     assert lib.he_step(h, *z.step_args, st) == _lib.HE_OK
