@@ -1126,9 +1126,13 @@ def policy_api(args, dev, K, stored_us, launches=100, warm_s=0.3):
     torch.cuda.synchronize(dev)
     us = a.elapsed_time(b) * 1e3 / launches
     env.close()
+    # SURVEY 8(d)'s fused-rollout bytes without the 8-B action read (the policy makes it in the kernel)
+    pol_bytes = n * (K * (SURVEY_ROLLOUT_B - 8) + SURVEY_ROLLOUT_STATE_B)
+    gbs = pol_bytes / (us * 1e-6) / 1e9
     return dict(policy="delta_every_step", launches=launches, rollout_k=K, kernel_us=round(us, 3),
                 value=round(n * K / us * 1e6, 1), unit="env-steps/s",
                 vs_stored_actions=round(stored_us / us, 4) if stored_us else None,
+                bytes_per_launch=int(pol_bytes), achieved_gbs=round(gbs, 1), frac=round(gbs / HBM_PEAK_GBS, 4),
                 what="device time per he_rollout_policy launch (HIP events around %d launches on the env's "
                      "stream): the actions come from the policy on each step's obs, not from memory" % launches)
 
