@@ -1521,3 +1521,47 @@ def test_evaluate_policy_returns_the_first_episodes_of_the_fused_rollouts():
     assert baseline_statistics(gs) == baseline_statistics(es)
     a.close()
     b.close()
+
+
+@pytest.mark.parametrize("mode", ["gbm", "replay"])
+def test_policy_rollout_full_size_lds_equals_tile(mode, monkeypatch):
+    """At the headline's size (65,536 envs, K = 256, with an episode end inside the launch): the
+    LDS policy rollout (delta_every_step) equals the tile path bit for bit -- actions, rewards, done
+    flags, a sample of obs rows, every episode record per env and the checkpointed state."""
+    from cantorrl_amd import _lib
+    from cantorrl_amd.vec_env import HedgingVecEnv
+    n, K = 65536, 256
+    bench = _bench_module()
+    envs = []
+    for lds in (True, False):
+        if not lds:
+            monkeypatch.setenv("HE_LDS_POLICY", "0")
+        if mode == "gbm":
+            envs.append(HedgingVecEnv(n, mode="gbm", generate=bench.GEN, seed=42, return_numpy=False, info_keys=(),
+                                      **bench.TRAIN_KW))
+        else:
+            envs.append(HedgingVecEnv(n, tables=bench.replay_tables(paths=2000, cols=253), variant=1, seed=42,
+                                      return_numpy=False, info_keys=()))
+        monkeypatch.delenv("HE_LDS_POLICY", raising=False)
+    outs = []
+    for e in envs:
+        e.reset_tensors()
+        a = torch.empty((K, n, 2), device="cuda")
+        o = torch.empty((K, n, 13), device="cuda")
+        r = torch.empty((K, n), device="cuda")
+        t = torch.empty((K, n), dtype=torch.uint8, device="cuda")
+        recs = torch.zeros((2 * n, 80), dtype=torch.uint8, device="cuda")
+        cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+        e.rollout_policy(K, "delta_every_step", a, o, r, t, recs, cnt)
+        torch.cuda.synchronize()
+        m = int(cnt.item())
+        rv = recs[:m].cpu().numpy().view(_lib.EPISODE_RECORD).reshape(m)
+        outs.append((a, o[:, ::97], r, t, np.sort(rv, order=["env_id", "length", "reward_sum"]), e.get_state()))
+    (a0, o0, r0, t0, rec0, st0), (a1, o1, r1, t1, rec1, st1) = outs
+    assert torch.equal(a0.view(torch.int32), a1.view(torch.int32))
+    assert torch.equal(o0.contiguous().view(torch.int32), o1.contiguous().view(torch.int32))
+    assert torch.equal(r0.view(torch.int32), r1.view(torch.int32)) and torch.equal(t0, t1)
+    assert len(rec0) == n and rec0.tobytes() == rec1.tobytes()   # one 252-step episode ends per env
+    assert np.array_equal(st0, st1)
+    for e in envs:
+        e.close()
